@@ -1,0 +1,208 @@
+// kf_bindings.cpp — pybind11 module `_kafka_hip`.
+// Pointers cross the boundary as integers (torch data_ptr()); streams as
+// torch.cuda.current_stream().cuda_stream.  `device=True` launches the gfx950
+// kernel on the given stream, `device=False` runs the identical per-pixel
+// code on the host (kf_host.cpp).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <stdexcept>
+#include <string>
+#include <vector>
+#include "kf_launch.h"
+#include "kf_stream.h"
+
+namespace py = pybind11;
+using namespace kf;
+
+template <typename T>
+static T* P(uintptr_t v) { return reinterpret_cast<T*>(v); }
+
+static void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+static void check_host(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string(what) + ": unsupported n_params on host runner");
+}
+
+template <typename A, size_t N>
+static void set_arr(A (&dst)[N], const std::vector<A>& v, const char* name) {
+  if (v.size() > N) throw std::runtime_error(std::string(name) + " too long");
+  for (size_t i = 0; i < N; ++i) dst[i] = i < v.size() ? v[i] : A(0);
+}
+template <typename A, size_t N>
+static std::vector<A> get_arr(const A (&src)[N]) { return std::vector<A>(src, src + N); }
+
+#define PTR_FIELD(cls, name, T)                                                                     \
+  def_property(#name, [](const cls& s) { return (uintptr_t)s.name; },                              \
+               [](cls& s, uintptr_t v) { s.name = reinterpret_cast<T>(v); })
+#define ARR_FIELD(cls, name, T)                                                                     \
+  def_property(#name, [](const cls& s) { return get_arr(s.name); },                                \
+               [](cls& s, const std::vector<T>& v) { set_arr(s.name, v, #name); })
+
+PYBIND11_MODULE(_kafka_hip, m) {
+  m.doc() = "KaFKA MI355X kernels (gfx950) + host runner of the same per-pixel code";
+  m.attr("MAX_D") = MAX_D;
+  m.attr("MAX_BLOCKS") = KF_MAX_BLOCKS;
+  m.attr("SIZEOF_BANDDESC") = (int)sizeof(BandDesc);
+
+  py::class_<BandDesc>(m, "BandDesc")
+      .def(py::init([]() { BandDesc b; memset(&b, 0, sizeof(b)); return b; }))
+      .def_readwrite("op", &BandDesc::op)
+      .def_readwrite("obs", &BandDesc::obs)
+      .def_readwrite("d", &BandDesc::d)
+      .def_readwrite("T", &BandDesc::T)
+      .ARR_FIELD(BandDesc, map, int32_t)
+      .def_readwrite("scale", &BandDesc::scale)
+      .def_readwrite("rel_unc", &BandDesc::rel_unc)
+      .def_readwrite("unc_floor", &BandDesc::unc_floor)
+      .def_readwrite("offset", &BandDesc::offset)
+      .ARR_FIELD(BandDesc, coef, float)
+      .ARR_FIELD(BandDesc, center, float)
+      .PTR_FIELD(BandDesc, gp, const float*)
+      .PTR_FIELD(BandDesc, y, const float*)
+      .PTR_FIELD(BandDesc, w, const float*)
+      .PTR_FIELD(BandDesc, mask, const uint8_t*)
+      .PTR_FIELD(BandDesc, dn, const uint16_t*)
+      .PTR_FIELD(BandDesc, aux, const float*)
+      .PTR_FIELD(BandDesc, pre_h0, const float*)
+      .PTR_FIELD(BandDesc, pre_h, const float*)
+      .PTR_FIELD(BandDesc, h0_out, float*)
+      .def_readwrite("pre_ld", &BandDesc::pre_ld);
+
+  m.def("pack_band_descs", [](const std::vector<BandDesc>& v) {
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(BandDesc));
+  });
+
+  py::class_<AnalysisArgs>(m, "AnalysisArgs")
+      .def(py::init([]() { AnalysisArgs a; memset(&a, 0, sizeof(a)); return a; }))
+      .def_readwrite("N", &AnalysisArgs::N)
+      .def_readwrite("ld", &AnalysisArgs::ld)
+      .def_readwrite("n_bands", &AnalysisArgs::n_bands)
+      .def_readwrite("solve", &AnalysisArgs::solve)
+      .PTR_FIELD(AnalysisArgs, bands, const BandDesc*)
+      .PTR_FIELD(AnalysisArgs, x_prev, const float*)
+      .PTR_FIELD(AnalysisArgs, x_f, const float*)
+      .PTR_FIELD(AnalysisArgs, pf_inv, const float*)
+      .PTR_FIELD(AnalysisArgs, x_out, float*)
+      .PTR_FIELD(AnalysisArgs, a_out, float*)
+      .PTR_FIELD(AnalysisArgs, b_out, float*)
+      .PTR_FIELD(AnalysisArgs, status, uint8_t*)
+      .PTR_FIELD(AnalysisArgs, partials, double*);
+
+  py::class_<GainArgs>(m, "GainArgs")
+      .def(py::init([]() { GainArgs a; memset(&a, 0, sizeof(a)); return a; }))
+      .def_readwrite("N", &GainArgs::N)
+      .def_readwrite("ld", &GainArgs::ld)
+      .def_readwrite("n_bands", &GainArgs::n_bands)
+      .def_readwrite("joseph", &GainArgs::joseph)
+      .PTR_FIELD(GainArgs, bands, const BandDesc*)
+      .PTR_FIELD(GainArgs, x_prev, const float*)
+      .PTR_FIELD(GainArgs, x_f, const float*)
+      .PTR_FIELD(GainArgs, p_f, const float*)
+      .PTR_FIELD(GainArgs, x_out, float*)
+      .PTR_FIELD(GainArgs, p_out, float*)
+      .PTR_FIELD(GainArgs, status, uint8_t*)
+      .PTR_FIELD(GainArgs, partials, double*);
+
+  py::class_<JacobiArgs>(m, "JacobiArgs")
+      .def(py::init([]() { JacobiArgs a; memset(&a, 0, sizeof(a)); return a; }))
+      .def_readwrite("N", &JacobiArgs::N)
+      .def_readwrite("ld", &JacobiArgs::ld)
+      .def_readwrite("ld_ext", &JacobiArgs::ld_ext)
+      .def_readwrite("gamma", &JacobiArgs::gamma)
+      .def_readwrite("reg_mask", &JacobiArgs::reg_mask)
+      .PTR_FIELD(JacobiArgs, a_in, const float*)
+      .PTR_FIELD(JacobiArgs, b_in, const float*)
+      .PTR_FIELD(JacobiArgs, x_ext, const float*)
+      .PTR_FIELD(JacobiArgs, nbr, const int32_t*)
+      .PTR_FIELD(JacobiArgs, x_ref, const float*)
+      .PTR_FIELD(JacobiArgs, x_out, float*)
+      .PTR_FIELD(JacobiArgs, a_out, float*)
+      .PTR_FIELD(JacobiArgs, partials, double*);
+
+  py::class_<PropArgs>(m, "PropArgs")
+      .def(py::init([]() { PropArgs a; memset(&a, 0, sizeof(a)); return a; }))
+      .def_readwrite("N", &PropArgs::N)
+      .def_readwrite("ld", &PropArgs::ld)
+      .def_readwrite("mode", &PropArgs::mode)
+      .def_readwrite("blend", &PropArgs::blend)
+      .def_readwrite("quirk_blend", &PropArgs::quirk_blend)
+      .def_readwrite("prop_mask", &PropArgs::prop_mask)
+      .PTR_FIELD(PropArgs, x_a, const float*)
+      .PTR_FIELD(PropArgs, p_a, const float*)
+      .PTR_FIELD(PropArgs, x_f, float*)
+      .PTR_FIELD(PropArgs, p_f, float*)
+      .ARR_FIELD(PropArgs, m, float)
+      .ARR_FIELD(PropArgs, q, float)
+      .PTR_FIELD(PropArgs, q_pix, const float*)
+      .ARR_FIELD(PropArgs, reset_mean, float)
+      .ARR_FIELD(PropArgs, reset_cinv, float)
+      .ARR_FIELD(PropArgs, blend_mean, float)
+      .ARR_FIELD(PropArgs, blend_cinv, float)
+      .PTR_FIELD(PropArgs, blend_mean_pix, const float*)
+      .PTR_FIELD(PropArgs, blend_cinv_pix, const float*)
+      .PTR_FIELD(PropArgs, status, uint8_t*);
+
+  m.def("supported_np", [](int np) { return host_supported(np); });
+  m.def("grid", [](int64_t N) { return dev_grid(N); });
+
+  m.def("analysis", [](int np, const AnalysisArgs& a, int grid, bool device, uintptr_t stream) {
+    if (device) check_hip(dev_analysis(np, a, grid, (hipStream_t)stream), "analysis");
+    else check_host(host_analysis(np, a, grid), "analysis");
+  });
+  m.def("gain", [](int np, const GainArgs& a, int grid, bool device, uintptr_t stream) {
+    if (device) check_hip(dev_gain(np, a, grid, (hipStream_t)stream), "gain");
+    else check_host(host_gain(np, a, grid), "gain");
+  });
+  m.def("jacobi", [](int np, const JacobiArgs& a, int grid, bool device, uintptr_t stream) {
+    if (device) check_hip(dev_jacobi(np, a, grid, (hipStream_t)stream), "jacobi");
+    else check_host(host_jacobi(np, a, grid), "jacobi");
+  });
+  m.def("propagate", [](int np, const PropArgs& a, bool device, uintptr_t stream) {
+    if (device) check_hip(dev_propagate(np, a, (hipStream_t)stream), "propagate");
+    else check_host(host_propagate(np, a), "propagate");
+  });
+  m.def("invert", [](int np, uintptr_t src, uintptr_t dst, int64_t N, int64_t ld, uintptr_t st, bool device,
+                     uintptr_t stream) {
+    if (device) check_hip(dev_invert(np, P<const float>(src), P<float>(dst), N, ld, P<uint8_t>(st),
+                                     (hipStream_t)stream), "invert");
+    else check_host(host_invert(np, P<const float>(src), P<float>(dst), N, ld, P<uint8_t>(st)), "invert");
+  });
+  m.def("operator_eval", [](int np, uintptr_t bands, int band, uintptr_t x, int64_t N, int64_t ld, uintptr_t h0,
+                            uintptr_t h, int64_t h_ld, uintptr_t ok, bool device, uintptr_t stream) {
+    if (device) check_hip(dev_operator(np, P<const BandDesc>(bands), band, P<const float>(x), N, ld, P<float>(h0),
+                                       P<float>(h), h_ld, P<uint8_t>(ok), (hipStream_t)stream), "operator_eval");
+    else check_host(host_operator(np, P<const BandDesc>(bands), band, P<const float>(x), N, ld, P<float>(h0),
+                                  P<float>(h), h_ld, P<uint8_t>(ok)), "operator_eval");
+  });
+  m.def("hessian", [](int np, uintptr_t bands, int nb, uintptr_t x, uintptr_t a, int64_t N, int64_t ld,
+                      bool device, uintptr_t stream) {
+    if (device) check_hip(dev_hessian(np, P<const BandDesc>(bands), nb, P<const float>(x), P<float>(a), N, ld,
+                                      (hipStream_t)stream), "hessian");
+    else check_host(host_hessian(np, P<const BandDesc>(bands), nb, P<const float>(x), P<float>(a), N, ld),
+                    "hessian");
+  });
+  m.def("unpack", [](int np, uintptr_t x, uintptr_t a, int64_t N, int64_t ld, uintptr_t idx, uintptr_t mean,
+                     uintptr_t unc, int64_t plane, bool device, uintptr_t stream) {
+    if (device) check_hip(dev_unpack(np, P<const float>(x), P<const float>(a), N, ld, P<const int64_t>(idx),
+                                     P<float>(mean), P<float>(unc), plane, (hipStream_t)stream), "unpack");
+    else check_host(host_unpack(np, P<const float>(x), P<const float>(a), N, ld, P<const int64_t>(idx),
+                                P<float>(mean), P<float>(unc), plane), "unpack");
+  });
+  m.def("reduce_partials", [](uintptr_t partials, int n, uintptr_t out, uintptr_t stream) {
+    check_hip(dev_reduce(P<const double>(partials), n, P<double>(out), (hipStream_t)stream), "reduce_partials");
+  });
+  m.def("gather", [](int elem_bytes, uintptr_t src, uintptr_t idx, uintptr_t dst, int64_t n, int rows,
+                     int64_t src_ld, int64_t dst_ld, uintptr_t stream) {
+    check_hip(dev_gather(elem_bytes, P<const void>(src), P<const int64_t>(idx), P<void>(dst), n, rows, src_ld,
+                         dst_ld, (hipStream_t)stream), "gather");
+  });
+  m.def("lut_nearest", [](uintptr_t lut, int M, int D, uintptr_t x, int64_t N, int64_t ld, uintptr_t out,
+                          bool device, uintptr_t stream) {
+    if (device) check_hip(dev_lut_nearest(P<const float>(lut), M, D, P<const float>(x), N, ld, P<int32_t>(out),
+                                          (hipStream_t)stream), "lut_nearest");
+    else host_lut_nearest(P<const float>(lut), M, D, P<const float>(x), N, ld, P<int32_t>(out));
+  });
+
+  bind_stream(m);
+}

@@ -1,0 +1,753 @@
+// kf_core.h — per-pixel math shared by the gfx950 kernels and the host runner.
+//
+// Every routine here is written once as __host__ __device__ code: the HIP
+// kernels in kf_kernels.hip run it one pixel per lane on MI355X, and
+// kf_host.cpp runs the *same* source over an OpenMP loop on the CPU (the
+// CPU path of the engine and the numerics harness for CI without a GPU).
+//
+// Reference semantics (QCDIS/KaFKA-InferenceEngine):
+//   * analysis  = kafka/inference/solvers.py:100-145 (variational_kalman_multiband)
+//                 with the Gauss-Newton linearisation of kafka/linear_kf.py:245-307
+//   * operators = kafka/inference/utils.py:130-219 (GP emulator operators),
+//                 kafka/observation_operators/sar_forward_model.py:13-106 (WCM)
+//   * propagators = kafka/inference/kf_tools.py:174-353, blend :75-96
+// The reference builds one (n_p N)x(n_p N) sparse system and factors it with
+// SuperLU; every block is n_p x n_p, so here each pixel's
+// block lives in registers as a packed upper triangle and is factored with an
+// unrolled Cholesky.
+#pragma once
+#include <stdint.h>
+#include <math.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define KF_HD __host__ __device__ __forceinline__
+#else
+#define KF_HD inline __attribute__((always_inline))
+#endif
+
+namespace kf {
+
+constexpr int MAX_D = 16;         // max mapped inputs per band / max state size
+constexpr int MAX_NT = 136;       // ntri(16)
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN10 = 2.302585092994046f;
+constexpr float LOG2_10 = 3.321928094887362f;
+constexpr float DEG2RAD = 0.017453292519943295f;
+
+KF_HD constexpr int ntri(int n) { return n * (n + 1) / 2; }
+// packed upper triangle, row-major: (0,0) (0,1) .. (0,n-1) (1,1) ..
+KF_HD constexpr int tri(int n, int i, int j) { return i * n - (i * (i - 1)) / 2 + (j - i); }
+template <int NP> KF_HD constexpr int sym(int i, int j) { return i <= j ? tri(NP, i, j) : tri(NP, j, i); }
+
+// ---------------------------------------------------------------------------
+// enums shared with Python (kafka_inferenceengine_amd/ops/_abi.py)
+enum ObsKind : int32_t { OBS_NONE = 0, OBS_F32 = 1, OBS_DN16 = 2 };
+enum OpKind : int32_t { OP_PRECOMP = 0, OP_LINEAR = 1, OP_GP = 2, OP_SAR = 3 };
+enum PropMode : int32_t {
+  PROP_PRIOR = 0,         // no_propagation: reset to prior (kf_tools.py:316-353)
+  PROP_PRIOR_PARTIAL = 1, // LAI propagator generalised (kf_tools.py:292-314)
+  PROP_INFO_APPROX = 2,   // diagonal information-filter approx (kf_tools.py:247-289)
+  PROP_INFO_EXACT = 3,    // (I + P^-1 Q)^-1 P^-1 (kf_tools.py:208-245)
+  PROP_STANDARD = 4,      // covariance form P + Q (kf_tools.py:174-205)
+  PROP_IDENTITY = 5       // x_f = M x_a, P_f^-1 = P_a^-1 (no inflation)
+};
+enum StatusBits : uint8_t {
+  ST_OK = 0, ST_NONSPD = 1, ST_NONFINITE = 2, ST_BAD_OP = 4, ST_NO_OBS = 8, ST_FALLBACK = 16
+};
+
+// One observation band as seen by the fused analysis kernel.  Built on the
+// host by kf_bindings (pack_band_descs) so the C++ layout is authoritative.
+struct BandDesc {
+  int32_t op, obs, d, T;
+  int32_t map[MAX_D];          // state index feeding input d of the operator
+  float scale, rel_unc, unc_floor, offset;
+  float coef[MAX_D];           // LINEAR: c_j per state j; GP: lambda_d; SAR: A,B,C,D,E,theta
+  float center[MAX_D];         // GP input centre (training mean), subtracted in-kernel
+  const float* gp;             // GP records [T][2d+2]: L, B[d], alpha, (alpha*t)[d]
+  const float* y;              // OBS_F32 observation
+  const float* w;              // OBS_F32 inverse variance (weight)
+  const uint8_t* mask;         // optional validity
+  const uint16_t* dn;          // OBS_DN16 digital numbers (0 = nodata)
+  const float* aux;            // per-pixel auxiliary (SAR incidence angle, deg)
+  const float* pre_h0;         // OP_PRECOMP H0 [N]
+  const float* pre_h;          // OP_PRECOMP h [NP][ld]
+  float* h0_out;               // optional diagnostics: H0 at the linearisation point
+  int64_t pre_ld;              // leading dim of pre_h
+};
+
+struct AnalysisArgs {
+  int64_t N, ld;
+  int32_t n_bands, solve;
+  const BandDesc* bands;
+  const float* x_prev;   // [NP][ld] linearisation point
+  const float* x_f;      // [NP][ld] forecast mean
+  const float* pf_inv;   // [NT][ld] forecast precision (packed)
+  float* x_out;          // [NP][ld]
+  float* a_out;          // [NT][ld] analysis precision (may be null)
+  float* b_out;          // [NP][ld] rhs (regulariser path, may be null)
+  uint8_t* status;       // per-pixel flags (may be null)
+  double* partials;      // per-block sum (x_out - x_prev)^2
+};
+
+struct PropArgs {
+  int64_t N, ld;
+  int32_t mode, blend, quirk_blend, pad0;
+  uint32_t prop_mask;    // PROP_PRIOR_PARTIAL: which parameters are propagated
+  const float* x_a;      // [NP][ld]
+  const float* p_a;      // [NT][ld] analysis precision (or covariance for STANDARD)
+  float* x_f;            // [NP][ld]
+  float* p_f;            // [NT][ld]
+  float m[MAX_D];        // diagonal trajectory model
+  float q[MAX_D];        // diagonal trajectory uncertainty
+  const float* q_pix;    // optional per-pixel Q [NP][ld]
+  float reset_mean[MAX_D];
+  float reset_cinv[MAX_NT];
+  float blend_mean[MAX_D];
+  float blend_cinv[MAX_NT];
+  const float* blend_mean_pix;   // optional per-pixel prior mean [NP][ld]
+  const float* blend_cinv_pix;   // optional per-pixel prior precision [NT][ld]
+  uint8_t* status;
+};
+
+// ---------------------------------------------------------------------------
+// small helpers
+template <int NP>
+KF_HD float gather_state(const float (&x)[NP], int idx) {
+  float v = x[0];
+#pragma unroll
+  for (int j = 1; j < NP; ++j) v = (idx == j) ? x[j] : v;
+  return v;
+}
+
+KF_HD float kexp2(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_exp2f(x);
+#else
+  return exp2f(x);
+#endif
+}
+
+KF_HD bool finitef(float v) { return v - v == 0.f; }
+
+// In-place packed Cholesky A = U^T U (U upper, stored in A's packed slots).
+template <int NP>
+KF_HD bool chol_packed(float (&A)[ntri(NP)]) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    float s = A[tri(NP, j, j)];
+#pragma unroll
+    for (int k = 0; k < j; ++k) s = fmaf(-A[tri(NP, k, j)], A[tri(NP, k, j)], s);
+    ok = ok && (s > 0.f) && finitef(s);
+    s = s > 0.f ? s : 1.f;
+    const float r = sqrtf(s);
+    const float inv = 1.f / r;
+    A[tri(NP, j, j)] = r;
+#pragma unroll
+    for (int i = j + 1; i < NP; ++i) {
+      float t = A[tri(NP, j, i)];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t = fmaf(-A[tri(NP, k, j)], A[tri(NP, k, i)], t);
+      A[tri(NP, j, i)] = t * inv;
+    }
+  }
+  return ok;
+}
+
+// Solve U^T U x = b with U from chol_packed (b overwritten by x).
+template <int NP>
+KF_HD void chol_solve(const float (&U)[ntri(NP)], float (&b)[NP]) {
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {  // U^T z = b
+    float t = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) t = fmaf(-U[tri(NP, k, i)], b[k], t);
+    b[i] = t / U[tri(NP, i, i)];
+  }
+#pragma unroll
+  for (int i = NP - 1; i >= 0; --i) {  // U x = z
+    float t = b[i];
+#pragma unroll
+    for (int k = i + 1; k < NP; ++k) t = fmaf(-U[tri(NP, i, k)], b[k], t);
+    b[i] = t / U[tri(NP, i, i)];
+  }
+}
+
+// Packed inverse of an SPD matrix from its Cholesky factor (column by column).
+template <int NP>
+KF_HD void chol_inverse(const float (&U)[ntri(NP)], float (&Ainv)[ntri(NP)]) {
+#pragma unroll
+  for (int c = 0; c < NP; ++c) {
+    float e[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) e[i] = (i == c) ? 1.f : 0.f;
+    chol_solve<NP>(U, e);
+#pragma unroll
+    for (int i = 0; i <= c; ++i) Ainv[tri(NP, i, c)] = e[i];
+  }
+}
+
+template <int NP>
+KF_HD void symv(const float (&A)[ntri(NP)], const float (&x)[NP], float (&y)[NP]) {
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) t = fmaf(A[sym<NP>(i, j)], x[j], t);
+    y[i] = t;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// observation decode: returns weight w (inverse variance, 0 when masked) and y
+KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y, float& w) {
+  if (bd.obs == OBS_DN16) {
+    const uint16_t dn = bd.dn[p];
+    y = (float)dn * bd.scale;
+    float sig = fmaxf(bd.rel_unc * y, bd.unc_floor);
+    w = (dn > 0 && sig > 0.f) ? 1.f / (sig * sig) : 0.f;
+    if (dn == 0) y = 0.f;
+  } else if (bd.obs == OBS_F32) {
+    y = bd.y[p];
+    w = bd.w[p];
+    if (bd.mask && !bd.mask[p]) w = 0.f;
+    if (!(w > 0.f) || !finitef(w) || !finitef(y)) { w = 0.f; y = 0.f; }
+  } else {
+    y = 0.f;
+    w = 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Observation operators: value H0 and Jacobian row h (length NP) at x.
+
+// RBF (ARD) Gaussian-process emulator, inputs centred on the training mean:
+//   f(x) = offset + sum_i alpha_i s exp(-1/2 sum_d lambda_d (x_d - t_id)^2)
+// records (host-built, ops/emulators.py): L_i = log2(s) - 1/2 log2e sum lambda t^2,
+// B_id = log2e lambda_d t_id, alpha_i, alpha_i t_id  (t centred).
+// Replaces gp.predict + the lil_matrix scatter of utils.py:181-219.
+template <int NP, int D>
+KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&h)[NP]) {
+  float xi[D];
+  float c = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    xi[d] = gather_state<NP>(x, bd.map[d]) - bd.center[d];
+    c = fmaf(bd.coef[d] * xi[d], xi[d], c);
+  }
+  c *= -0.5f * LOG2E;
+  float S0 = 0.f, S[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) S[d] = 0.f;
+  constexpr int R = 2 * D + 2;
+  const float* __restrict__ r = bd.gp;
+  const int T = bd.T;
+#pragma unroll 4
+  for (int i = 0; i < T; ++i) {
+    const float* __restrict__ ri = r + (int64_t)i * R;
+    float e = ri[0] + c;
+#pragma unroll
+    for (int d = 0; d < D; ++d) e = fmaf(ri[1 + d], xi[d], e);
+    const float k = kexp2(e);
+    S0 = fmaf(ri[1 + D], k, S0);
+#pragma unroll
+    for (int d = 0; d < D; ++d) S[d] = fmaf(ri[2 + D + d], k, S[d]);
+  }
+  H0 = bd.offset + S0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) h[j] = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const float g = -bd.coef[d] * fmaf(xi[d], S0, -S[d]);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) h[j] += (bd.map[d] == j) ? g : 0.f;
+  }
+}
+
+// Water Cloud Model (sar_forward_model.py:13-106), analytic gradient.
+// Returns false for LAI<=0 / SM<=0 (the reference raises ValueError there).
+template <int NP>
+KF_HD bool sar_eval(const BandDesc& bd, int64_t p, const float (&x)[NP], float& H0, float (&h)[NP]) {
+  const float V = gather_state<NP>(x, bd.map[0]);
+  const float SM = gather_state<NP>(x, bd.map[1]);
+  const float A = bd.coef[0], B = bd.coef[1], C = bd.coef[2], Dc = bd.coef[3], E = bd.coef[4];
+  const float th = bd.aux ? bd.aux[p] : bd.coef[5];
+  const float mu = cosf(th * DEG2RAD);
+  const bool ok = (V > 0.f) && (SM > 0.f);
+  const float Vs = ok ? V : 1.f;
+  const float tau = expf(-2.f * B / mu * Vs);
+  float z = powf(Vs, E);
+  if (!finitef(z)) z = 1.f;
+  float z1 = powf(Vs, E - 1.f);
+  if (!finitef(z1)) z1 = 1.f;
+  const float ssoil = kexp2(LOG2_10 * (C + Dc * SM) * 0.1f);
+  H0 = A * z * mu * (1.f - tau) + tau * ssoil;
+  const float dV = A * E * mu * z1 * (1.f - tau) + 2.f * A * B * z * tau - 2.f * B * tau * ssoil / mu;
+  const float dS = Dc * LN10 * 0.1f * tau * ssoil;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) h[j] = (bd.map[0] == j ? dV : 0.f) + (bd.map[1] == j ? dS : 0.f);
+  return ok;
+}
+
+template <int NP, int D = 1>
+KF_HD void gp_dispatch(const BandDesc& bd, const float (&x)[NP], float& H0, float (&h)[NP]) {
+  if constexpr (D <= NP && D <= 12) {
+    if (bd.d == D) { gp_eval<NP, D>(bd, x, H0, h); return; }
+    gp_dispatch<NP, D + 1>(bd, x, H0, h);
+  } else {
+    H0 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) h[j] = 0.f;
+  }
+}
+
+// Evaluate one band's operator.  Returns false when the operator is invalid here.
+template <int NP>
+KF_HD bool eval_operator(const BandDesc& bd, int64_t p, int64_t ld, const float (&x)[NP],
+                         float& H0, float (&h)[NP]) {
+  bool ok = true;
+  switch (bd.op) {
+    case OP_GP:
+      gp_dispatch<NP>(bd, x, H0, h);
+      break;
+    case OP_SAR:
+      ok = sar_eval<NP>(bd, p, x, H0, h);
+      break;
+    case OP_LINEAR: {
+      float t = bd.offset;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) { h[j] = bd.coef[j]; t = fmaf(h[j], x[j], t); }
+      H0 = t;
+    } break;
+    default: {  // OP_PRECOMP
+      H0 = bd.pre_h0[p];
+#pragma unroll
+      for (int j = 0; j < NP; ++j) h[j] = bd.pre_h[j * bd.pre_ld + p];
+    }
+  }
+  bool fin = finitef(H0);
+#pragma unroll
+  for (int j = 0; j < NP; ++j) fin = fin && finitef(h[j]);
+  return ok && fin;
+}
+
+// ---------------------------------------------------------------------------
+// K1: fused Gauss-Newton analysis for one pixel (information form).
+//   A = P_f^-1 + sum_b w_b h_b h_b^T,  b = P_f^-1 x_f + sum_b w_b h_b y'_b,
+//   y'_b = y_b + h_b . x0 - H0_b,      x_a = A^-1 b
+// Returns (x_a - x0)^2 summed over parameters.
+template <int NP>
+KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a.ld;
+  float x0[NP], A[NT], b[NP];
+  uint8_t st = 0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
+  {
+    float xf[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) xf[j] = a.x_f[j * ld + p];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) A[t] = a.pf_inv[t * ld + p];
+    symv<NP>(A, xf, b);
+  }
+  int nobs = 0;
+  for (int bi = 0; bi < a.n_bands; ++bi) {
+    const BandDesc& bd = a.bands[bi];
+    float y, w;
+    decode_obs(bd, p, y, w);
+    if (!(w > 0.f)) {
+      if (bd.h0_out) bd.h0_out[p] = 0.f;
+      continue;
+    }
+    float H0, h[NP];
+    const bool ok = eval_operator<NP>(bd, p, ld, x0, H0, h);
+    if (bd.h0_out) bd.h0_out[p] = H0;
+    if (!ok) { st |= ST_BAD_OP; continue; }
+    ++nobs;
+    float yp = y - H0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) yp = fmaf(h[j], x0[j], yp);
+    const float wy = w * yp;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const float wh = w * h[i];
+      b[i] = fmaf(h[i], wy, b[i]);
+#pragma unroll
+      for (int j = i; j < NP; ++j) A[tri(NP, i, j)] = fmaf(wh, h[j], A[tri(NP, i, j)]);
+    }
+  }
+  if (nobs == 0) st |= ST_NO_OBS;
+  if (a.a_out) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = A[t];
+  }
+  if (a.b_out) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) a.b_out[j * ld + p] = b[j];
+  }
+  float dn = 0.f;
+  if (a.solve) {
+    const bool spd = chol_packed<NP>(A);
+    chol_solve<NP>(A, b);
+    bool fin = true;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) fin = fin && finitef(b[j]);
+    if (!spd || !fin) {
+      // Health fallback: keep the forecast (prior) for this pixel.
+      st |= (!spd ? ST_NONSPD : 0) | (!fin ? ST_NONFINITE : 0) | ST_FALLBACK;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) b[j] = a.x_f[j * ld + p];
+      if (a.a_out) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = a.pf_inv[t * ld + p];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      a.x_out[j * ld + p] = b[j];
+      const float d = b[j] - x0[j];
+      dn = fmaf(d, d, dn);
+    }
+  }
+  if (a.status) a.status[p] = st;
+  return dn;
+}
+
+// ---------------------------------------------------------------------------
+// K4/K5: propagation and prior blending for one pixel.
+template <int NP>
+KF_HD void pixel_propagate(const PropArgs& a, int64_t p) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a.ld;
+  float xf[NP], P[NT];
+  uint8_t st = 0;
+  float q[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) q[j] = a.q_pix ? a.q_pix[j * ld + p] : a.q[j];
+
+  switch (a.mode) {
+    case PROP_PRIOR: {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) xf[j] = a.reset_mean[j];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) P[t] = a.reset_cinv[t];
+    } break;
+    case PROP_PRIOR_PARTIAL: {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) P[t] = a.reset_cinv[t];
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        const bool pj = (a.prop_mask >> j) & 1u;
+        xf[j] = pj ? a.m[j] * a.x_a[j * ld + p] : a.reset_mean[j];
+        if (pj) {
+          const float pa = a.p_a[tri(NP, j, j) * ld + p];
+          P[tri(NP, j, j)] = 1.f / (1.f / pa + q[j]);
+        }
+      }
+    } break;
+    case PROP_INFO_APPROX: {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) xf[j] = a.m[j] * a.x_a[j * ld + p];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) P[t] = 0.f;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        const float d = a.p_a[tri(NP, j, j) * ld + p];
+        P[tri(NP, j, j)] = d / (1.f + d * q[j]);
+      }
+    } break;
+    case PROP_INFO_EXACT: {
+      // P_f^-1 = (I + P_a^-1 Q)^-1 P_a^-1 = (P_a + Q)^-1
+#pragma unroll
+      for (int j = 0; j < NP; ++j) xf[j] = a.m[j] * a.x_a[j * ld + p];
+      float U[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) U[t] = a.p_a[t * ld + p];
+      bool ok = chol_packed<NP>(U);
+      float C[NT];
+      chol_inverse<NP>(U, C);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) C[tri(NP, j, j)] += q[j];
+      ok = chol_packed<NP>(C) && ok;
+      chol_inverse<NP>(C, P);
+      if (!ok) st |= ST_NONSPD;
+    } break;
+    case PROP_STANDARD: {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) xf[j] = a.m[j] * a.x_a[j * ld + p];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) P[t] = a.p_a[t * ld + p];
+#pragma unroll
+      for (int j = 0; j < NP; ++j) P[tri(NP, j, j)] += q[j];
+    } break;
+    default: {  // PROP_IDENTITY
+#pragma unroll
+      for (int j = 0; j < NP; ++j) xf[j] = a.m[j] * a.x_a[j * ld + p];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) P[t] = a.p_a[t * ld + p];
+    }
+  }
+
+  if (a.blend) {
+    // Gaussian product of forecast (xf, P) with prior (mu, C^-1) (kf_tools.py:75-96).
+    float mu[NP], Ci[NT];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) mu[j] = a.blend_mean_pix ? a.blend_mean_pix[j * ld + p] : a.blend_mean[j];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) Ci[t] = a.blend_cinv_pix ? a.blend_cinv_pix[t * ld + p] : a.blend_cinv[t];
+    float b1[NP], b2[NP];
+    if (a.quirk_blend) {  // reference operand swap (kf_tools.py:90)
+      symv<NP>(P, mu, b1);
+      symv<NP>(Ci, xf, b2);
+    } else {
+      symv<NP>(P, xf, b1);
+      symv<NP>(Ci, mu, b2);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) P[t] += Ci[t];
+    float U[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) U[t] = P[t];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) xf[j] = b1[j] + b2[j];
+    if (!chol_packed<NP>(U)) st |= ST_NONSPD;
+    chol_solve<NP>(U, xf);
+  }
+#pragma unroll
+  for (int j = 0; j < NP; ++j) a.x_f[j * ld + p] = xf[j];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) a.p_f[t * ld + p] = P[t];
+  if (a.status) a.status[p] |= st;
+}
+
+// Packed SPD inverse (covariance <-> precision conversion).
+template <int NP>
+KF_HD bool pixel_invert(const float* src, float* dst, int64_t ld, int64_t p) {
+  constexpr int NT = ntri(NP);
+  float U[NT], R[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) U[t] = src[t * ld + p];
+  const bool ok = chol_packed<NP>(U);
+  chol_inverse<NP>(U, R);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) dst[t * ld + p] = R[t];
+  return ok;
+}
+
+// ---------------------------------------------------------------------------
+// K1g: covariance / gain form, bands processed as sequential scalar updates
+// (equal to the joint update for diagonal R):
+//   s = h^T P h + 1/w,  k = P h / s,  x += k (y' - h^T x),  P -= k (P h)^T
+// with y' = y - H0 + h . x0 (iterated EKF linearised about x0).
+struct GainArgs {
+  int64_t N, ld;
+  int32_t n_bands, joseph;
+  const BandDesc* bands;
+  const float* x_prev;
+  const float* x_f;
+  const float* p_f;      // forecast covariance (packed)
+  float* x_out;
+  float* p_out;          // analysis covariance (packed)
+  uint8_t* status;
+  double* partials;
+};
+
+template <int NP>
+KF_HD float pixel_gain(const GainArgs& a, int64_t p) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a.ld;
+  float x0[NP], x[NP], P[NT];
+  uint8_t st = 0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) { x0[j] = a.x_prev[j * ld + p]; x[j] = a.x_f[j * ld + p]; }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) P[t] = a.p_f[t * ld + p];
+  for (int bi = 0; bi < a.n_bands; ++bi) {
+    const BandDesc& bd = a.bands[bi];
+    float y, w;
+    decode_obs(bd, p, y, w);
+    if (!(w > 0.f)) { if (bd.h0_out) bd.h0_out[p] = 0.f; continue; }
+    float H0, h[NP];
+    const bool ok = eval_operator<NP>(bd, p, ld, x0, H0, h);
+    if (bd.h0_out) bd.h0_out[p] = H0;
+    if (!ok) { st |= ST_BAD_OP; continue; }
+    float ph[NP];
+    symv<NP>(P, h, ph);
+    float s = 1.f / w, innov = y - H0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) { s = fmaf(h[j], ph[j], s); innov = fmaf(h[j], x0[j] - x[j], innov); }
+    const float is = 1.f / s;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) x[j] = fmaf(ph[j] * is, innov, x[j]);
+    if (a.joseph) {
+      // P = (I - k h^T) P (I - k h^T)^T + k k^T / w
+      float k[NP];
+#pragma unroll
+      for (int j = 0; j < NP; ++j) k[j] = ph[j] * is;
+      float hp[NP];  // h^T P  == ph (P symmetric)
+#pragma unroll
+      for (int j = 0; j < NP; ++j) hp[j] = ph[j];
+      const float hph = s - 1.f / w;
+#pragma unroll
+      for (int i = 0; i < NP; ++i)
+#pragma unroll
+        for (int j = i; j < NP; ++j)
+          P[tri(NP, i, j)] = P[tri(NP, i, j)] - k[i] * hp[j] - hp[i] * k[j] + k[i] * k[j] * (hph + 1.f / w);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NP; ++i)
+#pragma unroll
+        for (int j = i; j < NP; ++j) P[tri(NP, i, j)] = fmaf(-ph[i] * is, ph[j], P[tri(NP, i, j)]);
+    }
+  }
+  float dn = 0.f;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    a.x_out[j * ld + p] = x[j];
+    const float d = x[j] - x0[j];
+    dn = fmaf(d, d, dn);
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) a.p_out[t * ld + p] = P[t];
+  if (a.status) a.status[p] = st;
+  return dn;
+}
+
+// ---------------------------------------------------------------------------
+// K9: block-Jacobi sweep for the GMRF spatial regulariser (new capability):
+//   (A_p + g deg_p E_R) x_p = b_p + g E_R sum_q x_q
+// neighbours index an extended x (local pixels, then halo pixels).
+struct JacobiArgs {
+  int64_t N, ld, ld_ext;
+  float gamma;
+  uint32_t reg_mask;
+  const float* a_in;     // [NT][ld]
+  const float* b_in;     // [NP][ld]
+  const float* x_ext;    // [NP][ld_ext]
+  const int32_t* nbr;    // [4][N] index into x_ext, -1 if none
+  const float* x_ref;    // [NP][ld] linearisation point (for the norm)
+  float* x_out;          // [NP][ld]
+  float* a_out;          // optional: regularised precision written back
+  double* partials;
+};
+
+template <int NP>
+KF_HD float pixel_jacobi(const JacobiArgs& a, int64_t p) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a.ld;
+  float A[NT], b[NP];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) A[t] = a.a_in[t * ld + p];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) b[j] = a.b_in[j * ld + p];
+  int deg = 0;
+  float sx[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) sx[j] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int32_t q = a.nbr[k * a.N + p];
+    if (q >= 0) {
+      ++deg;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) sx[j] += a.x_ext[j * a.ld_ext + q];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    if ((a.reg_mask >> j) & 1u) {
+      A[tri(NP, j, j)] += a.gamma * (float)deg;
+      b[j] = fmaf(a.gamma, sx[j], b[j]);
+    }
+  }
+  if (a.a_out) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = A[t];
+  }
+  chol_packed<NP>(A);
+  chol_solve<NP>(A, b);
+  float dn = 0.f;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    a.x_out[j * ld + p] = b[j];
+    const float d = b[j] - a.x_ref[j * ld + p];
+    dn = fmaf(d, d, dn);
+  }
+  return dn;
+}
+
+// ---------------------------------------------------------------------------
+// K6: second-order (Hessian) correction for GP bands (kf_tools.py:26-72):
+//   A -= w r d2f/dx2,  r = y - H0 at x.
+template <int NP, int D>
+KF_HD void gp_hessian(const BandDesc& bd, const float (&x)[NP], float& f, float (&Hs)[ntri(NP)]) {
+  float xi[D];
+  float c = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    xi[d] = gather_state<NP>(x, bd.map[d]) - bd.center[d];
+    c = fmaf(bd.coef[d] * xi[d], xi[d], c);
+  }
+  c *= -0.5f * LOG2E;
+  float S0 = 0.f, S[D], S2[ntri(D)];
+#pragma unroll
+  for (int d = 0; d < D; ++d) S[d] = 0.f;
+#pragma unroll
+  for (int t = 0; t < ntri(D); ++t) S2[t] = 0.f;
+  constexpr int R = 2 * D + 2;
+  for (int i = 0; i < bd.T; ++i) {
+    const float* ri = bd.gp + (int64_t)i * R;
+    float e = ri[0] + c;
+#pragma unroll
+    for (int d = 0; d < D; ++d) e = fmaf(ri[1 + d], xi[d], e);
+    const float k = kexp2(e);
+    const float ak = ri[1 + D] * k;
+    S0 += ak;
+    float t[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      t[d] = ri[1 + d] / (LOG2E * bd.coef[d]);
+      S[d] = fmaf(ak, t[d], S[d]);
+    }
+#pragma unroll
+    for (int u = 0; u < D; ++u)
+#pragma unroll
+      for (int v = u; v < D; ++v) S2[tri(D, u, v)] = fmaf(ak * t[u], t[v], S2[tri(D, u, v)]);
+  }
+  f = bd.offset + S0;
+  // d2f/dxu dxv = lu lv [xu xv S0 - xu Sv - xv Su + Suv] - lu delta_uv S0
+#pragma unroll
+  for (int t = 0; t < ntri(NP); ++t) Hs[t] = 0.f;
+#pragma unroll
+  for (int u = 0; u < D; ++u)
+#pragma unroll
+    for (int v = u; v < D; ++v) {
+      const float lu = bd.coef[u], lv = bd.coef[v];
+      float val = lu * lv * (xi[u] * xi[v] * S0 - xi[u] * S[v] - xi[v] * S[u] + S2[tri(D, u, v)]);
+      if (u == v) val -= lu * S0;
+      const int ju = bd.map[u], jv = bd.map[v];
+#pragma unroll
+      for (int i = 0; i < NP; ++i)
+#pragma unroll
+        for (int j = i; j < NP; ++j) {
+          const bool hit = (ju == i && jv == j) || (ju == j && jv == i);
+          const bool dup = (u != v) && (ju == jv) && (ju == i) && (i == j);
+          Hs[tri(NP, i, j)] += hit ? (dup ? 2.f * val : val) : 0.f;
+        }
+    }
+}
+
+template <int NP, int D = 1>
+KF_HD bool gp_hessian_dispatch(const BandDesc& bd, const float (&x)[NP], float& f, float (&Hs)[ntri(NP)]) {
+  if constexpr (D <= NP && D <= 12) {
+    if (bd.d == D) { gp_hessian<NP, D>(bd, x, f, Hs); return true; }
+    return gp_hessian_dispatch<NP, D + 1>(bd, x, f, Hs);
+  } else {
+    return false;
+  }
+}
+
+}  // namespace kf

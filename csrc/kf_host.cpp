@@ -1,0 +1,157 @@
+// kf_host.cpp — CPU runner for the per-pixel kernels of kf_core.h.
+// Compiled by g++ (-fopenmp); the math is byte-for-byte the source the
+// gfx950 kernels run, so CPU CI exercises the kernel code paths.
+#include <omp.h>
+#include <string.h>
+#include "kf_launch.h"
+
+namespace kf {
+
+static constexpr int HBLOCK = 256;
+
+#define KF_HOST_NP_SWITCH(np, FN, ...)   \
+  switch (np) {                          \
+    case 1: return FN<1>(__VA_ARGS__);   \
+    case 2: return FN<2>(__VA_ARGS__);   \
+    case 3: return FN<3>(__VA_ARGS__);   \
+    case 4: return FN<4>(__VA_ARGS__);   \
+    case 7: return FN<7>(__VA_ARGS__);   \
+    case 10: return FN<10>(__VA_ARGS__); \
+    default: return -1;                  \
+  }
+
+bool host_supported(int np) { return np == 1 || np == 2 || np == 3 || np == 4 || np == 7 || np == 10; }
+
+// Block b handles pixels p = b*256 + t + k*grid*256 (same as the device).
+template <typename F>
+static void grid_stride(int64_t N, int grid, double* partials, F&& f) {
+  const int64_t stride = (int64_t)grid * HBLOCK;
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int b = 0; b < grid; ++b) {
+    double acc = 0.0;
+    for (int t = 0; t < HBLOCK; ++t)
+      for (int64_t p = (int64_t)b * HBLOCK + t; p < N; p += stride) acc += (double)f(p);
+    if (partials) partials[b] = acc;
+  }
+}
+
+template <int NP>
+static int h_analysis(const AnalysisArgs& a, int grid) {
+  grid_stride(a.N, grid, a.partials, [&](int64_t p) { return pixel_analysis<NP>(a, p); });
+  return 0;
+}
+template <int NP>
+static int h_gain(const GainArgs& a, int grid) {
+  grid_stride(a.N, grid, a.partials, [&](int64_t p) { return pixel_gain<NP>(a, p); });
+  return 0;
+}
+template <int NP>
+static int h_jacobi(const JacobiArgs& a, int grid) {
+  grid_stride(a.N, grid, a.partials, [&](int64_t p) { return pixel_jacobi<NP>(a, p); });
+  return 0;
+}
+template <int NP>
+static int h_propagate(const PropArgs& a) {
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < a.N; ++p) pixel_propagate<NP>(a, p);
+  return 0;
+}
+template <int NP>
+static int h_invert(const float* src, float* dst, int64_t N, int64_t ld, uint8_t* st) {
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < N; ++p) {
+    const bool ok = pixel_invert<NP>(src, dst, ld, p);
+    if (st && !ok) st[p] |= ST_NONSPD;
+  }
+  return 0;
+}
+template <int NP>
+static int h_operator(const BandDesc* b, int band, const float* x, int64_t N, int64_t ld, float* h0, float* h,
+                      int64_t h_ld, uint8_t* okp) {
+  const BandDesc& bd = b[band];
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < N; ++p) {
+    float xv[NP], hv[NP], H0;
+    for (int j = 0; j < NP; ++j) xv[j] = x[j * ld + p];
+    const bool ok = eval_operator<NP>(bd, p, ld, xv, H0, hv);
+    h0[p] = H0;
+    if (h)
+      for (int j = 0; j < NP; ++j) h[j * h_ld + p] = hv[j];
+    if (okp) okp[p] = ok ? 1 : 0;
+  }
+  return 0;
+}
+template <int NP>
+static int h_hessian(const BandDesc* bands, int nb, const float* x, float* a, int64_t N, int64_t ld) {
+  constexpr int NT = ntri(NP);
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < N; ++p) {
+    float xv[NP], acc[NT];
+    for (int j = 0; j < NP; ++j) xv[j] = x[j * ld + p];
+    for (int t = 0; t < NT; ++t) acc[t] = 0.f;
+    for (int bi = 0; bi < nb; ++bi) {
+      const BandDesc& bd = bands[bi];
+      if (bd.op != OP_GP) continue;
+      float y, w;
+      decode_obs(bd, p, y, w);
+      if (!(w > 0.f)) continue;
+      float f, Hs[NT];
+      if (!gp_hessian_dispatch<NP>(bd, xv, f, Hs)) continue;
+      const float s = w * (y - f);
+      for (int t = 0; t < NT; ++t) acc[t] = fmaf(s, Hs[t], acc[t]);
+    }
+    for (int t = 0; t < NT; ++t) a[t * ld + p] -= acc[t];
+  }
+  return 0;
+}
+template <int NP>
+static int h_unpack(const float* x, const float* a, int64_t N, int64_t ld, const int64_t* idx, float* mean,
+                    float* unc, int64_t plane) {
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < N; ++p) {
+    const int64_t r = idx ? idx[p] : p;
+    for (int j = 0; j < NP; ++j) {
+      if (mean) mean[j * plane + r] = x[j * ld + p];
+      if (unc) unc[j * plane + r] = 1.f / sqrtf(a[tri(NP, j, j) * ld + p]);
+    }
+  }
+  return 0;
+}
+
+int host_analysis(int np, const AnalysisArgs& a, int grid) { KF_HOST_NP_SWITCH(np, h_analysis, a, grid); }
+int host_gain(int np, const GainArgs& a, int grid) { KF_HOST_NP_SWITCH(np, h_gain, a, grid); }
+int host_jacobi(int np, const JacobiArgs& a, int grid) { KF_HOST_NP_SWITCH(np, h_jacobi, a, grid); }
+int host_propagate(int np, const PropArgs& a) { KF_HOST_NP_SWITCH(np, h_propagate, a); }
+int host_invert(int np, const float* src, float* dst, int64_t N, int64_t ld, uint8_t* st) {
+  KF_HOST_NP_SWITCH(np, h_invert, src, dst, N, ld, st);
+}
+int host_operator(int np, const BandDesc* b, int band, const float* x, int64_t N, int64_t ld, float* h0, float* h,
+                  int64_t h_ld, uint8_t* ok) {
+  KF_HOST_NP_SWITCH(np, h_operator, b, band, x, N, ld, h0, h, h_ld, ok);
+}
+int host_hessian(int np, const BandDesc* b, int nb, const float* x, float* a, int64_t N, int64_t ld) {
+  KF_HOST_NP_SWITCH(np, h_hessian, b, nb, x, a, N, ld);
+}
+int host_unpack(int np, const float* x, const float* a, int64_t N, int64_t ld, const int64_t* idx, float* mean,
+                float* unc, int64_t plane) {
+  KF_HOST_NP_SWITCH(np, h_unpack, x, a, N, ld, idx, mean, unc, plane);
+}
+int host_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out) {
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < N; ++p) {
+    float best = 3.4e38f;
+    int bi = 0;
+    for (int m = 0; m < M; ++m) {
+      float s = 0.f;
+      for (int d = 0; d < D; ++d) {
+        const float t = lut[m * D + d] - x[d * ld + p];
+        s = fmaf(t, t, s);
+      }
+      if (s < best) { best = s; bi = m; }
+    }
+    out[p] = bi;
+  }
+  return 0;
+}
+
+}  // namespace kf

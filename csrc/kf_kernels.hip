@@ -1,0 +1,310 @@
+// kf_kernels.hip — gfx950 (MI355X) kernels for the KaFKA engine.
+//
+// Design: every matrix the reference builds is block
+// diagonal with n_p x n_p per-pixel blocks, so the whole Gauss-Newton
+// analysis (operator + Jacobian, normal equations, Cholesky, convergence
+// partial) is one pixel per lane, SoA layout ([param][pixel], coalesced
+// 256-B wave loads), grid-stride over pixels, 256-thread workgroups
+// (4 wave64 per workgroup).  GP training records are wave-uniform and are
+// read through the scalar path (s_load) so they cost no VGPRs/LDS traffic.
+// Deterministic reductions: per-block f64 partials, summed in fixed order
+// by reduce_partials_kernel.
+#include <hip/hip_runtime.h>
+#include "kf_core.h"
+#include "kf_launch.h"
+
+namespace kf {
+
+constexpr int BLOCK = 256;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ void block_partial(double v, double* partials) {
+  __shared__ double red[BLOCK / 64];
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < BLOCK / 64; ++i) s += red[i];
+    partials[blockIdx.x] = s;
+  }
+}
+
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
+    acc += (double)pixel_analysis<NP>(a, p);
+  if (a.partials) block_partial(acc, a.partials);
+}
+
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void gain_kernel(GainArgs a) {
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
+    acc += (double)pixel_gain<NP>(a, p);
+  if (a.partials) block_partial(acc, a.partials);
+}
+
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void jacobi_kernel(JacobiArgs a) {
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
+    acc += (double)pixel_jacobi<NP>(a, p);
+  if (a.partials) block_partial(acc, a.partials);
+}
+
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void propagate_kernel(PropArgs a) {
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
+    pixel_propagate<NP>(a, p);
+}
+
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void invert_kernel(const float* src, float* dst, int64_t N, int64_t ld,
+                                                      uint8_t* status) {
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
+    const bool ok = pixel_invert<NP>(src, dst, ld, p);
+    if (status && !ok) status[p] |= ST_NONSPD;
+  }
+}
+
+// Standalone operator evaluation (H0 and Jacobian rows) for one band.
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void operator_kernel(const BandDesc* bands, int band, const float* x,
+                                                        int64_t N, int64_t ld, float* h0, float* h,
+                                                        int64_t h_ld, uint8_t* ok_out) {
+  const BandDesc& bd = bands[band];
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
+    float xv[NP], hv[NP], H0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) xv[j] = x[j * ld + p];
+    const bool ok = eval_operator<NP>(bd, p, ld, xv, H0, hv);
+    h0[p] = H0;
+    if (h) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) h[j * h_ld + p] = hv[j];
+    }
+    if (ok_out) ok_out[p] = ok ? 1 : 0;
+  }
+}
+
+// K6 Hessian correction: A -= w (y - H0(x)) d2f/dx2 for every GP band.
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void hessian_kernel(const BandDesc* bands, int n_bands, const float* x,
+                                                       float* a, int64_t N, int64_t ld) {
+  constexpr int NT = ntri(NP);
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
+    float xv[NP], acc[NT];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) xv[j] = x[j * ld + p];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = 0.f;
+    for (int bi = 0; bi < n_bands; ++bi) {
+      const BandDesc& bd = bands[bi];
+      if (bd.op != OP_GP) continue;
+      float y, w;
+      decode_obs(bd, p, y, w);
+      if (!(w > 0.f)) continue;
+      float f, Hs[NT];
+      if (!gp_hessian_dispatch<NP>(bd, xv, f, Hs)) continue;
+      const float s = w * (y - f);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = fmaf(s, Hs[t], acc[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) a[t * ld + p] -= acc[t];
+  }
+}
+
+// Output unpack (observations.py:374-376, 392-393): mean and 1/sqrt(diag(P^-1))
+// scattered onto the raster; idx==nullptr means the identity map.
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void unpack_kernel(const float* x, const float* a, int64_t N, int64_t ld,
+                                                      const int64_t* idx, float* mean, float* unc,
+                                                      int64_t plane) {
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
+    const int64_t r = idx ? idx[p] : p;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      if (mean) mean[j * plane + r] = x[j * ld + p];
+      if (unc) unc[j * plane + r] = 1.f / sqrtf(a[tri(NP, j, j) * ld + p]);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(BLOCK) void gather_kernel(const T* src, const int64_t* idx, T* dst, int64_t n,
+                                                      int rows, int64_t src_ld, int64_t dst_ld) {
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < n; p += stride) {
+    const int64_t s = idx[p];
+    for (int r = 0; r < rows; ++r) dst[r * dst_ld + p] = src[r * src_ld + s];
+  }
+}
+
+__global__ void reduce_partials_kernel(const double* partials, int n, double* out) {
+  // one wave, fixed order: lane-strided sums then a fixed shuffle tree
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 64) s += partials[i];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+// K7: nearest LUT entry (utils.py:225-234); LUT staged in LDS.
+__global__ __launch_bounds__(BLOCK) void lut_nearest_kernel(const float* lut, int M, int D, const float* x,
+                                                           int64_t N, int64_t ld, int32_t* out) {
+  extern __shared__ __attribute__((aligned(16))) float slut[];
+  for (int i = threadIdx.x; i < M * D; i += BLOCK) slut[i] = lut[i];
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
+    float xv[MAX_D];
+    for (int d = 0; d < D; ++d) xv[d] = x[d * ld + p];
+    float best = 3.4e38f;
+    int bi = 0;
+    for (int m = 0; m < M; ++m) {
+      float s = 0.f;
+      for (int d = 0; d < D; ++d) { const float t = slut[m * D + d] - xv[d]; s = fmaf(t, t, s); }
+      if (s < best) { best = s; bi = m; }
+    }
+    out[p] = bi;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+static inline int grid_for(int64_t N, int max_blocks) {
+  int64_t g = (N + BLOCK - 1) / BLOCK;
+  if (g > max_blocks) g = max_blocks;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+#define KF_NP_SWITCH(np, FN, ...)                 \
+  switch (np) {                                   \
+    case 1: FN<1>(__VA_ARGS__); break;            \
+    case 2: FN<2>(__VA_ARGS__); break;            \
+    case 3: FN<3>(__VA_ARGS__); break;            \
+    case 4: FN<4>(__VA_ARGS__); break;            \
+    case 7: FN<7>(__VA_ARGS__); break;            \
+    case 10: FN<10>(__VA_ARGS__); break;          \
+    default: return hipErrorInvalidValue;         \
+  }
+
+template <int NP>
+static void l_analysis(const AnalysisArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(analysis_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
+}
+template <int NP>
+static void l_gain(const GainArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(gain_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
+}
+template <int NP>
+static void l_jacobi(const JacobiArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(jacobi_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
+}
+template <int NP>
+static void l_propagate(const PropArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(propagate_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
+}
+template <int NP>
+static void l_invert(const float* src, float* dst, int64_t N, int64_t ld, uint8_t* st, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(invert_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, src, dst, N, ld, st);
+}
+template <int NP>
+static void l_operator(const BandDesc* b, int band, const float* x, int64_t N, int64_t ld, float* h0, float* h,
+                       int64_t h_ld, uint8_t* ok, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(operator_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, b, band, x, N, ld, h0, h, h_ld, ok);
+}
+template <int NP>
+static void l_hessian(const BandDesc* b, int nb, const float* x, float* a, int64_t N, int64_t ld, int grid,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(hessian_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, b, nb, x, a, N, ld);
+}
+template <int NP>
+static void l_unpack(const float* x, const float* a, int64_t N, int64_t ld, const int64_t* idx, float* mean,
+                     float* unc, int64_t plane, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(unpack_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, x, a, N, ld, idx, mean, unc, plane);
+}
+
+int dev_grid(int64_t N) { return grid_for(N, KF_MAX_BLOCKS); }
+
+hipError_t dev_analysis(int np, const AnalysisArgs& a, int grid, hipStream_t s) {
+  KF_NP_SWITCH(np, l_analysis, a, grid, s);
+  return hipGetLastError();
+}
+hipError_t dev_gain(int np, const GainArgs& a, int grid, hipStream_t s) {
+  KF_NP_SWITCH(np, l_gain, a, grid, s);
+  return hipGetLastError();
+}
+hipError_t dev_jacobi(int np, const JacobiArgs& a, int grid, hipStream_t s) {
+  KF_NP_SWITCH(np, l_jacobi, a, grid, s);
+  return hipGetLastError();
+}
+hipError_t dev_propagate(int np, const PropArgs& a, hipStream_t s) {
+  KF_NP_SWITCH(np, l_propagate, a, grid_for(a.N, KF_MAX_BLOCKS), s);
+  return hipGetLastError();
+}
+hipError_t dev_invert(int np, const float* src, float* dst, int64_t N, int64_t ld, uint8_t* st, hipStream_t s) {
+  KF_NP_SWITCH(np, l_invert, src, dst, N, ld, st, grid_for(N, KF_MAX_BLOCKS), s);
+  return hipGetLastError();
+}
+hipError_t dev_operator(int np, const BandDesc* b, int band, const float* x, int64_t N, int64_t ld, float* h0,
+                        float* h, int64_t h_ld, uint8_t* ok, hipStream_t s) {
+  KF_NP_SWITCH(np, l_operator, b, band, x, N, ld, h0, h, h_ld, ok, grid_for(N, KF_MAX_BLOCKS), s);
+  return hipGetLastError();
+}
+hipError_t dev_hessian(int np, const BandDesc* b, int nb, const float* x, float* a, int64_t N, int64_t ld,
+                       hipStream_t s) {
+  KF_NP_SWITCH(np, l_hessian, b, nb, x, a, N, ld, grid_for(N, KF_MAX_BLOCKS), s);
+  return hipGetLastError();
+}
+hipError_t dev_unpack(int np, const float* x, const float* a, int64_t N, int64_t ld, const int64_t* idx,
+                      float* mean, float* unc, int64_t plane, hipStream_t s) {
+  KF_NP_SWITCH(np, l_unpack, x, a, N, ld, idx, mean, unc, plane, grid_for(N, KF_MAX_BLOCKS), s);
+  return hipGetLastError();
+}
+hipError_t dev_reduce(const double* partials, int n, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(64), 0, s, partials, n, out);
+  return hipGetLastError();
+}
+hipError_t dev_gather(int elem_bytes, const void* src, const int64_t* idx, void* dst, int64_t n, int rows,
+                      int64_t src_ld, int64_t dst_ld, hipStream_t s) {
+  const int g = grid_for(n, KF_MAX_BLOCKS);
+  switch (elem_bytes) {
+    case 1: hipLaunchKernelGGL(gather_kernel<uint8_t>, dim3(g), dim3(BLOCK), 0, s, (const uint8_t*)src, idx,
+                               (uint8_t*)dst, n, rows, src_ld, dst_ld); break;
+    case 2: hipLaunchKernelGGL(gather_kernel<uint16_t>, dim3(g), dim3(BLOCK), 0, s, (const uint16_t*)src, idx,
+                               (uint16_t*)dst, n, rows, src_ld, dst_ld); break;
+    case 4: hipLaunchKernelGGL(gather_kernel<float>, dim3(g), dim3(BLOCK), 0, s, (const float*)src, idx,
+                               (float*)dst, n, rows, src_ld, dst_ld); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+hipError_t dev_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out,
+                           hipStream_t s) {
+  const size_t lds = (size_t)M * D * sizeof(float);
+  if (lds > 160 * 1024 || D > MAX_D) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(lut_nearest_kernel, dim3(grid_for(N, KF_MAX_BLOCKS)), dim3(BLOCK), lds, s, lut, M, D, x, N,
+                     ld, out);
+  return hipGetLastError();
+}
+
+}  // namespace kf

@@ -1,0 +1,49 @@
+// kf_launch.h — launcher entry points (device: kf_kernels.hip, host: kf_host.cpp).
+#pragma once
+#include <stdint.h>
+#include "kf_core.h"
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#else
+#include <hip/hip_runtime_api.h>
+#endif
+
+// Grid cap for the grid-stride kernels: 256 CUs x 8 resident blocks x 2.
+#define KF_MAX_BLOCKS 4096
+
+namespace kf {
+
+int dev_grid(int64_t N);
+hipError_t dev_analysis(int np, const AnalysisArgs& a, int grid, hipStream_t s);
+hipError_t dev_gain(int np, const GainArgs& a, int grid, hipStream_t s);
+hipError_t dev_jacobi(int np, const JacobiArgs& a, int grid, hipStream_t s);
+hipError_t dev_propagate(int np, const PropArgs& a, hipStream_t s);
+hipError_t dev_invert(int np, const float* src, float* dst, int64_t N, int64_t ld, uint8_t* st, hipStream_t s);
+hipError_t dev_operator(int np, const BandDesc* b, int band, const float* x, int64_t N, int64_t ld, float* h0,
+                        float* h, int64_t h_ld, uint8_t* ok, hipStream_t s);
+hipError_t dev_hessian(int np, const BandDesc* b, int nb, const float* x, float* a, int64_t N, int64_t ld,
+                       hipStream_t s);
+hipError_t dev_unpack(int np, const float* x, const float* a, int64_t N, int64_t ld, const int64_t* idx,
+                      float* mean, float* unc, int64_t plane, hipStream_t s);
+hipError_t dev_reduce(const double* partials, int n, double* out, hipStream_t s);
+hipError_t dev_gather(int elem_bytes, const void* src, const int64_t* idx, void* dst, int64_t n, int rows,
+                      int64_t src_ld, int64_t dst_ld, hipStream_t s);
+hipError_t dev_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out,
+                           hipStream_t s);
+
+// Host runner: the same per-pixel code over OpenMP; the block partition
+// mirrors the device grid-stride mapping so partials have the same meaning.
+bool host_supported(int np);
+int host_analysis(int np, const AnalysisArgs& a, int grid);
+int host_gain(int np, const GainArgs& a, int grid);
+int host_jacobi(int np, const JacobiArgs& a, int grid);
+int host_propagate(int np, const PropArgs& a);
+int host_invert(int np, const float* src, float* dst, int64_t N, int64_t ld, uint8_t* st);
+int host_operator(int np, const BandDesc* b, int band, const float* x, int64_t N, int64_t ld, float* h0, float* h,
+                  int64_t h_ld, uint8_t* ok);
+int host_hessian(int np, const BandDesc* b, int nb, const float* x, float* a, int64_t N, int64_t ld);
+int host_unpack(int np, const float* x, const float* a, int64_t N, int64_t ld, const int64_t* idx, float* mean,
+                float* unc, int64_t plane);
+int host_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out);
+
+}  // namespace kf

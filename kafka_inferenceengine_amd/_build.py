@@ -1,0 +1,108 @@
+"""In-tree build of the native extension ``_kafka_hip`` for gfx950.
+
+Drives ``hipcc --offload-arch=gfx950`` for the device kernels and ``g++``
+(OpenMP) for the host runner, then links one pybind11 module next to this
+file so it travels with the repository snapshot to the GPU box.  No hipify,
+no JIT cache: the object files live under ``build/`` and are rebuilt only
+when a source is newer.
+
+Usage: ``python -m kafka_inferenceengine_amd._build [--force] [--verbose]``.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+ROOT = PKG_DIR.parent
+CSRC = ROOT / "csrc"
+BUILD = ROOT / "build" / "kafka_hip"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("KAFKA_OFFLOAD_ARCH", "gfx950")
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+EXT_PATH = PKG_DIR / f"_kafka_hip{EXT_SUFFIX}"
+
+HEADERS = ["kf_core.h", "kf_launch.h", "kf_stream.h"]
+
+
+def _pybind_includes() -> list[str]:
+    import pybind11
+
+    return [f"-I{sysconfig.get_paths()['include']}", f"-I{pybind11.get_include()}"]
+
+
+def _hipcc() -> str:
+    exe = shutil.which("hipcc") or str(ROCM / "bin" / "hipcc")
+    if not Path(exe).exists():
+        raise RuntimeError("hipcc not found; set ROCM_PATH")
+    return exe
+
+
+def _stale(obj: Path, srcs: list[Path]) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return any(s.stat().st_mtime > t for s in srcs)
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=not verbose, text=True)
+    if r.returncode != 0:
+        msg = (r.stderr or "") + (r.stdout or "")
+        raise RuntimeError(f"build step failed ({r.returncode}): {' '.join(cmd)}\n{msg[-8000:]}")
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    hdrs = [CSRC / h for h in HEADERS]
+    common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}"]
+    hip_defs = ["-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}"]
+    hipcc = _hipcc()
+    objs = []
+
+    # 1. device kernels (gfx950 code objects embedded in the host object)
+    src, obj = CSRC / "kf_kernels.hip", BUILD / "kf_kernels.o"
+    if force or _stale(obj, [src] + hdrs):
+        _run([hipcc, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics", "-c", str(src), "-o", str(obj)],
+             verbose)
+    objs.append(obj)
+
+    # 2. host runner of the same per-pixel code (g++, OpenMP)
+    src, obj = CSRC / "kf_host.cpp", BUILD / "kf_host.o"
+    if force or _stale(obj, [src] + hdrs):
+        _run(["g++", *common, *hip_defs, "-fopenmp", "-mavx2", "-mfma", "-ffp-contract=fast", "-c", str(src),
+              "-o", str(obj)], verbose)
+    objs.append(obj)
+
+    # 3. bindings + ingest runtime (host code, HIP runtime API)
+    for name in ("kf_bindings.cpp", "kf_stream.cpp"):
+        src, obj = CSRC / name, BUILD / (Path(name).stem + ".o")
+        if force or _stale(obj, [src] + hdrs):
+            _run(["g++", *common, *hip_defs, *_pybind_includes(), "-fvisibility=hidden", "-c", str(src), "-o",
+                  str(obj)], verbose)
+        objs.append(obj)
+
+    if force or _stale(EXT_PATH, objs):
+        _run([hipcc, "-shared", "-fPIC", *map(str, objs), "-o", str(EXT_PATH), "-lgomp", "-lpthread",
+              f"-L{ROCM / 'lib'}", "-lamdhip64"], verbose)
+    return EXT_PATH
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    a = ap.parse_args()
+    p = build(force=a.force, verbose=a.verbose)
+    print(f"built {p}")
+
+
+if __name__ == "__main__":
+    sys.exit(main())

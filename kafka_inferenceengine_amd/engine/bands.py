@@ -1,0 +1,149 @@
+"""Assembly of per-band kernel descriptors (``BandDesc``) from an operator
+spec (``models.operators.OperatorSpec``) and device-resident observations.
+
+An observation band on the active-pixel grid is either the compact Sentinel-2
+encoding — uint16 digital numbers, reflectance = DN x scale, validity DN > 0,
+sigma = max(rel_unc x reflectance, floor) (``Sentinel2_Observations.py:163-179``)
+— decoded inside the analysis kernel, or explicit float32 ``(y, w, mask)``
+with ``w`` the inverse variance (the reference's ``uncertainty``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..models.operators import OP_GP, OP_LINEAR, OP_PRECOMP, OP_SAR, OperatorSpec
+from ..ops import kernels as K
+
+
+@dataclass
+class DeviceBand:
+    """One observation band on the active-pixel grid (device or CPU tensors)."""
+    kind: int                                   # K.OBS_DN16 | K.OBS_F32
+    dn: torch.Tensor | None = None              # uint16 bit patterns, stored as int16 [N]
+    y: torch.Tensor | None = None               # float32 [N]
+    w: torch.Tensor | None = None               # float32 [N] inverse variance
+    mask: torch.Tensor | None = None            # uint8 [N]
+    scale: float = 1e-4
+    rel_unc: float = 0.05
+    unc_floor: float = 0.0
+    metadata: dict = field(default_factory=dict)
+    emulator: object = None
+    aux: torch.Tensor | None = None             # float32 [N] (SAR incidence angle)
+
+    @property
+    def device(self):
+        t = self.dn if self.dn is not None else self.y
+        return t.device
+
+    def decode(self):
+        """(y, w) float32 on the same device (host-side reference of decode_obs)."""
+        if self.kind == K.OBS_DN16:
+            dn = self.dn.to(torch.int32) & 0xFFFF
+            y = dn.to(torch.float32) * self.scale
+            sig = torch.clamp(self.rel_unc * y, min=self.unc_floor)
+            valid = (dn > 0) & (sig > 0)
+            w = torch.where(valid, 1.0 / torch.where(valid, sig * sig, torch.ones_like(sig)), torch.zeros_like(y))
+            return torch.where(dn > 0, y, torch.zeros_like(y)), w
+        w = self.w.clone()
+        if self.mask is not None:
+            w = torch.where(self.mask.bool(), w, torch.zeros_like(w))
+        bad = ~torch.isfinite(w) | ~(w > 0) | ~torch.isfinite(self.y)
+        return torch.where(bad, torch.zeros_like(self.y), self.y), torch.where(bad, torch.zeros_like(w), w)
+
+
+class RecordCache:
+    """Uploads GP training records once per (emulator, device)."""
+
+    def __init__(self):
+        self._c = {}
+
+    def get(self, spec: OperatorSpec, device) -> torch.Tensor:
+        key = (id(spec.emulator) if spec.emulator is not None else id(spec.records), str(device))
+        t = self._c.get(key)
+        if t is None:
+            t = torch.from_numpy(np.ascontiguousarray(spec.records, dtype=np.float32)).to(device)
+            self._c[key] = (t, spec.records)  # keep the source alive so id() stays unique
+        else:
+            t = t[0]
+        return t
+
+
+def band_desc(spec: OperatorSpec, obs: DeviceBand | None, n_params: int, cache: RecordCache, h0_out=None,
+              pre_h0=None, pre_h=None, device=None, aux=None):
+    """Build one ``BandDesc``; returns (desc, tensors to keep alive)."""
+    E = K.ext()
+    d = E.BandDesc()
+    keep = []
+    device = obs.device if obs is not None else device
+    d.op = int(spec.kind)
+    if obs is not None:
+        d.obs = int(obs.kind)
+        d.scale, d.rel_unc, d.unc_floor = float(obs.scale), float(obs.rel_unc), float(obs.unc_floor)
+    d.offset = float(spec.offset)
+    if spec.kind == OP_GP:
+        if spec.d > 12 or spec.d > n_params:
+            raise ValueError(f"GP with {spec.d} inputs exceeds the compiled limit for n_params={n_params}")
+        rec = cache.get(spec, device)
+        d.d, d.T = spec.d, int(rec.shape[0])
+        d.gp = rec.data_ptr()
+        keep.append(rec)
+    elif spec.kind == OP_SAR:
+        d.d, d.T = 2, 0
+    elif spec.kind == OP_LINEAR:
+        d.d, d.T = n_params, 0
+    elif spec.kind == OP_PRECOMP:
+        if pre_h0 is None or pre_h is None:
+            raise ValueError("precomputed operator needs pre_h0/pre_h")
+        d.pre_h0, d.pre_h, d.pre_ld = pre_h0.data_ptr(), pre_h.data_ptr(), int(pre_h.shape[1])
+        keep += [pre_h0, pre_h]
+    else:
+        raise ValueError(f"unknown operator kind {spec.kind}")
+    smap = [int(i) for i in spec.state_map]
+    if any(i < 0 or i >= n_params for i in smap):
+        raise ValueError(f"state map {smap} out of range for n_params={n_params}")
+    d.map = smap
+    d.coef = [float(c) for c in spec.coef]
+    d.center = [float(c) for c in spec.center]
+    if obs is None:
+        d.obs = K.OBS_NONE
+    elif obs.kind == K.OBS_DN16:
+        d.dn = obs.dn.data_ptr()
+        keep.append(obs.dn)
+    else:
+        d.y, d.w = obs.y.data_ptr(), obs.w.data_ptr()
+        keep += [obs.y, obs.w]
+        if obs.mask is not None:
+            d.mask = obs.mask.data_ptr()
+            keep.append(obs.mask)
+    aux = obs.aux if (obs is not None and obs.aux is not None) else aux
+    if spec.kind == OP_SAR and aux is not None:
+        d.aux = aux.data_ptr()
+        keep.append(aux)
+    if h0_out is not None:
+        d.h0_out = h0_out.data_ptr()
+        keep.append(h0_out)
+    return d, keep
+
+
+def build_table(specs, obs_list, n_params, cache, device, h0_outs=None, pre=None) -> K.BandTable:
+    descs, keep = [], []
+    for i, (spec, ob) in enumerate(zip(specs, obs_list)):
+        h0 = None if h0_outs is None else h0_outs[i]
+        ph0, ph = (None, None) if pre is None or pre[i] is None else pre[i]
+        dsc, kp = band_desc(spec, ob, n_params, cache, h0, ph0, ph)
+        descs.append(dsc)
+        keep += kp
+    return K.make_band_table(descs, device, keep)
+
+
+def operator_table(specs, n_params, cache, device, aux=None) -> K.BandTable:
+    """Descriptors for operator evaluation only (no observations attached)."""
+    descs, keep = [], []
+    for spec in specs:
+        dsc, kp = band_desc(spec, None, n_params, cache, device=device, aux=aux)
+        descs.append(dsc)
+        keep += kp
+    return K.make_band_table(descs, device, keep)

@@ -1,0 +1,99 @@
+"""EngineConfig: every hard-coded constant of the reference as a named default.
+
+Reference constants: GN tolerance 1e-3, min iterations 2,
+bail-out after 25 (``linear_kf.py:246-247,297-304``); S2 uncertainty 5 %
+(``Sentinel2_Observations.py:174``), scale 1e-4 (:169); BHR 5 %/7 %, floor
+2.5e-3 (``observations.py:301-302``).
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+from dataclasses import dataclass, field
+
+import yaml
+
+
+@dataclass
+class EngineConfig:
+    # Gauss-Newton loop (linear_kf.py:245-307)
+    convergence_tolerance: float = 1e-3
+    min_iterations: int = 2
+    max_iterations: int = 25
+    # analysis
+    analysis_form: str = "information"        # 'information' (K1) | 'gain' (K1g)
+    joseph: bool = False                      # Joseph-form covariance update (gain form)
+    hessian_correction: bool = False          # K6 after convergence (off: linear_kf.py:313-319)
+    reference_quirks: bool = False            # swapped prior blend (kf_tools.py:90)
+    band_sequential: bool = False             # legacy per-band assimilation (linear_kf.py:325-425)
+    # spatial regulariser (new capability, off by default => reference results)
+    spatial_gamma: float = 0.0
+    spatial_params: list | None = None        # parameter indices smoothed (None: all)
+    jacobi_sweeps: int = 4
+    # runtime
+    device: str | None = None                 # 'cuda', 'cuda:1', 'cpu' (default: cuda if present)
+    prefetch: bool = True                     # overlap next date's ingest with compute
+    return_innovations: bool = False
+    metrics_path: str | None = None           # JSONL metrics (per date / timestep)
+    checkpoint_dir: str | None = None
+    checkpoint_every: int = 0                 # timesteps between checkpoints (0: off)
+    comm_timeout_s: float = 600.0
+    sync_timing: bool = False                 # device-synchronising per-phase timers
+    extra: dict = field(default_factory=dict)
+
+    def validate(self):
+        if self.analysis_form not in ("information", "gain"):
+            raise ValueError("analysis_form must be 'information' or 'gain'")
+        if self.spatial_gamma < 0:
+            raise ValueError("spatial_gamma must be >= 0")
+        if self.spatial_gamma > 0 and self.analysis_form != "information":
+            raise ValueError("the spatial regulariser runs in information form")
+        if self.min_iterations < 1 or self.max_iterations < self.min_iterations:
+            raise ValueError("bad iteration limits")
+        return self
+
+    # ------------------------------------------------------------- IO
+    @classmethod
+    def from_dict(cls, d: dict) -> "EngineConfig":
+        names = {f.name for f in dataclasses.fields(cls)}
+        known = {k: v for k, v in (d or {}).items() if k in names}
+        extra = {k: v for k, v in (d or {}).items() if k not in names}
+        cfg = cls(**known)
+        cfg.extra.update(extra)
+        return cfg.validate()
+
+    @classmethod
+    def from_yaml(cls, path) -> "EngineConfig":
+        with open(path) as f:
+            return cls.from_dict(yaml.safe_load(f) or {})
+
+    def to_dict(self) -> dict:
+        return dataclasses.asdict(self)
+
+    @classmethod
+    def add_arguments(cls, ap: argparse.ArgumentParser):
+        for f in dataclasses.fields(cls):
+            if f.name == "extra":
+                continue
+            flag = "--" + f.name.replace("_", "-")
+            if f.type in ("bool", bool):
+                ap.add_argument(flag, dest=f.name, action=argparse.BooleanOptionalAction, default=None)
+            elif f.type in ("int", int):
+                ap.add_argument(flag, dest=f.name, type=int, default=None)
+            elif f.type in ("float", float):
+                ap.add_argument(flag, dest=f.name, type=float, default=None)
+            else:
+                ap.add_argument(flag, dest=f.name, default=None)
+        ap.add_argument("--config", dest="config_file", default=None, help="YAML EngineConfig")
+        return ap
+
+    @classmethod
+    def from_args(cls, ns) -> "EngineConfig":
+        base = cls.from_yaml(ns.config_file).to_dict() if getattr(ns, "config_file", None) else {}
+        for f in dataclasses.fields(cls):
+            v = getattr(ns, f.name, None)
+            if v is not None:
+                base[f.name] = v
+        if base.get("spatial_params") and isinstance(base["spatial_params"], str):
+            base["spatial_params"] = [int(s) for s in base["spatial_params"].split(",")]
+        return cls.from_dict(base)

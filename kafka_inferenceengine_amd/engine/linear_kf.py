@@ -1,0 +1,639 @@
+"""LinearKalman — the engine driver (reference: ``kafka/linear_kf.py``).
+
+Same constructor, ``set_trajectory_model``, ``set_trajectory_uncertainty``,
+``run``, ``advance``, ``assimilate_multiple_bands``, ``do_all_bands``,
+``assimilate``/``assimilate_band``, ``solver``/``solver_multiband`` as
+``linear_kf.py:59-452``, but the state lives on the GPU as SoA tensors and each
+Gauss-Newton iteration is ONE fused gfx950 kernel (operator + Jacobian +
+normal equations + Cholesky + convergence partial) followed by a fixed-order
+reduction and — under tile-DP — a deterministic all-gather of one f64 per rank.
+
+Host loops that remain: the time grid, the observation
+dates of a step, and the Gauss-Newton iteration (one 8-byte D2H per
+iteration).  Objects that only speak the reference protocol (a user's
+observation class, operator factory, propagator or prior) are still accepted:
+the engine converts at the boundary and runs that piece on the host.
+"""
+from __future__ import annotations
+
+import logging
+import time
+from collections import namedtuple
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from ..inference.kf_tools import (PROP_IDENTITY, PROP_PRIOR, PROP_STANDARD, PropagatorSpec,
+                                  propagate_and_blend_prior, propagate_information_filter_LAI)
+from ..inference.solvers import variational_kalman, variational_kalman_multiband
+from ..inference.utils import iterate_time_grid
+from ..models.operators import OP_PRECOMP, OperatorSpec
+from ..ops import kernels as K
+from ..parallel.comm import Comm
+from ..parallel.partition import StripPartition
+from ..utils.blocks import ntri, pack_matrix, soa_to_interleaved, tri_pos
+from ..utils.metrics import MetricsLogger, PhaseTimer
+from .bands import DeviceBand, RecordCache, build_table
+from .config import EngineConfig
+from .state import COVARIANCE, PRECISION, KFState
+
+LOG = logging.getLogger(__name__ + ".linear_kf")
+
+Metadata = namedtuple("Metadata", "mask uncertainty")
+Previous_State = namedtuple("Previous_State", "timestamp x_vect cov_m icov_mv")
+AssimilationResult = namedtuple("AssimilationResult", "state n_iter norms innovations")
+
+
+def _resolve_device(device):
+    if device is not None:
+        return torch.device(device)
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+
+class LinearKalman:
+    """Iterated (Gauss-Newton) information-form Kalman filter over rasters."""
+
+    def __init__(self, observations, output, state_mask, create_observation_operator, parameters_list,
+                 state_propagation=propagate_information_filter_LAI, band_mapper=None, linear=True,
+                 diagnostics=True, prior=None, *, config: EngineConfig | None = None, device=None,
+                 comm: Comm | None = None, partition: StripPartition | None = None):
+        self.parameters_list = list(parameters_list)
+        self.n_params = len(self.parameters_list)
+        K.check_np(self.n_params)
+        self.observations = observations
+        self.output = output
+        self.diagnostics = diagnostics
+        self.linear = linear
+        if isinstance(state_mask, (str, bytes)):
+            from ..input_output.tiff import read_tiff
+            state_mask = read_tiff(state_mask)[0]
+        self.state_mask = np.asarray(state_mask).astype(bool)
+        self._state_propagator = state_propagation
+        self._advance = propagate_and_blend_prior
+        self.prior = prior
+        self.band_mapper = band_mapper
+        self._create_observation_operator = create_observation_operator
+        self.config = (config or EngineConfig()).validate()
+        self.comm = comm or Comm.single(_resolve_device(device or self.config.device))
+        self.device = _resolve_device(device or self.config.device) if comm is None else comm.device
+        self.partition = partition or getattr(observations, "partition", None) or \
+            StripPartition(self.state_mask, self.comm.rank, self.comm.world)
+        if self.partition.world != self.comm.world or self.partition.rank != self.comm.rank:
+            raise ValueError("partition does not match the communicator")
+        self.N = self.partition.N
+        self.n_state_elems = self.N
+        self.n_total = self.partition.N_total
+        self._m = np.ones(self.n_params)
+        self._q = np.zeros(self.n_params)
+        self._q_pix = None
+        self.trajectory_model = None
+        self.trajectory_uncertainty = None
+        self.current_timestep = None
+        self.previous_state = None
+        self._cache = RecordCache()
+        self._partials = K.partials_buffer(max(self.N, 1), self.device)
+        self._red = torch.zeros(1, dtype=torch.float64, device=self.device)
+        self.metrics = MetricsLogger(self.config.metrics_path, rank=self.comm.rank)
+        self.timer = PhaseTimer(self.device, sync=self.config.sync_timing)
+        self._reg = None
+        self.history = []
+        LOG.info("Starting KaFKA run!!!")
+
+    # ------------------------------------------------------------ model
+    def set_trajectory_model(self, m=None):
+        """Identity trajectory model (linear_kf.py:123-129); optional per-parameter diagonal."""
+        self._m = np.ones(self.n_params) if m is None else np.broadcast_to(np.asarray(m, float), (self.n_params,))
+        self.trajectory_model = "identity" if m is None else self._m.copy()
+
+    def set_trajectory_uncertainty(self, Q):
+        """Diagonal model error Q (linear_kf.py:131-146).  Accepts the reference's
+        interleaved vector over all pixels, or one value per parameter."""
+        Q = np.asarray(Q, dtype=np.float64).ravel()
+        n = self.n_params
+        if Q.size == n:
+            self._q, self._q_pix = Q.copy(), None
+        elif Q.size == n * self.n_total:
+            rows = Q.reshape(self.n_total, n)
+            if np.all(rows == rows[0]):
+                self._q, self._q_pix = rows[0].copy(), None
+            else:
+                loc = rows[self.partition.pixel_slice].T
+                self._q_pix = torch.from_numpy(np.ascontiguousarray(loc, dtype=np.float32)).to(self.device)
+        else:
+            raise ValueError(f"Q has {Q.size} entries; expected {n} or {n * self.n_total}")
+        self.trajectory_uncertainty = Q
+
+    # ------------------------------------------------------- overrides
+    def _set_plot_view(self, diag_string, timestep, obs):
+        pass
+
+    def _plotter_iteration_start(self, plot_obj, x, obs, mask):
+        pass
+
+    def _plotter_iteration_end(self, plot_obj, x, P, innovation, mask):
+        pass
+
+    # ------------------------------------------------------ conversion
+    def initial_state(self, x_forecast, P_forecast=None, P_forecast_inverse=None) -> KFState:
+        """Reference inputs (interleaved x over ALL active pixels, block-diagonal
+        P or P^-1) or a KFState / DevicePrior -> this rank's device state."""
+        if isinstance(x_forecast, KFState):
+            return x_forecast
+        want = COVARIANCE if self.config.analysis_form == "gain" else PRECISION
+        if P_forecast_inverse is not None:
+            st = KFState.from_reference(x_forecast, P_forecast_inverse, self.n_params, PRECISION, self.device,
+                                        self._pixel_slice_for(x_forecast))
+        elif P_forecast is not None:
+            st = KFState.from_reference(x_forecast, P_forecast, self.n_params, COVARIANCE, self.device,
+                                        self._pixel_slice_for(x_forecast))
+        else:
+            raise ValueError("need P_forecast or P_forecast_inverse")
+        return self._as_kind(st, want)
+
+    def _pixel_slice_for(self, x):
+        n = np.asarray(x).size // self.n_params
+        if n == self.n_total:
+            return self.partition.pixel_slice
+        if n == self.N:
+            return None
+        raise ValueError(f"state has {n} pixels; expected {self.n_total} (global) or {self.N} (local)")
+
+    def state_from_prior(self, prior=None) -> KFState:
+        """Initial state straight from a prior's per-pixel constants (no N² objects)."""
+        pr = (prior or self.prior).device_prior(None)
+        if not pr.constant:
+            raise ValueError("state_from_prior needs a per-pixel constant prior")
+        st = KFState.constant(pr.mean, pr.cinv, self.N, self.device, PRECISION)
+        return self._as_kind(st, COVARIANCE if self.config.analysis_form == "gain" else PRECISION)
+
+    def _as_kind(self, st: KFState, kind: str) -> KFState:
+        if st.kind == kind:
+            return st
+        out = torch.empty_like(st.P)
+        K.invert(self.n_params, st.P, out, N=st.N)
+        return KFState(st.x, out, kind, st.N)
+
+    # ------------------------------------------------------------ run
+    def run(self, time_grid, x_forecast, P_forecast, P_forecast_inverse, diag_str="diagnostics", band=None,
+            approx_diagonal=True, refine_diag=True, iter_obs_op=False, is_robust=False, dates=None,
+            resume_from=None):
+        """Full assimilation over ``time_grid`` (linear_kf.py:171-212).  Returns the
+        final analysis state (device).  ``resume_from`` restarts from a checkpoint."""
+        from ..input_output.checkpoint import CheckpointManager
+
+        ckpt = CheckpointManager(self.config.checkpoint_dir, self) if self.config.checkpoint_dir else None
+        resume_t = None
+        analysis = None
+        if resume_from is not None:
+            analysis, resume_t = CheckpointManager.load(resume_from, self)
+            forecast = None
+        else:
+            forecast = self.initial_state(x_forecast, P_forecast, P_forecast_inverse)
+        all_dates = list(self.observations.dates)
+        upcoming = []
+        for step_i, (timestep, locate_times, is_first) in enumerate(iterate_time_grid(time_grid, all_dates)):
+            if resume_t is not None and timestep <= resume_t:
+                continue
+            advance = analysis is not None and (not is_first or resume_t is not None)
+            analysis = self.step(timestep, locate_times, analysis if advance else forecast, advance, all_dates)
+            if ckpt is not None and self.config.checkpoint_every and (step_i + 1) % self.config.checkpoint_every == 0:
+                ckpt.save(timestep, analysis)
+        self.final_state = analysis
+        return analysis
+
+    def step(self, timestep, locate_times, state: KFState, advance: bool = True, all_dates=None) -> KFState:
+        """One time-grid step: advance (unless ``advance`` is False, i.e. ``state``
+        already is the forecast), assimilate every date in ``locate_times``,
+        dump.  Returns the analysis state."""
+        self.current_timestep = timestep
+        t0 = time.perf_counter()
+        forecast = state
+        if advance:
+            LOG.info("Advancing state, %s" % timestep.strftime("%Y-%m-%d"))
+            forecast = self.advance_state(state, timestep)
+        if len(locate_times) == 0:
+            analysis = forecast
+            LOG.info("No observations in this time")
+            info = {"n_dates": 0}
+        else:
+            all_dates = list(self.observations.dates) if all_dates is None else all_dates
+            upcoming = [d for d in all_dates if d >= locate_times[0]]
+            analysis, info = self._assimilate_dates(locate_times, forecast, upcoming)
+        LOG.info("Dumping results to disk")
+        self._dump(timestep, analysis)
+        rec = {"event": "timestep", "timestep": timestep.isoformat(), "wall_s": time.perf_counter() - t0,
+               "n_pixels": self.n_total, **info}
+        self.metrics.log(rec)
+        self.history.append(rec)
+        return analysis
+
+    # --------------------------------------------------------- advance
+    def advance(self, x_analysis, P_analysis, P_analysis_inverse, trajectory_model=None, trajectory_uncertainty=None):
+        """Reference-signature advance (linear_kf.py:99-108) on reference objects."""
+        if isinstance(x_analysis, KFState):
+            return self.advance_state(x_analysis, self.current_timestep)
+        P = P_analysis_inverse if P_analysis_inverse is not None else P_analysis
+        kind = PRECISION if P_analysis_inverse is not None else COVARIANCE
+        st = KFState.from_reference(x_analysis, P, self.n_params, kind, self.device, self._pixel_slice_for(x_analysis))
+        f = self.advance_state(st, self.current_timestep)
+        x, Pl = f.to_reference()
+        return (x, None, Pl) if f.kind == PRECISION else (x, Pl, None)
+
+    def advance_state(self, analysis: KFState, date) -> KFState:
+        """Propagation + prior blend on device (kf_tools.py:136-171 semantics)."""
+        with self.timer.phase("propagate"):
+            prop = self._state_propagator
+            spec = getattr(prop, "device_spec", None) if prop is not None else None
+            prior_dev = self.prior.device_prior(date) if (self.prior is not None and
+                                                          hasattr(self.prior, "device_prior")) else None
+            if (prop is not None and spec is None) or (self.prior is not None and prior_dev is None):
+                return self._advance_host(analysis, date)
+            n = self.n_params
+            d = {"m": self._m, "q": self._q}
+            if prop is None and self.prior is None:
+                spec = PropagatorSpec(PROP_IDENTITY)
+            elif prop is None:
+                spec = PropagatorSpec(PROP_PRIOR, reset_mean=np.zeros(n), reset_cinv=np.zeros((n, n)))
+            d["mode"] = spec.mode
+            mask = 0
+            for k in spec.propagated:
+                mask |= 1 << int(k)
+            d["prop_mask"] = mask
+            if spec.reset_mean is not None:
+                d["reset_mean"] = np.asarray(spec.reset_mean)
+                d["reset_cinv"] = pack_matrix(np.asarray(spec.reset_cinv))
+            in_kind = COVARIANCE if spec.mode == PROP_STANDARD else PRECISION
+            src = self._as_kind(analysis, in_kind)
+            out_kind = COVARIANCE if spec.output == "covariance" else PRECISION
+            blend_pix = (None, None)
+            if self.prior is not None:
+                if out_kind == COVARIANCE:
+                    # covariance-form propagator + prior: blend in precision form afterwards
+                    fc = self._run_propagate(d, src, None, COVARIANCE)
+                    fc = self._as_kind(fc, PRECISION)
+                    d2 = {"mode": PROP_IDENTITY, "m": np.ones(n), "q": np.zeros(n)}
+                    self._fill_blend(d2, prior_dev)
+                    out = self._run_propagate(d2, fc, self._blend_pix(prior_dev), PRECISION)
+                    return self._as_kind(out, self._analysis_kind())
+                self._fill_blend(d, prior_dev)
+                blend_pix = self._blend_pix(prior_dev)
+            out = self._run_propagate(d, src, blend_pix, out_kind)
+            return self._as_kind(out, self._analysis_kind())
+
+    def _analysis_kind(self):
+        return COVARIANCE if self.config.analysis_form == "gain" else PRECISION
+
+    def _fill_blend(self, d, prior_dev):
+        d["blend"] = True
+        d["quirk_blend"] = bool(self.config.reference_quirks)
+        if prior_dev.constant:
+            d["blend_mean"] = np.asarray(prior_dev.mean)
+            d["blend_cinv"] = pack_matrix(np.asarray(prior_dev.cinv))
+
+    def _blend_pix(self, prior_dev):
+        if prior_dev.constant:
+            return (None, None)
+        return (prior_dev.mean_soa, prior_dev.cinv_packed)
+
+    def _run_propagate(self, d, src: KFState, blend_pix, out_kind) -> KFState:
+        out = KFState.empty(self.n_params, self.N, self.device, out_kind, ld=src.x.shape[1])
+        bm, bc = blend_pix if blend_pix else (None, None)
+        if self.N:
+            K.propagate(self.n_params, d, src.x, src.P, out.x, out.P, N=self.N, q_pix=self._q_pix,
+                        blend_mean_pix=bm, blend_cinv_pix=bc)
+        return out
+
+    def _advance_host(self, analysis: KFState, date) -> KFState:
+        """Reference propagator/prior objects: run them on the host."""
+        x, P = analysis.to_reference()
+        n = self.n_params * self.N
+        M = sp.eye(n, n, format="csr") * 1.0
+        if not np.all(self._m == 1):
+            M = sp.diags(np.tile(self._m, self.N)).tocsr()
+        if self._q_pix is not None:
+            qv = soa_to_interleaved(self._q_pix.cpu().numpy().astype(np.float64))
+        else:
+            qv = np.tile(self._q, self.N)
+        Q = sp.diags(qv).tocsr()
+        if analysis.kind == PRECISION:
+            xf, Pf, Pfi = self._advance(x, None, P.tocsr(), M, Q, prior=self.prior, date=date,
+                                        state_propagator=self._state_propagator)
+        else:
+            xf, Pf, Pfi = self._advance(x, P.tocsr(), None, M, Q, prior=self.prior, date=date,
+                                        state_propagator=self._state_propagator)
+        if xf is None:
+            return analysis
+        if Pfi is not None:
+            st = KFState.from_reference(xf, Pfi, self.n_params, PRECISION, self.device)
+        else:
+            st = KFState.from_reference(xf, Pf, self.n_params, COVARIANCE, self.device)
+        return self._as_kind(st, self._analysis_kind())
+
+    # ------------------------------------------------------ assimilate
+    def assimilate_multiple_bands(self, locate_times, x_forecast, P_forecast, P_forecast_inverse,
+                                  approx_diagonal=True, refine_diag=False, iter_obs_op=False, is_robust=False,
+                                  diag_str="diag"):
+        """All bands of each date jointly (linear_kf.py:214-242); reference objects in/out."""
+        st = self.initial_state(x_forecast, P_forecast, P_forecast_inverse)
+        out, _ = self._assimilate_dates(locate_times, st, list(locate_times))
+        x, P = out.to_reference()
+        return (x, None, P) if out.kind == PRECISION else (x, P, None)
+
+    def _assimilate_dates(self, locate_times, forecast: KFState, upcoming):
+        info = {"n_dates": len(locate_times), "gn_iterations": [], "norms": []}
+        for i, step in enumerate(locate_times):
+            LOG.info("Assimilating %s..." % step.strftime("%Y-%m-%d"))
+            t0 = time.perf_counter()
+            if self.config.band_sequential:
+                res = self._assimilate_sequential(step, forecast)
+            else:
+                bands = self._device_bands(step)
+                if self.config.prefetch and hasattr(self.observations, "prefetch"):
+                    nxt = [d for d in upcoming if d > step]
+                    if nxt:
+                        self.observations.prefetch(nxt[0])
+                res = self.do_all_bands_state(step, bands, forecast)
+            forecast = res.state
+            info["gn_iterations"].append(res.n_iter)
+            info["norms"].append(res.norms[-1] if res.norms else None)
+            rec = {"event": "date", "date": step.isoformat(), "n_iter": res.n_iter, "norms": res.norms,
+                   "wall_s": time.perf_counter() - t0, "phases_ms": self.timer.snapshot()}
+            self.metrics.log(rec)
+        return forecast, info
+
+    # ----------------------------------------------------- observations
+    def _device_bands(self, date):
+        """-> list of (OperatorSpec, DeviceBand) for every band of ``date``."""
+        obs = self.observations
+        nb = obs.bands_per_observation[date]
+        out = []
+        with self.timer.phase("ingest"):
+            for b in range(nb):
+                if hasattr(obs, "get_device_band_data"):
+                    db = obs.get_device_band_data(date, b)
+                else:
+                    db = self._band_from_reference(obs.get_band_data(date, b))
+                spec = self._operator_spec(db, b, date)
+                out.append((spec, db))
+        return out
+
+    def _band_from_reference(self, data) -> DeviceBand:
+        """Reference record (full strip rasters, sparse diagonal inverse variance)."""
+        part = self.partition
+        sm = part.local_mask
+        y = np.asarray(data.observations, dtype=np.float64)
+        unc = data.uncertainty
+        if sp.issparse(unc):
+            w = np.asarray(unc.diagonal(), dtype=np.float64)
+        else:
+            u = np.asarray(unc, dtype=np.float64)
+            w = u.ravel() if u.shape == sm.shape else np.diag(u)
+        m = np.asarray(data.mask).astype(bool)
+        if y.shape != sm.shape:
+            raise ValueError(f"observation raster {y.shape} does not match the strip {sm.shape}")
+        yl, wl, ml = y[sm], w[sm.ravel()], m[sm]
+        wl = np.where(ml & np.isfinite(wl), wl, 0.0)
+        dev = self.device
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+        aux = None
+        meta = data.metadata if isinstance(data.metadata, dict) else {}
+        if meta.get("incidence_angle") is not None:
+            a = np.asarray(meta["incidence_angle"], dtype=np.float32)
+            aux = t(a[sm] if a.shape == sm.shape else np.broadcast_to(a.ravel(), (self.N,)), np.float32)
+        return DeviceBand(K.OBS_F32, y=t(np.where(ml, yl, 0.0), np.float32), w=t(wl, np.float32),
+                          mask=t(ml, np.uint8), metadata=meta, emulator=data.emulator, aux=aux)
+
+    def _operator_spec(self, db: DeviceBand, band, date) -> OperatorSpec:
+        spec_fn = getattr(self._create_observation_operator, "device_spec", None)
+        spec = None
+        if hasattr(self.observations, "band_spec"):
+            spec = self.observations.band_spec(date, band)
+        if spec is None and spec_fn is not None:
+            spec = spec_fn(self.n_params, db.emulator, db.metadata, band, self.band_mapper)
+        if spec is None:
+            spec = OperatorSpec(OP_PRECOMP, list(range(self.n_params)), [0.0] * self.n_params)
+        return spec
+
+    def _precompute_host(self, specs, bands, x_prev: torch.Tensor):
+        """Host evaluation of reference-protocol factories (OP_PRECOMP bands)."""
+        pre = []
+        x_flat = None
+        for b, (spec, db) in enumerate(zip(specs, bands)):
+            if spec.kind != OP_PRECOMP:
+                pre.append(None)
+                continue
+            if x_flat is None:
+                x_flat = soa_to_interleaved(x_prev[:, :self.N].cpu().numpy().astype(np.float64))
+            mask = np.zeros(self.partition.local_mask.shape, dtype=bool)
+            mask[self.partition.local_mask] = db.decode()[1].cpu().numpy() > 0
+            H = self._create_observation_operator(self.n_params, db.emulator, db.metadata, mask,
+                                                  self.partition.local_mask, x_flat, b)
+            if isinstance(H, (tuple, list)) and len(H) == 2:
+                H0, Hm = H
+                H0 = np.broadcast_to(np.asarray(H0, dtype=np.float64), (self.N,))
+            else:
+                Hm = H
+                H0 = np.asarray(Hm.dot(x_flat)).ravel()
+            Hm = sp.csr_matrix(Hm)
+            rows = np.arange(self.N)
+            h = np.stack([np.asarray(Hm[rows, rows * self.n_params + j]).ravel() for j in range(self.n_params)])
+            dev = self.device
+            pre.append((torch.from_numpy(np.ascontiguousarray(H0, dtype=np.float32)).to(dev),
+                        torch.from_numpy(np.ascontiguousarray(h, dtype=np.float32)).to(dev)))
+        return pre
+
+    # ------------------------------------------------------ GN solver
+    def do_all_bands(self, timestep, current_data, x_forecast, P_forecast, P_forecast_inverse,
+                     convergence_tolerance=1e-3, min_iterations=2):
+        """Reference-signature joint analysis (linear_kf.py:245-323); ``current_data``
+        are reference band records.  Returns (x_a, P_a, P_a^-1, innovations)."""
+        st = self.initial_state(x_forecast, P_forecast, P_forecast_inverse)
+        bands = []
+        for b, data in enumerate(current_data):
+            db = self._band_from_reference(data)
+            bands.append((self._operator_spec(db, b, timestep), db))
+        old = (self.config.convergence_tolerance, self.config.min_iterations)
+        self.config.convergence_tolerance, self.config.min_iterations = convergence_tolerance, min_iterations
+        try:
+            res = self.do_all_bands_state(timestep, bands, st, innovations=True)
+        finally:
+            self.config.convergence_tolerance, self.config.min_iterations = old
+        x, P = res.state.to_reference()
+        inn = np.hstack([i.cpu().numpy() for i in res.innovations]) if res.innovations else None
+        return (x, None, P, inn) if res.state.kind == PRECISION else (x, P, None, inn)
+
+    def do_all_bands_state(self, timestep, bands, forecast: KFState, innovations=None) -> AssimilationResult:
+        """Gauss-Newton loop on device (linear_kf.py:245-307)."""
+        cfg = self.config
+        n = self.n_params
+        N = self.N
+        specs = [s for s, _ in bands]
+        dbs = [d for _, d in bands]
+        need_inn = cfg.return_innovations if innovations is None else innovations
+        h0_outs = [torch.zeros(max(N, 1), dtype=torch.float32, device=self.device) for _ in bands] \
+            if need_inn else None
+        gain = cfg.analysis_form == "gain"
+        fc = self._as_kind(forecast, COVARIANCE if gain else PRECISION)
+        ld = fc.x.shape[1]
+        x_prev = fc.x.clone()
+        x_new = torch.empty_like(fc.x)
+        P_out = torch.empty_like(fc.P)
+        status = torch.zeros(max(N, 1), dtype=torch.uint8, device=self.device)
+        precomp = any(s.kind == OP_PRECOMP for s in specs)
+        table = None if precomp else build_table(specs, dbs, n, self._cache, self.device, h0_outs)
+        norms = []
+        n_iter = 1
+        len_x = float(n * self.n_total)
+        while True:
+            if precomp:
+                pre = self._precompute_host(specs, dbs, x_prev)
+                table = build_table(specs, dbs, n, self._cache, self.device, h0_outs, pre)
+            with self.timer.phase("analysis"):
+                if N:
+                    if gain:
+                        K.gain(n, table, x_prev, fc.x, fc.P, x_new, P_out, status, self._partials, N=N,
+                               joseph=cfg.joseph)
+                    elif cfg.spatial_gamma > 0:
+                        self._regularised_iteration(table, x_prev, fc, x_new, P_out, status)
+                    else:
+                        K.analysis(n, table, x_prev, fc.x, fc.P, x_new, P_out, None, status, self._partials, N=N)
+                    K.reduce_partials(self._partials, self._red)
+                else:
+                    self._red.zero_()
+            with self.timer.phase("converge"):
+                total = self.comm.sum_f64(self._red)
+            convergence_norm = float(np.sqrt(max(total, 0.0)) / len_x)
+            norms.append(convergence_norm)
+            LOG.info("Band {:d}, Iteration # {:d}, convergence norm: {:g}".format(len(bands) - 1, n_iter,
+                                                                                 convergence_norm))
+            x_prev, x_new = x_new, x_prev
+            if convergence_norm < cfg.convergence_tolerance and n_iter >= cfg.min_iterations:
+                break
+            if n_iter > cfg.max_iterations:
+                LOG.warning("Bailing out after 25 iterations!!!!!!")
+                break
+            n_iter += 1
+        if ld != x_prev.shape[1]:
+            raise RuntimeError("leading dimension changed")
+        state = KFState(x_prev, P_out, COVARIANCE if gain else PRECISION, N)
+        if cfg.hessian_correction and not gain and N:
+            with self.timer.phase("hessian"):
+                K.hessian(n, table, state.x, state.P, N=N)
+        self.last_status = status
+        inn = None
+        if need_inn:
+            inn = []
+            for db, h0 in zip(dbs, h0_outs):
+                y, w = db.decode()
+                inn.append(torch.where(w > 0, y - h0[:N], torch.zeros_like(y)))
+        return AssimilationResult(state, n_iter, norms, inn)
+
+    def _regularised_iteration(self, table, x_prev, fc: KFState, x_out, A_out, status):
+        """Assemble (A, b) with the fused kernel, then block-Jacobi sweeps of the
+        GMRF smoother with halo exchange between sweeps (K9 + C2)."""
+        from ..parallel.halo import HaloExchanger
+
+        if self._reg is None:
+            self._reg = HaloExchanger(self.partition, self.comm, self.n_params, self.device,
+                                      self.config.spatial_params)
+        reg = self._reg
+        n, N = self.n_params, self.N
+        b = torch.empty_like(fc.x)
+        K.analysis(n, table, x_prev, fc.x, fc.P, None, A_out, b, status, None, N=N, solve=False)
+        x_cur = x_prev
+        sweeps = max(1, int(self.config.jacobi_sweeps))
+        for s in range(sweeps):
+            x_ext = reg.extend(x_cur)
+            last = s == sweeps - 1
+            dst = x_out if last else reg.scratch(x_cur)
+            K.jacobi(n, A_out, b, x_ext, reg.nbr, x_prev, dst, self.config.spatial_gamma, reg.reg_mask, N,
+                     a_out=None, partials=self._partials if last else None)
+            x_cur = dst
+        # analysis precision includes the smoother's diagonal contribution
+        reg.add_regulariser_diagonal(A_out, self.config.spatial_gamma)
+
+    # --------------------------------------------------- band-sequential
+    def _assimilate_sequential(self, step, forecast: KFState) -> AssimilationResult:
+        bands = self._device_bands(step)
+        total_iter, norms = 0, []
+        st = forecast
+        for b, band in enumerate(bands):
+            cfg = self.config
+            old = cfg.min_iterations
+            cfg.min_iterations = 1
+            try:
+                res = self._band_gn_masked(step, band, st)
+            finally:
+                cfg.min_iterations = old
+            st = res.state
+            total_iter += res.n_iter
+            norms += res.norms
+        self.previous_state = Previous_State(step, st.x, None, st.P)
+        return AssimilationResult(st, total_iter, norms, None)
+
+    def _band_gn_masked(self, step, band, st):
+        """Single band with the masked convergence norm (linear_kf.py:356-425)."""
+        spec, db = band
+        _, w = db.decode()
+        n_valid = self.comm.sum_int(int((w > 0).sum().item()))
+        scale = (self.n_params * self.n_total) / max(self.n_params * n_valid, 1)
+        old_tol = self.config.convergence_tolerance
+        self.config.convergence_tolerance = old_tol / scale
+        try:
+            res = self.do_all_bands_state(step, [band], st)
+        finally:
+            self.config.convergence_tolerance = old_tol
+        if self.config.hessian_correction is False and spec.kind != OP_PRECOMP and self.N:
+            table = build_table([spec], [db], self.n_params, self._cache, self.device)
+            K.hessian(self.n_params, table, res.state.x, res.state.P, N=self.N)
+        return res
+
+    def assimilate(self, locate_times, x_forecast, P_forecast, P_forecast_inverse, approx_diagonal=True,
+                   refine_diag=False, iter_obs_op=False, is_robust=False, diag_str="diag"):
+        """Band-sequential assimilation (linear_kf.py:325-354)."""
+        st = self.initial_state(x_forecast, P_forecast, P_forecast_inverse)
+        for step in locate_times:
+            st = self._assimilate_sequential(step, st).state
+        x, P = st.to_reference()
+        return (x, None, P) if st.kind == PRECISION else (x, P, None)
+
+    def assimilate_band(self, band, timestep, x_forecast, P_forecast, P_forecast_inverse,
+                        convergence_tolerance=1e-3, min_iterations=1):
+        st = self.initial_state(x_forecast, P_forecast, P_forecast_inverse)
+        bands = self._device_bands(timestep)
+        res = self._band_gn_masked(timestep, bands[band], st)
+        x, P = res.state.to_reference()
+        return x, None, P, None
+
+    # ------------------------------------------------- reference shims
+    def solver(self, observations, mask, H_matrix, x_forecast, P_forecast, P_forecast_inv, R_mat, the_metadata):
+        return variational_kalman(observations, mask, self.state_mask, R_mat, H_matrix, self.n_params, x_forecast,
+                                  P_forecast, P_forecast_inv, the_metadata)
+
+    def solver_multiband(self, observations, mask, H_matrix, x0, x_forecast, P_forecast, P_forecast_inv, R_mat,
+                         the_metadata):
+        return variational_kalman_multiband(observations, mask, self.state_mask, R_mat, H_matrix, self.n_params, x0,
+                                            x_forecast, P_forecast, P_forecast_inv, the_metadata)
+
+    # ------------------------------------------------------------ output
+    def _dump(self, timestep, state: KFState):
+        if self.output is None:
+            return
+        with self.timer.phase("output"):
+            if hasattr(self.output, "dump_state"):
+                self.output.dump_state(timestep, state, self)
+                return
+            x, P = state.to_reference()
+            if state.kind == PRECISION:
+                self.output.dump_data(timestep, x, None, P, self.partition.local_mask, self.n_params)
+            else:
+                prec = self._as_kind(state, PRECISION)
+                self.output.dump_data(timestep, x, P, prec.to_reference()[1], self.partition.local_mask,
+                                      self.n_params)
+
+    def unc(self, state: KFState) -> torch.Tensor:
+        """1/sqrt(diag(P^-1)) per parameter, [n_p, N] (observations.py:392-393)."""
+        prec = self._as_kind(state, PRECISION)
+        idx = [tri_pos(self.n_params, j, j) for j in range(self.n_params)]
+        return 1.0 / torch.sqrt(prec.P[idx, :self.N])

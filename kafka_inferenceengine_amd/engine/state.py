@@ -1,0 +1,99 @@
+"""Device-resident Kalman state: SoA mean ``x[n_p, ld]`` and packed symmetric
+blocks ``P[n_p(n_p+1)/2, ld]`` (precision or covariance).
+
+Replaces the reference's interleaved vector + (n_p·N)² sparse matrices
+(``linear_kf.py:171``, ``kf_tools.py:131``).  Conversions to/from the
+reference representation are provided for the compatibility paths.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from ..utils.blocks import (LazyBlockDiag, interleaved_to_soa, ntri, pack_blocks, pack_matrix, soa_to_interleaved,
+                            sparse_to_blocks)
+
+PRECISION = "precision"
+COVARIANCE = "covariance"
+
+
+@dataclass
+class KFState:
+    x: torch.Tensor          # [n_p, ld] float32
+    P: torch.Tensor          # [ntri, ld] float32 (packed upper triangle)
+    kind: str                # PRECISION | COVARIANCE
+    N: int                   # active pixels (<= ld)
+
+    @property
+    def n_params(self) -> int:
+        return int(self.x.shape[0])
+
+    @property
+    def device(self):
+        return self.x.device
+
+    def clone(self) -> "KFState":
+        return KFState(self.x.clone(), self.P.clone(), self.kind, self.N)
+
+    def copy_(self, other: "KFState") -> "KFState":
+        self.x.copy_(other.x)
+        self.P.copy_(other.P)
+        self.kind = other.kind
+        return self
+
+    @classmethod
+    def empty(cls, n_params, N, device, kind=PRECISION, ld=None) -> "KFState":
+        ld = N if ld is None else ld
+        x = torch.zeros((n_params, ld), dtype=torch.float32, device=device)
+        P = torch.zeros((ntri(n_params), ld), dtype=torch.float32, device=device)
+        return cls(x, P, kind, N)
+
+    @classmethod
+    def constant(cls, mean, mat, N, device, kind=PRECISION) -> "KFState":
+        """Every pixel = (mean, mat) — e.g. a prior.  Built on the device."""
+        mean = np.asarray(mean, dtype=np.float64)
+        n = mean.size
+        s = cls.empty(n, N, device, kind)
+        s.x.copy_(torch.from_numpy(mean.astype(np.float32))[:, None].expand(n, N))
+        s.P.copy_(torch.from_numpy(pack_matrix(np.asarray(mat)).astype(np.float32))[:, None].expand(-1, N))
+        return s
+
+    # ------------------------------------------------- reference interop
+    @classmethod
+    def from_reference(cls, x_flat, P_mat, n_params, kind, device, pixel_slice=None) -> "KFState":
+        """Interleaved vector + block-diagonal matrix (sparse/dense/None) -> state.
+
+        ``pixel_slice`` selects this rank's pixels (global -> local)."""
+        x = interleaved_to_soa(np.asarray(x_flat, dtype=np.float64), n_params)
+        if pixel_slice is not None:
+            x = x[:, pixel_slice]
+        N = x.shape[1]
+        if P_mat is None:
+            packed = np.zeros((ntri(n_params), N))
+        elif isinstance(P_mat, LazyBlockDiag):
+            packed = P_mat.packed
+            if pixel_slice is not None:
+                packed = packed[:, pixel_slice]
+        else:
+            if pixel_slice is not None and sp.issparse(P_mat):
+                sl = np.arange(P_mat.shape[0]).reshape(-1, n_params)[pixel_slice].ravel()
+                P_mat = sp.csr_matrix(P_mat)[sl][:, sl]
+            blocks = sparse_to_blocks(P_mat, n_params, check=True)
+            if pixel_slice is not None and not sp.issparse(P_mat):
+                blocks = blocks[pixel_slice]
+            packed = pack_blocks(blocks)
+        xt = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(device)
+        Pt = torch.from_numpy(np.ascontiguousarray(packed, dtype=np.float32)).to(device)
+        return cls(xt, Pt, kind, N)
+
+    def to_reference(self):
+        """(x_flat numpy, LazyBlockDiag of P) — the reference's (x, P / P^-1)."""
+        x = self.x[:, :self.N].detach().cpu().numpy().astype(np.float64)
+        P = self.P[:, :self.N].detach().cpu().numpy()
+        return soa_to_interleaved(x), LazyBlockDiag(P, self.n_params)
+
+    def numpy(self):
+        return (self.x[:, :self.N].detach().cpu().numpy(), self.P[:, :self.N].detach().cpu().numpy())

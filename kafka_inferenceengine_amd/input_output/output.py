@@ -1,0 +1,193 @@
+"""Output writers (plug-in point L1: ``dump_data`` / device ``dump_state``).
+
+* ``KafkaOutput`` — per parameter and timestep a Float32 GeoTIFF of the mean
+  and one of 1/sqrt(diag(P^-1)) (the conditional std), file names
+  ``{param}_A%Y%j[_{prefix}].tif`` / ``..._unc.tif`` (``observations.py:338-394``).
+  Rasters are produced on the device by the unpack kernel and written by a
+  background thread.
+* ``KafkaOutputMemory`` — in-memory dict {timestep: {param: values}}
+  (``kafka_test.py:135-145``; fixed to accept the engine's 6 arguments).
+* ``DeviceOutput`` — keeps the latest mean/unc rasters on the device
+  (the benchmark's writer: no host traffic in the timed loop).
+"""
+from __future__ import annotations
+
+import os
+import threading
+from queue import Queue
+
+import numpy as np
+import torch
+
+from ..ops import kernels as K
+from .tiff import write_tiff
+
+
+def _fname(folder, param, timestep, prefix, suffix=""):
+    core = f"{param}_{timestep.strftime('A%Y%j')}"
+    if prefix is not None:
+        core += f"_{prefix}"
+    return os.path.join(folder, core + suffix + ".tif")
+
+
+class _Writer:
+    def __init__(self):
+        self.q = Queue(maxsize=4)
+        self.err = None
+        self.t = threading.Thread(target=self._run, daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while True:
+            job = self.q.get()
+            if job is None:
+                return
+            try:
+                job()
+            except Exception as e:  # surfaced on flush()
+                self.err = e
+            finally:
+                self.q.task_done()
+
+    def submit(self, job):
+        if self.err:
+            raise self.err
+        self.q.put(job)
+
+    def flush(self):
+        self.q.join()
+        if self.err:
+            raise self.err
+
+
+def _device_rasters(state, engine, mean=True, unc=True):
+    """(mean, unc) as [n_p, H_strip, W] float32 CPU arrays (inactive = 0)."""
+    part = engine.partition
+    n = engine.n_params
+    H, W = part.strip_shape
+    dev = state.x.device
+    prec = engine._as_kind(state, "precision")
+    m = torch.zeros((n, H * W), dtype=torch.float32, device=dev) if mean else None
+    u = torch.zeros((n, H * W), dtype=torch.float32, device=dev) if unc else None
+    idx = torch.from_numpy(part.local_idx).to(dev)
+    if state.N:
+        K.unpack(n, prec.x, prec.P, m, u, idx=idx, N=state.N)
+    return (None if m is None else m.view(n, H, W).cpu().numpy(),
+            None if u is None else u.view(n, H, W).cpu().numpy())
+
+
+class KafkaOutput:
+    """GeoTIFF writer (``observations.py:338-394``)."""
+
+    def __init__(self, parameter_list, geotransform, projection, folder, prefix=None, fmt="GTiff",
+                 compress="deflate", asynchronous=True):
+        self.geotransform = geotransform
+        self.projection = projection
+        self.folder = folder
+        self.fmt = fmt
+        self.parameter_list = list(parameter_list)
+        self.prefix = prefix
+        self.compress = compress
+        os.makedirs(folder, exist_ok=True)
+        self._w = _Writer() if asynchronous else None
+        self.written = []
+
+    def _geo(self, engine=None):
+        gt = list(self.geotransform) if self.geotransform is not None else None
+        if gt is not None and engine is not None and engine.partition.r0:
+            gt[3] = gt[3] + engine.partition.r0 * gt[5]
+        return gt
+
+    def _prefix(self, engine):
+        if engine is not None and engine.comm.world > 1:
+            return f"{self.prefix}_r{engine.comm.rank}" if self.prefix is not None else f"r{engine.comm.rank}"
+        return self.prefix
+
+    def _write_all(self, timestep, mean, unc, gt, prefix):
+        for ii, param in enumerate(self.parameter_list):
+            fn = _fname(self.folder, param, timestep, prefix)
+            write_tiff(fn, mean[ii], gt, self.projection, self.compress)
+            self.written.append(fn)
+        for ii, param in enumerate(self.parameter_list):
+            fn = _fname(self.folder, param, timestep, prefix, "_unc")
+            write_tiff(fn, unc[ii], gt, self.projection, self.compress)
+            self.written.append(fn)
+
+    def dump_state(self, timestep, state, engine):
+        mean, unc = _device_rasters(state, engine)
+        gt, pf = self._geo(engine), self._prefix(engine)
+        if self._w is not None:
+            self._w.submit(lambda: self._write_all(timestep, mean, unc, gt, pf))
+        else:
+            self._write_all(timestep, mean, unc, gt, pf)
+
+    def dump_data(self, timestep, x_analysis, P_analysis, P_analysis_inv, state_mask, n_params):
+        """Reference signature: interleaved x and block-diagonal P^-1."""
+        sm = np.asarray(state_mask).astype(bool)
+        mean = np.zeros((n_params,) + sm.shape, dtype=np.float32)
+        unc = np.zeros_like(mean)
+        d = P_analysis_inv.diagonal()
+        for ii in range(n_params):
+            mean[ii][sm] = x_analysis[ii::n_params]
+            unc[ii][sm] = 1. / np.sqrt(d[ii::n_params])
+        self._write_all(timestep, mean, unc, self.geotransform, self.prefix)
+
+    def flush(self):
+        if self._w is not None:
+            self._w.flush()
+
+
+class KafkaOutputMemory:
+    """In-memory output (kafka_test.py:135-145)."""
+
+    def __init__(self, parameter_list):
+        self.parameter_list = list(parameter_list)
+        self.output = {}
+
+    def dump_data(self, timestep, x_analysis, P_analysis, P_analysis_inv, state_mask, n_params=None):
+        n = n_params or len(self.parameter_list)
+        sol = {p: np.asarray(x_analysis)[ii::n].copy() for ii, p in enumerate(self.parameter_list)}
+        if P_analysis_inv is not None:
+            d = P_analysis_inv.diagonal()
+            for ii, p in enumerate(self.parameter_list):
+                sol[p + "_unc"] = 1. / np.sqrt(d[ii::n])
+        self.output[timestep] = sol
+
+
+class DeviceOutput:
+    """Keeps the latest analysis rasters on the device (mean and unc planes on
+    the strip grid) — the unpack kernel runs every timestep, nothing leaves
+    the GPU unless ``to_host`` is called."""
+
+    def __init__(self, parameter_list, keep_history: bool = False):
+        self.parameter_list = list(parameter_list)
+        self.keep_history = keep_history
+        self.mean = None
+        self.unc = None
+        self.timestep = None
+        self.history = {}
+
+    def dump_state(self, timestep, state, engine):
+        part = engine.partition
+        n = engine.n_params
+        H, W = part.strip_shape
+        dev = state.x.device
+        if self.mean is None or self.mean.device != dev:
+            self.mean = torch.zeros((n, H * W), dtype=torch.float32, device=dev)
+            self.unc = torch.zeros((n, H * W), dtype=torch.float32, device=dev)
+            self._idx = torch.from_numpy(part.local_idx).to(dev)
+            self._identity = part.N == H * W
+        prec = engine._as_kind(state, "precision")
+        if state.N:
+            K.unpack(n, prec.x, prec.P, self.mean, self.unc, idx=None if self._identity else self._idx, N=state.N)
+        self.timestep = timestep
+        if self.keep_history:
+            self.history[timestep] = (self.mean.clone(), self.unc.clone())
+
+    def to_host(self, shape=None):
+        n = self.mean.shape[0]
+        m = self.mean.cpu().numpy()
+        u = self.unc.cpu().numpy()
+        if shape is not None:
+            m, u = m.reshape((n,) + tuple(shape)), u.reshape((n,) + tuple(shape))
+        return m, u

@@ -1,0 +1,81 @@
+"""Double-buffered observation ingest: pinned host pool -> device on a side stream.
+
+A date's bands live contiguously in one pinned ``HostRing`` slot (native,
+``csrc/kf_stream.cpp``).  ``prefetch(k)`` issues the H2D copy of pool entry k
+into the idle device buffer on the ingest stream after that buffer's last
+consumer finished; ``acquire(k)`` makes the compute stream wait on the copy's
+event only.  H2D of date t+1 therefore overlaps the Gauss-Newton kernels of
+date t.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import _ext
+
+
+class DateStreamer:
+    def __init__(self, n_pool: int, entry_shape, dtype, device, n_threads: int = 2):
+        self.device = torch.device(device)
+        self.entry_shape = tuple(entry_shape)
+        self.dtype = dtype
+        numel = 1
+        for s in self.entry_shape:
+            numel *= s
+        self.entry_bytes = numel * torch.empty((), dtype=dtype).element_size()
+        self.ring = _ext.require_ext().HostRing(n_pool, self.entry_bytes, n_threads)
+        self.n_pool = n_pool
+        self.bufs = [torch.empty(self.entry_shape, dtype=dtype, device=self.device) for _ in range(2)]
+        self.loaded = [None, None]          # pool index held by each device buffer
+        self.cuda = self.device.type == "cuda"
+        self.stream = torch.cuda.Stream(self.device) if self.cuda else None
+        self.bytes_h2d = 0
+
+    @property
+    def pinned(self) -> bool:
+        return bool(self.ring.pinned)
+
+    def host_view(self, k: int) -> torch.Tensor:
+        """Writable CPU tensor aliasing pool slot k (fill once at setup)."""
+        import ctypes
+
+        numel = self.entry_bytes // torch.empty((), dtype=self.dtype).element_size()
+        buf = (ctypes.c_char * self.entry_bytes).from_address(self.ring.slot(k))
+        return torch.frombuffer(buf, dtype=self.dtype, count=numel).view(self.entry_shape)
+
+    def fill_from_file(self, k: int, path: str, offset: int = 0):
+        """Background read of a raw file into slot k (native reader threads)."""
+        self.ring.read_file_async(k, str(path), int(offset), self.entry_bytes, 0)
+
+    def _slot_for(self, k: int) -> int:
+        if self.loaded[0] == k:
+            return 0
+        if self.loaded[1] == k:
+            return 1
+        return -1
+
+    def prefetch(self, k: int) -> int:
+        b = self._slot_for(k)
+        if b >= 0:
+            return b
+        # evict the buffer that does not hold the entry being consumed
+        b = 1 if (self._current is not None and self.loaded[0] == self._current) else 0
+        dst = self.bufs[b]
+        if self.cuda:
+            # the buffer's previous consumer is everything queued so far on the compute stream
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            self.ring.h2d(k, dst.data_ptr(), self.entry_bytes, 0, int(self.stream.cuda_stream))
+        else:
+            self.ring.h2d(k, dst.data_ptr(), self.entry_bytes, 0, 0)
+        self.loaded[b] = k
+        self.bytes_h2d += self.entry_bytes
+        return b
+
+    _current = None
+
+    def acquire(self, k: int) -> torch.Tensor:
+        b = self.prefetch(k)
+        if self.cuda:
+            self.ring.stream_wait(k, int(torch.cuda.current_stream(self.device).cuda_stream))
+        self._current = k
+        return self.bufs[b]

@@ -1,0 +1,161 @@
+"""Minimal GeoTIFF writer/reader (GDAL is not available in this stack).
+
+Writes single-band rasters (float32 / uint8 / uint16 / int16 / float64) as
+classic or BigTIFF, striped, uncompressed or DEFLATE (the reference writes
+DEFLATE/BIGTIFF/TILED Float32, ``observations.py:366-371``), with GeoTIFF
+georeferencing: ModelPixelScale (33550), ModelTiepoint (33922), a
+GeoKeyDirectory (34735) and the projection WKT in GTCitationGeoKey (34737).
+The reader handles what the writer produces plus the uncompressed / DEFLATE
+striped files of the reference (e.g. ``Barrax_pivots.tif``).
+"""
+from __future__ import annotations
+
+import struct
+import zlib
+
+import numpy as np
+
+_DT = {np.dtype("uint8"): (1, 8), np.dtype("uint16"): (1, 16), np.dtype("int16"): (2, 16),
+       np.dtype("int32"): (2, 32), np.dtype("uint32"): (1, 32), np.dtype("float32"): (3, 32),
+       np.dtype("float64"): (3, 64)}
+# TIFF field types
+SHORT, LONG, DOUBLE, ASCII, LONG8 = 3, 4, 12, 2, 16
+_TSIZE = {1: 1, 2: 1, 3: 2, 4: 4, 5: 8, 11: 4, 12: 8, 16: 8}
+_TFMT = {1: "B", 2: "c", 3: "H", 4: "I", 11: "f", 12: "d", 16: "Q"}
+
+
+def write_tiff(path, array, geotransform=None, projection: str | None = None, compress: str | None = "deflate",
+               rows_per_strip: int = 64, bigtiff: bool | None = None, nodata=None):
+    a = np.ascontiguousarray(np.asarray(array))
+    if a.ndim != 2:
+        raise ValueError("write_tiff writes single-band 2-D rasters")
+    if a.dtype == np.bool_:
+        a = a.astype(np.uint8)
+    if a.dtype not in _DT:
+        raise TypeError(f"unsupported dtype {a.dtype}")
+    fmt_code, bits = _DT[a.dtype]
+    a = a.astype(a.dtype.newbyteorder("<"), copy=False)
+    H, W = a.shape
+    rps = max(1, min(rows_per_strip, H))
+    strips = []
+    for r in range(0, H, rps):
+        raw = a[r:r + rps].tobytes()
+        strips.append(zlib.compress(raw, 6) if compress == "deflate" else raw)
+    total = sum(len(s) for s in strips)
+    if bigtiff is None:
+        bigtiff = total > 3_500_000_000
+    tags = [(256, LONG, [W]), (257, LONG, [H]), (258, SHORT, [bits]), (259, SHORT, [8 if compress == "deflate" else 1]),
+            (262, SHORT, [1]), (277, SHORT, [1]), (278, LONG, [rps]), (284, SHORT, [1]), (339, SHORT, [fmt_code])]
+    if geotransform is not None:
+        gt = [float(v) for v in geotransform]
+        tags.append((33550, DOUBLE, [gt[1], -gt[5], 0.0]))
+        tags.append((33922, DOUBLE, [0.0, 0.0, 0.0, gt[0], gt[3], 0.0]))
+        cit = (projection or "unknown") + "|"
+        keys = [1, 1, 0, 3, 1024, 0, 1, 1, 1025, 0, 1, 1, 1026, 34737, len(cit), 0]
+        tags.append((34735, SHORT, keys))
+        tags.append((34737, ASCII, cit))
+    if nodata is not None:
+        tags.append((42113, ASCII, str(nodata)))
+    # data first, IFD after
+    hdr = 16 if bigtiff else 8
+    body = bytearray()
+    offsets = []
+    for s in strips:
+        offsets.append(hdr + len(body))
+        body += s
+        if len(body) % 2:
+            body += b"\0"
+    off_type = LONG8 if bigtiff else LONG
+    tags.append((273, off_type, offsets))
+    tags.append((279, off_type, [len(s) for s in strips]))
+    tags.sort(key=lambda t: t[0])
+    ifd_off = hdr + len(body)
+    ent = 20 if bigtiff else 12
+    cnt_sz = 8 if bigtiff else 2
+    inline = 8 if bigtiff else 4
+    ext = bytearray()
+    ext_base = ifd_off + cnt_sz + ent * len(tags) + (8 if bigtiff else 4)
+    entries = bytearray()
+    for tag, typ, vals in tags:
+        if typ == ASCII:
+            payload = (vals if isinstance(vals, bytes) else vals.encode()) + b"\0"
+            count = len(payload)
+        else:
+            payload = struct.pack("<" + _TFMT[typ] * len(vals), *vals)
+            count = len(vals)
+        if len(payload) <= inline:
+            val = payload.ljust(inline, b"\0")
+        else:
+            val = struct.pack("<Q" if bigtiff else "<I", ext_base + len(ext))
+            ext += payload
+            if len(ext) % 2:
+                ext += b"\0"
+        entries += struct.pack("<HHQ" if bigtiff else "<HHI", tag, typ, count) + val
+    with open(path, "wb") as f:
+        if bigtiff:
+            f.write(b"II" + struct.pack("<HHHQ", 43, 8, 0, ifd_off))
+        else:
+            f.write(b"II" + struct.pack("<HI", 42, ifd_off))
+        f.write(body)
+        f.write(struct.pack("<Q" if bigtiff else "<H", len(tags)))
+        f.write(entries)
+        f.write(struct.pack("<Q" if bigtiff else "<I", 0))
+        f.write(ext)
+
+
+def read_tiff(path):
+    """-> (array, info dict with geotransform/projection)."""
+    with open(path, "rb") as f:
+        b = f.read()
+    bo = "<" if b[:2] == b"II" else ">"
+    magic = struct.unpack(bo + "H", b[2:4])[0]
+    big = magic == 43
+    ifd = struct.unpack(bo + ("Q" if big else "I"), b[8:16] if big else b[4:8])[0]
+    n = struct.unpack(bo + ("Q" if big else "H"), b[ifd:ifd + (8 if big else 2)])[0]
+    p = ifd + (8 if big else 2)
+    ent = 20 if big else 12
+    tags = {}
+    for i in range(n):
+        e = b[p + i * ent:p + (i + 1) * ent]
+        if big:
+            tag, typ, cnt = struct.unpack(bo + "HHQ", e[:12])
+            raw = e[12:20]
+            inline = 8
+        else:
+            tag, typ, cnt = struct.unpack(bo + "HHI", e[:8])
+            raw = e[8:12]
+            inline = 4
+        sz = _TSIZE.get(typ, 1) * cnt
+        if sz > inline:
+            off = struct.unpack(bo + ("Q" if big else "I"), raw)[0]
+            data = b[off:off + sz]
+        else:
+            data = raw[:sz]
+        if typ == ASCII:
+            tags[tag] = data.rstrip(b"\0").decode(errors="replace")
+        else:
+            tags[tag] = list(struct.unpack(bo + _TFMT[typ] * cnt, data))
+    W, H = tags[256][0], tags[257][0]
+    bits = tags.get(258, [8])[0]
+    fmt = tags.get(339, [1])[0]
+    comp = tags.get(259, [1])[0]
+    dt = {(1, 8): "u1", (1, 16): "u2", (2, 16): "i2", (1, 32): "u4", (2, 32): "i4", (3, 32): "f4",
+          (3, 64): "f8"}[(fmt, bits)]
+    dtype = np.dtype(bo + dt)
+    out = bytearray()
+    for off, cnt in zip(tags[273], tags[279]):
+        chunk = b[off:off + cnt]
+        if comp in (8, 32946):
+            chunk = zlib.decompress(chunk)
+        elif comp != 1:
+            raise ValueError(f"unsupported TIFF compression {comp}")
+        out += chunk
+    arr = np.frombuffer(bytes(out[:W * H * dtype.itemsize]), dtype=dtype).reshape(H, W)
+    info = {"shape": (H, W)}
+    if 33550 in tags and 33922 in tags:
+        sx, sy = tags[33550][0], tags[33550][1]
+        tp = tags[33922]
+        info["geotransform"] = [tp[3] - tp[0] * sx, sx, 0.0, tp[4] + tp[1] * sy, 0.0, -sy]
+    if 34737 in tags:
+        info["projection"] = tags[34737].rstrip("|")
+    return arr.astype(dtype.newbyteorder("=")), info

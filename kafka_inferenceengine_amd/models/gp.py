@@ -1,0 +1,175 @@
+"""Gaussian-process emulators (the "PROSAIL/SAIL/JRC-TIP" observation model).
+
+The reference loads pickled ``gp_emulator.GaussianProcess`` objects and calls
+``predict(X, do_unc=False) -> (H, dH)`` (``kafka/inference/utils.py:86-90``)
+and optionally ``hessian(x)`` (``kf_tools.py:28``).  No pickles ship with the
+reference and unpickling is not allowed here, so this module provides a
+self-contained RBF/ARD GP with the same protocol, fitted on synthetic
+radiative-transfer-like targets ("random-init emulators", BASELINE.json).
+
+Kernel:  f(x) = mu + sum_i alpha_i * s * exp(-1/2 sum_d lambda_d (x_d - t_id)^2)
+
+``records()`` emits the packed per-training-point rows the gfx950 kernel
+streams through the scalar path (``csrc/kf_core.h`` ``gp_eval``).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+LOG2E = 1.4426950408889634
+
+
+class GaussianProcessEmulator:
+    """RBF (ARD) GP emulator with analytic gradient and Hessian."""
+
+    def __init__(self, inputs, alpha, lam, signal: float = 1.0, mean: float = 0.0, name: str = "gp"):
+        self.inputs = np.asarray(inputs, dtype=np.float64)      # [T, D]
+        self.alpha = np.asarray(alpha, dtype=np.float64)        # [T]
+        self.lam = np.asarray(lam, dtype=np.float64)            # [D]  (1/lengthscale^2)
+        self.signal = float(signal)
+        self.mean = float(mean)
+        self.name = name
+        if self.inputs.ndim != 2 or self.inputs.shape[0] != self.alpha.shape[0]:
+            raise ValueError("inputs must be [T, D] and alpha [T]")
+        if self.lam.shape != (self.inputs.shape[1],):
+            raise ValueError("lam must have one entry per input dimension")
+        self._records = None
+
+    # ------------------------------------------------------------------ shape
+    @property
+    def n_inputs(self) -> int:
+        return self.inputs.shape[1]
+
+    @property
+    def n_train(self) -> int:
+        return self.inputs.shape[0]
+
+    # ------------------------------------------------------------- numerics
+    def _kernel(self, X):
+        X = np.atleast_2d(np.asarray(X, dtype=np.float64))
+        diff = X[:, None, :] - self.inputs[None, :, :]                 # [n, T, D]
+        k = self.signal * np.exp(-0.5 * np.einsum("ntd,d->nt", diff * diff, self.lam))
+        return X, diff, k
+
+    def predict(self, X, do_unc: bool = False, chunk: int = 65536):
+        """(H, dH) like gp_emulator; with ``do_unc`` returns (H, var, dH)."""
+        X = np.atleast_2d(np.asarray(X, dtype=np.float64))
+        H = np.empty(X.shape[0])
+        dH = np.empty_like(X)
+        for s in range(0, X.shape[0], chunk):
+            _, diff, k = self._kernel(X[s:s + chunk])
+            ak = k * self.alpha[None, :]
+            H[s:s + chunk] = self.mean + ak.sum(1)
+            dH[s:s + chunk] = -self.lam[None, :] * np.einsum("nt,ntd->nd", ak, diff)
+        if do_unc:
+            return H, np.zeros_like(H), dH
+        return H, dH
+
+    def hessian(self, X):
+        """d2f/dx2, [n, D, D]."""
+        _, diff, k = self._kernel(X)
+        ak = k * self.alpha[None, :]
+        ld = diff * self.lam[None, None, :]
+        H = np.einsum("nt,ntu,ntv->nuv", ak, ld, ld)
+        H -= np.einsum("nt,u->nu", ak, self.lam)[:, :, None] * np.eye(self.n_inputs)[None]
+        return H
+
+    # ---------------------------------------------------------- kernel ABI
+    def center(self) -> np.ndarray:
+        return self.inputs.mean(0)
+
+    def records(self) -> np.ndarray:
+        """float32 [T, 2D+2] rows: L, B[D], alpha, alpha*t[D] (inputs centred)."""
+        if self._records is None:
+            c = self.center()
+            t = self.inputs - c[None, :]
+            L = np.log2(self.signal) - 0.5 * LOG2E * (t * t * self.lam[None, :]).sum(1)
+            B = LOG2E * self.lam[None, :] * t
+            at = self.alpha[:, None] * t
+            rec = np.concatenate([L[:, None], B, self.alpha[:, None], at], axis=1)
+            self._records = np.ascontiguousarray(rec.astype(np.float32))
+        return self._records
+
+    # ------------------------------------------------------------ building
+    @classmethod
+    def fit(cls, X, y, lengthscale, signal=None, noise=1e-6, name="gp"):
+        X = np.asarray(X, dtype=np.float64)
+        y = np.asarray(y, dtype=np.float64)
+        lam = 1.0 / np.asarray(lengthscale, dtype=np.float64) ** 2
+        mu = float(y.mean())
+        s = float(np.var(y)) if signal is None else float(signal)
+        s = max(s, 1e-12)
+        diff = X[:, None, :] - X[None, :, :]
+        K = s * np.exp(-0.5 * np.einsum("ijd,d->ij", diff * diff, lam))
+        K[np.diag_indices_from(K)] += noise * s + 1e-10
+        alpha = np.linalg.solve(K, y - mu)
+        return cls(X, alpha, lam, s, mu, name=name)
+
+    @classmethod
+    def synthetic(cls, target, lo, hi, n_train: int = 500, seed: int = 0, length_frac: float = 0.35,
+                  noise: float = 1e-5, name: str = "gp"):
+        """Fit an emulator to ``target`` on a Latin-hypercube design in [lo, hi]."""
+        rng = np.random.default_rng(seed)
+        lo = np.asarray(lo, dtype=np.float64)
+        hi = np.asarray(hi, dtype=np.float64)
+        D = lo.size
+        u = (np.argsort(rng.random((D, n_train)), axis=1).T + rng.random((n_train, D))) / n_train
+        X = lo + u * (hi - lo)
+        y = target(X)
+        return cls.fit(X, y, length_frac * (hi - lo), noise=noise, name=name)
+
+
+# --------------------------------------------------------------------------
+# synthetic targets ("random-init" physics stand-ins)
+
+def tip_bhr_target(band: int):
+    """Two-stream-like broadband albedo of (omega, asym, TLAI, soil) — the input
+    order of the JRC-TIP band mapper ``[0,1,6,2]``/``[3,4,6,5]``
+    (kafka/inference/utils.py:148-153)."""
+    def f(X):
+        w, d, t, s = X[:, 0], X[:, 1], np.clip(X[:, 2], 0.0, 1.0), X[:, 3]
+        canopy = w * (1.0 - t) * (0.45 + 0.08 * np.tanh(d - 1.0)) / (1.0 - 0.3 * w * (1.0 - t))
+        return canopy + s * t * t + (0.01 if band == 0 else 0.03)
+    return f
+
+
+def prosail_target(band: int, n_params: int = 10):
+    """Smooth reflectance-like function of the 10 transformed PROSAIL parameters."""
+    rng = np.random.default_rng(1000 + band)
+    w = rng.normal(0, 0.08, n_params)
+    b = rng.uniform(0.5, 2.0, n_params)
+
+    def f(X):
+        lai_t = np.clip(X[:, 6], 0.0, 1.0)  # exp(-LAI/2)
+        soil = 0.1 + 0.1 * X[:, min(8, X.shape[1] - 1)]
+        base = 0.05 + 0.02 * band + np.tanh(X @ (w * b)) * 0.05
+        return base * (1.0 - lai_t) + soil * lai_t + 0.02 * np.sin(X[:, 1] * (1 + band % 3))
+    return f
+
+
+TIP_RANGES = {
+    0: (np.array([0.0, 0.0, 0.0, 0.0]), np.array([0.6, 3.5, 1.0, 0.5])),
+    1: (np.array([0.2, 0.0, 0.0, 0.0]), np.array([1.0, 6.5, 1.0, 0.8])),
+}
+
+
+def make_tip_emulators(n_train: int = 500, seed: int = 0):
+    """Two JRC-TIP band emulators (VIS, NIR), 4 inputs each."""
+    ems = []
+    for band in (0, 1):
+        lo, hi = TIP_RANGES[band]
+        ems.append(GaussianProcessEmulator.synthetic(tip_bhr_target(band), lo, hi, n_train, seed + band,
+                                                     name=f"tip_{'vis' if band == 0 else 'nir'}"))
+    return ems
+
+
+def make_prosail_emulators(n_bands: int = 10, n_train: int = 250, seed: int = 0, n_params: int = 10):
+    """Per-band PROSAIL-like emulators over the 10 transformed parameters."""
+    from .priors import sail_prior
+
+    mean, covar, _ = sail_prior()
+    sig = np.sqrt(np.diag(covar))
+    lo = mean - 3 * np.maximum(sig, 0.05)
+    hi = mean + 3 * np.maximum(sig, 0.05)
+    return [GaussianProcessEmulator.synthetic(prosail_target(b, n_params), lo[:n_params], hi[:n_params], n_train,
+                                              seed + b, name=f"prosail_b{b}") for b in range(n_bands)]

@@ -1,0 +1,293 @@
+"""Torch-facing wrappers of the gfx950 kernels (``csrc/kf_kernels.hip``).
+
+Every op takes SoA tensors — state ``[n_p, ld]``, packed symmetric blocks
+``[n_p(n_p+1)/2, ld]``, per-pixel vectors ``[N]`` — validates shape, dtype,
+device and contiguity on the host (the kernels trust their arguments), and
+launches on the current HIP stream of the tensors' device.  CPU tensors run
+the identical per-pixel source through the OpenMP host runner.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ..utils.blocks import ntri
+from . import _ext
+
+OBS_NONE, OBS_F32, OBS_DN16 = 0, 1, 2
+ST_NONSPD, ST_NONFINITE, ST_BAD_OP, ST_NO_OBS, ST_FALLBACK = 1, 2, 4, 8, 16
+SUPPORTED_NP = (1, 2, 3, 4, 7, 10)
+
+
+def ext():
+    return _ext.require_ext()
+
+
+def _ptr(t):
+    return 0 if t is None else int(t.data_ptr())
+
+
+def _dev(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+def _stream(t: torch.Tensor) -> int:
+    return int(torch.cuda.current_stream(t.device).cuda_stream) if _dev(t) else 0
+
+
+def _check_soa(t, rows, N, name, dtype=torch.float32, device=None):
+    if t is None:
+        return
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if t.dim() != 2 or t.shape[0] != rows or t.shape[1] < N:
+        raise ValueError(f"{name}: expected [{rows}, >={N}], got {tuple(t.shape)}")
+    if t.stride(1) != 1 or t.stride(0) != t.shape[1]:
+        raise ValueError(f"{name}: must be a contiguous [rows, ld] tensor")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name}: on {t.device}, expected {device}")
+
+
+def _check_vec(t, N, name, dtype, device):
+    if t is None:
+        return
+    if t.dtype != dtype or t.dim() != 1 or t.shape[0] < N or not t.is_contiguous():
+        raise ValueError(f"{name}: expected contiguous {dtype}[>={N}], got {t.dtype}{tuple(t.shape)}")
+    if t.device != device:
+        raise ValueError(f"{name}: on {t.device}, expected {device}")
+
+
+def check_np(n_params: int):
+    if n_params not in SUPPORTED_NP:
+        raise ValueError(f"n_params={n_params} has no compiled kernel (supported: {SUPPORTED_NP}); "
+                         "pad the state (engine.padding) to a supported size")
+
+
+def grid_for(N: int) -> int:
+    return int(ext().grid(int(N)))
+
+
+def partials_buffer(N: int, device) -> torch.Tensor:
+    return torch.zeros(grid_for(N), dtype=torch.float64, device=device)
+
+
+@dataclass
+class BandTable:
+    """Packed ``BandDesc`` array resident on the target device plus the tensors
+    it points into (kept alive as long as the table)."""
+    buf: torch.Tensor
+    n: int
+    keepalive: tuple
+
+    @property
+    def ptr(self) -> int:
+        return int(self.buf.data_ptr())
+
+
+def make_band_table(descs: list, device, keepalive=()) -> BandTable:
+    raw = ext().pack_band_descs(descs)
+    cpu = torch.frombuffer(bytearray(raw), dtype=torch.uint8) if raw else torch.zeros(8, dtype=torch.uint8)
+    buf = cpu.to(device) if torch.device(device).type == "cuda" else cpu.clone()
+    return BandTable(buf, len(descs), tuple(keepalive))
+
+
+# ------------------------------------------------------------------ ops
+def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=None, b_out=None, status=None,
+             partials=None, N=None, solve=True):
+    """K1 fused Gauss-Newton analysis (information form)."""
+    check_np(n_params)
+    N = int(x_prev.shape[1] if N is None else N)
+    dev = x_prev.device
+    nt = ntri(n_params)
+    for t, r, nm in ((x_prev, n_params, "x_prev"), (x_f, n_params, "x_f"), (pf_inv, nt, "pf_inv"),
+                     (x_out, n_params, "x_out"), (a_out, nt, "a_out"), (b_out, n_params, "b_out")):
+        _check_soa(t, r, N, nm, device=dev)
+    ld = x_prev.shape[1]
+    for t in (x_f, pf_inv, x_out, a_out, b_out):
+        if t is not None and t.shape[1] != ld:
+            raise ValueError("all SoA operands must share the leading dimension")
+    if solve and x_out is None:
+        raise ValueError("solve=True needs x_out")
+    _check_vec(status, N, "status", torch.uint8, dev)
+    if partials is not None and (partials.dtype != torch.float64 or partials.numel() < grid_for(N)):
+        raise ValueError("partials must be float64 with >= grid_for(N) entries")
+    a = ext().AnalysisArgs()
+    a.N, a.ld, a.n_bands, a.solve = N, ld, bands.n, int(bool(solve))
+    a.bands = bands.ptr
+    a.x_prev, a.x_f, a.pf_inv = _ptr(x_prev), _ptr(x_f), _ptr(pf_inv)
+    a.x_out, a.a_out, a.b_out = _ptr(x_out), _ptr(a_out), _ptr(b_out)
+    a.status, a.partials = _ptr(status), _ptr(partials)
+    grid = grid_for(N)
+    ext().analysis(n_params, a, grid, _dev(x_prev), _stream(x_prev))
+    return partials
+
+
+def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out, status=None, partials=None, N=None,
+         joseph=False):
+    """K1g covariance/gain-form analysis (sequential scalar band updates)."""
+    check_np(n_params)
+    N = int(x_prev.shape[1] if N is None else N)
+    dev = x_prev.device
+    nt = ntri(n_params)
+    for t, r, nm in ((x_prev, n_params, "x_prev"), (x_f, n_params, "x_f"), (p_f, nt, "p_f"),
+                     (x_out, n_params, "x_out"), (p_out, nt, "p_out")):
+        _check_soa(t, r, N, nm, device=dev)
+    _check_vec(status, N, "status", torch.uint8, dev)
+    a = ext().GainArgs()
+    a.N, a.ld, a.n_bands, a.joseph = N, x_prev.shape[1], bands.n, int(bool(joseph))
+    a.bands = bands.ptr
+    a.x_prev, a.x_f, a.p_f, a.x_out, a.p_out = map(_ptr, (x_prev, x_f, p_f, x_out, p_out))
+    a.status, a.partials = _ptr(status), _ptr(partials)
+    ext().gain(n_params, a, grid_for(N), _dev(x_prev), _stream(x_prev))
+    return partials
+
+
+def jacobi(n_params, a_in, b_in, x_ext, nbr, x_ref, x_out, gamma, reg_mask, N, a_out=None, partials=None):
+    """K9 block-Jacobi sweep of the GMRF spatial regulariser."""
+    check_np(n_params)
+    dev = a_in.device
+    _check_soa(a_in, ntri(n_params), N, "a_in", device=dev)
+    _check_soa(b_in, n_params, N, "b_in", device=dev)
+    _check_soa(x_ref, n_params, N, "x_ref", device=dev)
+    _check_soa(x_out, n_params, N, "x_out", device=dev)
+    _check_soa(x_ext, n_params, N, "x_ext", device=dev)
+    if nbr.dtype != torch.int32 or nbr.shape != (4, N) or not nbr.is_contiguous():
+        raise ValueError("nbr must be contiguous int32 [4, N]")
+    a = ext().JacobiArgs()
+    a.N, a.ld, a.ld_ext = N, a_in.shape[1], x_ext.shape[1]
+    a.gamma, a.reg_mask = float(gamma), int(reg_mask)
+    a.a_in, a.b_in, a.x_ext, a.nbr, a.x_ref, a.x_out = map(_ptr, (a_in, b_in, x_ext, nbr, x_ref, x_out))
+    a.a_out, a.partials = _ptr(a_out), _ptr(partials)
+    ext().jacobi(n_params, a, grid_for(N), _dev(a_in), _stream(a_in))
+    return partials
+
+
+def propagate(n_params, spec: dict, x_a, p_a, x_f, p_f, N=None, status=None, q_pix=None,
+              blend_mean_pix=None, blend_cinv_pix=None):
+    """K4/K5 propagation (+ optional prior blend).  ``spec`` keys: mode, m, q,
+    prop_mask, reset_mean, reset_cinv (packed), blend, quirk_blend,
+    blend_mean, blend_cinv (packed)."""
+    check_np(n_params)
+    N = int(x_a.shape[1] if N is None else N)
+    dev = x_a.device
+    nt = ntri(n_params)
+    _check_soa(x_a, n_params, N, "x_a", device=dev)
+    _check_soa(p_a, nt, N, "p_a", device=dev)
+    _check_soa(x_f, n_params, N, "x_f", device=dev)
+    _check_soa(p_f, nt, N, "p_f", device=dev)
+    _check_soa(q_pix, n_params, N, "q_pix", device=dev)
+    _check_soa(blend_mean_pix, n_params, N, "blend_mean_pix", device=dev)
+    _check_soa(blend_cinv_pix, nt, N, "blend_cinv_pix", device=dev)
+    a = ext().PropArgs()
+    a.N, a.ld = N, x_a.shape[1]
+    a.mode = int(spec["mode"])
+    a.blend = int(bool(spec.get("blend", False)))
+    a.quirk_blend = int(bool(spec.get("quirk_blend", False)))
+    a.prop_mask = int(spec.get("prop_mask", 0))
+    a.m = [float(v) for v in spec.get("m", np.ones(n_params))]
+    a.q = [float(v) for v in spec.get("q", np.zeros(n_params))]
+    for key in ("reset_mean", "reset_cinv", "blend_mean", "blend_cinv"):
+        if spec.get(key) is not None:
+            setattr(a, key, [float(v) for v in np.asarray(spec[key]).ravel()])
+    a.x_a, a.p_a, a.x_f, a.p_f = map(_ptr, (x_a, p_a, x_f, p_f))
+    a.q_pix, a.blend_mean_pix, a.blend_cinv_pix = map(_ptr, (q_pix, blend_mean_pix, blend_cinv_pix))
+    a.status = _ptr(status)
+    ext().propagate(n_params, a, _dev(x_a), _stream(x_a))
+
+
+def invert(n_params, src, dst, N=None, status=None):
+    """Packed SPD inverse (covariance <-> precision)."""
+    check_np(n_params)
+    N = int(src.shape[1] if N is None else N)
+    _check_soa(src, ntri(n_params), N, "src")
+    _check_soa(dst, ntri(n_params), N, "dst", device=src.device)
+    if src.shape[1] != dst.shape[1]:
+        raise ValueError("src/dst leading dims differ")
+    ext().invert(n_params, _ptr(src), _ptr(dst), N, src.shape[1], _ptr(status), _dev(src), _stream(src))
+
+
+def operator_eval(n_params, bands: BandTable, band: int, x, h0, h=None, ok=None, N=None):
+    """Evaluate one band's operator and Jacobian at x (standalone K2/K3)."""
+    check_np(n_params)
+    N = int(x.shape[1] if N is None else N)
+    _check_soa(x, n_params, N, "x")
+    _check_vec(h0, N, "h0", torch.float32, x.device)
+    _check_soa(h, n_params, N, "h", device=x.device)
+    _check_vec(ok, N, "ok", torch.uint8, x.device)
+    if not 0 <= band < bands.n:
+        raise IndexError("band out of range")
+    ext().operator_eval(n_params, bands.ptr, band, _ptr(x), N, x.shape[1], _ptr(h0), _ptr(h),
+                        0 if h is None else h.shape[1], _ptr(ok), _dev(x), _stream(x))
+
+
+def hessian(n_params, bands: BandTable, x, a, N=None):
+    """K6: A -= sum_b w (y - f) d2f/dx2 over GP bands (in place)."""
+    check_np(n_params)
+    N = int(x.shape[1] if N is None else N)
+    _check_soa(x, n_params, N, "x")
+    _check_soa(a, ntri(n_params), N, "a", device=x.device)
+    ext().hessian(n_params, bands.ptr, bands.n, _ptr(x), _ptr(a), N, x.shape[1], _dev(x), _stream(x))
+
+
+def unpack(n_params, x, a, mean=None, unc=None, idx=None, N=None):
+    """Scatter mean and 1/sqrt(diag(P^-1)) onto raster planes [n_p, H*W]."""
+    check_np(n_params)
+    N = int(x.shape[1] if N is None else N)
+    _check_soa(x, n_params, N, "x")
+    if unc is not None:
+        _check_soa(a, ntri(n_params), N, "a", device=x.device)
+    plane = (mean if mean is not None else unc).shape[1]
+    for t in (mean, unc):
+        if t is not None:
+            _check_soa(t, n_params, 0, "out", device=x.device)
+    if idx is not None:
+        _check_vec(idx, N, "idx", torch.int64, x.device)
+    elif plane < N:
+        raise ValueError("output plane smaller than N without an index map")
+    ext().unpack(n_params, _ptr(x), _ptr(a), N, x.shape[1], _ptr(idx), _ptr(mean), _ptr(unc), plane, _dev(x),
+                 _stream(x))
+
+
+def reduce_partials(partials: torch.Tensor, out: torch.Tensor | None = None):
+    """Fixed-order f64 sum of per-block partials (device: one-wave kernel)."""
+    if _dev(partials):
+        if out is None:
+            out = torch.empty(1, dtype=torch.float64, device=partials.device)
+        ext().reduce_partials(_ptr(partials), int(partials.numel()), _ptr(out), _stream(partials))
+        return out
+    val = float(np.sum(partials.numpy()))
+    if out is None:
+        return torch.tensor([val], dtype=torch.float64)
+    out.fill_(val)
+    return out
+
+
+def gather(src, idx, out=None, rows=None):
+    """out[r, p] = src[r, idx[p]] (compaction of raster rows onto active pixels)."""
+    if src.dim() == 1:
+        src2, squeeze = src.view(1, -1), True
+    else:
+        src2, squeeze = src, False
+    n = idx.numel()
+    if out is None:
+        out = torch.empty((src2.shape[0], n), dtype=src.dtype, device=src.device)
+    if not _dev(src):
+        out.view(src2.shape[0], -1)[:, :n] = src2[:, idx]
+        return out.view(-1) if squeeze else out
+    eb = src.element_size()
+    ext().gather(eb, _ptr(src2), _ptr(idx), _ptr(out), n, src2.shape[0], src2.stride(0),
+                 out.view(src2.shape[0], -1).stride(0), _stream(src))
+    return out.view(-1) if squeeze else out
+
+
+def lut_nearest(lut, x, out=None, N=None):
+    """K7 nearest LUT row for every pixel (x as [D, ld])."""
+    N = int(x.shape[1] if N is None else N)
+    lut = lut.contiguous()
+    M, D = lut.shape
+    if out is None:
+        out = torch.empty(N, dtype=torch.int32, device=x.device)
+    ext().lut_nearest(_ptr(lut), M, D, _ptr(x), N, x.shape[1], _ptr(out), _dev(x), _stream(x))
+    return out

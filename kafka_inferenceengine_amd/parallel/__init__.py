@@ -1,0 +1,3 @@
+"""Tile data parallelism over row strips with RCCL collectives (one process per GPU)."""
+from .comm import Comm  # noqa: F401
+from .partition import StripPartition, strip_bounds  # noqa: F401

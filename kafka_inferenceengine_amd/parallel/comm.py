@@ -1,0 +1,143 @@
+"""Communication layer: one process per GPU, ``torch.distributed`` over RCCL.
+
+Collectives used by the engine (SURVEY.md §2.7 C1–C4):
+  C1  deterministic global sum of the Gauss-Newton convergence partials —
+      ``all_gather`` of one f64 per rank, summed in rank order on every rank
+      (bit-identical decision everywhere; the reference's criterion is global
+      over the chunk, ``linear_kf.py:293``);
+  C2  halo exchange with the ±1 strip neighbours (``batch_isend_irecv``,
+      point-to-point — one xGMI link per direction);
+  C3  gather of output strips to rank 0 (optional);
+  C4  broadcast of setup objects.
+Backend ``nccl`` is RCCL on ROCm; ``gloo`` is only the CPU test harness.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self, rank: int = 0, world: int = 1, device=None, group=None):
+        self.rank = rank
+        self.world = world
+        self.group = group
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+
+    # ------------------------------------------------------------ setup
+    @classmethod
+    def single(cls, device=None) -> "Comm":
+        return cls(0, 1, device)
+
+    @classmethod
+    def from_env(cls, device=None, backend: str | None = None, timeout_s: float = 600.0) -> "Comm":
+        """Initialise from torchrun env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        if world <= 1 and not dist.is_initialized():
+            return cls.single(device)
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if device is None:
+            if torch.cuda.is_available():
+                torch.cuda.set_device(local)
+                device = torch.device("cuda", local)
+            else:
+                device = torch.device("cpu")
+        device = torch.device(device)
+        if not dist.is_initialized():
+            backend = backend or ("nccl" if device.type == "cuda" else "gloo")
+            kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+            if backend == "nccl":
+                kw["device_id"] = device
+            dist.init_process_group(**kw)
+        return cls(dist.get_rank(), dist.get_world_size(), device)
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+    # ----------------------------------------------------- collectives
+    def sum_f64(self, local: torch.Tensor) -> float:
+        """C1: deterministic global sum of a 1-element f64 tensor."""
+        if not self.distributed:
+            return float(local.item())
+        local = local.reshape(1).to(torch.float64)
+        out = [torch.zeros_like(local) for _ in range(self.world)]
+        dist.all_gather(out, local, group=self.group)
+        vals = torch.cat(out).cpu().tolist()
+        total = 0.0
+        for v in vals:  # fixed rank order
+            total += v
+        return total
+
+    def sum_int(self, v: int) -> int:
+        if not self.distributed:
+            return int(v)
+        t = torch.tensor([int(v)], dtype=torch.int64, device=self.device)
+        dist.all_reduce(t, group=self.group)
+        return int(t.item())
+
+    def max_float(self, v: float) -> float:
+        if not self.distributed:
+            return float(v)
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+    def barrier(self):
+        if self.distributed:
+            if self.device.type == "cuda":
+                dist.barrier(group=self.group, device_ids=[self.device.index])
+            else:
+                dist.barrier(group=self.group)
+
+    def broadcast_object(self, obj, src: int = 0):
+        """C4: broadcast a picklable setup object from ``src`` (objects created by
+        this process only — never data read from untrusted files)."""
+        if not self.distributed:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src, group=self.group)
+        return lst[0]
+
+    def exchange_halo(self, send_up: torch.Tensor | None, send_down: torch.Tensor | None,
+                      recv_up: torch.Tensor | None, recv_down: torch.Tensor | None):
+        """C2: send my first rows to rank-1 / last rows to rank+1 and receive their
+        boundary rows.  Empty tensors are skipped consistently on both sides."""
+        if not self.distributed:
+            return
+        ops = []
+        if self.rank > 0:
+            if send_up is not None and send_up.numel():
+                ops.append(dist.P2POp(dist.isend, send_up.contiguous(), self.rank - 1, group=self.group))
+            if recv_up is not None and recv_up.numel():
+                ops.append(dist.P2POp(dist.irecv, recv_up, self.rank - 1, group=self.group))
+        if self.rank < self.world - 1:
+            if send_down is not None and send_down.numel():
+                ops.append(dist.P2POp(dist.isend, send_down.contiguous(), self.rank + 1, group=self.group))
+            if recv_down is not None and recv_down.numel():
+                ops.append(dist.P2POp(dist.irecv, recv_down, self.rank + 1, group=self.group))
+        if ops:
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+
+    def gather_to_root(self, t: torch.Tensor, sizes: list[int]):
+        """C3: gather variable-length pixel blocks [rows, n_i] onto rank 0."""
+        if not self.distributed:
+            return t
+        rows = t.shape[0]
+        maxn = max(sizes)
+        pad = torch.zeros((rows, maxn), dtype=t.dtype, device=t.device)
+        pad[:, :t.shape[1]] = t
+        out = [torch.zeros_like(pad) for _ in range(self.world)] if self.rank == 0 else None
+        dist.gather(pad, out, dst=0, group=self.group)
+        if self.rank != 0:
+            return None
+        return torch.cat([o[:, :n] for o, n in zip(out, sizes)], dim=1)
+
+    def destroy(self):
+        if self.distributed and dist.is_initialized():
+            dist.destroy_process_group()

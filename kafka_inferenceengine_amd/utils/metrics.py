@@ -1,0 +1,75 @@
+"""Metrics and timers.
+
+* ``MetricsLogger`` — structured JSONL per date / timestep (GN iterations,
+  convergence norms, per-phase ms, wall time), one file per rank.
+* ``PhaseTimer`` — hipEvent-based (``torch.cuda.Event``) per-phase timing on
+  the compute stream; host clock on CPU.  Non-synchronising by default: the
+  event pairs are resolved lazily in ``snapshot()``.
+"""
+from __future__ import annotations
+
+import contextlib
+import json
+import os
+import time
+from collections import defaultdict
+
+import torch
+
+
+class MetricsLogger:
+    def __init__(self, path=None, rank: int = 0):
+        self.path = None
+        self.records = []
+        if path:
+            root, ext = os.path.splitext(str(path))
+            self.path = f"{root}.rank{rank}{ext or '.jsonl'}" if rank else str(path)
+            os.makedirs(os.path.dirname(os.path.abspath(self.path)), exist_ok=True)
+        self.rank = rank
+
+    def log(self, rec: dict):
+        rec = {"rank": self.rank, "t": time.time(), **rec}
+        self.records.append(rec)
+        if self.path:
+            with open(self.path, "a") as f:
+                f.write(json.dumps(rec, default=str) + "\n")
+
+
+class PhaseTimer:
+    def __init__(self, device, sync: bool = False):
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.sync = sync
+        self._pending = []
+        self.totals = defaultdict(float)
+
+    @contextlib.contextmanager
+    def phase(self, name: str):
+        if self.cuda:
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            try:
+                yield
+            finally:
+                e.record()
+                self._pending.append((name, s, e))
+                if self.sync:
+                    e.synchronize()
+        else:
+            t0 = time.perf_counter()
+            try:
+                yield
+            finally:
+                self.totals[name] += 1e3 * (time.perf_counter() - t0)
+
+    def snapshot(self, reset: bool = True) -> dict:
+        if self._pending:
+            self._pending[-1][2].synchronize()
+            for name, s, e in self._pending:
+                self.totals[name] += s.elapsed_time(e)
+            self._pending = []
+        out = {k: round(v, 3) for k, v in self.totals.items()}
+        if reset:
+            self.totals = defaultdict(float)
+        return out

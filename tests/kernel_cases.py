@@ -1,0 +1,81 @@
+"""Random problem instances shared by the host-runner and GPU kernel tests."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+import kafka_inferenceengine_amd as k
+from kafka_inferenceengine_amd.engine.bands import DeviceBand, RecordCache, build_table, operator_table
+from kafka_inferenceengine_amd.ops import kernels as K
+from kafka_inferenceengine_amd.utils.blocks import pack_blocks
+
+
+def spd_blocks(rng, N, n, scale=10.0):
+    A = rng.normal(size=(N, n, n))
+    return np.einsum("nij,nkj->nik", A, A) + scale * np.eye(n)[None]
+
+
+def tip_problem(N=3000, seed=0, n_train=64, dn16=False, mask_frac=0.2):
+    """7-param TIP state, 2 GP bands; returns numpy inputs + descriptors factory."""
+    rng = np.random.default_rng(seed)
+    ems = k.make_tip_emulators(n_train=n_train, seed=seed)
+    mu, P, Pi = k.tip_prior()
+    x = mu[None, :] + rng.normal(size=(N, 7)) * np.sqrt(np.diag(P)) * 0.3
+    x[:, 6] = np.clip(x[:, 6], 0.05, 0.95)
+    xf = mu[None, :] + rng.normal(size=(N, 7)) * 0.01
+    Pf = np.broadcast_to(Pi, (N, 7, 7)) + 0.0
+    specs = [k.gp_spec(ems[b], k.TIP_BAND_MAPPER[b]) for b in range(2)]
+    bands_np = []
+    raw = []
+    for b in range(2):
+        H, _ = ems[b].predict(x[:, k.TIP_BAND_MAPPER[b]])
+        y = np.clip(H + rng.normal(size=N) * 0.01, 0.01, 1.0)
+        valid = rng.random(N) > mask_frac
+        if dn16:
+            dn = np.where(valid, np.clip(np.round(y / 1e-4), 1, 65535), 0).astype(np.int32)
+            yy = dn * 1e-4
+            sig = np.maximum(0.05 * yy, 2.5e-3)
+            w = np.where(dn > 0, 1 / sig ** 2, 0.0)
+            raw.append(dict(dn=np.where(dn > 32767, dn - 65536, dn).astype(np.int16)))
+            yv = np.where(dn > 0, yy, 0.0)
+        else:
+            w = np.where(valid, 1 / 0.01 ** 2, 0.0)
+            raw.append(dict(y=y.astype(np.float32), w=w.astype(np.float32)))
+            yv = y
+        bands_np.append((yv, w))
+    return dict(x=x, xf=xf, Pf=Pf, specs=specs, ems=ems, bands=bands_np, raw=raw, dn16=dn16, N=N, n=7)
+
+
+def device_bands(prob, device):
+    obs = []
+    for r in prob["raw"]:
+        if prob["dn16"]:
+            obs.append(DeviceBand(K.OBS_DN16, dn=torch.from_numpy(r["dn"]).to(device), scale=1e-4, rel_unc=0.05,
+                                  unc_floor=2.5e-3))
+        else:
+            obs.append(DeviceBand(K.OBS_F32, y=torch.from_numpy(r["y"]).to(device),
+                                  w=torch.from_numpy(r["w"]).to(device)))
+    return obs
+
+
+def table(prob, device, h0_outs=None):
+    return build_table(prob["specs"], device_bands(prob, device), prob["n"], RecordCache(), device, h0_outs)
+
+
+def soa(a, device):
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(a).T, dtype=np.float32)).to(device)
+
+
+def packed(blocks, device):
+    return torch.from_numpy(np.ascontiguousarray(pack_blocks(blocks), dtype=np.float32)).to(device)
+
+
+def oracle_bands(prob, x_lin):
+    out = []
+    for b, (y, w) in enumerate(prob["bands"]):
+        mp = k.TIP_BAND_MAPPER[b]
+        H, dH = prob["ems"][b].predict(x_lin[:, mp])
+        h = np.zeros((prob["N"], prob["n"]))
+        h[:, mp] = dH
+        out.append((H, h, y, w))
+    return out

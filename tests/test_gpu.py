@@ -1,0 +1,155 @@
+"""HIP kernels on an MI355X: each compared with the host runner of the same
+source, the float64 oracle, or a plain PyTorch fp32 reference."""
+import datetime as dt
+
+import numpy as np
+import pytest
+import torch
+
+import kafka_inferenceengine_amd as k
+from kafka_inferenceengine_amd.inference import analysis_blocks
+from kafka_inferenceengine_amd.ops import kernels as K
+from kafka_inferenceengine_amd.utils.blocks import unpack_blocks
+
+import kernel_cases as C
+
+pytestmark = pytest.mark.gpu
+
+
+def _analysis(prob, device):
+    N, n = prob["N"], prob["n"]
+    tab = C.table(prob, device)
+    xo = torch.zeros((n, N), device=device)
+    ao = torch.zeros((28, N), device=device)
+    st = torch.zeros(N, dtype=torch.uint8, device=device)
+    part = K.partials_buffer(N, device)
+    K.analysis(n, tab, C.soa(prob["x"], device), C.soa(prob["xf"], device), C.packed(prob["Pf"], device), xo, ao,
+               None, st, part)
+    red = K.reduce_partials(part)
+    return xo.cpu(), ao.cpu(), st.cpu(), float(red.cpu().item())
+
+
+def test_native_extension_is_loaded(cuda):
+    from kafka_inferenceengine_amd.ops import ext_path
+    assert ext_path() is not None and ext_path().endswith(".so")
+
+
+@pytest.mark.parametrize("dn16", [False, True])
+def test_analysis_device_vs_host_and_oracle(cuda, dn16):
+    prob = C.tip_problem(N=20000, dn16=dn16, seed=11)
+    xd, ad, sd, rd = _analysis(prob, cuda)
+    xh, ah, sh, rh = _analysis(prob, "cpu")
+    assert torch.equal(sd, sh)
+    assert torch.allclose(xd, xh, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(ad, ah, rtol=1e-5, atol=1e-3)
+    assert abs(rd - rh) / rh < 1e-4
+    xr, Ar = analysis_blocks(prob["x"], prob["xf"], prob["Pf"], C.oracle_bands(prob, prob["x"]))
+    assert np.max(np.abs(xd.numpy().T - xr) / (np.abs(xr) + 0.05)) < 2e-3
+
+
+def test_propagate_and_invert_device(cuda):
+    rng = np.random.default_rng(1)
+    N, n = 5000, 7
+    A = C.spd_blocks(rng, N, n)
+    xa = rng.normal(size=(N, n))
+    mu, _, Pi = k.tip_prior()
+    from kafka_inferenceengine_amd.utils.blocks import pack_matrix
+    for mode in range(6):
+        spec = {"mode": mode, "m": np.ones(n), "q": np.full(n, 0.05), "prop_mask": 1 << 6, "reset_mean": mu,
+                "reset_cinv": pack_matrix(Pi), "blend": mode != 4, "blend_mean": mu, "blend_cinv": pack_matrix(Pi)}
+        outs = []
+        for dev in (cuda, "cpu"):
+            xf = torch.zeros((n, N), device=dev)
+            pf = torch.zeros((28, N), device=dev)
+            K.propagate(n, spec, C.soa(xa, dev), C.packed(A, dev), xf, pf)
+            outs.append((xf.cpu(), pf.cpu()))
+        assert torch.allclose(outs[0][0], outs[1][0], rtol=1e-4, atol=1e-5), mode
+        assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-4), mode
+    out = torch.zeros((28, N), device=cuda)
+    K.invert(n, C.packed(A, cuda), out)
+    ref = torch.linalg.inv(torch.tensor(A, dtype=torch.float32))
+    assert torch.allclose(torch.tensor(unpack_blocks(out.cpu().numpy(), n)), ref, rtol=1e-4, atol=1e-6)
+
+
+def test_gain_jacobi_hessian_unpack_device(cuda):
+    prob = C.tip_problem(N=4000, seed=12)
+    n, N = 7, 4000
+    res = []
+    for dev in (cuda, "cpu"):
+        tab = C.table(prob, dev)
+        Pcov = np.linalg.inv(prob["Pf"])
+        xo = torch.zeros((n, N), device=dev)
+        po = torch.zeros((28, N), device=dev)
+        K.gain(n, tab, C.soa(prob["x"], dev), C.soa(prob["xf"], dev), C.packed(Pcov, dev), xo, po)
+        a = C.packed(prob["Pf"], dev)
+        K.hessian(n, tab, C.soa(prob["x"], dev), a)
+        mean = torch.zeros((n, N), device=dev)
+        unc = torch.zeros((n, N), device=dev)
+        K.unpack(n, xo, C.packed(prob["Pf"], dev), mean, unc)
+        res.append([t.cpu() for t in (xo, po, a, mean, unc)])
+    for d, h in zip(*res):
+        assert torch.allclose(d, h, rtol=2e-4, atol=1e-4)
+
+
+def test_operator_device_vs_numpy(cuda):
+    prob = C.tip_problem(N=10000, seed=13)
+    tab = C.table(prob, cuda)
+    xs = C.soa(prob["x"], cuda)
+    for b in range(2):
+        h0 = torch.zeros(10000, device=cuda)
+        h = torch.zeros((7, 10000), device=cuda)
+        K.operator_eval(7, tab, b, xs, h0, h)
+        H, dH = prob["ems"][b].predict(prob["x"][:, k.TIP_BAND_MAPPER[b]])
+        assert np.allclose(h0.cpu().numpy(), H, atol=5e-6)
+        full = np.zeros((10000, 7))
+        full[:, k.TIP_BAND_MAPPER[b]] = dH
+        assert np.allclose(h.cpu().numpy().T, full, atol=5e-5)
+
+
+def test_engine_gpu_matches_cpu(cuda):
+    mask = np.ones((48, 40), bool)
+    mask[:5, :6] = False
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
+    outs = []
+    for dev in (cuda, "cpu"):
+        obs = k.SyntheticBHRObservations(mask, n_train=100, device=dev, stream=True, n_pool=3, field_cell=8)
+        prior = k.JRCPrior(k.TIP_PARAMETERS, mask)
+        kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_nonlinear_observation_operator,
+                            k.TIP_PARAMETERS, device=dev)
+        kf.set_trajectory_model()
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        st = kf.run(grid, kf.state_from_prior(prior), None, None)
+        outs.append((st.x.cpu(), st.P.cpu(), [h.get("gn_iterations") for h in kf.history]))
+    assert outs[0][2] == outs[1][2]
+    assert torch.allclose(outs[0][0], outs[1][0], rtol=1e-3, atol=1e-4)
+    rowmax = outs[1][1].abs().amax(1, keepdim=True).clamp(min=1)
+    assert ((outs[0][1] - outs[1][1]).abs() / rowmax).max() < 1e-3
+
+
+def test_streamer_pinned_and_overlaps(cuda):
+    from kafka_inferenceengine_amd.input_output.streaming import DateStreamer
+    s = DateStreamer(3, (2, 1 << 20), torch.int16, cuda)
+    assert s.pinned
+    for kk in range(3):
+        s.host_view(kk).fill_(kk + 1)
+    a = s.acquire(0)
+    s.prefetch(1)
+    assert int(a[0, 0]) == 1
+    b = s.acquire(1)
+    assert int(b[1, -1]) == 2
+    c = s.acquire(2)
+    assert int(c.sum()) == 3 * 2 * (1 << 20)
+
+
+def test_spatial_regulariser_gpu_matches_cpu(cuda):
+    mask = np.ones((32, 32), bool)
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(3)]
+    outs = []
+    for dev in (cuda, "cpu"):
+        obs = k.SyntheticBHRObservations(mask, n_train=60, device=dev, stream=False, n_pool=2, field_cell=8)
+        kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device=dev,
+                            config=k.EngineConfig(spatial_gamma=20.0, spatial_params=[6]))
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
+        outs.append(st.x.cpu())
+    assert torch.allclose(outs[0], outs[1], rtol=1e-3, atol=1e-4)

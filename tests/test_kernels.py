@@ -1,0 +1,282 @@
+"""Kernel numerics against the float64 oracle and plain-PyTorch references.
+
+Every test runs on the CPU through the host runner (the same per-pixel source
+as the gfx950 kernels); the ``gpu``-marked twins in test_gpu.py run the HIP
+kernels and compare them to these references."""
+import numpy as np
+import pytest
+import torch
+
+import kafka_inferenceengine_amd as k
+from kafka_inferenceengine_amd.inference import analysis_blocks, gain_blocks
+from kafka_inferenceengine_amd.ops import kernels as K
+from kafka_inferenceengine_amd.utils.blocks import pack_blocks, pack_matrix, unpack_blocks
+
+import kernel_cases as C
+
+
+def _run_analysis(prob, device):
+    N, n = prob["N"], prob["n"]
+    tab = C.table(prob, device)
+    xo = torch.zeros((n, N), device=device)
+    ao = torch.zeros((28, N), device=device)
+    st = torch.zeros(N, dtype=torch.uint8, device=device)
+    part = K.partials_buffer(N, device)
+    K.analysis(n, tab, C.soa(prob["x"], device), C.soa(prob["xf"], device), C.packed(prob["Pf"], device), xo, ao,
+               None, st, part)
+    return xo.cpu().numpy().T, unpack_blocks(ao.cpu().numpy(), n), st.cpu().numpy(), K.reduce_partials(part).cpu()
+
+
+@pytest.mark.parametrize("dn16", [False, True])
+def test_analysis_vs_oracle(dn16):
+    prob = C.tip_problem(dn16=dn16)
+    xa, A, st, red = _run_analysis(prob, "cpu")
+    xr, Ar = analysis_blocks(prob["x"], prob["xf"], prob["Pf"], C.oracle_bands(prob, prob["x"]))
+    assert np.max(np.abs(xa - xr) / (np.abs(xr) + 0.05)) < 2e-3
+    assert np.max(np.abs(A - Ar)) / np.abs(Ar).max() < 1e-5
+    assert abs(red.item() - ((xr - prob["x"]) ** 2).sum()) / red.item() < 1e-3
+    nobs = np.array([(w > 0) for _, w in prob["bands"]]).sum(0)
+    assert np.all((st == K.ST_NO_OBS) == (nobs == 0))
+
+
+def test_analysis_vs_torch_fp32_reference():
+    """Plain PyTorch fp32 reference of the same op (batched normal equations)."""
+    prob = C.tip_problem(seed=1)
+    xa, A, _, _ = _run_analysis(prob, "cpu")
+    bands = C.oracle_bands(prob, prob["x"])
+    Pf = torch.tensor(prob["Pf"], dtype=torch.float32)
+    x0 = torch.tensor(prob["x"], dtype=torch.float32)
+    xf = torch.tensor(prob["xf"], dtype=torch.float32)
+    At = Pf.clone()
+    bt = (Pf @ xf[..., None])[..., 0]
+    for H0, h, y, w in bands:
+        h = torch.tensor(h, dtype=torch.float32)
+        w = torch.tensor(w, dtype=torch.float32)
+        yp = torch.tensor(y, dtype=torch.float32) + (h * x0).sum(1) - torch.tensor(H0, dtype=torch.float32)
+        At += w[:, None, None] * h[:, :, None] * h[:, None, :]
+        bt += (w * yp)[:, None] * h
+    xt = torch.linalg.solve(At, bt).numpy()
+    assert np.max(np.abs(xa - xt) / (np.abs(xt) + 0.05)) < 3e-3
+
+
+def test_nonspd_fallback_keeps_forecast():
+    prob = C.tip_problem(N=256, seed=2)
+    prob["Pf"] = prob["Pf"].copy()
+    prob["Pf"][:10] = -np.eye(7)[None]          # indefinite forecast precision
+    for bd in prob["raw"]:
+        bd["w"][:10] = 0.0
+    for i, (y, w) in enumerate(prob["bands"]):
+        w[:10] = 0.0
+    xa, A, st, _ = _run_analysis(prob, "cpu")
+    assert np.all(st[:10] & K.ST_FALLBACK)
+    assert np.allclose(xa[:10], prob["xf"][:10].astype(np.float32))
+    assert np.all(np.isfinite(xa))
+
+
+def test_gain_kernel_vs_oracle():
+    prob = C.tip_problem(seed=3)
+    N, n = prob["N"], prob["n"]
+    Pcov = np.linalg.inv(prob["Pf"])
+    tab = C.table(prob, "cpu")
+    xo = torch.zeros((n, N))
+    po = torch.zeros((28, N))
+    K.gain(n, tab, C.soa(prob["x"], "cpu"), C.soa(prob["xf"], "cpu"), C.packed(Pcov, "cpu"), xo, po)
+    xr, Pr = gain_blocks(prob["x"], prob["xf"], Pcov, C.oracle_bands(prob, prob["x"]))
+    xi, _ = analysis_blocks(prob["x"], prob["xf"], prob["Pf"], C.oracle_bands(prob, prob["x"]))
+    assert np.allclose(xr, xi, atol=1e-6)  # oracle: gain form == information form
+    assert np.max(np.abs(xo.numpy().T - xr) / (np.abs(xr) + 0.05)) < 2e-3
+    assert np.max(np.abs(unpack_blocks(po.numpy(), n) - Pr)) / np.abs(Pr).max() < 1e-3
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 7, 10])
+def test_invert(n):
+    rng = np.random.default_rng(n)
+    B = C.spd_blocks(rng, 500, n)
+    out = torch.zeros((n * (n + 1) // 2, 500))
+    K.invert(n, C.packed(B, "cpu"), out)
+    ref = torch.linalg.inv(torch.tensor(B, dtype=torch.float32)).numpy()
+    assert np.allclose(unpack_blocks(out.numpy(), n), ref, rtol=1e-4, atol=1e-6)
+
+
+def _prop(mode, n=7, N=400, blend=False, quirk=False, seed=0, prop_mask=0):
+    rng = np.random.default_rng(seed)
+    A = C.spd_blocks(rng, N, n, 5.0)
+    xa = rng.normal(size=(N, n))
+    mu, cov, Pi = k.tip_prior()
+    q = rng.uniform(0.01, 0.2, n)
+    m = rng.uniform(0.9, 1.1, n)
+    spec = {"mode": mode, "m": m, "q": q, "prop_mask": prop_mask, "reset_mean": mu, "reset_cinv": pack_matrix(Pi),
+            "blend": blend, "quirk_blend": quirk, "blend_mean": mu * 1.1, "blend_cinv": pack_matrix(Pi * 0.5)}
+    xf = torch.zeros((n, N))
+    pf = torch.zeros((28, N))
+    K.propagate(n, spec, C.soa(xa, "cpu"), C.packed(A, "cpu"), xf, pf)
+    return xa, A, mu, Pi, q, m, xf.numpy().T, unpack_blocks(pf.numpy(), n)
+
+
+def test_propagate_modes_vs_reference_api():
+    import scipy.sparse as sp
+    from kafka_inferenceengine_amd.inference import kf_tools as T
+    from kafka_inferenceengine_amd.utils.blocks import blocks_to_sparse, interleaved_to_soa, sparse_to_blocks
+
+    # exact information filter
+    xa, A, mu, Pi, q, m, xf, Pf = _prop(T.PROP_INFO_EXACT)
+    Q = sp.diags(np.tile(q, 400))
+    M = sp.diags(np.tile(m, 400))
+    xr, _, Pr = T.propagate_information_filter_SLOW(xa.ravel(), None, blocks_to_sparse(A), M, Q, n_params=7)
+    assert np.allclose(xf, xr.reshape(400, 7), rtol=1e-5)
+    assert np.allclose(Pf, sparse_to_blocks(Pr, 7, check=False), rtol=2e-3, atol=1e-3)
+    # diagonal approximation
+    xa, A, mu, Pi, q, m, xf, Pf = _prop(T.PROP_INFO_APPROX)
+    _, _, Pr = T.propagate_information_filter_approx_SLOW(xa.ravel(), None, blocks_to_sparse(A), M, Q)
+    assert np.allclose(Pf, sparse_to_blocks(Pr, 7, check=False), rtol=1e-5)
+    # LAI (partial prior reset)
+    xa, A, mu, Pi, q, m, xf, Pf = _prop(T.PROP_PRIOR_PARTIAL, prop_mask=1 << 6)
+    xr, _, Pr = T.propagate_information_filter_LAI(xa.ravel(), None, blocks_to_sparse(A), M, Q)
+    assert np.allclose(xf, xr.reshape(400, 7), rtol=1e-5)
+    assert np.allclose(Pf, sparse_to_blocks(Pr, 7, check=False), rtol=1e-5, atol=1e-4)
+    # standard (covariance form)
+    xa, A, mu, Pi, q, m, xf, Pf = _prop(T.PROP_STANDARD)
+    assert np.allclose(Pf, A + np.diag(q)[None], rtol=1e-6)
+    # prior reset
+    xa, A, mu, Pi, q, m, xf, Pf = _prop(T.PROP_PRIOR)
+    assert np.allclose(xf, mu[None]) and np.allclose(Pf, Pi[None], rtol=1e-5)
+
+
+@pytest.mark.parametrize("quirk", [False, True])
+def test_blend_vs_reference_api(quirk):
+    from kafka_inferenceengine_amd.inference import kf_tools as T
+    from kafka_inferenceengine_amd.utils.blocks import blocks_to_sparse, sparse_to_blocks
+
+    xa, A, mu, Pi, q, m, xf, Pf = _prop(T.PROP_IDENTITY, blend=True, quirk=quirk)
+    N = xa.shape[0]
+    xr, Cr = T.blend_prior(np.tile(mu * 1.1, N), blocks_to_sparse(np.broadcast_to(Pi * 0.5, (N, 7, 7)).copy()),
+                           (xa * m).ravel(), blocks_to_sparse(A), quirk=quirk, n_params=7)
+    assert np.allclose(xf, xr.reshape(N, 7), rtol=2e-3, atol=2e-4)
+    assert np.allclose(Pf, sparse_to_blocks(Cr, 7, check=False), rtol=1e-5)
+
+
+def test_operator_gp_sar_linear_vs_numpy():
+    prob = C.tip_problem(N=800, seed=4)
+    tab = C.table(prob, "cpu")
+    xs = C.soa(prob["x"], "cpu")
+    for b in range(2):
+        h0 = torch.zeros(800)
+        h = torch.zeros((7, 800))
+        K.operator_eval(7, tab, b, xs, h0, h)
+        H, dH = prob["ems"][b].predict(prob["x"][:, k.TIP_BAND_MAPPER[b]])
+        full = np.zeros((800, 7))
+        full[:, k.TIP_BAND_MAPPER[b]] = dH
+        assert np.allclose(h0.numpy(), H, atol=5e-6)
+        assert np.allclose(h.numpy().T, full, atol=5e-5)
+    # SAR
+    from kafka_inferenceengine_amd.engine.bands import RecordCache, operator_table
+    from kafka_inferenceengine_amd.models.operators import _sar_device_spec
+    rng = np.random.default_rng(5)
+    x = np.stack([rng.uniform(0.2, 5, 600), rng.uniform(0.05, 0.45, 600)], 1)
+    th = torch.tensor(rng.uniform(25, 45, 600), dtype=torch.float32)
+    specs = [_sar_device_spec(2, None, None, b) for b in range(2)]
+    tab = operator_table(specs, 2, RecordCache(), "cpu", aux=th)
+    for b, pol in enumerate(("VV", "VH")):
+        h0 = torch.zeros(600)
+        h = torch.zeros((2, 600))
+        K.operator_eval(2, tab, b, C.soa(x, "cpu"), h0, h)
+        s0, g = k.sar_observation_operator(x, th.numpy().astype(np.float64), pol)
+        assert np.allclose(h0.numpy(), s0, rtol=2e-5)
+        assert np.allclose(h.numpy().T, g, rtol=2e-4, atol=1e-7)
+    # linear
+    lin = k.models.operators._linear_device_spec(4, k.LinearOperator(np.array([0.5, -1., 2., 0.]), 0.3), None, 0)
+    tab = operator_table([lin], 4, RecordCache(), "cpu")
+    x = rng.normal(size=(100, 4))
+    h0 = torch.zeros(100)
+    K.operator_eval(4, tab, 0, C.soa(x, "cpu"), h0)
+    assert np.allclose(h0.numpy(), 0.3 + x @ np.array([0.5, -1., 2., 0.]), atol=1e-5)
+
+
+def test_hessian_vs_numpy():
+    prob = C.tip_problem(N=300, seed=6)
+    tab = C.table(prob, "cpu")
+    a = torch.zeros((28, 300))
+    K.hessian(7, tab, C.soa(prob["x"], "cpu"), a)
+    ref = np.zeros((300, 7, 7))
+    for b, (y, w) in enumerate(prob["bands"]):
+        mp = k.TIP_BAND_MAPPER[b]
+        f, _ = prob["ems"][b].predict(prob["x"][:, mp])
+        Hs = prob["ems"][b].hessian(prob["x"][:, mp])
+        ref[np.ix_(np.arange(300), mp, mp)] -= (w * (y - f))[:, None, None] * Hs
+    got = unpack_blocks(a.numpy(), 7)
+    assert np.max(np.abs(got - ref)) / (np.abs(ref).max() + 1e-9) < 2e-3
+
+
+def test_gp_hessian_finite_difference():
+    em = k.make_tip_emulators(n_train=40)[0]
+    x = np.array([[0.3, 1.2, 0.4, 0.2]])
+    Hs = em.hessian(x)[0]
+    eps = 1e-5
+    for j in range(4):
+        e = np.zeros(4)
+        e[j] = eps
+        gp = em.predict(x + e)[1][0]
+        gm = em.predict(x - e)[1][0]
+        assert np.allclose((gp - gm) / (2 * eps), Hs[:, j], rtol=1e-4, atol=1e-6)
+
+
+def test_unpack_and_gather_and_lut():
+    rng = np.random.default_rng(7)
+    N = 200
+    x = rng.normal(size=(N, 7))
+    A = C.spd_blocks(rng, N, 7)
+    idx = torch.tensor(np.sort(rng.choice(400, N, replace=False)), dtype=torch.int64)
+    mean = torch.zeros((7, 400))
+    unc = torch.zeros((7, 400))
+    K.unpack(7, C.soa(x, "cpu"), C.packed(A, "cpu"), mean, unc, idx=idx)
+    assert np.allclose(mean.numpy()[:, idx.numpy()], x.T.astype(np.float32))
+    assert np.allclose(unc.numpy()[:, idx.numpy()], 1 / np.sqrt(np.einsum("nii->ni", A)).T, rtol=1e-6)
+    src = torch.arange(1000, dtype=torch.float32)
+    g = K.gather(src, idx)
+    assert torch.equal(g, src[idx])
+    lut = torch.tensor(rng.normal(size=(50, 3)), dtype=torch.float32)
+    pts = torch.tensor(rng.normal(size=(3, 300)), dtype=torch.float32)
+    got = K.lut_nearest(lut, pts)
+    ref = torch.cdist(pts.T, lut).argmin(1)
+    assert torch.equal(got.long(), ref)
+
+
+def test_jacobi_sweep_vs_numpy():
+    from kafka_inferenceengine_amd.parallel import StripPartition
+    rng = np.random.default_rng(8)
+    mask = rng.random((12, 9)) > 0.2
+    part = StripPartition(mask)
+    N, n = part.N, 4
+    A = C.spd_blocks(rng, N, n)
+    b = rng.normal(size=(N, n))
+    x = rng.normal(size=(N, n))
+    nbr = torch.from_numpy(part.neighbour_table())
+    out = torch.zeros((n, N))
+    gamma, regmask = 3.0, 0b0101
+    K.jacobi(n, C.packed(A, "cpu"), C.soa(b, "cpu"), C.soa(x, "cpu"), nbr, C.soa(x, "cpu"), out, gamma, regmask, N)
+    nb = nbr.numpy()
+    ref = np.zeros((N, n))
+    for p in range(N):
+        Ap, bp = A[p].copy(), b[p].copy()
+        qs = [q for q in nb[:, p] if q >= 0]
+        for j in range(n):
+            if (regmask >> j) & 1:
+                Ap[j, j] += gamma * len(qs)
+                bp[j] += gamma * sum(x[q, j] for q in qs)
+        ref[p] = np.linalg.solve(Ap, bp)
+    assert np.allclose(out.numpy().T, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_neighbour_table_matches_raster():
+    from kafka_inferenceengine_amd.parallel import StripPartition
+    rng = np.random.default_rng(9)
+    mask = rng.random((10, 7)) > 0.3
+    part = StripPartition(mask)
+    nb = part.neighbour_table()
+    lid = -np.ones(mask.shape, dtype=int)
+    lid[mask] = np.arange(mask.sum())
+    for p, flat in enumerate(part.local_idx):
+        r, c = divmod(flat, 7)
+        exp = [lid[r - 1, c] if r > 0 else -1, lid[r + 1, c] if r < 9 else -1,
+               lid[r, c - 1] if c > 0 else -1, lid[r, c + 1] if c < 6 else -1]
+        assert list(nb[:, p]) == exp
