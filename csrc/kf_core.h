@@ -130,6 +130,17 @@ KF_HD float kexp2(float x) {
 
 KF_HD bool finitef(float v) { return v - v == 0.f; }
 
+// Wave-uniform read-only data (band descriptors, GP training records) is read
+// through the constant address space so hipcc emits scalar s_load/s_buffer
+// loads into SGPRs (one fetch per wave, no VGPRs, no vector-memory traffic).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define KF_CONST_AS __attribute__((address_space(4)))
+#else
+#define KF_CONST_AS
+#endif
+template <typename T>
+KF_HD const KF_CONST_AS T* cptr(const T* p) { return (const KF_CONST_AS T*)(p); }
+
 // In-place packed Cholesky A = U^T U (U upper, stored in A's packed slots).
 template <int NP>
 KF_HD bool chol_packed(float (&A)[ntri(NP)]) {
@@ -241,11 +252,11 @@ KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&
 #pragma unroll
   for (int d = 0; d < D; ++d) S[d] = 0.f;
   constexpr int R = 2 * D + 2;
-  const float* __restrict__ r = bd.gp;
+  const KF_CONST_AS float* __restrict__ r = cptr(bd.gp);
   const int T = bd.T;
 #pragma unroll 4
   for (int i = 0; i < T; ++i) {
-    const float* __restrict__ ri = r + (int64_t)i * R;
+    const KF_CONST_AS float* __restrict__ ri = r + (int64_t)i * R;
     float e = ri[0] + c;
 #pragma unroll
     for (int d = 0; d < D; ++d) e = fmaf(ri[1 + d], xi[d], e);
@@ -355,7 +366,7 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
   }
   int nobs = 0;
   for (int bi = 0; bi < a.n_bands; ++bi) {
-    const BandDesc& bd = a.bands[bi];
+    const BandDesc bd = cptr(a.bands)[bi];
     float y, w;
     decode_obs(bd, p, y, w);
     if (!(w > 0.f)) {
@@ -566,7 +577,7 @@ KF_HD float pixel_gain(const GainArgs& a, int64_t p) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) P[t] = a.p_f[t * ld + p];
   for (int bi = 0; bi < a.n_bands; ++bi) {
-    const BandDesc& bd = a.bands[bi];
+    const BandDesc bd = cptr(a.bands)[bi];
     float y, w;
     decode_obs(bd, p, y, w);
     if (!(w > 0.f)) { if (bd.h0_out) bd.h0_out[p] = 0.f; continue; }
@@ -699,7 +710,7 @@ KF_HD void gp_hessian(const BandDesc& bd, const float (&x)[NP], float& f, float 
   for (int t = 0; t < ntri(D); ++t) S2[t] = 0.f;
   constexpr int R = 2 * D + 2;
   for (int i = 0; i < bd.T; ++i) {
-    const float* ri = bd.gp + (int64_t)i * R;
+    const KF_CONST_AS float* ri = cptr(bd.gp) + (int64_t)i * R;
     float e = ri[0] + c;
 #pragma unroll
     for (int d = 0; d < D; ++d) e = fmaf(ri[1 + d], xi[d], e);

@@ -86,7 +86,7 @@ template <int NP>
 __global__ __launch_bounds__(BLOCK) void operator_kernel(const BandDesc* bands, int band, const float* x,
                                                         int64_t N, int64_t ld, float* h0, float* h,
                                                         int64_t h_ld, uint8_t* ok_out) {
-  const BandDesc& bd = bands[band];
+  const BandDesc bd = cptr(bands)[band];
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
     float xv[NP], hv[NP], H0;
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(BLOCK) void hessian_kernel(const BandDesc* bands, i
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = 0.f;
     for (int bi = 0; bi < n_bands; ++bi) {
-      const BandDesc& bd = bands[bi];
+      const BandDesc bd = cptr(bands)[bi];
       if (bd.op != OP_GP) continue;
       float y, w;
       decode_obs(bd, p, y, w);
