@@ -46,7 +46,15 @@ def main():
     ap.add_argument("--pool", type=int, default=3, help="distinct synthetic dates kept in pinned host memory")
     ap.add_argument("--metrics", default=None)
     ap.add_argument("--device", default=None)
+    ap.add_argument("--watchdog", type=float, default=0, help="dump Python stacks every N s (hang triage)")
+    ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()
+    if a.watchdog > 0:
+        import faulthandler
+        faulthandler.dump_traceback_later(a.watchdog, repeat=True, file=sys.stderr)
+    if a.verbose:
+        import logging
+        logging.basicConfig(level=logging.INFO, stream=sys.stderr)
 
     from kafka_inferenceengine_amd import (DeviceOutput, EngineConfig, JRCPrior, LinearKalman,
                                            SyntheticBHRObservations, TIP_PARAMETERS,
@@ -55,7 +63,13 @@ def main():
     from kafka_inferenceengine_amd.parallel import Comm, StripPartition
 
     comm = Comm.from_env(device=a.device)
-    dev = comm.device if comm.distributed else torch.device(a.device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    if comm.distributed:
+        dev = comm.device
+    else:
+        dev = torch.device(a.device or ("cuda" if torch.cuda.is_available() else "cpu"))
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        comm = Comm.single(dev)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     world, rank = comm.world, comm.rank

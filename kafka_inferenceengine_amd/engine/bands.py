@@ -130,7 +130,12 @@ def band_desc(spec: OperatorSpec, obs: DeviceBand | None, n_params: int, cache: 
 
 def build_table(specs, obs_list, n_params, cache, device, h0_outs=None, pre=None) -> K.BandTable:
     descs, keep = [], []
+    want = torch.device(device)
     for i, (spec, ob) in enumerate(zip(specs, obs_list)):
+        for t in (ob.dn, ob.y, ob.w, ob.mask, ob.aux):
+            if t is not None and (t.device.type != want.type or
+                                  (want.type == "cuda" and want.index is not None and t.device.index != want.index)):
+                raise ValueError(f"band {i}: observation tensor on {t.device}, engine runs on {want}")
         h0 = None if h0_outs is None else h0_outs[i]
         ph0, ph = (None, None) if pre is None or pre[i] is None else pre[i]
         dsc, kp = band_desc(spec, ob, n_params, cache, h0, ph0, ph)

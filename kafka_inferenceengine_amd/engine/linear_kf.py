@@ -47,7 +47,10 @@ AssimilationResult = namedtuple("AssimilationResult", "state n_iter norms innova
 
 def _resolve_device(device):
     if device is not None:
-        return torch.device(device)
+        d = torch.device(device)
+        if d.type == "cuda" and d.index is None:
+            d = torch.device("cuda", torch.cuda.current_device())
+        return d
     return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
 
