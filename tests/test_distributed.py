@@ -1,0 +1,121 @@
+"""Tile-DP over row strips with world_size 2 on the CPU (gloo) — the logic
+harness of the RCCL path (tier 3b)."""
+import datetime as dt
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _problem(world, rank):
+    import kafka_inferenceengine_amd as k
+    from kafka_inferenceengine_amd.parallel import Comm, StripPartition
+
+    mask = np.ones((30, 22), bool)
+    mask[4:9, 3:12] = False
+    comm = Comm(rank, world, "cpu") if world > 1 else Comm.single("cpu")
+    part = StripPartition(mask, rank, world)
+    obs = k.SyntheticBHRObservations(mask, n_train=60, device="cpu", stream=True, n_pool=4, partition=part,
+                                     field_cell=6, seed=3)
+    return k, mask, comm, part, obs
+
+
+def _run(world, rank, cfg, out_q):
+    k, mask, comm, part, obs = _problem(world, rank)
+    kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device="cpu",
+                        comm=comm, partition=part, config=k.EngineConfig(**cfg))
+    kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+    prior = k.JRCPrior(k.TIP_PARAMETERS, mask)
+    x0, Pinv = prior.process_prior(None)
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
+    st = kf.run(grid, x0, None, Pinv)
+    norms = [r["norms"] for r in kf.metrics.records if r.get("event") == "date"]
+    out_q.put((rank, part.offset, st.x.numpy().copy(), st.P.numpy().copy(), norms))
+
+
+def _worker(rank, world, port, cfg, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _run(world, rank, cfg, q)
+    finally:
+        dist.destroy_process_group()
+
+
+def _gather(world, cfg):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    if world == 1:
+        _run(1, 0, cfg, q)
+        res = [q.get()]
+    else:
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=300) for _ in range(world)]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    res.sort(key=lambda t: t[0])
+    x = np.concatenate([r[2] for r in res], 1)
+    P = np.concatenate([r[3] for r in res], 1)
+    return x, P, [r[4] for r in res]
+
+
+@pytest.mark.parametrize("cfg", [{}, {"spatial_gamma": 30.0, "spatial_params": [6], "jacobi_sweeps": 5}],
+                         ids=["independent", "regularised-halo"])
+def test_two_ranks_equal_one_rank(cfg):
+    x1, P1, n1 = _gather(1, cfg)
+    x2, P2, n2 = _gather(2, cfg)
+    assert x1.shape == x2.shape
+    # per-pixel math is identical; only the f64 norm summation order differs
+    assert np.allclose(x1, x2, rtol=1e-5, atol=1e-6)
+    assert np.allclose(P1, P2, rtol=1e-5, atol=1e-3)
+    # the global convergence decision is identical on every rank
+    assert n2[0] == n2[1]
+    assert [len(a) for a in n1[0]] == [len(a) for a in n2[0]]
+
+
+def test_strip_partition_balances_active_pixels():
+    from kafka_inferenceengine_amd.parallel import StripPartition
+    rng = np.random.default_rng(0)
+    mask = rng.random((400, 50)) < np.linspace(0.1, 0.9, 400)[:, None]
+    parts = [StripPartition(mask, r, 4) for r in range(4)]
+    counts = [p.N for p in parts]
+    assert sum(counts) == mask.sum()
+    assert max(counts) - min(counts) <= mask.sum(1).max()
+    assert parts[0].offset == 0 and parts[3].offset == sum(counts[:3])
+    g = np.concatenate([p.global_index() for p in parts])
+    assert np.array_equal(g, np.flatnonzero(mask.ravel()))
+
+
+def test_bench_torchrun_gloo_two_ranks():
+    """bench.py under torch.distributed.run with 2 CPU ranks (gloo)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--size", "96", "--n-train", "40", "--device", "cpu"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["config"]["finite"]
