@@ -79,6 +79,9 @@ PYBIND11_MODULE(_kafka_hip, m) {
       .def_readwrite("ld", &AnalysisArgs::ld)
       .def_readwrite("n_bands", &AnalysisArgs::n_bands)
       .def_readwrite("solve", &AnalysisArgs::solve)
+      .def_readwrite("fast_d", &AnalysisArgs::fast_d)
+      .def_readwrite("fast_obs", &AnalysisArgs::fast_obs)
+      .def_readwrite("variant", &AnalysisArgs::variant)
       .PTR_FIELD(AnalysisArgs, bands, const BandDesc*)
       .PTR_FIELD(AnalysisArgs, x_prev, const float*)
       .PTR_FIELD(AnalysisArgs, x_f, const float*)

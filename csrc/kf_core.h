@@ -79,6 +79,8 @@ struct BandDesc {
 struct AnalysisArgs {
   int64_t N, ld;
   int32_t n_bands, solve;
+  int32_t fast_d, fast_obs;  // host hint: all bands GP with fast_d inputs, one encoding (0: generic)
+  int32_t variant, pad1;     // kernel variant selector (tuning; 0 = default)
   const BandDesc* bands;
   const float* x_prev;   // [NP][ld] linearisation point
   const float* x_f;      // [NP][ld] forecast mean
@@ -212,14 +214,16 @@ KF_HD void symv(const float (&A)[ntri(NP)], const float (&x)[NP], float (&y)[NP]
 
 // ---------------------------------------------------------------------------
 // observation decode: returns weight w (inverse variance, 0 when masked) and y
+// FOBS != 0 compiles a single encoding (fast-path kernels).
+template <int FOBS = 0>
 KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y, float& w) {
-  if (bd.obs == OBS_DN16) {
+  if (FOBS == OBS_DN16 || (FOBS == 0 && bd.obs == OBS_DN16)) {
     const uint16_t dn = bd.dn[p];
     y = (float)dn * bd.scale;
     float sig = fmaxf(bd.rel_unc * y, bd.unc_floor);
     w = (dn > 0 && sig > 0.f) ? 1.f / (sig * sig) : 0.f;
     if (dn == 0) y = 0.f;
-  } else if (bd.obs == OBS_F32) {
+  } else if (FOBS == OBS_F32 || (FOBS == 0 && bd.obs == OBS_F32)) {
     y = bd.y[p];
     w = bd.w[p];
     if (bd.mask && !bd.mask[p]) w = 0.f;
@@ -235,10 +239,18 @@ KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y, float& w) {
 
 // RBF (ARD) Gaussian-process emulator, inputs centred on the training mean:
 //   f(x) = offset + sum_i alpha_i s exp(-1/2 sum_d lambda_d (x_d - t_id)^2)
-// records (host-built, ops/emulators.py): L_i = log2(s) - 1/2 log2e sum lambda t^2,
-// B_id = log2e lambda_d t_id, alpha_i, alpha_i t_id  (t centred).
+// records (host-built, models/gp.py): L_i = log2(s) - 1/2 log2e sum lambda t^2,
+// B_id = log2e lambda_d t_id, alpha_i, alpha_i t_id  (t centred), stored as
+// training-point PAIRS, field-major: rec[pair][field][2] (T padded to even
+// with alpha = 0).  On gfx950 one pair is one v_pk_fma_f32 per field with the
+// pair's two values as one 64-bit SGPR operand: the exponent and the five
+// weighted sums run at the packed-f32 rate (2 points per lane per issue).
 // Replaces gp.predict + the lil_matrix scatter of utils.py:181-219.
-template <int NP, int D>
+KF_HD float gp_rec(const KF_CONST_AS float* r, int R, int i, int f) {
+  return r[((int64_t)(i >> 1) * R + f) * 2 + (i & 1)];
+}
+
+template <int NP, int D, int UNR = 2>
 KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&h)[NP]) {
   float xi[D];
   float c = 0.f;
@@ -248,23 +260,51 @@ KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&
     c = fmaf(bd.coef[d] * xi[d], xi[d], c);
   }
   c *= -0.5f * LOG2E;
-  float S0 = 0.f, S[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) S[d] = 0.f;
+  float S0, S[D];
   constexpr int R = 2 * D + 2;
-  const KF_CONST_AS float* __restrict__ r = cptr(bd.gp);
-  const int T = bd.T;
-#pragma unroll 4
-  for (int i = 0; i < T; ++i) {
-    const KF_CONST_AS float* __restrict__ ri = r + (int64_t)i * R;
-    float e = ri[0] + c;
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const KF_CONST_AS f2* __restrict__ r2 = (const KF_CONST_AS f2*)cptr(bd.gp);
+  const int T2 = bd.T >> 1;
+  f2 S0v = {0.f, 0.f}, Sv[D], xv[D];
+  const f2 cv = {c, c};
 #pragma unroll
-    for (int d = 0; d < D; ++d) e = fmaf(ri[1 + d], xi[d], e);
-    const float k = kexp2(e);
-    S0 = fmaf(ri[1 + D], k, S0);
+  for (int d = 0; d < D; ++d) { Sv[d] = f2{0.f, 0.f}; xv[d] = f2{xi[d], xi[d]}; }
+#pragma unroll UNR
+  for (int i = 0; i < T2; ++i) {
+    const KF_CONST_AS f2* __restrict__ ri = r2 + (int64_t)i * R;
+    f2 e = ri[0] + cv;
 #pragma unroll
-    for (int d = 0; d < D; ++d) S[d] = fmaf(ri[2 + D + d], k, S[d]);
+    for (int d = 0; d < D; ++d) e = __builtin_elementwise_fma(ri[1 + d], xv[d], e);
+    f2 k;
+    k.x = kexp2(e.x);
+    k.y = kexp2(e.y);
+    S0v = __builtin_elementwise_fma(ri[1 + D], k, S0v);
+#pragma unroll
+    for (int d = 0; d < D; ++d) Sv[d] = __builtin_elementwise_fma(ri[2 + D + d], k, Sv[d]);
   }
+  S0 = S0v.x + S0v.y;
+#pragma unroll
+  for (int d = 0; d < D; ++d) S[d] = Sv[d].x + Sv[d].y;
+#else
+  const float* r = bd.gp;
+  float S0a[2] = {0.f, 0.f}, Sa[2][D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) Sa[0][d] = Sa[1][d] = 0.f;
+  for (int i = 0; i < bd.T; ++i) {
+    const int l = i & 1;
+    float e = gp_rec(r, R, i, 0) + c;
+#pragma unroll
+    for (int d = 0; d < D; ++d) e = fmaf(gp_rec(r, R, i, 1 + d), xi[d], e);
+    const float k = kexp2(e);
+    S0a[l] = fmaf(gp_rec(r, R, i, 1 + D), k, S0a[l]);
+#pragma unroll
+    for (int d = 0; d < D; ++d) Sa[l][d] = fmaf(gp_rec(r, R, i, 2 + D + d), k, Sa[l][d]);
+  }
+  S0 = S0a[0] + S0a[1];
+#pragma unroll
+  for (int d = 0; d < D; ++d) S[d] = Sa[0][d] + Sa[1][d];
+#endif
   H0 = bd.offset + S0;
 #pragma unroll
   for (int j = 0; j < NP; ++j) h[j] = 0.f;
@@ -348,7 +388,9 @@ KF_HD bool eval_operator(const BandDesc& bd, int64_t p, int64_t ld, const float 
 //   A = P_f^-1 + sum_b w_b h_b h_b^T,  b = P_f^-1 x_f + sum_b w_b h_b y'_b,
 //   y'_b = y_b + h_b . x0 - H0_b,      x_a = A^-1 b
 // Returns (x_a - x0)^2 summed over parameters.
-template <int NP>
+// FD > 0: fast path where every band is a GP with FD inputs and FOBS encoding
+// (the compiler then drops the SAR/linear/precomputed code and its registers).
+template <int NP, int FD = 0, int FOBS = 0, int UNR = 2>
 KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a.ld;
@@ -368,13 +410,21 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
   for (int bi = 0; bi < a.n_bands; ++bi) {
     const BandDesc bd = cptr(a.bands)[bi];
     float y, w;
-    decode_obs(bd, p, y, w);
+    decode_obs<FOBS>(bd, p, y, w);
     if (!(w > 0.f)) {
       if (bd.h0_out) bd.h0_out[p] = 0.f;
       continue;
     }
     float H0, h[NP];
-    const bool ok = eval_operator<NP>(bd, p, ld, x0, H0, h);
+    bool ok;
+    if constexpr (FD > 0) {
+      gp_eval<NP, FD, UNR>(bd, x0, H0, h);
+      ok = finitef(H0);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);
+    } else {
+      ok = eval_operator<NP>(bd, p, ld, x0, H0, h);
+    }
     if (bd.h0_out) bd.h0_out[p] = H0;
     if (!ok) { st |= ST_BAD_OP; continue; }
     ++nobs;
@@ -709,18 +759,18 @@ KF_HD void gp_hessian(const BandDesc& bd, const float (&x)[NP], float& f, float 
 #pragma unroll
   for (int t = 0; t < ntri(D); ++t) S2[t] = 0.f;
   constexpr int R = 2 * D + 2;
+  const KF_CONST_AS float* rr = cptr(bd.gp);
   for (int i = 0; i < bd.T; ++i) {
-    const KF_CONST_AS float* ri = cptr(bd.gp) + (int64_t)i * R;
-    float e = ri[0] + c;
+    float e = gp_rec(rr, R, i, 0) + c;
 #pragma unroll
-    for (int d = 0; d < D; ++d) e = fmaf(ri[1 + d], xi[d], e);
+    for (int d = 0; d < D; ++d) e = fmaf(gp_rec(rr, R, i, 1 + d), xi[d], e);
     const float k = kexp2(e);
-    const float ak = ri[1 + D] * k;
+    const float ak = gp_rec(rr, R, i, 1 + D) * k;
     S0 += ak;
     float t[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      t[d] = ri[1 + d] / (LOG2E * bd.coef[d]);
+      t[d] = gp_rec(rr, R, i, 1 + d) / (LOG2E * bd.coef[d]);
       S[d] = fmaf(ak, t[d], S[d]);
     }
 #pragma unroll

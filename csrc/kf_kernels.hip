@@ -37,12 +37,12 @@ __device__ __forceinline__ void block_partial(double v, double* partials) {
   }
 }
 
-template <int NP>
+template <int NP, int FD = 0, int FOBS = 0, int UNR = 2>
 __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
-    acc += (double)pixel_analysis<NP>(a, p);
+    acc += (double)pixel_analysis<NP, FD, FOBS, UNR>(a, p);
   if (a.partials) block_partial(acc, a.partials);
 }
 
@@ -207,9 +207,39 @@ static inline int grid_for(int64_t N, int max_blocks) {
     default: return hipErrorInvalidValue;         \
   }
 
+template <int NP, int FD>
+static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
+  if (a.fast_obs == OBS_DN16) {
+    if (a.variant == 1)
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 1>), dim3(grid), dim3(BLOCK), 0, s, a);
+    else if (a.variant == 2)
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 4>), dim3(grid), dim3(BLOCK), 0, s, a);
+    else
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
+  } else if (a.fast_obs == OBS_F32) {
+    hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_F32>), dim3(grid), dim3(BLOCK), 0, s, a);
+  } else {
+    return false;
+  }
+  return true;
+}
+
+// Fast-path instantiations: JRC-TIP (7 params, 4-input band GPs), PROSAIL
+// (10 params, full-state GPs) and full-state GPs for small states.
 template <int NP>
 static void l_analysis(const AnalysisArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(analysis_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
+  bool done = false;
+  if (a.fast_d > 0) {
+    if constexpr (NP == 7) {
+      if (a.fast_d == 4) done = l_analysis_fast<7, 4>(a, grid, s);
+      else if (a.fast_d == 7) done = l_analysis_fast<7, 7>(a, grid, s);
+    } else if constexpr (NP == 10) {
+      if (a.fast_d == 10) done = l_analysis_fast<10, 10>(a, grid, s);
+    } else if constexpr (NP <= 4) {
+      if (a.fast_d == NP) done = l_analysis_fast<NP, NP>(a, grid, s);
+    }
+  }
+  if (!done) hipLaunchKernelGGL(analysis_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
 }
 template <int NP>
 static void l_gain(const GainArgs& a, int grid, hipStream_t s) {

@@ -87,7 +87,9 @@ def band_desc(spec: OperatorSpec, obs: DeviceBand | None, n_params: int, cache: 
         if spec.d > 12 or spec.d > n_params:
             raise ValueError(f"GP with {spec.d} inputs exceeds the compiled limit for n_params={n_params}")
         rec = cache.get(spec, device)
-        d.d, d.T = spec.d, int(rec.shape[0])
+        if rec.dim() != 3 or rec.shape[1] != 2 * spec.d + 2 or rec.shape[2] != 2:
+            raise ValueError(f"GP records must be [T/2, 2d+2, 2], got {tuple(rec.shape)}")
+        d.d, d.T = spec.d, 2 * int(rec.shape[0])
         d.gp = rec.data_ptr()
         keep.append(rec)
     elif spec.kind == OP_SAR:

@@ -79,16 +79,26 @@ class GaussianProcessEmulator:
         return self.inputs.mean(0)
 
     def records(self) -> np.ndarray:
-        """float32 [T, 2D+2] rows: L, B[D], alpha, alpha*t[D] (inputs centred)."""
+        """float32 kernel records, training-point pairs field-major:
+        [ceil(T/2), 2D+2, 2] with fields L, B[D], alpha, alpha*t[D] (inputs
+        centred); an odd T is padded with an alpha = 0 point."""
         if self._records is None:
             c = self.center()
             t = self.inputs - c[None, :]
             L = np.log2(self.signal) - 0.5 * LOG2E * (t * t * self.lam[None, :]).sum(1)
             B = LOG2E * self.lam[None, :] * t
             at = self.alpha[:, None] * t
-            rec = np.concatenate([L[:, None], B, self.alpha[:, None], at], axis=1)
-            self._records = np.ascontiguousarray(rec.astype(np.float32))
+            rec = np.concatenate([L[:, None], B, self.alpha[:, None], at], axis=1)   # [T, R]
+            if rec.shape[0] % 2:
+                rec = np.concatenate([rec, np.zeros((1, rec.shape[1]))], axis=0)
+            pairs = rec.reshape(-1, 2, rec.shape[1]).transpose(0, 2, 1)           # [T2, R, 2]
+            self._records = np.ascontiguousarray(pairs.astype(np.float32))
         return self._records
+
+    @property
+    def n_records(self) -> int:
+        """Padded number of training points the kernel iterates over."""
+        return 2 * self.records().shape[0]
 
     # ------------------------------------------------------------ building
     @classmethod

@@ -76,26 +76,39 @@ def partials_buffer(N: int, device) -> torch.Tensor:
 @dataclass
 class BandTable:
     """Packed ``BandDesc`` array resident on the target device plus the tensors
-    it points into (kept alive as long as the table)."""
+    it points into (kept alive as long as the table).  ``fast_d``/``fast_obs``
+    select the specialised analysis kernel when every band is a GP with the
+    same input count and observation encoding (0: generic kernel)."""
     buf: torch.Tensor
     n: int
     keepalive: tuple
+    fast_d: int = 0
+    fast_obs: int = 0
 
     @property
     def ptr(self) -> int:
         return int(self.buf.data_ptr())
 
 
+OP_GP = 2
+
+
 def make_band_table(descs: list, device, keepalive=()) -> BandTable:
     raw = ext().pack_band_descs(descs)
     cpu = torch.frombuffer(bytearray(raw), dtype=torch.uint8) if raw else torch.zeros(8, dtype=torch.uint8)
     buf = cpu.to(device) if torch.device(device).type == "cuda" else cpu.clone()
-    return BandTable(buf, len(descs), tuple(keepalive))
+    fast_d = fast_obs = 0
+    if descs and all(d.op == OP_GP for d in descs):
+        ds = {d.d for d in descs}
+        obs = {d.obs for d in descs}
+        if len(ds) == 1 and len(obs) == 1 and next(iter(obs)) in (OBS_F32, OBS_DN16):
+            fast_d, fast_obs = next(iter(ds)), next(iter(obs))
+    return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs)
 
 
 # ------------------------------------------------------------------ ops
 def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=None, b_out=None, status=None,
-             partials=None, N=None, solve=True):
+             partials=None, N=None, solve=True, fast=True, variant=0):
     """K1 fused Gauss-Newton analysis (information form)."""
     check_np(n_params)
     N = int(x_prev.shape[1] if N is None else N)
@@ -115,6 +128,8 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
         raise ValueError("partials must be float64 with >= grid_for(N) entries")
     a = ext().AnalysisArgs()
     a.N, a.ld, a.n_bands, a.solve = N, ld, bands.n, int(bool(solve))
+    a.fast_d, a.fast_obs = (bands.fast_d, bands.fast_obs) if fast else (0, 0)
+    a.variant = int(variant)
     a.bands = bands.ptr
     a.x_prev, a.x_f, a.pf_inv = _ptr(x_prev), _ptr(x_f), _ptr(pf_inv)
     a.x_out, a.a_out, a.b_out = _ptr(x_out), _ptr(a_out), _ptr(b_out)

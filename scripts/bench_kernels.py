@@ -1,0 +1,64 @@
+#!/usr/bin/env python
+"""Interleaved A/B timing of analysis-kernel variants in ONE process
+(cdna_hip_programming.md §5.4 rule 24) on the bench problem (TIP, 2 GP bands,
+DN16 observations)."""
+import argparse
+import json
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
+
+import kafka_inferenceengine_amd as k  # noqa: E402
+from kafka_inferenceengine_amd.engine.bands import RecordCache, build_table  # noqa: E402
+from kafka_inferenceengine_amd.ops import kernels as K  # noqa: E402
+from kafka_inferenceengine_amd.utils.blocks import pack_matrix  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--n-train", type=int, default=500)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", default="g,0,1,2")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    mask = np.ones((a.size, a.size), bool)
+    obs = k.SyntheticBHRObservations(mask, n_train=a.n_train, device=dev, stream=False, n_pool=1)
+    date = obs.dates[0]
+    bands = [(obs.band_specs[b], obs.get_device_band_data(date, b)) for b in range(2)]
+    tab = build_table([s for s, _ in bands], [d for _, d in bands], 7, RecordCache(), dev)
+    N = obs.N
+    mu, _, Pi = k.tip_prior()
+    xf = torch.tensor(mu, dtype=torch.float32, device=dev)[:, None].expand(7, N).contiguous()
+    Pf = torch.tensor(pack_matrix(Pi), dtype=torch.float32, device=dev)[:, None].expand(28, N).contiguous()
+    xo = torch.empty_like(xf)
+    ao = torch.empty_like(Pf)
+    part = K.partials_buffer(N, dev)
+    variants = a.variants.split(",")
+    times = {v: [] for v in variants}
+    outs = {}
+    for r in range(a.rounds + 1):
+        for v in variants:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            K.analysis(7, tab, xf, xf, Pf, xo, ao, None, None, part, fast=(v != "g"),
+                       variant=0 if v == "g" else int(v))
+            e.record()
+            e.synchronize()
+            if r:
+                times[v].append(s.elapsed_time(e))
+            outs[v] = xo.clone()
+    ref = outs[variants[0]]
+    res = {}
+    for v in variants:
+        t = np.array(times[v])
+        res[v] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
+                  "max_abs_diff_vs_first": float((outs[v] - ref).abs().max())}
+    print(json.dumps({"size": a.size, "N": N, "n_train": a.n_train, "variants": res}))
+
+
+if __name__ == "__main__":
+    main()
