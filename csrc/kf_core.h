@@ -250,7 +250,7 @@ KF_HD float gp_rec(const KF_CONST_AS float* r, int R, int i, int f) {
   return r[((int64_t)(i >> 1) * R + f) * 2 + (i & 1)];
 }
 
-template <int NP, int D, int UNR = 2>
+template <int NP, int D, int UNR = 4>
 KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&h)[NP]) {
   float xi[D];
   float c = 0.f;
@@ -390,7 +390,7 @@ KF_HD bool eval_operator(const BandDesc& bd, int64_t p, int64_t ld, const float 
 // Returns (x_a - x0)^2 summed over parameters.
 // FD > 0: fast path where every band is a GP with FD inputs and FOBS encoding
 // (the compiler then drops the SAR/linear/precomputed code and its registers).
-template <int NP, int FD = 0, int FOBS = 0, int UNR = 2>
+template <int NP, int FD = 0, int FOBS = 0, int UNR = 4>
 KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a.ld;

@@ -37,7 +37,7 @@ __device__ __forceinline__ void block_partial(double v, double* partials) {
   }
 }
 
-template <int NP, int FD = 0, int FOBS = 0, int UNR = 2>
+template <int NP, int FD = 0, int FOBS = 0, int UNR = 4>
 __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
@@ -214,6 +214,10 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 1>), dim3(grid), dim3(BLOCK), 0, s, a);
     else if (a.variant == 2)
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 4>), dim3(grid), dim3(BLOCK), 0, s, a);
+    else if (a.variant == 3)
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 8>), dim3(grid), dim3(BLOCK), 0, s, a);
+    else if (a.variant == 4)
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 16>), dim3(grid), dim3(BLOCK), 0, s, a);
     else
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
   } else if (a.fast_obs == OBS_F32) {
