@@ -1,19 +1,25 @@
 #!/usr/bin/env python
-"""Headline benchmark: pixel-state updates/s on a full 10980² Sentinel-2 tile,
-7-parameter JRC-TIP state (BASELINE.json).
+"""Benchmarks: pixel-state updates/s (BASELINE.json).
 
-One *step* = one 16-day time-grid step of ``LinearKalman``: propagation
-(LAI propagator, Q[TLAI]=0.04, ``kafka_test.py:207-208``), ingest of one
-observation date (2 bands as uint16 DN streamed from pinned host memory over a
-side stream), Gauss-Newton iterations to the reference's global convergence
-criterion (each iteration = GP emulator (T=500 training points, 4 inputs per
-band) + Jacobian + normal equations + Cholesky for every pixel), and the
-device output unpack (mean and 1/sqrt(diag P^-1) rasters).
-A *pixel-state update* is one active pixel's full analysis for one date
-(BASELINE.md), so updates/step = active pixels.
+Headline (default ``--config tip7``): full 10980² Sentinel-2 tile, 7-parameter
+JRC-TIP state.  One *step* = one 16-day time-grid step of ``LinearKalman``:
+propagation (LAI propagator, Q[TLAI]=0.04, ``kafka_test.py:207-208``), ingest
+of one observation date (2 bands of uint16 DN streamed from pinned host memory
+on a side stream), Gauss-Newton iterations to the reference's global
+convergence criterion (each iteration = GP emulator (T=500 training points, 4
+inputs per band) + Jacobian + normal equations + Cholesky for every pixel), and
+the device output unpack (mean and 1/sqrt(diag P^-1) rasters).  A pixel-state
+update is one active pixel's full analysis for one date, so
+updates/step = active pixels.
 
-Multi-GPU: tile-DP over row strips, one process per GPU (torchrun), RCCL
-collectives for the global convergence norm; the tile is fixed, so scaling is
+Other BASELINE.json configs: ``identity7`` (1024² tile, identity operator,
+bf16 observations), ``prosail10`` (S2 granule, 10-param PROSAIL, 10 band GP
+emulators, SAIL prior reset — kafka_test_S2.py), ``spatial`` (TIP with the GMRF
+spatial prior and RCCL halo exchange), ``multisensor`` (S2 13-band + OLCI-like
+21-band joint operator on the PROSAIL state).
+
+Multi-GPU: tile-DP over row strips, one process per GPU (torchrun), RCCL for
+the global convergence norm (and halos); the tile is fixed, so scaling is
 strong.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -21,18 +27,84 @@ from __future__ import annotations
 import argparse
 import datetime as dt
 import json
-import os
 import sys
 import time
 
 import numpy as np
 import torch
 
-BASELINE_UPDATES_PER_S = 50250.0  # 8 Xeon cores, 7p-2b, chunk-parallel (kafka_test_Py36.py:254)
+# 8 Xeon cores, chunk-parallel (kafka_test_Py36.py:254): 7p-2b 50,250/s;
+# 10p-10b ~4,600/s (581/s x 8, linear scaling assumed).
+BASELINE_7P = 50250.0
+BASELINE_10P = 4600.0
+HEADLINE_METRIC = "pixel-state updates/sec (whole node), 10980^2 S2 tile, 7-param state"
+
+CONFIGS = {
+    "tip7": dict(size=10980, n_train=500, model="JRC-TIP 7-param, 2-band GP-emulator operator, LAI propagator",
+                 baseline=BASELINE_7P),
+    "identity7": dict(size=1024, model="7-param state, identity observation operator (7 bands), "
+                                       "bf16 observations, LAI propagator", baseline=BASELINE_7P),
+    "prosail10": dict(size=10980, n_train=250, model="PROSAIL 10-param, 10-band S2 GP emulators, SAIL prior reset",
+                      baseline=BASELINE_10P),
+    "spatial": dict(size=10980, n_train=500, gamma=5.0, sweeps=4,
+                    model="JRC-TIP 7-param + GMRF spatial prior on TLAI (block-Jacobi, halo exchange)",
+                    baseline=BASELINE_7P),
+    "multisensor": dict(size=10980, n_train=250, model="PROSAIL 10-param, S2 13-band + OLCI-like 21-band joint "
+                                                       "GP operator", baseline=BASELINE_10P),
+}
 
 
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def build(cfg_name, a, mask, part, dev, comm):
+    import kafka_inferenceengine_amd as k
+
+    c = CONFIGS[cfg_name]
+    n_dates = a.warmup + a.steps + 1
+    seed = 0
+    if cfg_name in ("tip7", "spatial"):
+        dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(n_dates)]
+        obs = k.SyntheticBHRObservations(mask, dates=dates, n_train=a.n_train or c["n_train"], partition=part,
+                                         device=dev, n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=seed)
+        cfg = k.EngineConfig(metrics_path=a.metrics)
+        if cfg_name == "spatial":
+            cfg = k.EngineConfig(metrics_path=a.metrics, spatial_gamma=c["gamma"], spatial_params=[6],
+                                 jacobi_sweeps=c["sweeps"])
+        kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_nonlinear_observation_operator,
+                            k.TIP_PARAMETERS, state_propagation=k.propagate_information_filter_LAI, config=cfg,
+                            comm=comm, partition=part)
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        state = kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask))
+    elif cfg_name == "identity7":
+        dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(n_dates)]
+        obs = k.SyntheticIdentityObservations(mask, dates=dates, partition=part, device=dev, n_pool=a.pool,
+                                              stream=True, cloud_fraction=a.cloud, seed=seed)
+        kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_linear_observation_operator,
+                            k.TIP_PARAMETERS, state_propagation=k.propagate_information_filter_LAI,
+                            config=k.EngineConfig(metrics_path=a.metrics), comm=comm, partition=part)
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        state = kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask))
+    else:
+        dates = [dt.datetime(2017, 7, 3) + dt.timedelta(days=2 * i) for i in range(n_dates)]
+        T = a.n_train or c["n_train"]
+        if cfg_name == "prosail10":
+            obs = k.SyntheticS2Observations(mask, dates=dates, n_bands=10, n_train=T, partition=part, device=dev,
+                                            n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=seed)
+        else:
+            s2 = k.SyntheticS2Observations(mask, dates=dates, n_bands=13, n_train=T, partition=part, device=dev,
+                                           n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=seed)
+            olci = k.SyntheticOLCIObservations(mask, dates=dates, n_bands=21, n_train=T, partition=part,
+                                               device=dev, n_pool=a.pool, stream=True, cloud_fraction=a.cloud,
+                                               seed=seed + 21)
+            obs = k.MultiSensorObservations([s2, olci])
+        prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
+        kf = k.LinearKalman(obs, k.DeviceOutput(k.SAIL_PARAMETERS), mask, k.create_prosail_observation_operator,
+                            k.SAIL_PARAMETERS, state_propagation=None, prior=prior,
+                            config=k.EngineConfig(metrics_path=a.metrics), comm=comm, partition=part)
+        state = kf.state_from_prior(prior)
+    return obs, kf, state, dates
 
 
 def main():
@@ -40,12 +112,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--size", type=int, default=10980, help="tile edge (pixels)")
-    ap.add_argument("--n-train", type=int, default=500, help="GP training points per band emulator")
+    ap.add_argument("--config", default="tip7", choices=sorted(CONFIGS))
+    ap.add_argument("--size", type=int, default=None, help="tile edge (pixels); default per config")
+    ap.add_argument("--n-train", type=int, default=None, help="GP training points per band emulator")
     ap.add_argument("--cloud", type=float, default=0.2, help="cloud (masked) fraction per date")
     ap.add_argument("--pool", type=int, default=3, help="distinct synthetic dates kept in pinned host memory")
     ap.add_argument("--metrics", default=None)
     ap.add_argument("--device", default=None)
+    ap.add_argument("--profile", default=None, help="write a torch.profiler chrome trace here (rank 0)")
     ap.add_argument("--watchdog", type=float, default=0, help="dump Python stacks every N s (hang triage)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()
@@ -56,9 +130,6 @@ def main():
         import logging
         logging.basicConfig(level=logging.INFO, stream=sys.stderr)
 
-    from kafka_inferenceengine_amd import (DeviceOutput, EngineConfig, JRCPrior, LinearKalman,
-                                           SyntheticBHRObservations, TIP_PARAMETERS,
-                                           create_nonlinear_observation_operator, propagate_information_filter_LAI)
     from kafka_inferenceengine_amd.inference import iterate_time_grid
     from kafka_inferenceengine_amd.parallel import Comm, StripPartition
 
@@ -75,71 +146,67 @@ def main():
     world, rank = comm.world, comm.rank
     if a.gpus != world:
         log(f"--gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-
-    H = W = a.size
+    c = CONFIGS[a.config]
+    H = W = a.size or c["size"]
     mask = np.ones((H, W), dtype=bool)
     part = StripPartition(mask, rank, world)
     t_setup = time.time()
-    n_dates = a.warmup + a.steps + 1
-    dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(n_dates)]
-    obs = SyntheticBHRObservations(mask, dates=dates, n_train=a.n_train, partition=part, device=dev,
-                                   n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=0)
-    prior = JRCPrior(TIP_PARAMETERS, mask)
-    cfg = EngineConfig(metrics_path=a.metrics)
-    kf = LinearKalman(obs, DeviceOutput(TIP_PARAMETERS), mask, create_nonlinear_observation_operator,
-                      TIP_PARAMETERS, state_propagation=propagate_information_filter_LAI, prior=None, config=cfg,
-                      comm=comm, partition=part)
-    kf.set_trajectory_model()
-    Q = np.zeros(7)
-    Q[6] = 0.04
-    kf.set_trajectory_uncertainty(Q)
-    state = kf.state_from_prior(prior)
-    obs._ensure_pool()
+    obs, kf, state, dates = build(a.config, a, mask, part, dev, comm)
+    srcs = getattr(obs, "sources", [obs])
+    for s in srcs:
+        s._ensure_pool()
     if dev.type == "cuda":
         torch.cuda.synchronize()
-    log(f"rank {rank}/{world}: strip rows {part.r0}-{part.r1}, {part.N} px, setup {time.time() - t_setup:.1f}s, "
-        f"pinned={obs._streamer.pinned}")
+    log(f"rank {rank}/{world}: {a.config} strip rows {part.r0}-{part.r1}, {part.N} px, "
+        f"setup {time.time() - t_setup:.1f}s")
 
     grid = [dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in dates]
     steps = list(iterate_time_grid(grid, dates))
+    prof = None
     first = True
-    times = []
-    t_start = None
     for i, (t, loc, is_first) in enumerate(steps[:a.warmup + a.steps]):
         if i == a.warmup:
             comm.barrier()
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             t_start = time.perf_counter()
+            if a.profile and rank == 0:
+                prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                          torch.profiler.ProfilerActivity.CUDA])
+                prof.__enter__()
         t0 = time.perf_counter()
         state = kf.step(t, loc, state, advance=not first, all_dates=dates)
         first = False
-        if dev.type == "cuda" and (i < a.warmup):
+        if dev.type == "cuda" and i < a.warmup:
             torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
-        log(f"step {i} {'(warmup)' if i < a.warmup else ''} {times[-1] * 1e3:.1f} ms "
+        log(f"step {i}{' (warmup)' if i < a.warmup else ''} {(time.perf_counter() - t0) * 1e3:.1f} ms "
             f"gn_iters={kf.history[-1].get('gn_iterations')}")
     comm.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    elapsed = comm.max_float(elapsed)
+    elapsed = comm.max_float(time.perf_counter() - t_start)
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        prof.export_chrome_trace(a.profile)
     ok = bool(torch.isfinite(state.x[:, :state.N]).all().item())
-    updates = float(part.N_total) * a.steps
-    value = updates / elapsed
+    value = float(part.N_total) * a.steps / elapsed
     if rank == 0:
         gn = [h.get("gn_iterations") for h in kf.history[a.warmup:]]
-        rec = {"metric": "pixel-state updates/sec (whole node), 10980^2 S2 tile, 7-param state",
-               "value": round(value, 1), "unit": "pixel-state updates/s", "n_gpus": world, "steps": a.steps,
-               "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 3), "higher_is_better": True,
-               "scaling": "strong", "vs_baseline": round(value / BASELINE_UPDATES_PER_S, 2), "dtype": "fp32",
-               "data": f"synthetic (smooth random truth -> GP emulators -> 5% noise, {a.cloud:.0%} clouds, "
-                       f"uint16 DN), random-init GP emulators (T={a.n_train})",
-               "config": {"model": "JRC-TIP 7-param, 2-band GP-emulator operator, LAI propagator",
-                          "tile": f"{H}x{W}", "active_pixels": part.N_total, "global_batch": part.N_total,
-                          "seq_len": 1, "bands": 2, "gp_train_points": a.n_train,
-                          "parallelism": f"tile-dp{world}", "gn_iterations": gn, "finite": ok,
-                          "ingest_bytes_per_step": obs.ingest_bytes() // max(1, len(steps))}}
+        metric = HEADLINE_METRIC if a.config == "tip7" and H == 10980 else \
+            f"pixel-state updates/sec (whole node), {H}x{W} tile, {a.config}"
+        ingest = sum(s.ingest_bytes() for s in srcs) // max(1, a.warmup + a.steps)
+        rec = {"metric": metric, "value": round(value, 1), "unit": "pixel-state updates/s", "n_gpus": world,
+               "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 3),
+               "higher_is_better": True, "scaling": "strong",
+               "vs_baseline": round(value / c["baseline"], 2), "dtype": "fp32" if a.config != "identity7"
+               else "fp32 state / bf16 observations",
+               "data": f"synthetic (smooth random truth -> observation operators -> noise, {a.cloud:.0%} clouds), "
+                       "random-init GP emulators",
+               "config": {"name": a.config, "model": c["model"], "tile": f"{H}x{W}", "active_pixels": part.N_total,
+                          "global_batch": part.N_total, "seq_len": 1,
+                          "gp_train_points": a.n_train or c.get("n_train"), "parallelism": f"tile-dp{world}",
+                          "gn_iterations": gn, "finite": ok, "ingest_bytes_per_step": ingest,
+                          "baseline_updates_per_s": c["baseline"]}}
         print(json.dumps(rec), flush=True)
     comm.destroy()
 

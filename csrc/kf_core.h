@@ -42,7 +42,7 @@ template <int NP> KF_HD constexpr int sym(int i, int j) { return i <= j ? tri(NP
 
 // ---------------------------------------------------------------------------
 // enums shared with Python (kafka_inferenceengine_amd/ops/_abi.py)
-enum ObsKind : int32_t { OBS_NONE = 0, OBS_F32 = 1, OBS_DN16 = 2 };
+enum ObsKind : int32_t { OBS_NONE = 0, OBS_F32 = 1, OBS_DN16 = 2, OBS_BF16 = 3 };
 enum OpKind : int32_t { OP_PRECOMP = 0, OP_LINEAR = 1, OP_GP = 2, OP_SAR = 3 };
 enum PropMode : int32_t {
   PROP_PRIOR = 0,         // no_propagation: reset to prior (kf_tools.py:316-353)
@@ -212,6 +212,13 @@ KF_HD void symv(const float (&A)[ntri(NP)], const float (&x)[NP], float (&y)[NP]
   }
 }
 
+KF_HD float bf16_to_f32(uint16_t b) {
+  const uint32_t u = (uint32_t)b << 16;
+  float f;
+  __builtin_memcpy(&f, &u, 4);
+  return f;
+}
+
 // ---------------------------------------------------------------------------
 // observation decode: returns weight w (inverse variance, 0 when masked) and y
 // FOBS != 0 compiles a single encoding (fast-path kernels).
@@ -226,6 +233,12 @@ KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y, float& w) {
   } else if (FOBS == OBS_F32 || (FOBS == 0 && bd.obs == OBS_F32)) {
     y = bd.y[p];
     w = bd.w[p];
+    if (bd.mask && !bd.mask[p]) w = 0.f;
+    if (!(w > 0.f) || !finitef(w) || !finitef(y)) { w = 0.f; y = 0.f; }
+  } else if (FOBS == OBS_BF16 || (FOBS == 0 && bd.obs == OBS_BF16)) {
+    // bf16 (y, w) pairs: half the ingest bytes of f32; math stays f32
+    y = bf16_to_f32(reinterpret_cast<const uint16_t*>(bd.y)[p]);
+    w = bf16_to_f32(reinterpret_cast<const uint16_t*>(bd.w)[p]);
     if (bd.mask && !bd.mask[p]) w = 0.f;
     if (!(w > 0.f) || !finitef(w) || !finitef(y)) { w = 0.f; y = 0.f; }
   } else {

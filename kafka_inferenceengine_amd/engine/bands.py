@@ -47,6 +47,17 @@ class DeviceBand:
             valid = (dn > 0) & (sig > 0)
             w = torch.where(valid, 1.0 / torch.where(valid, sig * sig, torch.ones_like(sig)), torch.zeros_like(y))
             return torch.where(dn > 0, y, torch.zeros_like(y)), w
+        if self.kind == K.OBS_BF16:
+            yy = (self.y.to(torch.int32) << 16).view(torch.float32)
+            w = (self.w.to(torch.int32) << 16).view(torch.float32)
+        else:
+            yy, w = self.y, self.w.clone()
+        if self.mask is not None:
+            w = torch.where(self.mask.bool(), w, torch.zeros_like(w))
+        bad = ~torch.isfinite(w) | ~(w > 0) | ~torch.isfinite(yy)
+        return torch.where(bad, torch.zeros_like(yy), yy), torch.where(bad, torch.zeros_like(w), w)
+
+    def _decode_f32(self):
         w = self.w.clone()
         if self.mask is not None:
             w = torch.where(self.mask.bool(), w, torch.zeros_like(w))

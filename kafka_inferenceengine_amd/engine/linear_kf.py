@@ -256,6 +256,12 @@ class LinearKalman:
             d = {"m": self._m, "q": self._q}
             if prop is None and self.prior is None:
                 spec = PropagatorSpec(PROP_IDENTITY)
+            elif prop is None and prior_dev.constant:
+                # prior only (kf_tools.py:165-166): reset to the prior, no blend needed
+                d.update(mode=PROP_PRIOR, prop_mask=0, reset_mean=np.asarray(prior_dev.mean),
+                         reset_cinv=pack_matrix(np.asarray(prior_dev.cinv)))
+                out = self._run_propagate(d, analysis, None, PRECISION)
+                return self._as_kind(out, self._analysis_kind())
             elif prop is None:
                 spec = PropagatorSpec(PROP_PRIOR, reset_mean=np.zeros(n), reset_cinv=np.zeros((n, n)))
             d["mode"] = spec.mode

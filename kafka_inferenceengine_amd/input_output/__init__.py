@@ -3,6 +3,7 @@ from .checkpoint import CheckpointManager  # noqa: F401
 from .observations import ArrayObservations, BHRObservationsTest, bhr_uncertainty, get_modis_dates  # noqa: F401
 from .output import DeviceOutput, KafkaOutput, KafkaOutputMemory  # noqa: F401
 from .synthetic import (MultiSensorObservations, SyntheticBHRObservations, SyntheticObservations,  # noqa: F401
-                        SyntheticOLCIObservations, SyntheticS1Observations, SyntheticS2Observations)
+                        SyntheticIdentityObservations, SyntheticOLCIObservations, SyntheticS1Observations,
+                        SyntheticS2Observations)
 from .tiff import read_tiff, write_tiff  # noqa: F401
 from .utils import find_overlap, get_chunks, raster_extent, reproject_image  # noqa: F401

@@ -185,6 +185,8 @@ class SyntheticObservations:
         clear = cloud.at(g) <= thr
         if self.encoding == "dn16":
             out = torch.empty((self.n_bands, self.N), dtype=torch.int16, device=self.device)
+        elif self.encoding == "bf16":
+            out = torch.empty((2 * self.n_bands, self.N), dtype=torch.int16, device=self.device)
         else:
             out = torch.empty((2 * self.n_bands, self.N), dtype=torch.float32, device=self.device)
         for b in range(self.n_bands):
@@ -197,8 +199,14 @@ class SyntheticObservations:
                 out[b] = torch.where(dn > 32767, dn - 65536, dn).to(torch.int16)  # uint16 bit pattern
             else:
                 sig = torch.clamp(self.rel_unc * yb.abs(), min=max(self.unc_floor, 1e-12))
-                out[b] = torch.where(ok, yb, torch.zeros_like(yb))
-                out[self.n_bands + b] = torch.where(ok, 1.0 / (sig * sig), torch.zeros_like(yb))
+                yv = torch.where(ok, yb, torch.zeros_like(yb))
+                wv = torch.where(ok, 1.0 / (sig * sig), torch.zeros_like(yb))
+                if self.encoding == "bf16":
+                    out[b] = yv.to(torch.bfloat16).view(torch.int16)
+                    out[self.n_bands + b] = wv.to(torch.bfloat16).view(torch.int16)
+                else:
+                    out[b] = yv
+                    out[self.n_bands + b] = wv
         return out
 
     def _entry_shape(self):
@@ -208,7 +216,7 @@ class SyntheticObservations:
         if self._streamer is not None or self._pool:
             return
         if self.stream_mode:
-            dtype = torch.int16 if self.encoding == "dn16" else torch.float32
+            dtype = torch.int16 if self.encoding in ("dn16", "bf16") else torch.float32
             self._streamer = DateStreamer(self.n_pool, self._entry_shape(), dtype, self.device)
             for k in range(self.n_pool):
                 data = self._synthesize(k)
@@ -244,7 +252,8 @@ class SyntheticObservations:
             return DeviceBand(K.OBS_DN16, dn=e[band],
                               scale=self.scale, rel_unc=self.rel_unc, unc_floor=self.unc_floor, metadata=meta,
                               emulator=spec.emulator, aux=aux)
-        return DeviceBand(K.OBS_F32, y=e[band], w=e[self.n_bands + band], metadata=meta, emulator=spec.emulator,
+        kind = K.OBS_BF16 if self.encoding == "bf16" else K.OBS_F32
+        return DeviceBand(kind, y=e[band], w=e[self.n_bands + band], metadata=meta, emulator=spec.emulator,
                           aux=aux)
 
     def get_device_bands(self, date):
@@ -375,6 +384,30 @@ class SyntheticS1Observations(SyntheticObservations):
         kw.setdefault("encoding", "f32")
         kw.setdefault("temporal_params", (0, 1))
         super().__init__(state_mask, dates, specs, center, spread, lo, hi, aux=theta, **kw)
+
+
+class SyntheticIdentityObservations(SyntheticObservations):
+    """Direct (identity) observations of every state element — band k observes
+    parameter k (BASELINE config 2; the reference's identity operator,
+    utils.py:119-126, fixed).  Default encoding: bf16 (y, w) pairs."""
+
+    sensor = "identity"
+
+    def __init__(self, state_mask, dates=None, n_params=7, mean=None, sigma=None, **kw):
+        from ..models.operators import _linear_device_spec
+        from ..models.priors import tip_prior
+
+        if mean is None:
+            mean, cov, _ = tip_prior()
+            sigma = np.sqrt(np.diag(cov))
+        mean = np.asarray(mean, dtype=np.float64)[:n_params]
+        sigma = np.asarray(sigma, dtype=np.float64)[:n_params]
+        specs = [_linear_device_spec(n_params, None, None, b) for b in range(n_params)]
+        dates = dates or _date_list(dt.datetime(2017, 1, 1), 30, 5)
+        kw.setdefault("encoding", "bf16")
+        kw.setdefault("rel_unc", 0.1)
+        kw.setdefault("unc_floor", 0.01)
+        super().__init__(state_mask, dates, specs, mean, 0.5 * sigma, mean - 2 * sigma, mean + 2 * sigma, **kw)
 
 
 class MultiSensorObservations:

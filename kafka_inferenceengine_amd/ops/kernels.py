@@ -16,7 +16,7 @@ import torch
 from ..utils.blocks import ntri
 from . import _ext
 
-OBS_NONE, OBS_F32, OBS_DN16 = 0, 1, 2
+OBS_NONE, OBS_F32, OBS_DN16, OBS_BF16 = 0, 1, 2, 3
 ST_NONSPD, ST_NONFINITE, ST_BAD_OP, ST_NO_OBS, ST_FALLBACK = 1, 2, 4, 8, 16
 SUPPORTED_NP = (1, 2, 3, 4, 7, 10)
 
