@@ -89,6 +89,8 @@ PYBIND11_MODULE(_kafka_hip, m) {
       .PTR_FIELD(AnalysisArgs, x_out, float*)
       .PTR_FIELD(AnalysisArgs, a_out, float*)
       .PTR_FIELD(AnalysisArgs, b_out, float*)
+      .PTR_FIELD(AnalysisArgs, a_in, const float*)
+      .PTR_FIELD(AnalysisArgs, b_in, const float*)
       .PTR_FIELD(AnalysisArgs, status, uint8_t*)
       .PTR_FIELD(AnalysisArgs, partials, double*);
 
@@ -177,6 +179,14 @@ PYBIND11_MODULE(_kafka_hip, m) {
                                        P<float>(h), h_ld, P<uint8_t>(ok), (hipStream_t)stream), "operator_eval");
     else check_host(host_operator(np, P<const BandDesc>(bands), band, P<const float>(x), N, ld, P<float>(h0),
                                   P<float>(h), h_ld, P<uint8_t>(ok)), "operator_eval");
+  });
+  m.def("gp_operator_supported", [](int np, int d) { return gp_operator_supported(np, d); });
+  m.def("gp_operator", [](int np, int d, uintptr_t bands, int nb, uintptr_t x, int64_t N, int64_t ld, uintptr_t h0,
+                          uintptr_t h, int64_t ldh, bool device, uintptr_t stream) {
+    if (device) check_hip(dev_gp_operator(np, d, P<const BandDesc>(bands), nb, P<const float>(x), N, ld, P<float>(h0),
+                                          P<float>(h), ldh, (hipStream_t)stream), "gp_operator");
+    else check_host(host_gp_operator(np, P<const BandDesc>(bands), nb, P<const float>(x), N, ld, P<float>(h0),
+                                     P<float>(h), ldh), "gp_operator");
   });
   m.def("hessian", [](int np, uintptr_t bands, int nb, uintptr_t x, uintptr_t a, int64_t N, int64_t ld,
                       bool device, uintptr_t stream) {

@@ -87,7 +87,9 @@ struct AnalysisArgs {
   const float* pf_inv;   // [NT][ld] forecast precision (packed)
   float* x_out;          // [NP][ld]
   float* a_out;          // [NT][ld] analysis precision (may be null)
-  float* b_out;          // [NP][ld] rhs (regulariser path, may be null)
+  float* b_out;          // [NP][ld] rhs (regulariser / band-chunk path, may be null)
+  const float* a_in;     // [NT][ld] band-chunk accumulation: start from (a_in, b_in) instead of the prior
+  const float* b_in;     // [NP][ld]
   uint8_t* status;       // per-pixel flags (may be null)
   double* partials;      // per-block sum (x_out - x_prev)^2
 };
@@ -411,7 +413,13 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
   uint8_t st = 0;
 #pragma unroll
   for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
-  {
+  if (a.a_in) {
+    // band-chunked accumulation: continue from a previous chunk's (A, b)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) A[t] = a.a_in[t * ld + p];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) b[j] = a.b_in[j * ld + p];
+  } else {
     float xf[NP];
 #pragma unroll
     for (int j = 0; j < NP; ++j) xf[j] = a.x_f[j * ld + p];

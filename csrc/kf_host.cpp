@@ -82,6 +82,26 @@ static int h_operator(const BandDesc* b, int band, const float* x, int64_t N, in
   return 0;
 }
 template <int NP>
+static int h_gp_operator(const BandDesc* bands, int nb, const float* x, int64_t N, int64_t ld, float* h0, float* h,
+                         int64_t ldh) {
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < N; ++p) {
+    float xv[NP];
+    for (int j = 0; j < NP; ++j) xv[j] = x[j * ld + p];
+    for (int b = 0; b < nb; ++b) {
+      const BandDesc& bd = bands[b];
+      float y, w, H0 = 0.f, hv[NP];
+      for (int j = 0; j < NP; ++j) hv[j] = 0.f;
+      decode_obs(bd, p, y, w);
+      if (w > 0.f) eval_operator<NP>(bd, p, ld, xv, H0, hv);
+      h0[b * ldh + p] = H0;
+      for (int j = 0; j < NP; ++j) h[((int64_t)b * NP + j) * ldh + p] = hv[j];
+    }
+  }
+  return 0;
+}
+
+template <int NP>
 static int h_hessian(const BandDesc* bands, int nb, const float* x, float* a, int64_t N, int64_t ld) {
   constexpr int NT = ntri(NP);
 #pragma omp parallel for schedule(static)
@@ -128,6 +148,10 @@ int host_invert(int np, const float* src, float* dst, int64_t N, int64_t ld, uin
 int host_operator(int np, const BandDesc* b, int band, const float* x, int64_t N, int64_t ld, float* h0, float* h,
                   int64_t h_ld, uint8_t* ok) {
   KF_HOST_NP_SWITCH(np, h_operator, b, band, x, N, ld, h0, h, h_ld, ok);
+}
+int host_gp_operator(int np, const BandDesc* b, int nb, const float* x, int64_t N, int64_t ld, float* h0, float* h,
+                     int64_t ldh) {
+  KF_HOST_NP_SWITCH(np, h_gp_operator, b, nb, x, N, ld, h0, h, ldh);
 }
 int host_hessian(int np, const BandDesc* b, int nb, const float* x, float* a, int64_t N, int64_t ld) {
   KF_HOST_NP_SWITCH(np, h_hessian, b, nb, x, a, N, ld);

@@ -102,6 +102,34 @@ __global__ __launch_bounds__(BLOCK) void operator_kernel(const BandDesc* bands, 
   }
 }
 
+// K2 split path: GP emulator value + Jacobian for a chunk of bands into HBM
+// (h0[b][p], h[b*NP+j][p]).  Without the analysis' packed A/b in registers it
+// runs at high occupancy; used for large input counts (PROSAIL D=10) and many
+// bands (multi-sensor), followed by the OP_PRECOMP analysis kernel.  Pixels
+// whose observation is masked skip the GP (wave-level skip under clouds).
+template <int NP, int D>
+__global__ __launch_bounds__(BLOCK) void gp_operator_kernel(const BandDesc* bands, int nb, const float* x,
+                                                           int64_t N, int64_t ld, float* h0, float* h,
+                                                           int64_t ldh) {
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
+    float xv[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) xv[j] = x[j * ld + p];
+    for (int b = 0; b < nb; ++b) {
+      const BandDesc bd = cptr(bands)[b];
+      float y, w, H0 = 0.f, hv[NP];
+#pragma unroll
+      for (int j = 0; j < NP; ++j) hv[j] = 0.f;
+      decode_obs(bd, p, y, w);
+      if (w > 0.f) gp_eval<NP, D>(bd, xv, H0, hv);
+      h0[b * ldh + p] = H0;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) h[((int64_t)b * NP + j) * ldh + p] = hv[j];
+    }
+  }
+}
+
 // K6 Hessian correction: A -= w (y - H0(x)) d2f/dx2 for every GP band.
 template <int NP>
 __global__ __launch_bounds__(BLOCK) void hessian_kernel(const BandDesc* bands, int n_bands, const float* x,
@@ -279,6 +307,10 @@ static void l_unpack(const float* x, const float* a, int64_t N, int64_t ld, cons
 
 int dev_grid(int64_t N) { return grid_for(N, KF_MAX_BLOCKS); }
 
+bool gp_operator_supported(int np, int d) {
+  return (np == 10 && (d == 10 || d == 4)) || (np == 7 && (d == 7 || d == 4)) || (np == d && np >= 2 && np <= 4);
+}
+
 hipError_t dev_analysis(int np, const AnalysisArgs& a, int grid, hipStream_t s) {
   KF_NP_SWITCH(np, l_analysis, a, grid, s);
   return hipGetLastError();
@@ -304,6 +336,20 @@ hipError_t dev_operator(int np, const BandDesc* b, int band, const float* x, int
   KF_NP_SWITCH(np, l_operator, b, band, x, N, ld, h0, h, h_ld, ok, grid_for(N, KF_MAX_BLOCKS), s);
   return hipGetLastError();
 }
+hipError_t dev_gp_operator(int np, int d, const BandDesc* b, int nb, const float* x, int64_t N, int64_t ld,
+                           float* h0, float* h, int64_t ldh, hipStream_t s) {
+  const int g = grid_for(N, KF_MAX_BLOCKS);
+#define KF_GPOP(NP_, D_)                                                                                  \
+  if (np == NP_ && d == D_) {                                                                            \
+    hipLaunchKernelGGL((gp_operator_kernel<NP_, D_>), dim3(g), dim3(BLOCK), 0, s, b, nb, x, N, ld, h0, h, \
+                       ldh);                                                                             \
+    return hipGetLastError();                                                                            \
+  }
+  KF_GPOP(10, 10) KF_GPOP(10, 4) KF_GPOP(7, 7) KF_GPOP(7, 4) KF_GPOP(4, 4) KF_GPOP(3, 3) KF_GPOP(2, 2)
+#undef KF_GPOP
+  return hipErrorInvalidValue;
+}
+
 hipError_t dev_hessian(int np, const BandDesc* b, int nb, const float* x, float* a, int64_t N, int64_t ld,
                        hipStream_t s) {
   KF_NP_SWITCH(np, l_hessian, b, nb, x, a, N, ld, grid_for(N, KF_MAX_BLOCKS), s);

@@ -23,6 +23,9 @@ hipError_t dev_operator(int np, const BandDesc* b, int band, const float* x, int
                         float* h, int64_t h_ld, uint8_t* ok, hipStream_t s);
 hipError_t dev_hessian(int np, const BandDesc* b, int nb, const float* x, float* a, int64_t N, int64_t ld,
                        hipStream_t s);
+hipError_t dev_gp_operator(int np, int d, const BandDesc* b, int nb, const float* x, int64_t N, int64_t ld,
+                           float* h0, float* h, int64_t ldh, hipStream_t s);
+bool gp_operator_supported(int np, int d);
 hipError_t dev_unpack(int np, const float* x, const float* a, int64_t N, int64_t ld, const int64_t* idx,
                       float* mean, float* unc, int64_t plane, hipStream_t s);
 hipError_t dev_reduce(const double* partials, int n, double* out, hipStream_t s);
@@ -42,6 +45,8 @@ int host_invert(int np, const float* src, float* dst, int64_t N, int64_t ld, uin
 int host_operator(int np, const BandDesc* b, int band, const float* x, int64_t N, int64_t ld, float* h0, float* h,
                   int64_t h_ld, uint8_t* ok);
 int host_hessian(int np, const BandDesc* b, int nb, const float* x, float* a, int64_t N, int64_t ld);
+int host_gp_operator(int np, const BandDesc* b, int nb, const float* x, int64_t N, int64_t ld, float* h0, float* h,
+                     int64_t ldh);
 int host_unpack(int np, const float* x, const float* a, int64_t N, int64_t ld, const int64_t* idx, float* mean,
                 float* unc, int64_t plane);
 int host_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out);

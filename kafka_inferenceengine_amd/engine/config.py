@@ -30,6 +30,12 @@ class EngineConfig:
     spatial_gamma: float = 0.0
     spatial_params: list | None = None        # parameter indices smoothed (None: all)
     jacobi_sweeps: int = 4
+    # GP operator placement: fused into the analysis kernel, or "split" (high-
+    # occupancy operator kernel -> HBM -> analysis over band chunks)
+    gp_split: str = "auto"                    # 'auto' | 'always' | 'never'
+    gp_split_min_d: int = 7                   # auto: split when a GP band has >= this many inputs
+    gp_split_min_bands: int = 13              # auto: ... or when a date has >= this many GP bands
+    band_chunk: int = 10                      # bands per operator/accumulation chunk in split mode
     # runtime
     device: str | None = None                 # 'cuda', 'cuda:1', 'cpu' (default: cuda if present)
     prefetch: bool = True                     # overlap next date's ingest with compute

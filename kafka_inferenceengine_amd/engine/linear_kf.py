@@ -490,7 +490,8 @@ class LinearKalman:
         P_out = torch.empty_like(fc.P)
         status = torch.zeros(max(N, 1), dtype=torch.uint8, device=self.device)
         precomp = any(s.kind == OP_PRECOMP for s in specs)
-        table = None if precomp else build_table(specs, dbs, n, self._cache, self.device, h0_outs)
+        split = None if (precomp or gain or cfg.spatial_gamma > 0) else self._split_plan(specs, dbs, h0_outs)
+        table = None if (precomp or split) else build_table(specs, dbs, n, self._cache, self.device, h0_outs)
         norms = []
         n_iter = 1
         len_x = float(n * self.n_total)
@@ -505,6 +506,8 @@ class LinearKalman:
                                joseph=cfg.joseph)
                     elif cfg.spatial_gamma > 0:
                         self._regularised_iteration(table, x_prev, fc, x_new, P_out, status)
+                    elif split is not None:
+                        self._split_iteration(split, x_prev, fc, x_new, P_out, status)
                     else:
                         K.analysis(n, table, x_prev, fc.x, fc.P, x_new, P_out, None, status, self._partials, N=N)
                     K.reduce_partials(self._partials, self._red)
@@ -537,6 +540,59 @@ class LinearKalman:
                 y, w = db.decode()
                 inn.append(torch.where(w > 0, y - h0[:N], torch.zeros_like(y)))
         return AssimilationResult(state, n_iter, norms, inn)
+
+    # ------------------------------------------------ split GP operator path
+    def _split_plan(self, specs, dbs, h0_outs):
+        """Band chunks for the split path, or None for the fused kernel."""
+        from ..models.operators import OP_GP
+        cfg = self.config
+        if cfg.gp_split == "never" or not specs or any(s.kind != OP_GP for s in specs):
+            return None
+        ds = {s.d for s in specs}
+        if len(ds) != 1:
+            return None
+        d = ds.pop()
+        on_dev = self.device.type == "cuda"
+        if on_dev and not K.gp_operator_supported(self.n_params, d):
+            return None
+        if cfg.gp_split == "auto" and d < cfg.gp_split_min_d and len(specs) < cfg.gp_split_min_bands:
+            return None
+        n, N = self.n_params, self.N
+        C = max(1, min(int(cfg.band_chunk), len(specs)))
+        ldh = max(N, 1)
+        h0_buf = torch.empty((C, ldh), dtype=torch.float32, device=self.device)
+        h_buf = torch.empty((C * n, ldh), dtype=torch.float32, device=self.device)
+        chunks = []
+        for c0 in range(0, len(specs), C):
+            idx = list(range(c0, min(c0 + C, len(specs))))
+            op_tab = build_table([specs[i] for i in idx], [dbs[i] for i in idx], n, self._cache, self.device)
+            pre_specs = [OperatorSpec(OP_PRECOMP, list(range(n)), [0.0] * n) for _ in idx]
+            pre = [(h0_buf[j], h_buf[j * n:(j + 1) * n]) for j in range(len(idx))]
+            h0s = None if h0_outs is None else [h0_outs[i] for i in idx]
+            an_tab = build_table(pre_specs, [dbs[i] for i in idx], n, self._cache, self.device, h0s, pre)
+            chunks.append((op_tab, an_tab, len(idx)))
+        acc = None
+        if len(chunks) > 1:
+            acc = [(torch.empty((ntri(n), ldh), dtype=torch.float32, device=self.device),
+                    torch.empty((n, ldh), dtype=torch.float32, device=self.device)) for _ in range(2)]
+        return {"d": d, "chunks": chunks, "h0": h0_buf, "h": h_buf, "acc": acc}
+
+    def _split_iteration(self, plan, x_prev, fc: KFState, x_out, A_out, status):
+        n, N = self.n_params, self.N
+        chunks = plan["chunks"]
+        prev = None
+        for ci, (op_tab, an_tab, nb) in enumerate(chunks):
+            K.gp_operator(n, op_tab, x_prev, plan["h0"][:nb], plan["h"][:nb * n], N=N, d=plan["d"])
+            last = ci == len(chunks) - 1
+            a_in, b_in = prev if prev is not None else (None, None)
+            if last:
+                K.analysis(n, an_tab, x_prev, fc.x, fc.P, x_out, A_out, None, status, self._partials, N=N,
+                           a_in=a_in, b_in=b_in)
+            else:
+                A_c, b_c = plan["acc"][ci % 2]
+                K.analysis(n, an_tab, x_prev, fc.x, fc.P, None, A_c, b_c, status, None, N=N, solve=False,
+                           a_in=a_in, b_in=b_in)
+                prev = (A_c, b_c)
 
     def _regularised_iteration(self, table, x_prev, fc: KFState, x_out, A_out, status):
         """Assemble (A, b) with the fused kernel, then block-Jacobi sweeps of the

@@ -1,0 +1,284 @@
+"""File-based sensor readers (Sentinel-2 L2A granules, Sentinel-1 sigma0,
+MODIS MCD43 BRDF kernels) with the reference observation protocol.
+
+GDAL/NetCDF/HDF4 are not available in this stack, so the readers consume
+GeoTIFF rasters (``input_output.tiff``) laid out like the reference's inputs:
+
+* Sentinel-2 (``Sentinel2_Observations.py:85-185``): a granule folder
+  ``.../YYYY/MM/DD/<granule>/`` containing ``aot.tif`` (discovery marker),
+  ``B{02..12}_sur.tif`` (uint16 surface reflectance x 1e4, 0 = no data) and
+  ``metadata.xml`` (mean sun/view angles, ``parse_xml``).  The emulator is
+  chosen per date by nearest (sza, vza, raa) from file names
+  ``*_{vza}_{sza}_{raa}.npz`` (``_find_emulator``, :133-145) and loaded with
+  ``numpy.load(allow_pickle=False)`` — never unpickled.
+* Sentinel-1 (``Sentinel1_Observations.py:56-197``): ``S1_*_{YYYYmmddTHHMMSS}_*``
+  folders with ``sigma0_VV.tif``, ``sigma0_VH.tif``, ``theta.tif``; -999 = no data;
+  5 % uncertainty.
+* MCD43 BHR (``observations.py:214-310``): per date ``{date}_kernels_b{band}.tif``
+  3-band-as-3-files kernel weights + ``{date}_qa.tif``; BHR = K . [1, 0.189184,
+  -1.377622]; sigma = max(2.5e-3, 5 %/7 % BHR) by QA level.
+"""
+from __future__ import annotations
+
+import datetime
+import glob
+import os
+import xml.etree.ElementTree as ET
+from collections import namedtuple
+
+import numpy as np
+import scipy.sparse as sp
+
+from ..models.gp import GaussianProcessEmulator
+from .tiff import read_tiff
+
+S2MSIdata = namedtuple("S2MSIdata", "observations uncertainty mask metadata emulator")
+SARdata = namedtuple("SARdata", "observations uncertainty mask metadata emulator")
+BHR_data = namedtuple("BHR_data", "observations mask uncertainty metadata emulator")
+MOD09_data = namedtuple("MOD09_data", "reflectance mask uncertainty obs_op sza vza raa")
+
+S2_BAND_MAP = ["02", "03", "04", "05", "06", "07", "08", "8A", "09", "12"]
+S2_EMULATOR_BANDS = [2, 3, 4, 5, 6, 7, 8, 9, 12, 13]
+TO_BHR = np.array([1.0, 0.189184, -1.377622])
+WRONG_VALUE = -999.0
+
+
+# ------------------------------------------------------------- emulators
+def save_emulator(path, em: GaussianProcessEmulator, **extra):
+    """Emulator -> .npz (plain arrays only; loadable without pickle)."""
+    np.savez(path, inputs=em.inputs, alpha=em.alpha, lam=em.lam, signal=np.array(em.signal),
+             mean=np.array(em.mean), name=np.array(em.name), **extra)
+
+
+def load_emulator(path) -> GaussianProcessEmulator:
+    with np.load(path, allow_pickle=False) as z:
+        return GaussianProcessEmulator(z["inputs"], z["alpha"], z["lam"], float(z["signal"]), float(z["mean"]),
+                                       name=str(z["name"]))
+
+
+def load_emulator_set(path) -> dict:
+    """Multi-band emulator file: keys ``{band}__inputs`` etc. -> {band: emulator}."""
+    out = {}
+    with np.load(path, allow_pickle=False) as z:
+        bands = sorted({k.split("__")[0] for k in z.files if "__" in k})
+        for b in bands:
+            out[b] = GaussianProcessEmulator(z[f"{b}__inputs"], z[f"{b}__alpha"], z[f"{b}__lam"],
+                                             float(z[f"{b}__signal"]), float(z[f"{b}__mean"]), name=b)
+    return out
+
+
+def save_emulator_set(path, ems: dict):
+    arrs = {}
+    for b, em in ems.items():
+        arrs.update({f"{b}__inputs": em.inputs, f"{b}__alpha": em.alpha, f"{b}__lam": em.lam,
+                     f"{b}__signal": np.array(em.signal), f"{b}__mean": np.array(em.mean)})
+    np.savez(path, **arrs)
+
+
+# ------------------------------------------------------------- helpers
+def parse_xml(meta_file):
+    """Mean sun/view zenith/azimuth from an S2 L1C tile metadata XML (:23-53)."""
+    tree = ET.parse(meta_file)
+    root = tree.getroot()
+
+    def first(tag):
+        for el in root.iter():
+            if el.tag.split("}")[-1] == tag:
+                return el
+        return None
+    sun = first("Mean_Sun_Angle")
+    sza = float(sun.find("ZENITH_ANGLE").text)
+    saa = float(sun.find("AZIMUTH_ANGLE").text)
+    vzas, vaas = [], []
+    for el in root.iter():
+        if el.tag.split("}")[-1] == "Mean_Viewing_Incidence_Angle":
+            vzas.append(float(el.find("ZENITH_ANGLE").text))
+            vaas.append(float(el.find("AZIMUTH_ANGLE").text))
+    return sza, saa, float(np.mean(vzas)), float(np.mean(vaas))
+
+
+def write_s2_metadata(path, sza, saa, vza, vaa, n_bands=13):
+    views = "".join(f'<Mean_Viewing_Incidence_Angle bandId="{b}"><ZENITH_ANGLE unit="deg">{vza}</ZENITH_ANGLE>'
+                    f'<AZIMUTH_ANGLE unit="deg">{vaa}</AZIMUTH_ANGLE></Mean_Viewing_Incidence_Angle>'
+                    for b in range(n_bands))
+    xml = (f'<?xml version="1.0"?><Level-1C_Tile_ID><Geometric_Info><Tile_Angles><Mean_Sun_Angle>'
+           f'<ZENITH_ANGLE unit="deg">{sza}</ZENITH_ANGLE><AZIMUTH_ANGLE unit="deg">{saa}</AZIMUTH_ANGLE>'
+           f'</Mean_Sun_Angle><Mean_Viewing_Incidence_Angle_List>{views}</Mean_Viewing_Incidence_Angle_List>'
+           f'</Tile_Angles></Geometric_Info></Level-1C_Tile_ID>')
+    with open(path, "w") as f:
+        f.write(xml)
+
+
+def _weights(sigma, mask):
+    with np.errstate(divide="ignore"):
+        w = np.where(mask & (sigma > 0), 1.0 / np.where(sigma > 0, sigma, 1.0) ** 2, 0.0)
+    return sp.dia_matrix((w.ravel(), 0), shape=(w.size, w.size)).tocsr()
+
+
+def _crop(a, roi):
+    if roi is None:
+        return a
+    ulx, uly, lrx, lry = roi
+    return a[uly:lry, ulx:lrx]
+
+
+# ------------------------------------------------------------- Sentinel-2
+class Sentinel2Observations:
+    def __init__(self, parent_folder, emulator_folder, state_mask, chunk=None, roi=None, rel_unc=0.05):
+        if not os.path.exists(parent_folder):
+            raise IOError("S2 data folder doesn't exist")
+        self.parent = parent_folder
+        self.emulator_folder = emulator_folder
+        self.state_mask = state_mask
+        self.roi = roi
+        self.rel_unc = rel_unc
+        self.band_map = list(S2_BAND_MAP)
+        self.emulator_files = sorted(glob.glob(os.path.join(emulator_folder, "*.npz")))
+        self._find_granules(parent_folder)
+        self._emu_cache = {}
+        self.chunk = chunk
+
+    def _find_granules(self, parent_folder):
+        self.dates, self.date_data = [], {}
+        for root, dirs, files in os.walk(parent_folder):
+            if "aot.tif" in files:
+                parts = root.rstrip("/").split("/")
+                y, m, d = (int(v) for v in parts[-4:-1])
+                date = datetime.datetime(y, m, d)
+                self.dates.append(date)
+                self.date_data[date] = root
+        self.dates.sort()
+        self.bands_per_observation = {d: len(self.band_map) for d in self.dates}
+
+    def define_output(self):
+        ref = glob.glob(os.path.join(self.date_data[self.dates[0]], "B02_sur.tif"))
+        info = read_tiff(ref[0])[1] if ref else {}
+        return info.get("projection", ""), info.get("geotransform", [0, 1, 0, 0, 0, -1])
+
+    def _find_emulator(self, sza, saa, vza, vaa):
+        raa = vaa - saa
+        vzas = np.array([float(os.path.basename(s).split("_")[-3]) for s in self.emulator_files])
+        szas = np.array([float(os.path.basename(s).split("_")[-2]) for s in self.emulator_files])
+        raas = np.array([float(os.path.basename(s).split("_")[-1].rsplit(".", 1)[0]) for s in self.emulator_files])
+        e1 = szas == szas[np.argmin(np.abs(szas - sza))]
+        e2 = vzas == vzas[np.argmin(np.abs(vzas - vza))]
+        e3 = raas == raas[np.argmin(np.abs(raas - raa))]
+        hit = np.where(e1 * e2 * e3)[0]
+        if hit.size:
+            return self.emulator_files[hit[0]]
+        # no file matches all three independently-nearest angles (the reference
+        # would raise IndexError here): nearest in joint angle space
+        dist = (szas - sza) ** 2 + (vzas - vza) ** 2 + (raas - raa) ** 2
+        return self.emulator_files[int(np.argmin(dist))]
+
+    def get_band_data(self, timestep, band):
+        folder = self.date_data[timestep]
+        sza, saa, vza, vaa = parse_xml(os.path.join(folder, "metadata.xml"))
+        metadata = dict(zip(["sza", "saa", "vza", "vaa"], [sza, saa, vza, vaa]))
+        efile = self._find_emulator(sza, saa, vza, vaa)
+        if efile not in self._emu_cache:  # the reference re-unpickled per band and iteration
+            self._emu_cache[efile] = load_emulator_set(efile)
+        rho, _ = read_tiff(os.path.join(folder, f"B{self.band_map[band]}_sur.tif"))
+        rho = _crop(rho.astype(np.float64), self.roi)
+        mask = rho > 0
+        rho = np.where(mask, rho / 10000., 0.0)
+        unc = _weights(rho * self.rel_unc, mask)
+        key = f"S2A_MSI_{S2_EMULATOR_BANDS[band]:02d}"
+        return S2MSIdata(rho, unc, mask, metadata, self._emu_cache[efile].get(key))
+
+
+# ------------------------------------------------------------- Sentinel-1
+class S1Observations:
+    POLS = ("VV", "VH")
+
+    def __init__(self, data_folder, state_mask, emulators=None, roi=None, rel_unc=0.05):
+        self.state_mask = state_mask
+        self.roi = roi
+        self.rel_unc = rel_unc
+        self.dates, self.date_data = [], {}
+        for d in sorted(glob.glob(os.path.join(data_folder, "S1_*"))):
+            fields = os.path.basename(d).split("_")
+            date = datetime.datetime.strptime(fields[5] if len(fields) > 5 else fields[-1], "%Y%m%dT%H%M%S")
+            self.dates.append(date)
+            self.date_data[date] = d
+        self.emulators = emulators or {"VV": None, "VH": None}
+        self.bands_per_observation = {d: 2 for d in self.dates}
+
+    def get_band_data(self, timestep, band):
+        pol = self.POLS[band]
+        folder = self.date_data[timestep]
+        s0, _ = read_tiff(os.path.join(folder, f"sigma0_{pol}.tif"))
+        s0 = _crop(s0.astype(np.float64), self.roi)
+        mask = s0 != WRONG_VALUE
+        unc = _weights(np.where(mask, s0 * self.rel_unc, 0.0), mask)
+        theta, _ = read_tiff(os.path.join(folder, "theta.tif"))
+        meta = {"incidence_angle": _crop(theta.astype(np.float64), self.roi)}
+        return SARdata(np.where(mask, s0, 0.0), unc, mask, meta, self.emulators.get(pol))
+
+
+# ------------------------------------------------------------- MODIS BHR
+class BHRObservations:
+    """MCD43-like broadband BHR observations (VIS/NIR) from kernel-weight rasters."""
+
+    def __init__(self, emulator, folder, start_time=None, end_time=None, period=16, ulx=0, uly=0, lrx=None,
+                 lry=None):
+        self.emulator = emulator if not isinstance(emulator, (str, os.PathLike)) else load_emulator_set(emulator)
+        files = sorted(glob.glob(os.path.join(folder, "*_kernels_b0_k0.tif")))
+        dates = [datetime.datetime.strptime(os.path.basename(f).split("_")[0], "A%Y%j") for f in files]
+        if start_time is not None:
+            dates = [d for d in dates if d >= start_time]
+        if end_time is not None:
+            dates = [d for d in dates if d <= end_time]
+        self.folder = folder
+        self.dates = dates[::period]
+        self.bands_per_observation = {d: 2 for d in self.dates}
+        self.apply_roi(ulx, uly, lrx, lry)
+
+    def apply_roi(self, ulx, uly, lrx, lry):
+        self.ulx, self.uly, self.lrx, self.lry = ulx, uly, lrx, lry
+        self.roi = None if lrx is None else [ulx, uly, lrx, lry]
+
+    def define_output(self):
+        f = glob.glob(os.path.join(self.folder, self.dates[0].strftime("A%Y%j") + "_kernels_b0_k0.tif"))[0]
+        info = read_tiff(f)[1]
+        gt = list(info.get("geotransform", [0, 1, 0, 0, 0, -1]))
+        gt[0] += self.ulx * gt[1]
+        gt[3] += self.uly * gt[5]
+        return info.get("projection", ""), gt
+
+    def get_band_data(self, the_date, band_no):
+        tag = the_date.strftime("A%Y%j")
+        try:
+            K = np.stack([read_tiff(os.path.join(self.folder, f"{tag}_kernels_b{band_no}_k{k}.tif"))[0]
+                          for k in range(3)]).astype(np.float64)
+        except FileNotFoundError:
+            return None
+        qa, _ = read_tiff(os.path.join(self.folder, f"{tag}_qa.tif"))
+        K = np.stack([_crop(k, self.roi) for k in K])
+        qa = _crop(qa, self.roi)
+        mask = (qa <= 1) & np.all(np.isfinite(K), axis=0)
+        bhr = np.where(mask, np.tensordot(TO_BHR, K, axes=1), 0.0)
+        sig = np.where(qa == 1, np.maximum(2.5e-3, 0.07 * bhr), np.maximum(2.5e-3, 0.05 * bhr))
+        em = self.emulator[band_no] if isinstance(self.emulator, (list, tuple)) else \
+            (self.emulator.get(str(band_no)) if isinstance(self.emulator, dict) else self.emulator)
+        return BHR_data(bhr, mask, _weights(sig, mask), None, em)
+
+
+# ------------------------------------------------------------- Ross-Li
+def ross_li_kernels(vza, sza, raa, br=1.0, hb=2.0):
+    """RossThick and LiSparse-Reciprocal BRDF kernels (angles in degrees) — the
+    MODIS kernel model the reference obtains from SIAC (observations.py:141-143)."""
+    vz, sz, ra = (np.deg2rad(np.asarray(a, dtype=np.float64)) for a in (vza, sza, raa))
+    cos_xi = np.cos(sz) * np.cos(vz) + np.sin(sz) * np.sin(vz) * np.cos(ra)
+    xi = np.arccos(np.clip(cos_xi, -1, 1))
+    k_vol = ((np.pi / 2 - xi) * cos_xi + np.sin(xi)) / (np.cos(sz) + np.cos(vz)) - np.pi / 4
+    tvp = np.arctan(br * np.tan(vz))
+    tip = np.arctan(br * np.tan(sz))
+    cos_xip = np.cos(tip) * np.cos(tvp) + np.sin(tip) * np.sin(tvp) * np.cos(ra)
+    D = np.sqrt(np.tan(tip) ** 2 + np.tan(tvp) ** 2 - 2 * np.tan(tip) * np.tan(tvp) * np.cos(ra))
+    sec = 1 / np.cos(tip) + 1 / np.cos(tvp)
+    cos_t = np.clip(hb * np.sqrt(D ** 2 + (np.tan(tip) * np.tan(tvp) * np.sin(ra)) ** 2) / sec, -1, 1)
+    t = np.arccos(cos_t)
+    O = (t - np.sin(t) * cos_t) * sec / np.pi
+    k_geo = O - sec + 0.5 * (1 + cos_xip) / np.cos(tip) / np.cos(tvp)
+    return np.ones_like(k_vol), k_vol, k_geo

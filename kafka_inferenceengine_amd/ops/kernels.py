@@ -107,8 +107,28 @@ def make_band_table(descs: list, device, keepalive=()) -> BandTable:
 
 
 # ------------------------------------------------------------------ ops
+def gp_operator(n_params, bands: BandTable, x, h0, h, N=None, d=None):
+    """K2 split path: GP value/Jacobian of every band of ``bands`` at x into
+    h0 [nb, ldh] and h [nb*n_params, ldh] (masked pixels: zeros)."""
+    check_np(n_params)
+    N = int(x.shape[1] if N is None else N)
+    _check_soa(x, n_params, N, "x")
+    nb = bands.n
+    d = bands.fast_d if d is None else d
+    if h0.shape[0] != nb or h.shape[0] != nb * n_params or h0.shape[1] != h.shape[1] or h0.shape[1] < N:
+        raise ValueError("h0 must be [nb, ldh] and h [nb*n_params, ldh]")
+    if _dev(x) and not ext().gp_operator_supported(n_params, int(d)):
+        raise ValueError(f"no gp_operator kernel for n_params={n_params}, d={d}")
+    ext().gp_operator(n_params, int(d), bands.ptr, nb, _ptr(x), N, x.shape[1], _ptr(h0), _ptr(h), h0.shape[1],
+                      _dev(x), _stream(x))
+
+
+def gp_operator_supported(n_params, d) -> bool:
+    return bool(ext().gp_operator_supported(int(n_params), int(d)))
+
+
 def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=None, b_out=None, status=None,
-             partials=None, N=None, solve=True, fast=True, variant=0):
+             partials=None, N=None, solve=True, fast=True, variant=0, a_in=None, b_in=None):
     """K1 fused Gauss-Newton analysis (information form)."""
     check_np(n_params)
     N = int(x_prev.shape[1] if N is None else N)
@@ -133,6 +153,11 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     a.bands = bands.ptr
     a.x_prev, a.x_f, a.pf_inv = _ptr(x_prev), _ptr(x_f), _ptr(pf_inv)
     a.x_out, a.a_out, a.b_out = _ptr(x_out), _ptr(a_out), _ptr(b_out)
+    if (a_in is None) != (b_in is None):
+        raise ValueError("a_in and b_in go together")
+    _check_soa(a_in, nt, N, "a_in", device=dev)
+    _check_soa(b_in, n_params, N, "b_in", device=dev)
+    a.a_in, a.b_in = _ptr(a_in), _ptr(b_in)
     a.status, a.partials = _ptr(status), _ptr(partials)
     grid = grid_for(N)
     ext().analysis(n_params, a, grid, _dev(x_prev), _stream(x_prev))

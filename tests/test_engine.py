@@ -184,3 +184,22 @@ def test_sar_engine_runs_and_recovers():
 def test_invalid_n_params_rejected():
     with pytest.raises(ValueError):
         k.LinearKalman(None, None, np.ones((2, 2), bool), None, ["a"] * 11)
+
+
+@pytest.mark.parametrize("chunk", [10, 3])
+def test_split_gp_operator_path_equals_fused(chunk):
+    """Split path (operator kernel -> HBM -> band-chunked accumulation) == fused kernel."""
+    mask = np.ones((10, 9), bool)
+    obs = k.SyntheticS2Observations(mask, n_bands=10, n_train=30, device="cpu", stream=False, n_pool=2,
+                                    field_cell=4)
+    prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
+    x0, Pinv = prior.process_prior(None)
+    grid = [obs.dates[0] - dt.timedelta(days=1), obs.dates[1] + dt.timedelta(days=1)]
+    res = []
+    for mode in ("never", "always"):
+        kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
+                            state_propagation=None, prior=prior, device="cpu",
+                            config=k.EngineConfig(gp_split=mode, band_chunk=chunk, return_innovations=True))
+        res.append(kf.run(grid, x0, None, Pinv))
+    assert torch.allclose(res[0].x, res[1].x, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(res[0].P, res[1].P, rtol=1e-4, atol=1e-2)

@@ -161,3 +161,18 @@ def test_spatial_regulariser_gpu_matches_cpu(cuda):
         st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
         outs.append(st.x.cpu())
     assert close(outs[0], outs[1], 2e-3)
+
+
+def test_split_gp_path_gpu_matches_fused(cuda):
+    mask = np.ones((40, 32), bool)
+    outs = []
+    for mode in ("never", "always"):
+        obs = k.SyntheticS2Observations(mask, n_bands=10, n_train=40, device=cuda, stream=False, n_pool=2,
+                                        field_cell=8)
+        prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
+        kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
+                            state_propagation=None, prior=prior, device=cuda,
+                            config=k.EngineConfig(gp_split=mode, band_chunk=4))
+        grid = [obs.dates[0] - dt.timedelta(days=1), obs.dates[1] + dt.timedelta(days=1)]
+        outs.append(kf.run(grid, kf.state_from_prior(prior), None, None).x.cpu())
+    assert close(outs[0], outs[1], 1e-3)
