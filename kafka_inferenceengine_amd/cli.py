@@ -1,0 +1,219 @@
+"""Command-line drivers (the reference's de-facto CLI are its three driver
+scripts):
+
+  run    — assimilation run: TIP/BHR (kafka_test.py), S2 PROSAIL (kafka_test_S2.py),
+           S1 SAR, identity, multi-sensor; synthetic sensors or file readers;
+           GeoTIFF or in-memory output; checkpoint/resume; metrics JSONL.
+           Launch with torchrun for tile-DP over GPUs.
+  farm   — chunk farming over ranks (kafka_test_Py36.py: get_chunks + client.map).
+  chunks — print get_chunks(nx, ny, block).
+  info   — device, native extension and compiled kernel sizes.
+
+Examples:
+  python -m kafka_inferenceengine_amd run --sensor bhr --size 2400 2400 --steps 23 --out /tmp/kafka
+  torchrun --nproc-per-node 8 -m kafka_inferenceengine_amd run --sensor s2 --size 10980 10980
+  python -m kafka_inferenceengine_amd run --sensor s2 --s2-folder DATA --emulator-folder EMUS --mask mask.tif
+"""
+from __future__ import annotations
+
+import argparse
+import datetime as dt
+import json
+import logging
+import sys
+
+import numpy as np
+
+
+def _mask(args):
+    from .input_output.tiff import read_tiff
+
+    if args.mask:
+        m, info = read_tiff(args.mask)
+        return m.astype(bool), info
+    h, w = args.size
+    return np.ones((h, w), dtype=bool), {}
+
+
+def _build(args, comm):
+    import kafka_inferenceengine_amd as k
+    from .parallel import StripPartition
+
+    mask, info = _mask(args)
+    part = StripPartition(mask, comm.rank, comm.world)
+    dev = comm.device
+    cfg = k.EngineConfig.from_args(args)
+    syn = dict(partition=part, device=dev, stream=True, cloud_fraction=args.cloud, seed=args.seed)
+    if args.sensor == "bhr":
+        obs = k.SyntheticBHRObservations(mask, n_train=args.n_train or 500, **syn)
+        params, factory = k.TIP_PARAMETERS, k.create_nonlinear_observation_operator
+        prior = k.JRCPrior(params, mask)
+        prop = k.propagate_information_filter_LAI
+        q = np.array([0, 0, 0, 0, 0, 0, 0.04])
+        step = 16
+    elif args.sensor in ("s2", "multisensor"):
+        if args.s2_folder:
+            from .input_output.sentinel import Sentinel2Observations
+            obs = Sentinel2Observations(args.s2_folder, args.emulator_folder, mask)
+        elif args.sensor == "s2":
+            obs = k.SyntheticS2Observations(mask, n_bands=10, n_train=args.n_train or 250, **syn)
+        else:
+            obs = k.MultiSensorObservations([
+                k.SyntheticS2Observations(mask, n_bands=13, n_train=args.n_train or 250, **syn),
+                k.SyntheticOLCIObservations(mask, n_bands=21, n_train=args.n_train or 250,
+                                            **{**syn, "seed": args.seed + 21})])
+        params, factory = k.SAIL_PARAMETERS, k.create_prosail_observation_operator
+        prior = k.SAILPrior(params, mask)
+        prop, q, step = None, None, 2
+    elif args.sensor == "s1":
+        obs = k.SyntheticS1Observations(mask, **syn)
+        params, factory = ["lai", "sm"], k.create_sar_observation_operator
+        prior = k.GaussianPrior(params, mask, [2.0, 0.25], np.diag([1.0, 0.01]))
+        prop, q, step = None, None, 6
+    elif args.sensor == "identity":
+        obs = k.SyntheticIdentityObservations(mask, **syn)
+        params, factory = k.TIP_PARAMETERS, k.create_linear_observation_operator
+        prior = k.JRCPrior(params, mask)
+        prop = k.propagate_information_filter_LAI
+        q = np.array([0, 0, 0, 0, 0, 0, 0.04])
+        step = 5
+    else:
+        raise SystemExit(f"unknown sensor {args.sensor}")
+    if args.out:
+        out = k.KafkaOutput(params, info.get("geotransform", [0, 1, 0, 0, 0, -1]), info.get("projection", ""),
+                            args.out, prefix=args.prefix)
+    else:
+        out = k.DeviceOutput(params)
+    kf = k.LinearKalman(obs, out, mask, factory, params, state_propagation=prop,
+                        prior=None if prop is not None else prior, config=cfg, comm=comm, partition=part)
+    kf.set_trajectory_model()
+    if q is not None:
+        kf.set_trajectory_uncertainty(q)
+    dates = sorted(obs.dates)
+    n = min(args.steps, len(dates)) if args.steps else len(dates)
+    grid = [dates[0] - dt.timedelta(days=1)] + [dates[0] + dt.timedelta(days=step * (i + 1) - 1) for i in range(n)]
+    return kf, prior, grid, out
+
+
+def cmd_run(args):
+    from .parallel import Comm
+
+    comm = Comm.from_env(device=args.device)
+    if not comm.distributed:
+        import torch
+        dev = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
+        comm = Comm.single(dev if dev != "cuda" else torch.device("cuda", torch.cuda.current_device()))
+    kf, prior, grid, out = _build(args, comm)
+    start = None
+    if args.resume:
+        from .input_output.checkpoint import CheckpointManager
+        path = CheckpointManager.latest(args.resume) if not args.resume.endswith("manifest.json") else args.resume
+        state = kf.run(grid, None, None, None, resume_from=path)
+    else:
+        start = kf.state_from_prior(prior)
+        state = kf.run(grid, start, None, None)
+    if hasattr(out, "flush"):
+        out.flush()
+    if comm.rank == 0:
+        print(json.dumps({"timesteps": len(kf.history), "pixels": kf.n_total,
+                          "gn_iterations": [h.get("gn_iterations") for h in kf.history],
+                          "finite": bool(np.isfinite(state.x[:, :state.N].cpu().numpy()).all())}))
+    comm.destroy()
+
+
+def cmd_farm(args):
+    """Independent engine per chunk, chunks round-robin over ranks."""
+    import torch
+
+    import kafka_inferenceengine_amd as k
+    from .parallel import Comm
+    from .parallel.farm import run_chunks
+
+    comm = Comm.from_env(device=args.device)
+    mask, _ = _mask(args)
+    H, W = mask.shape
+
+    def fn(chunk):
+        x0, y0, w, h, no = chunk
+        sub = mask[y0:y0 + h, x0:x0 + w]
+        dev = comm.device if comm.distributed else torch.device("cuda" if torch.cuda.is_available() else "cpu")
+        obs = k.SyntheticBHRObservations(sub, n_train=args.n_train or 200, device=dev, stream=False,
+                                         seed=args.seed + no)
+        out = k.KafkaOutput(k.TIP_PARAMETERS, None, "", args.out, prefix=hex(no)) if args.out else None
+        kf = k.LinearKalman(obs, out, sub, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device=dev)
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.025]))
+        grid = [obs.dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in obs.dates[:args.steps]]
+        st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, sub)), None, None)
+        if out is not None:
+            out.flush()
+        return int(st.N)
+
+    res = run_chunks(W, H, args.block, fn, comm if comm.distributed else None, skip_empty_mask=mask)
+    if res is not None:
+        print(json.dumps({"chunks": len(res), "pixels": sum(v or 0 for v in res.values())}))
+    comm.destroy()
+
+
+def cmd_chunks(args):
+    from .input_output.utils import get_chunks
+
+    for c in get_chunks(args.nx, args.ny, args.block):
+        print(*c)
+
+
+def cmd_info(args):
+    import torch
+
+    from .ops import SUPPORTED_NP, ext_path
+
+    print(json.dumps({"torch": torch.__version__, "hip": torch.version.hip, "gpu": torch.cuda.is_available(),
+                      "device_name": torch.cuda.get_device_name(0) if torch.cuda.is_available() else None,
+                      "extension": ext_path(), "compiled_n_params": list(SUPPORTED_NP)}))
+
+
+def main(argv=None):
+    from .engine.config import EngineConfig
+
+    ap = argparse.ArgumentParser(prog="kafka_inferenceengine_amd")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    r = sub.add_parser("run", help="assimilation run")
+    r.add_argument("--sensor", default="bhr", choices=["bhr", "s2", "s1", "identity", "multisensor"])
+    r.add_argument("--size", type=int, nargs=2, default=[512, 512], metavar=("H", "W"))
+    r.add_argument("--mask", default=None, help="state mask GeoTIFF (non-zero = active)")
+    r.add_argument("--s2-folder", default=None)
+    r.add_argument("--emulator-folder", default=None)
+    r.add_argument("--steps", type=int, default=0, help="time steps (0: all dates)")
+    r.add_argument("--n-train", type=int, default=None)
+    r.add_argument("--cloud", type=float, default=0.2)
+    r.add_argument("--seed", type=int, default=0)
+    r.add_argument("--out", default=None, help="GeoTIFF output folder (default: device-resident output)")
+    r.add_argument("--prefix", default=None)
+    r.add_argument("--resume", default=None, help="checkpoint directory (latest) or checkpoint path")
+    r.add_argument("--log-level", default="WARNING")
+    EngineConfig.add_arguments(r)
+    r.set_defaults(fn=cmd_run)
+    f = sub.add_parser("farm", help="chunk farming over ranks (kafka_test_Py36.py)")
+    f.add_argument("--size", type=int, nargs=2, default=[512, 512], metavar=("H", "W"))
+    f.add_argument("--mask", default=None)
+    f.add_argument("--block", type=int, nargs=2, default=[256, 256])
+    f.add_argument("--steps", type=int, default=4)
+    f.add_argument("--n-train", type=int, default=None)
+    f.add_argument("--seed", type=int, default=0)
+    f.add_argument("--out", default=None)
+    f.add_argument("--device", default=None)
+    f.set_defaults(fn=cmd_farm)
+    c = sub.add_parser("chunks", help="print get_chunks")
+    c.add_argument("nx", type=int)
+    c.add_argument("ny", type=int)
+    c.add_argument("--block", type=int, nargs=2, default=[256, 256])
+    c.set_defaults(fn=cmd_chunks)
+    i = sub.add_parser("info")
+    i.set_defaults(fn=cmd_info)
+    args = ap.parse_args(argv)
+    if getattr(args, "log_level", None):
+        logging.basicConfig(level=getattr(logging, args.log_level.upper()), stream=sys.stderr)
+    args.fn(args)
+
+
+if __name__ == "__main__":
+    main()
