@@ -73,6 +73,10 @@ PYBIND11_MODULE(_kafka_hip, m) {
     return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(BandDesc));
   });
 
+  m.def("pack_prop_args", [](const PropArgs& a) {
+    return py::bytes(reinterpret_cast<const char*>(&a), sizeof(PropArgs));
+  });
+
   py::class_<AnalysisArgs>(m, "AnalysisArgs")
       .def(py::init([]() { AnalysisArgs a; memset(&a, 0, sizeof(a)); return a; }))
       .def_readwrite("N", &AnalysisArgs::N)
@@ -92,7 +96,8 @@ PYBIND11_MODULE(_kafka_hip, m) {
       .PTR_FIELD(AnalysisArgs, a_in, const float*)
       .PTR_FIELD(AnalysisArgs, b_in, const float*)
       .PTR_FIELD(AnalysisArgs, status, uint8_t*)
-      .PTR_FIELD(AnalysisArgs, partials, double*);
+      .PTR_FIELD(AnalysisArgs, partials, double*)
+      .PTR_FIELD(AnalysisArgs, prop, const PropArgs*);
 
   py::class_<GainArgs>(m, "GainArgs")
       .def(py::init([]() { GainArgs a; memset(&a, 0, sizeof(a)); return a; }))

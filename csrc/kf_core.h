@@ -76,24 +76,6 @@ struct BandDesc {
   int64_t pre_ld;              // leading dim of pre_h
 };
 
-struct AnalysisArgs {
-  int64_t N, ld;
-  int32_t n_bands, solve;
-  int32_t fast_d, fast_obs;  // host hint: all bands GP with fast_d inputs, one encoding (0: generic)
-  int32_t variant, pad1;     // kernel variant selector (tuning; 0 = default)
-  const BandDesc* bands;
-  const float* x_prev;   // [NP][ld] linearisation point
-  const float* x_f;      // [NP][ld] forecast mean
-  const float* pf_inv;   // [NT][ld] forecast precision (packed)
-  float* x_out;          // [NP][ld]
-  float* a_out;          // [NT][ld] analysis precision (may be null)
-  float* b_out;          // [NP][ld] rhs (regulariser / band-chunk path, may be null)
-  const float* a_in;     // [NT][ld] band-chunk accumulation: start from (a_in, b_in) instead of the prior
-  const float* b_in;     // [NP][ld]
-  uint8_t* status;       // per-pixel flags (may be null)
-  double* partials;      // per-block sum (x_out - x_prev)^2
-};
-
 struct PropArgs {
   int64_t N, ld;
   int32_t mode, blend, quirk_blend, pad0;
@@ -113,6 +95,27 @@ struct PropArgs {
   const float* blend_cinv_pix;   // optional per-pixel prior precision [NT][ld]
   uint8_t* status;
 };
+
+struct AnalysisArgs {
+  int64_t N, ld;
+  int32_t n_bands, solve;
+  int32_t fast_d, fast_obs;  // host hint: all bands GP with fast_d inputs, one encoding (0: generic)
+  int32_t variant;           // kernel variant selector (tuning; 0 = default)
+  int32_t pad1;
+  const BandDesc* bands;
+  const float* x_prev;   // [NP][ld] linearisation point
+  const float* x_f;      // [NP][ld] forecast mean
+  const float* pf_inv;   // [NT][ld] forecast precision (packed)
+  float* x_out;          // [NP][ld]
+  float* a_out;          // [NT][ld] analysis precision (may be null)
+  float* b_out;          // [NP][ld] rhs (regulariser / band-chunk path, may be null)
+  const float* a_in;     // [NT][ld] band-chunk accumulation: start from (a_in, b_in) instead of the prior
+  const float* b_in;     // [NP][ld]
+  uint8_t* status;       // per-pixel flags (may be null)
+  double* partials;      // per-block sum (x_out - x_prev)^2
+  const PropArgs* prop;  // fused propagation (device copy; x_f / pf_inv unused, x_prev null = linearise at the forecast)
+};
+
 
 // ---------------------------------------------------------------------------
 // small helpers
@@ -144,6 +147,18 @@ KF_HD bool finitef(float v) { return v - v == 0.f; }
 #endif
 template <typename T>
 KF_HD const KF_CONST_AS T* cptr(const T* p) { return (const KF_CONST_AS T*)(p); }
+
+// Opaque copy of a wave-uniform pointer: loads through the result cannot be
+// hoisted out of the enclosing (pixel) loop, so rarely used constants are
+// re-fetched with s_load where needed instead of pinning SGPRs (and spilling
+// them to VGPR lanes) across the GP loop.
+template <typename T>
+KF_HD const KF_CONST_AS T* opaque(const KF_CONST_AS T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+s"(p));
+#endif
+  return p;
+}
 
 // In-place packed Cholesky A = U^T U (U upper, stored in A's packed slots).
 template <int NP>
@@ -399,112 +414,36 @@ KF_HD bool eval_operator(const BandDesc& bd, int64_t p, int64_t ld, const float 
 }
 
 // ---------------------------------------------------------------------------
-// K1: fused Gauss-Newton analysis for one pixel (information form).
-//   A = P_f^-1 + sum_b w_b h_b h_b^T,  b = P_f^-1 x_f + sum_b w_b h_b y'_b,
-//   y'_b = y_b + h_b . x0 - H0_b,      x_a = A^-1 b
-// Returns (x_a - x0)^2 summed over parameters.
-// FD > 0: fast path where every band is a GP with FD inputs and FOBS encoding
-// (the compiler then drops the SAR/linear/precomputed code and its registers).
-template <int NP, int FD = 0, int FOBS = 0, int UNR = 4>
-KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
+// K4/K5: propagation and prior blending for one pixel.
+// Forecast fused into the analysis kernel: the partial prior reset, one
+// compile-time formula (a runtime mode switch in the analysis prologue costs
+// ~35 VGPRs across the GP loop).  The host maps PROP_PRIOR (mask 0) and
+// PROP_INFO_APPROX (all propagated, zero reset precision) onto it:
+//   xf_j = m_j x_a,j (propagated) | mu_j (reset)
+//   Pf   = C^-1 with diag_j = 1 / (1 / P_a,jj + q_j) for propagated j.
+template <int NP>
+KF_HD void forecast_partial(const KF_CONST_AS PropArgs* a, int64_t p, float (&xf)[NP], float (&P)[ntri(NP)]) {
   constexpr int NT = ntri(NP);
-  const int64_t ld = a.ld;
-  float x0[NP], A[NT], b[NP];
-  uint8_t st = 0;
+  const int64_t ld = a->ld;
 #pragma unroll
-  for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
-  if (a.a_in) {
-    // band-chunked accumulation: continue from a previous chunk's (A, b)
+  for (int t = 0; t < NT; ++t) P[t] = a->reset_cinv[t];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) A[t] = a.a_in[t * ld + p];
-#pragma unroll
-    for (int j = 0; j < NP; ++j) b[j] = a.b_in[j * ld + p];
-  } else {
-    float xf[NP];
-#pragma unroll
-    for (int j = 0; j < NP; ++j) xf[j] = a.x_f[j * ld + p];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) A[t] = a.pf_inv[t * ld + p];
-    symv<NP>(A, xf, b);
-  }
-  int nobs = 0;
-  for (int bi = 0; bi < a.n_bands; ++bi) {
-    const BandDesc bd = cptr(a.bands)[bi];
-    float y, w;
-    decode_obs<FOBS>(bd, p, y, w);
-    if (!(w > 0.f)) {
-      if (bd.h0_out) bd.h0_out[p] = 0.f;
-      continue;
-    }
-    float H0, h[NP];
-    bool ok;
-    if constexpr (FD > 0) {
-      gp_eval<NP, FD, UNR>(bd, x0, H0, h);
-      ok = finitef(H0);
-#pragma unroll
-      for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);
-    } else {
-      ok = eval_operator<NP>(bd, p, ld, x0, H0, h);
-    }
-    if (bd.h0_out) bd.h0_out[p] = H0;
-    if (!ok) { st |= ST_BAD_OP; continue; }
-    ++nobs;
-    float yp = y - H0;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) yp = fmaf(h[j], x0[j], yp);
-    const float wy = w * yp;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const float wh = w * h[i];
-      b[i] = fmaf(h[i], wy, b[i]);
-#pragma unroll
-      for (int j = i; j < NP; ++j) A[tri(NP, i, j)] = fmaf(wh, h[j], A[tri(NP, i, j)]);
+  for (int j = 0; j < NP; ++j) {
+    xf[j] = a->reset_mean[j];
+    if ((a->prop_mask >> j) & 1u) {
+      const float q = a->q_pix ? a->q_pix[j * ld + p] : a->q[j];
+      xf[j] = a->m[j] * a->x_a[j * ld + p];
+      P[tri(NP, j, j)] = 1.f / (1.f / a->p_a[tri(NP, j, j) * ld + p] + q);
     }
   }
-  if (nobs == 0) st |= ST_NO_OBS;
-  if (a.a_out) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = A[t];
-  }
-  if (a.b_out) {
-#pragma unroll
-    for (int j = 0; j < NP; ++j) a.b_out[j * ld + p] = b[j];
-  }
-  float dn = 0.f;
-  if (a.solve) {
-    const bool spd = chol_packed<NP>(A);
-    chol_solve<NP>(A, b);
-    bool fin = true;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) fin = fin && finitef(b[j]);
-    if (!spd || !fin) {
-      // Health fallback: keep the forecast (prior) for this pixel.
-      st |= (!spd ? ST_NONSPD : 0) | (!fin ? ST_NONFINITE : 0) | ST_FALLBACK;
-#pragma unroll
-      for (int j = 0; j < NP; ++j) b[j] = a.x_f[j * ld + p];
-      if (a.a_out) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = a.pf_inv[t * ld + p];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      a.x_out[j * ld + p] = b[j];
-      const float d = b[j] - x0[j];
-      dn = fmaf(d, d, dn);
-    }
-  }
-  if (a.status) a.status[p] = st;
-  return dn;
 }
 
-// ---------------------------------------------------------------------------
-// K4/K5: propagation and prior blending for one pixel.
+// forecast_pixel computes the forecast (xf, P) of pixel p without storing it;
+// the analysis kernel calls it directly when the propagation is fused.
 template <int NP>
-KF_HD void pixel_propagate(const PropArgs& a, int64_t p) {
+KF_HD uint8_t forecast_pixel(const PropArgs& a, int64_t p, float (&xf)[NP], float (&P)[ntri(NP)]) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a.ld;
-  float xf[NP], P[NT];
   uint8_t st = 0;
   float q[NP];
 #pragma unroll
@@ -598,11 +537,140 @@ KF_HD void pixel_propagate(const PropArgs& a, int64_t p) {
     if (!chol_packed<NP>(U)) st |= ST_NONSPD;
     chol_solve<NP>(U, xf);
   }
+  return st;
+}
+
+template <int NP>
+KF_HD void pixel_propagate(const PropArgs& a, int64_t p) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a.ld;
+  float xf[NP], P[NT];
+  const uint8_t st = forecast_pixel<NP>(a, p, xf, P);
 #pragma unroll
   for (int j = 0; j < NP; ++j) a.x_f[j * ld + p] = xf[j];
 #pragma unroll
   for (int t = 0; t < NT; ++t) a.p_f[t * ld + p] = P[t];
   if (a.status) a.status[p] |= st;
+}
+
+// ---------------------------------------------------------------------------
+// K1: fused Gauss-Newton analysis for one pixel (information form).
+//   A = P_f^-1 + sum_b w_b h_b h_b^T,  b = P_f^-1 x_f + sum_b w_b h_b y'_b,
+//   y'_b = y_b + h_b . x0 - H0_b,      x_a = A^-1 b
+// Returns (x_a - x0)^2 summed over parameters.
+// FD > 0: fast path where every band is a GP with FD inputs and FOBS encoding
+// (the compiler then drops the SAR/linear/precomputed code and its registers).
+template <int NP, int FD = 0, int FOBS = 0, int UNR = 4>
+KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a.ld;
+  float x0[NP], A[NT], b[NP];
+  uint8_t st = 0;
+  if (a.x_prev) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
+  }
+  if (a.prop) {
+    // fused propagation: forecast of this pixel from the previous analysis,
+    // never written to HBM (saves the propagate pass and its 2 x 140 B/px)
+    float xf[NP];
+    forecast_partial<NP>(opaque(cptr(a.prop)), p, xf, A);
+    symv<NP>(A, xf, b);
+    if (!a.x_prev) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) x0[j] = xf[j];
+    }
+  } else if (a.a_in) {
+    // band-chunked accumulation: continue from a previous chunk's (A, b)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) A[t] = a.a_in[t * ld + p];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) b[j] = a.b_in[j * ld + p];
+  } else {
+    float xf[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) xf[j] = a.x_f[j * ld + p];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) A[t] = a.pf_inv[t * ld + p];
+    symv<NP>(A, xf, b);
+  }
+  int nobs = 0;
+  for (int bi = 0; bi < a.n_bands; ++bi) {
+    const BandDesc bd = cptr(a.bands)[bi];
+    float y, w;
+    decode_obs<FOBS>(bd, p, y, w);
+    if (!(w > 0.f)) {
+      if (bd.h0_out) bd.h0_out[p] = 0.f;
+      continue;
+    }
+    float H0, h[NP];
+    bool ok;
+    if constexpr (FD > 0) {
+      gp_eval<NP, FD, UNR>(bd, x0, H0, h);
+      ok = finitef(H0);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);
+    } else {
+      ok = eval_operator<NP>(bd, p, ld, x0, H0, h);
+    }
+    if (bd.h0_out) bd.h0_out[p] = H0;
+    if (!ok) { st |= ST_BAD_OP; continue; }
+    ++nobs;
+    float yp = y - H0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) yp = fmaf(h[j], x0[j], yp);
+    const float wy = w * yp;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const float wh = w * h[i];
+      b[i] = fmaf(h[i], wy, b[i]);
+#pragma unroll
+      for (int j = i; j < NP; ++j) A[tri(NP, i, j)] = fmaf(wh, h[j], A[tri(NP, i, j)]);
+    }
+  }
+  if (nobs == 0) st |= ST_NO_OBS;
+  if (a.a_out) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = A[t];
+  }
+  if (a.b_out) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) a.b_out[j * ld + p] = b[j];
+  }
+  float dn = 0.f;
+  if (a.solve) {
+    const bool spd = chol_packed<NP>(A);
+    chol_solve<NP>(A, b);
+    bool fin = true;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) fin = fin && finitef(b[j]);
+    if (!spd || !fin) {
+      // Health fallback: keep the forecast (prior) for this pixel.
+      st |= (!spd ? ST_NONSPD : 0) | (!fin ? ST_NONFINITE : 0) | ST_FALLBACK;
+      if (a.prop) {
+        forecast_partial<NP>(opaque(cptr(a.prop)), p, b, A);   // rare path: recompute instead of keeping it live
+        if (a.a_out) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = A[t];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NP; ++j) b[j] = a.x_f[j * ld + p];
+        if (a.a_out) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = a.pf_inv[t * ld + p];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      a.x_out[j * ld + p] = b[j];
+      const float d = b[j] - x0[j];
+      dn = fmaf(d, d, dn);
+    }
+  }
+  if (a.status) a.status[p] = st;
+  return dn;
 }
 
 // Packed SPD inverse (covariance <-> precision conversion).

@@ -39,6 +39,7 @@ class EngineConfig:
     # runtime
     device: str | None = None                 # 'cuda', 'cuda:1', 'cpu' (default: cuda if present)
     prefetch: bool = True                     # overlap next date's ingest with compute
+    fuse_propagation: bool = True             # evaluate the forecast inside the analysis kernel
     return_innovations: bool = False
     metrics_path: str | None = None           # JSONL metrics (per date / timestep)
     checkpoint_dir: str | None = None

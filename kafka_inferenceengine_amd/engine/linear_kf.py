@@ -36,7 +36,7 @@ from ..utils.blocks import ntri, pack_matrix, soa_to_interleaved, tri_pos
 from ..utils.metrics import MetricsLogger, PhaseTimer
 from .bands import DeviceBand, RecordCache, build_table
 from .config import EngineConfig
-from .state import COVARIANCE, PRECISION, KFState
+from .state import COVARIANCE, PRECISION, KFState, LazyForecast
 
 LOG = logging.getLogger(__name__ + ".linear_kf")
 
@@ -170,7 +170,12 @@ class LinearKalman:
         st = KFState.constant(pr.mean, pr.cinv, self.N, self.device, PRECISION)
         return self._as_kind(st, COVARIANCE if self.config.analysis_form == "gain" else PRECISION)
 
+    @staticmethod
+    def _materialize(st):
+        return st.materialize() if isinstance(st, LazyForecast) else st
+
     def _as_kind(self, st: KFState, kind: str) -> KFState:
+        st = self._materialize(st)
         if st.kind == kind:
             return st
         out = torch.empty_like(st.P)
@@ -214,9 +219,9 @@ class LinearKalman:
         forecast = state
         if advance:
             LOG.info("Advancing state, %s" % timestep.strftime("%Y-%m-%d"))
-            forecast = self.advance_state(state, timestep)
+            forecast = self.advance_state(state, timestep, lazy=self.config.fuse_propagation)
         if len(locate_times) == 0:
-            analysis = forecast
+            analysis = self._materialize(forecast)
             LOG.info("No observations in this time")
             info = {"n_dates": 0}
         else:
@@ -243,8 +248,13 @@ class LinearKalman:
         x, Pl = f.to_reference()
         return (x, None, Pl) if f.kind == PRECISION else (x, Pl, None)
 
-    def advance_state(self, analysis: KFState, date) -> KFState:
-        """Propagation + prior blend on device (kf_tools.py:136-171 semantics)."""
+    def advance_state(self, analysis: KFState, date, lazy: bool = False):
+        """Propagation + prior blend on device (kf_tools.py:136-171 semantics).
+
+        ``lazy``: when the propagation is a single propagate pass producing a
+        precision-form forecast, return a :class:`LazyForecast` instead; the
+        fused analysis kernel then computes the forecast per pixel and it is
+        never written to memory."""
         with self.timer.phase("propagate"):
             prop = self._state_propagator
             spec = getattr(prop, "device_spec", None) if prop is not None else None
@@ -260,6 +270,8 @@ class LinearKalman:
                 # prior only (kf_tools.py:165-166): reset to the prior, no blend needed
                 d.update(mode=PROP_PRIOR, prop_mask=0, reset_mean=np.asarray(prior_dev.mean),
                          reset_cinv=pack_matrix(np.asarray(prior_dev.cinv)))
+                if lazy and self._analysis_kind() == PRECISION:
+                    return self._lazy(d, analysis, None)
                 out = self._run_propagate(d, analysis, None, PRECISION)
                 return self._as_kind(out, self._analysis_kind())
             elif prop is None:
@@ -287,8 +299,20 @@ class LinearKalman:
                     return self._as_kind(out, self._analysis_kind())
                 self._fill_blend(d, prior_dev)
                 blend_pix = self._blend_pix(prior_dev)
+            if lazy and out_kind == PRECISION and self._analysis_kind() == PRECISION:
+                return self._lazy(d, src, blend_pix)
             out = self._run_propagate(d, src, blend_pix, out_kind)
             return self._as_kind(out, self._analysis_kind())
+
+    def _lazy(self, d, src: KFState, blend_pix):
+        timer = self.timer
+
+        def materialize():
+            with timer.phase("propagate"):
+                return self._run_propagate(d, src, blend_pix, PRECISION)
+        if not K.prop_is_light(d["mode"], d.get("blend", False)):
+            return materialize()
+        return LazyForecast(src, d, blend_pix, self._q_pix, materialize)
 
     def _analysis_kind(self):
         return COVARIANCE if self.config.analysis_form == "gain" else PRECISION
@@ -355,7 +379,7 @@ class LinearKalman:
             LOG.info("Assimilating %s..." % step.strftime("%Y-%m-%d"))
             t0 = time.perf_counter()
             if self.config.band_sequential:
-                res = self._assimilate_sequential(step, forecast)
+                res = self._assimilate_sequential(step, self._materialize(forecast))
             else:
                 bands = self._device_bands(step)
                 if self.config.prefetch and hasattr(self.observations, "prefetch"):
@@ -483,15 +507,27 @@ class LinearKalman:
         h0_outs = [torch.zeros(max(N, 1), dtype=torch.float32, device=self.device) for _ in bands] \
             if need_inn else None
         gain = cfg.analysis_form == "gain"
-        fc = self._as_kind(forecast, COVARIANCE if gain else PRECISION)
-        ld = fc.x.shape[1]
-        x_prev = fc.x.clone()
-        x_new = torch.empty_like(fc.x)
-        P_out = torch.empty_like(fc.P)
-        status = torch.zeros(max(N, 1), dtype=torch.uint8, device=self.device)
         precomp = any(s.kind == OP_PRECOMP for s in specs)
         split = None if (precomp or gain or cfg.spatial_gamma > 0) else self._split_plan(specs, dbs, h0_outs)
         table = None if (precomp or split) else build_table(specs, dbs, n, self._cache, self.device, h0_outs)
+        prop = None
+        if isinstance(forecast, LazyForecast) and not (gain or precomp or split or cfg.spatial_gamma > 0) and N:
+            # fused propagation: the kernel computes the forecast per pixel from
+            # the previous analysis; the first iteration linearises at it
+            prop = forecast.handle()
+            src = forecast.src
+            fc = None
+            x_prev = None
+            x_new = torch.empty_like(src.x)
+            P_out = torch.empty_like(src.P)
+            ld = src.x.shape[1]
+        else:
+            fc = self._as_kind(forecast, COVARIANCE if gain else PRECISION)
+            ld = fc.x.shape[1]
+            x_prev = fc.x.clone()
+            x_new = torch.empty_like(fc.x)
+            P_out = torch.empty_like(fc.P)
+        status = torch.zeros(max(N, 1), dtype=torch.uint8, device=self.device)
         norms = []
         n_iter = 1
         len_x = float(n * self.n_total)
@@ -508,6 +544,9 @@ class LinearKalman:
                         self._regularised_iteration(table, x_prev, fc, x_new, P_out, status)
                     elif split is not None:
                         self._split_iteration(split, x_prev, fc, x_new, P_out, status)
+                    elif prop is not None:
+                        K.analysis(n, table, x_prev, None, None, x_new, P_out, None, status, self._partials, N=N,
+                                   prop=prop)
                     else:
                         K.analysis(n, table, x_prev, fc.x, fc.P, x_new, P_out, None, status, self._partials, N=N)
                     K.reduce_partials(self._partials, self._red)
@@ -519,7 +558,7 @@ class LinearKalman:
             norms.append(convergence_norm)
             LOG.info("Band {:d}, Iteration # {:d}, convergence norm: {:g}".format(len(bands) - 1, n_iter,
                                                                                  convergence_norm))
-            x_prev, x_new = x_new, x_prev
+            x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
             if convergence_norm < cfg.convergence_tolerance and n_iter >= cfg.min_iterations:
                 break
             if n_iter > cfg.max_iterations:

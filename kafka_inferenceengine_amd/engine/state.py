@@ -97,3 +97,37 @@ class KFState:
 
     def numpy(self):
         return (self.x[:, :self.N].detach().cpu().numpy(), self.P[:, :self.N].detach().cpu().numpy())
+
+
+class LazyForecast:
+    """A forecast that has not been written to memory: the previous analysis
+    plus the propagation arguments.  The fused analysis kernel evaluates it per
+    pixel (``AnalysisArgs.prop``); every other consumer calls
+    :meth:`materialize`, which runs the propagate kernel."""
+
+    kind = PRECISION
+
+    def __init__(self, src: KFState, spec: dict, blend_pix, q_pix, materialize):
+        self.src, self.spec, self.blend_pix, self.q_pix = src, spec, blend_pix, q_pix
+        self._materialize = materialize
+
+    @property
+    def N(self) -> int:
+        return self.src.N
+
+    @property
+    def n_params(self) -> int:
+        return self.src.n_params
+
+    @property
+    def device(self):
+        return self.src.device
+
+    def handle(self):
+        from ..ops import kernels as K
+        bm, bc = self.blend_pix if self.blend_pix else (None, None)
+        return K.prop_args(self.n_params, self.spec, self.src.x, self.src.P, N=self.N, q_pix=self.q_pix,
+                           blend_mean_pix=bm, blend_cinv_pix=bc, fused=True)
+
+    def materialize(self) -> KFState:
+        return self._materialize()

@@ -128,19 +128,33 @@ def gp_operator_supported(n_params, d) -> bool:
 
 
 def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=None, b_out=None, status=None,
-             partials=None, N=None, solve=True, fast=True, variant=0, a_in=None, b_in=None):
-    """K1 fused Gauss-Newton analysis (information form)."""
+             partials=None, N=None, solve=True, fast=True, variant=0, a_in=None, b_in=None, prop=None):
+    """K1 fused Gauss-Newton analysis (information form).
+
+    ``prop`` (from :func:`prop_args`) fuses the propagation: the forecast is
+    computed per pixel from the previous analysis inside the kernel and
+    ``x_f``/``pf_inv`` must be None; ``x_prev=None`` then linearises at the
+    forecast (first Gauss-Newton iteration)."""
     check_np(n_params)
-    N = int(x_prev.shape[1] if N is None else N)
-    dev = x_prev.device
+    ref = next(t for t in (x_prev, x_f, x_out, a_out) if t is not None)
+    N = int(ref.shape[1] if N is None else N)
+    dev = ref.device
     nt = ntri(n_params)
+    if prop is None and (x_prev is None or x_f is None or pf_inv is None):
+        raise ValueError("x_prev, x_f and pf_inv are required unless the propagation is fused")
+    if prop is not None and (x_f is not None or pf_inv is not None or a_in is not None):
+        raise ValueError("fused propagation replaces x_f/pf_inv and excludes a_in")
     for t, r, nm in ((x_prev, n_params, "x_prev"), (x_f, n_params, "x_f"), (pf_inv, nt, "pf_inv"),
                      (x_out, n_params, "x_out"), (a_out, nt, "a_out"), (b_out, n_params, "b_out")):
         _check_soa(t, r, N, nm, device=dev)
-    ld = x_prev.shape[1]
-    for t in (x_f, pf_inv, x_out, a_out, b_out):
+    ld = ref.shape[1]
+    for t in (x_prev, x_f, pf_inv, x_out, a_out, b_out):
         if t is not None and t.shape[1] != ld:
             raise ValueError("all SoA operands must share the leading dimension")
+    if prop is not None and (prop.args.ld != ld or prop.args.N < N or prop.device != dev):
+        raise ValueError("fused propagation arguments do not match the analysis layout/device")
+    if prop is not None and not prop.fused:
+        raise ValueError("analysis(prop=...) needs prop_args(..., fused=True)")
     if solve and x_out is None:
         raise ValueError("solve=True needs x_out")
     _check_vec(status, N, "status", torch.uint8, dev)
@@ -159,8 +173,10 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     _check_soa(b_in, n_params, N, "b_in", device=dev)
     a.a_in, a.b_in = _ptr(a_in), _ptr(b_in)
     a.status, a.partials = _ptr(status), _ptr(partials)
+    if prop is not None:
+        a.prop = _ptr(prop.device_copy())
     grid = grid_for(N)
-    ext().analysis(n_params, a, grid, _dev(x_prev), _stream(x_prev))
+    ext().analysis(n_params, a, grid, _dev(ref), _stream(ref))
     return partials
 
 
@@ -204,24 +220,44 @@ def jacobi(n_params, a_in, b_in, x_ext, nbr, x_ref, x_out, gamma, reg_mask, N, a
     return partials
 
 
-def propagate(n_params, spec: dict, x_a, p_a, x_f, p_f, N=None, status=None, q_pix=None,
-              blend_mean_pix=None, blend_cinv_pix=None):
-    """K4/K5 propagation (+ optional prior blend).  ``spec`` keys: mode, m, q,
-    prop_mask, reset_mean, reset_cinv (packed), blend, quirk_blend,
-    blend_mean, blend_cinv (packed)."""
+def prop_args(n_params, spec: dict, x_a, p_a, x_f=None, p_f=None, N=None, status=None, q_pix=None,
+              blend_mean_pix=None, blend_cinv_pix=None, fused=False):
+    """Validated ``PropArgs`` for :func:`propagate` or, with ``fused=True``, for
+    a fused :func:`analysis`.  ``spec`` keys: mode, m, q, prop_mask,
+    reset_mean, reset_cinv (packed), blend, quirk_blend, blend_mean,
+    blend_cinv (packed).  The fused kernel evaluates one formula (partial
+    prior reset, kf_core.h:forecast_partial); PROP_PRIOR and PROP_INFO_APPROX
+    are mapped onto it here."""
     check_np(n_params)
+    if fused:
+        if not prop_is_light(spec["mode"], spec.get("blend", False)):
+            raise ValueError("only PRIOR / PRIOR_PARTIAL / INFO_APPROX without blend can be fused")
+        spec = dict(spec)
+        mode = int(spec["mode"])
+        if mode == 0:        # PROP_PRIOR: nothing propagated
+            spec["prop_mask"] = 0
+        elif mode == 2:      # PROP_INFO_APPROX: everything propagated, diagonal precision only
+            spec["prop_mask"] = (1 << n_params) - 1
+            spec["reset_mean"] = np.zeros(n_params)
+            spec["reset_cinv"] = np.zeros(ntri(n_params))
+        spec["mode"] = 1
+        spec["blend"] = False
     N = int(x_a.shape[1] if N is None else N)
     dev = x_a.device
     nt = ntri(n_params)
-    _check_soa(x_a, n_params, N, "x_a", device=dev)
+    _check_soa(x_a, n_params, N, "x_a")
     _check_soa(p_a, nt, N, "p_a", device=dev)
     _check_soa(x_f, n_params, N, "x_f", device=dev)
     _check_soa(p_f, nt, N, "p_f", device=dev)
     _check_soa(q_pix, n_params, N, "q_pix", device=dev)
     _check_soa(blend_mean_pix, n_params, N, "blend_mean_pix", device=dev)
     _check_soa(blend_cinv_pix, nt, N, "blend_cinv_pix", device=dev)
+    ld = x_a.shape[1]
+    for t in (p_a, x_f, p_f, q_pix, blend_mean_pix, blend_cinv_pix):
+        if t is not None and t.shape[1] != ld:
+            raise ValueError("all SoA operands must share the leading dimension")
     a = ext().PropArgs()
-    a.N, a.ld = N, x_a.shape[1]
+    a.N, a.ld = N, ld
     a.mode = int(spec["mode"])
     a.blend = int(bool(spec.get("blend", False)))
     a.quirk_blend = int(bool(spec.get("quirk_blend", False)))
@@ -234,7 +270,39 @@ def propagate(n_params, spec: dict, x_a, p_a, x_f, p_f, N=None, status=None, q_p
     a.x_a, a.p_a, a.x_f, a.p_f = map(_ptr, (x_a, p_a, x_f, p_f))
     a.q_pix, a.blend_mean_pix, a.blend_cinv_pix = map(_ptr, (q_pix, blend_mean_pix, blend_cinv_pix))
     a.status = _ptr(status)
-    ext().propagate(n_params, a, _dev(x_a), _stream(x_a))
+    return PropHandle(a, dev, (x_a, p_a, x_f, p_f, q_pix, blend_mean_pix, blend_cinv_pix, status), fused)
+
+
+LIGHT_PROP_MODES = (0, 1, 2)   # PROP_PRIOR, PROP_PRIOR_PARTIAL, PROP_INFO_APPROX
+
+
+def prop_is_light(mode, blend=False) -> bool:
+    """Propagations the analysis kernel can evaluate in-kernel (kf_core.h:forecast_partial)."""
+    return (not blend) and int(mode) in LIGHT_PROP_MODES
+
+
+class PropHandle:
+    """PropArgs plus the device and the tensors its pointers refer to (kept alive)."""
+
+    def __init__(self, args, device, tensors, fused=False):
+        self.args, self.device, self._tensors, self.fused = args, device, tensors, fused
+        self._buf = None
+
+    def device_copy(self) -> torch.Tensor:
+        """The PropArgs bytes on the device (read by the kernel through s_load)."""
+        if self._buf is None:
+            raw = torch.frombuffer(bytearray(ext().pack_prop_args(self.args)), dtype=torch.uint8)
+            self._buf = raw.to(self.device, copy=True)
+        return self._buf
+
+
+def propagate(n_params, spec: dict, x_a, p_a, x_f, p_f, N=None, status=None, q_pix=None,
+              blend_mean_pix=None, blend_cinv_pix=None):
+    """K4/K5 propagation (+ optional prior blend); see :func:`prop_args`."""
+    if x_f is None or p_f is None:
+        raise ValueError("propagate needs x_f and p_f outputs")
+    h = prop_args(n_params, spec, x_a, p_a, x_f, p_f, N, status, q_pix, blend_mean_pix, blend_cinv_pix)
+    ext().propagate(n_params, h.args, _dev(x_a), _stream(x_a))
 
 
 def invert(n_params, src, dst, N=None, status=None):

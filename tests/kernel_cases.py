@@ -79,3 +79,45 @@ def oracle_bands(prob, x_lin):
         h[:, mp] = dH
         out.append((H, h, y, w))
     return out
+
+
+def fused_vs_materialized(device, mode, blend=False, quirk=False, prop_mask=0, N=2000, seed=3):
+    """Analysis with the propagation fused into the kernel vs propagate pass +
+    analysis; both linearise at the forecast (first Gauss-Newton iteration) and
+    then at a perturbed point.  Returns the two (x, A, status) results."""
+    from kafka_inferenceengine_amd.utils.blocks import pack_matrix
+    prob = tip_problem(N=N, seed=seed)
+    rng = np.random.default_rng(seed)
+    n = prob["n"]
+    mu, _, Pi = k.tip_prior()
+    A = spd_blocks(rng, N, n, 5.0) * 0.2 + prob["Pf"]
+    spec = {"mode": mode, "m": np.ones(n), "q": rng.uniform(0.01, 0.1, n), "prop_mask": prop_mask,
+            "reset_mean": mu, "reset_cinv": pack_matrix(Pi), "blend": blend, "quirk_blend": quirk,
+            "blend_mean": mu * 1.05, "blend_cinv": pack_matrix(Pi * 0.5)}
+    xa, pa = soa(prob["x"], device), packed(A, device)
+    tab = table(prob, device)
+    nt = n * (n + 1) // 2
+    res = []
+    for fused in (False, True):
+        out = []
+        x_lin = None
+        for it in range(2):
+            xo = torch.zeros((n, N), device=device)
+            ao = torch.zeros((nt, N), device=device)
+            st = torch.zeros(N, dtype=torch.uint8, device=device)
+            if fused:
+                h = K.prop_args(n, spec, xa, pa, fused=True)
+                K.analysis(n, tab, x_lin, None, None, xo, ao, None, st, None, prop=h)
+            else:
+                xf = torch.zeros((n, N), device=device)
+                pf = torch.zeros((nt, N), device=device)
+                K.propagate(n, spec, xa, pa, xf, pf)
+                K.analysis(n, tab, xf if x_lin is None else x_lin, xf, pf, xo, ao, None, st, None)
+            out.append((xo.cpu().numpy(), ao.cpu().numpy(), st.cpu().numpy()))
+            x_lin = soa(prob["x"] * 0.5 + 0.5 * xo.cpu().numpy().T, device)
+        res.append(out)
+    return res
+
+
+FUSED_CASES = [(1, False, False, 1 << 6), (1, False, False, 0b1010011), (0, False, False, 0),
+               (2, False, False, 0)]

@@ -203,3 +203,20 @@ def test_split_gp_operator_path_equals_fused(chunk):
         res.append(kf.run(grid, x0, None, Pinv))
     assert torch.allclose(res[0].x, res[1].x, rtol=1e-4, atol=1e-5)
     assert torch.allclose(res[0].P, res[1].P, rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("with_prior", [False, True])
+def test_fused_propagation_engine_equals_materialized(with_prior):
+    """EngineConfig.fuse_propagation: the forecast evaluated inside the analysis
+    kernel gives the same run as the propagate pass + analysis (blend => the
+    engine falls back to materialising)."""
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=5)
+    grid = _grid(4)
+    runs = []
+    for fuse in (False, True):
+        kf = _engine(mask, obs, Q, prior=prior if with_prior else None, fuse_propagation=fuse)
+        runs.append((kf.run(grid, x0, None, Pinv), [h["gn_iterations"] for h in kf.history]))
+    (a, ia), (b, ib) = runs
+    assert ia == ib
+    assert torch.allclose(a.x, b.x, rtol=1e-6, atol=1e-7)
+    assert torch.allclose(a.P, b.P, rtol=1e-6, atol=1e-6)

@@ -176,3 +176,15 @@ def test_split_gp_path_gpu_matches_fused(cuda):
         grid = [obs.dates[0] - dt.timedelta(days=1), obs.dates[1] + dt.timedelta(days=1)]
         outs.append(kf.run(grid, kf.state_from_prior(prior), None, None).x.cpu())
     assert close(outs[0], outs[1], 1e-3)
+
+
+@pytest.mark.parametrize("mode,blend,quirk,pmask", C.FUSED_CASES[:3])
+def test_fused_propagation_device(cuda, mode, blend, quirk, pmask):
+    """Fused forecast in the gfx950 analysis kernel vs the propagate kernel +
+    analysis on the device, and vs the host runner."""
+    ref, fused = C.fused_vs_materialized(cuda, mode, blend, quirk, pmask, N=20000)
+    host, _ = C.fused_vs_materialized("cpu", mode, blend, quirk, pmask, N=20000)
+    for (x1, a1, s1), (x2, a2, s2), (x3, a3, s3) in zip(ref, fused, host):
+        assert np.array_equal(s1, s2)
+        assert close(x2, x1, 1e-4) and close(a2, a1, 1e-5)
+        assert close(x2, x3) and close(a2, a3, 1e-5)

@@ -280,3 +280,19 @@ def test_neighbour_table_matches_raster():
         exp = [lid[r - 1, c] if r > 0 else -1, lid[r + 1, c] if r < 9 else -1,
                lid[r, c - 1] if c > 0 else -1, lid[r, c + 1] if c < 6 else -1]
         assert list(nb[:, p]) == exp
+
+
+@pytest.mark.parametrize("mode,blend,quirk,pmask", C.FUSED_CASES)
+def test_fused_propagation_equals_materialized(mode, blend, quirk, pmask):
+    ref, fused = C.fused_vs_materialized("cpu", mode, blend, quirk, pmask)
+    def rel(a, b):   # row-scaled: diag-approx forecasts are ill-conditioned per pixel
+        return np.max(np.abs(a - b) / np.maximum(np.abs(b).max(1, keepdims=True), 1e-3))
+    for (x1, a1, s1), (x2, a2, s2) in zip(ref, fused):
+        assert np.array_equal(s1, s2)
+        assert rel(x2, x1) < 1e-4 and rel(a2, a1) < 1e-4
+
+
+@pytest.mark.parametrize("mode,blend", [(3, False), (4, False), (5, False), (1, True)])
+def test_heavy_propagation_is_not_fused(mode, blend):
+    with pytest.raises(ValueError, match="fused"):
+        C.fused_vs_materialized("cpu", mode, blend, N=64)
