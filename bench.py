@@ -68,9 +68,9 @@ def build(cfg_name, a, mask, part, dev, comm):
         dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(n_dates)]
         obs = k.SyntheticBHRObservations(mask, dates=dates, n_train=a.n_train or c["n_train"], partition=part,
                                          device=dev, n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=seed)
-        cfg = k.EngineConfig(metrics_path=a.metrics)
+        cfg = k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel)
         if cfg_name == "spatial":
-            cfg = k.EngineConfig(metrics_path=a.metrics, spatial_gamma=c["gamma"], spatial_params=[6],
+            cfg = k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel, spatial_gamma=c["gamma"], spatial_params=[6],
                                  jacobi_sweeps=c["sweeps"])
         kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_nonlinear_observation_operator,
                             k.TIP_PARAMETERS, state_propagation=k.propagate_information_filter_LAI, config=cfg,
@@ -83,7 +83,7 @@ def build(cfg_name, a, mask, part, dev, comm):
                                               stream=True, cloud_fraction=a.cloud, seed=seed)
         kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_linear_observation_operator,
                             k.TIP_PARAMETERS, state_propagation=k.propagate_information_filter_LAI,
-                            config=k.EngineConfig(metrics_path=a.metrics), comm=comm, partition=part)
+                            config=k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel), comm=comm, partition=part)
         kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
         state = kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask))
     else:
@@ -102,7 +102,7 @@ def build(cfg_name, a, mask, part, dev, comm):
         prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
         kf = k.LinearKalman(obs, k.DeviceOutput(k.SAIL_PARAMETERS), mask, k.create_prosail_observation_operator,
                             k.SAIL_PARAMETERS, state_propagation=None, prior=prior,
-                            config=k.EngineConfig(metrics_path=a.metrics), comm=comm, partition=part)
+                            config=k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel), comm=comm, partition=part)
         state = kf.state_from_prior(prior)
     return obs, kf, state, dates
 
@@ -122,6 +122,8 @@ def main():
     ap.add_argument("--profile", default=None, help="write a torch.profiler chrome trace here (rank 0)")
     ap.add_argument("--watchdog", type=float, default=0, help="dump Python stacks every N s (hang triage)")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--band-parallel", type=int, default=1,
+                    help="ranks per band group (strips x band groups; multi-band configs)")
     a = ap.parse_args()
     if a.watchdog > 0:
         import faulthandler
@@ -133,8 +135,8 @@ def main():
     from kafka_inferenceengine_amd.inference import iterate_time_grid
     from kafka_inferenceengine_amd.parallel import Comm, StripPartition
 
-    comm = Comm.from_env(device=a.device)
-    if comm.distributed:
+    comm = Comm.from_env(device=a.device, band_parallel=a.band_parallel)
+    if comm.distributed or comm.band is not None:
         dev = comm.device
     else:
         dev = torch.device(a.device or ("cuda" if torch.cuda.is_available() else "cpu"))
@@ -143,9 +145,12 @@ def main():
         comm = Comm.single(dev)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
-    world, rank = comm.world, comm.rank
-    if a.gpus != world:
-        log(f"--gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    world, rank = comm.world, comm.rank                 # strips (tile-DP)
+    B = comm.band.world if comm.band is not None else 1  # band groups
+    n_ranks = world * B
+    g_rank = comm.ranks[rank] if comm.band is None else comm.band.ranks[comm.band.rank]
+    if a.gpus != n_ranks:
+        log(f"--gpus {a.gpus} but WORLD_SIZE {n_ranks}; using WORLD_SIZE")
     c = CONFIGS[a.config]
     H = W = a.size or c["size"]
     mask = np.ones((H, W), dtype=bool)
@@ -157,7 +162,7 @@ def main():
         s._ensure_pool()
     if dev.type == "cuda":
         torch.cuda.synchronize()
-    log(f"rank {rank}/{world}: {a.config} strip rows {part.r0}-{part.r1}, {part.N} px, "
+    log(f"rank {g_rank}/{n_ranks}: {a.config} strip rows {part.r0}-{part.r1}, {part.N} px, "
         f"setup {time.time() - t_setup:.1f}s")
 
     grid = [dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in dates]
@@ -170,7 +175,7 @@ def main():
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             t_start = time.perf_counter()
-            if a.profile and rank == 0:
+            if a.profile and g_rank == 0:
                 prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
                                                           torch.profiler.ProfilerActivity.CUDA])
                 prof.__enter__()
@@ -190,12 +195,12 @@ def main():
         prof.export_chrome_trace(a.profile)
     ok = bool(torch.isfinite(state.x[:, :state.N]).all().item())
     value = float(part.N_total) * a.steps / elapsed
-    if rank == 0:
+    if g_rank == 0:
         gn = [h.get("gn_iterations") for h in kf.history[a.warmup:]]
         metric = HEADLINE_METRIC if a.config == "tip7" and H == 10980 else \
             f"pixel-state updates/sec (whole node), {H}x{W} tile, {a.config}"
         ingest = sum(s.ingest_bytes() for s in srcs) // max(1, a.warmup + a.steps)
-        rec = {"metric": metric, "value": round(value, 1), "unit": "pixel-state updates/s", "n_gpus": world,
+        rec = {"metric": metric, "value": round(value, 1), "unit": "pixel-state updates/s", "n_gpus": n_ranks,
                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 3),
                "higher_is_better": True, "scaling": "strong",
                "vs_baseline": round(value / c["baseline"], 2), "dtype": "fp32" if a.config != "identity7"
@@ -204,7 +209,7 @@ def main():
                        "random-init GP emulators",
                "config": {"name": a.config, "model": c["model"], "tile": f"{H}x{W}", "active_pixels": part.N_total,
                           "global_batch": part.N_total, "seq_len": 1,
-                          "gp_train_points": a.n_train or c.get("n_train"), "parallelism": f"tile-dp{world}",
+                          "gp_train_points": a.n_train or c.get("n_train"), "parallelism": f"tile-dp{world}" + (f" x band-tp{B}" if B > 1 else ""),
                           "gn_iterations": gn, "finite": ok, "ingest_bytes_per_step": ingest,
                           "baseline_updates_per_s": c["baseline"]}}
         print(json.dumps(rec), flush=True)

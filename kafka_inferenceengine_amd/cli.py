@@ -98,8 +98,8 @@ def _build(args, comm):
 def cmd_run(args):
     from .parallel import Comm
 
-    comm = Comm.from_env(device=args.device)
-    if not comm.distributed:
+    comm = Comm.from_env(device=args.device, band_parallel=getattr(args, "band_parallel", None) or 1)
+    if not comm.distributed and comm.band is None:
         import torch
         dev = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
         comm = Comm.single(dev if dev != "cuda" else torch.device("cuda", torch.cuda.current_device()))

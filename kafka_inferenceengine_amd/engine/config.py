@@ -36,6 +36,9 @@ class EngineConfig:
     gp_split_min_d: int = 7                   # auto: split when a GP band has >= this many inputs
     gp_split_min_bands: int = 13              # auto: ... or when a date has >= this many GP bands
     band_chunk: int = 10                      # bands per operator/accumulation chunk in split mode
+    # band-parallel (TP-like) decomposition: ranks = strips x band_parallel;
+    # the B ranks of a strip split the bands and all-reduce the normal equations
+    band_parallel: int = 1
     # runtime
     device: str | None = None                 # 'cuda', 'cuda:1', 'cpu' (default: cuda if present)
     prefetch: bool = True                     # overlap next date's ingest with compute
@@ -55,6 +58,8 @@ class EngineConfig:
             raise ValueError("spatial_gamma must be >= 0")
         if self.spatial_gamma > 0 and self.analysis_form != "information":
             raise ValueError("the spatial regulariser runs in information form")
+        if self.band_parallel < 1:
+            raise ValueError("band_parallel must be >= 1")
         if self.min_iterations < 1 or self.max_iterations < self.min_iterations:
             raise ValueError("bad iteration limits")
         return self

@@ -100,6 +100,9 @@ class LinearKalman:
         self.metrics = MetricsLogger(self.config.metrics_path, rank=self.comm.rank)
         self.timer = PhaseTimer(self.device, sync=self.config.sync_timing)
         self._reg = None
+        band = getattr(self.comm, "band", None)
+        self.band_comm = band if (band is not None and band.world > 1) else None
+        self._bp_buf = None
         self.history = []
         LOG.info("Starting KaFKA run!!!")
 
@@ -401,8 +404,12 @@ class LinearKalman:
         obs = self.observations
         nb = obs.bands_per_observation[date]
         out = []
+        mine = range(nb)
+        if self.band_comm is not None and not self.config.band_sequential:
+            # band-parallel: this rank owns bands b = slot, slot + B, ...
+            mine = range(self.band_comm.rank, nb, self.band_comm.world)
         with self.timer.phase("ingest"):
-            for b in range(nb):
+            for b in mine:
                 if hasattr(obs, "get_device_band_data"):
                     db = obs.get_device_band_data(date, b)
                 else:
@@ -508,10 +515,14 @@ class LinearKalman:
             if need_inn else None
         gain = cfg.analysis_form == "gain"
         precomp = any(s.kind == OP_PRECOMP for s in specs)
-        split = None if (precomp or gain or cfg.spatial_gamma > 0) else self._split_plan(specs, dbs, h0_outs)
+        bp = self.band_comm is not None
+        if bp and (gain or cfg.spatial_gamma > 0 or cfg.hessian_correction):
+            raise ValueError("band_parallel runs the information form without regulariser / Hessian correction")
+        split = None if (precomp or gain or bp or cfg.spatial_gamma > 0) else self._split_plan(specs, dbs, h0_outs)
         table = None if (precomp or split) else build_table(specs, dbs, n, self._cache, self.device, h0_outs)
         prop = None
-        if isinstance(forecast, LazyForecast) and not (gain or precomp or split or cfg.spatial_gamma > 0) and N:
+        if isinstance(forecast, LazyForecast) and not (gain or precomp or split or bp or cfg.spatial_gamma > 0) \
+                and N:
             # fused propagation: the kernel computes the forecast per pixel from
             # the previous analysis; the first iteration linearises at it
             prop = forecast.handle()
@@ -542,6 +553,8 @@ class LinearKalman:
                                joseph=cfg.joseph)
                     elif cfg.spatial_gamma > 0:
                         self._regularised_iteration(table, x_prev, fc, x_new, P_out, status)
+                    elif bp:
+                        self._band_parallel_iteration(table, x_prev, fc, x_new, P_out, status)
                     elif split is not None:
                         self._split_iteration(split, x_prev, fc, x_new, P_out, status)
                     elif prop is not None:
@@ -571,6 +584,8 @@ class LinearKalman:
         if cfg.hessian_correction and not gain and N:
             with self.timer.phase("hessian"):
                 K.hessian(n, table, state.x, state.P, N=N)
+        if bp:
+            status = self._band_parallel_status(status)
         self.last_status = status
         inn = None
         if need_inn:
@@ -656,6 +671,43 @@ class LinearKalman:
             x_cur = dst
         # analysis precision includes the smoother's diagonal contribution
         reg.add_regulariser_diagonal(A_out, self.config.spatial_gamma)
+
+    # ------------------------------------------------ band-parallel (TP-like)
+    def _band_parallel_iteration(self, table, x_prev, fc: KFState, x_out, A_out, status):
+        """C5: this rank accumulates sum_b w h h^T and sum_b w h y' over its own
+        bands (band slot 0 also adds the forecast precision), one RCCL
+        all-reduce of the packed [A | b] per pixel within the band group, then
+        every member solves redundantly (identical x on the group)."""
+        n, N = self.n_params, self.N
+        nt = ntri(n)
+        ld = fc.x.shape[1]
+        if self._bp_buf is None or self._bp_buf.shape[1] != ld:
+            self._bp_buf = torch.zeros((nt + n, ld), dtype=torch.float32, device=self.device)
+            self._bp_solve_tab = build_table([], [], n, self._cache, self.device)
+            self._bp_status = torch.zeros(max(N, 1), dtype=torch.uint8, device=self.device)
+        A_part, b_part = self._bp_buf[:nt], self._bp_buf[nt:]
+        if N:
+            if self.band_comm.rank == 0:
+                K.analysis(n, table, x_prev, fc.x, fc.P, None, A_part, b_part, status, None, N=N, solve=False)
+            else:
+                self._bp_buf.zero_()
+                K.analysis(n, table, x_prev, fc.x, fc.P, None, A_part, b_part, status, None, N=N, solve=False,
+                           a_in=A_part, b_in=b_part)
+        with self.timer.phase("band_allreduce"):
+            self.band_comm.all_reduce_(self._bp_buf)
+        if N:
+            K.analysis(n, self._bp_solve_tab, x_prev, fc.x, fc.P, x_out, A_out, None, self._bp_status,
+                       self._partials, N=N, a_in=A_part, b_in=b_part)
+
+    def _band_parallel_status(self, status):
+        """Combine per-rank band flags (BAD_OP any, NO_OBS all) with the solve flags."""
+        N = self.N
+        flags = torch.stack([(status & K.ST_BAD_OP) > 0, (status & K.ST_NO_OBS) == 0]).to(torch.int32)
+        self.band_comm.all_reduce_(flags, op="max")
+        out = self._bp_status & ~torch.tensor(K.ST_NO_OBS, dtype=torch.uint8, device=status.device)
+        out = out | torch.where(flags[0] > 0, K.ST_BAD_OP, 0).to(torch.uint8)
+        out = out | torch.where(flags[1] > 0, 0, K.ST_NO_OBS).to(torch.uint8)
+        return out[:max(N, 1)]
 
     # --------------------------------------------------- band-sequential
     def _assimilate_sequential(self, step, forecast: KFState) -> AssimilationResult:

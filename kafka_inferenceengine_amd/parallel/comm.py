@@ -8,8 +8,16 @@ Collectives used by the engine (SURVEY.md §2.7 C1–C4):
   C2  halo exchange with the ±1 strip neighbours (``batch_isend_irecv``,
       point-to-point — one xGMI link per direction);
   C3  gather of output strips to rank 0 (optional);
-  C4  broadcast of setup objects.
+  C4  broadcast of setup objects;
+  C5  band-parallel (TP-like): all-reduce of the per-pixel
+      packed normal equations (A, b) inside a band group.
 Backend ``nccl`` is RCCL on ROCm; ``gloo`` is only the CPU test harness.
+
+Layout with ``band_parallel = B``: world = S x B; global rank r is strip
+``r // B`` and band slot ``r % B``.  The returned Comm spans the S strips that
+share a band slot (C1-C4 run there; halo peers are neighbouring strips) and
+``Comm.band`` spans the B ranks of one strip (C5).  Band groups are
+consecutive ranks, i.e. neighbouring GPUs on the xGMI mesh.
 """
 from __future__ import annotations
 
@@ -21,10 +29,12 @@ import torch.distributed as dist
 
 
 class Comm:
-    def __init__(self, rank: int = 0, world: int = 1, device=None, group=None):
+    def __init__(self, rank: int = 0, world: int = 1, device=None, group=None, ranks=None, band=None):
         self.rank = rank
         self.world = world
         self.group = group
+        self.ranks = list(ranks) if ranks is not None else list(range(world))   # global rank of each member
+        self.band = band                                                       # band-parallel sub-comm (C5)
         self.device = torch.device(device) if device is not None else torch.device("cpu")
 
     # ------------------------------------------------------------ setup
@@ -33,8 +43,10 @@ class Comm:
         return cls(0, 1, device)
 
     @classmethod
-    def from_env(cls, device=None, backend: str | None = None, timeout_s: float = 600.0) -> "Comm":
-        """Initialise from torchrun env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+    def from_env(cls, device=None, backend: str | None = None, timeout_s: float = 600.0,
+                 band_parallel: int = 1) -> "Comm":
+        """Initialise from torchrun env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*).
+        ``band_parallel`` > 1 splits the world into strips x band groups."""
         world = int(os.environ.get("WORLD_SIZE", "1"))
         if world <= 1 and not dist.is_initialized():
             return cls.single(device)
@@ -53,7 +65,21 @@ class Comm:
             if backend == "nccl":
                 kw["device_id"] = device
             dist.init_process_group(**kw)
-        return cls(dist.get_rank(), dist.get_world_size(), device)
+        rank, world = dist.get_rank(), dist.get_world_size()
+        B = int(band_parallel)
+        if B <= 1:
+            return cls(rank, world, device)
+        if world % B:
+            raise ValueError(f"world size {world} is not a multiple of band_parallel={B}")
+        S = world // B
+        # every rank creates every group in the same order (torch.distributed contract)
+        band_groups = [list(range(s * B, (s + 1) * B)) for s in range(S)]
+        strip_groups = [list(range(b, world, B)) for b in range(B)]
+        bg = [dist.new_group(r) for r in band_groups]
+        sg = [dist.new_group(r) for r in strip_groups]
+        s_idx, b_idx = rank // B, rank % B
+        band = cls(b_idx, B, device, bg[s_idx], band_groups[s_idx])
+        return cls(s_idx, S, device, sg[b_idx], strip_groups[b_idx], band=band)
 
     @property
     def distributed(self) -> bool:
@@ -81,18 +107,30 @@ class Comm:
         return int(t.item())
 
     def max_float(self, v: float) -> float:
+        """Max over every rank of the job (strips and band groups)."""
+        if self.band is not None:
+            v = self.band.max_float(v)
         if not self.distributed:
             return float(v)
         t = torch.tensor([float(v)], dtype=torch.float64, device=self.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return float(t.item())
 
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """C5: in-place all-reduce over this communicator (sum | max)."""
+        if self.distributed:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX, group=self.group)
+        return t
+
     def barrier(self):
+        """Barrier over every rank of the job (strips and band groups)."""
         if self.distributed:
             if self.device.type == "cuda":
                 dist.barrier(group=self.group, device_ids=[self.device.index])
             else:
                 dist.barrier(group=self.group)
+        if self.band is not None:
+            self.band.barrier()
 
     def broadcast_object(self, obj, src: int = 0):
         """C4: broadcast a picklable setup object from ``src`` (objects created by
@@ -100,7 +138,7 @@ class Comm:
         if not self.distributed:
             return obj
         lst = [obj]
-        dist.broadcast_object_list(lst, src=src, group=self.group)
+        dist.broadcast_object_list(lst, src=self.ranks[src], group=self.group)
         return lst[0]
 
     def exchange_halo(self, send_up: torch.Tensor | None, send_down: torch.Tensor | None,
@@ -112,14 +150,14 @@ class Comm:
         ops = []
         if self.rank > 0:
             if send_up is not None and send_up.numel():
-                ops.append(dist.P2POp(dist.isend, send_up.contiguous(), self.rank - 1, group=self.group))
+                ops.append(dist.P2POp(dist.isend, send_up.contiguous(), self.ranks[self.rank - 1], group=self.group))
             if recv_up is not None and recv_up.numel():
-                ops.append(dist.P2POp(dist.irecv, recv_up, self.rank - 1, group=self.group))
+                ops.append(dist.P2POp(dist.irecv, recv_up, self.ranks[self.rank - 1], group=self.group))
         if self.rank < self.world - 1:
             if send_down is not None and send_down.numel():
-                ops.append(dist.P2POp(dist.isend, send_down.contiguous(), self.rank + 1, group=self.group))
+                ops.append(dist.P2POp(dist.isend, send_down.contiguous(), self.ranks[self.rank + 1], group=self.group))
             if recv_down is not None and recv_down.numel():
-                ops.append(dist.P2POp(dist.irecv, recv_down, self.rank + 1, group=self.group))
+                ops.append(dist.P2POp(dist.irecv, recv_down, self.ranks[self.rank + 1], group=self.group))
         if ops:
             for r in dist.batch_isend_irecv(ops):
                 r.wait()
@@ -133,11 +171,11 @@ class Comm:
         pad = torch.zeros((rows, maxn), dtype=t.dtype, device=t.device)
         pad[:, :t.shape[1]] = t
         out = [torch.zeros_like(pad) for _ in range(self.world)] if self.rank == 0 else None
-        dist.gather(pad, out, dst=0, group=self.group)
+        dist.gather(pad, out, dst=self.ranks[0], group=self.group)
         if self.rank != 0:
             return None
         return torch.cat([o[:, :n] for o, n in zip(out, sizes)], dim=1)
 
     def destroy(self):
-        if self.distributed and dist.is_initialized():
+        if (self.distributed or self.band is not None) and dist.is_initialized():
             dist.destroy_process_group()

@@ -106,12 +106,14 @@ def test_strip_partition_balances_active_pixels():
     assert np.array_equal(g, np.flatnonzero(mask.ravel()))
 
 
-def test_bench_torchrun_gloo_two_ranks():
+@pytest.mark.parametrize("extra", [[], ["--config", "prosail10", "--size", "40", "--band-parallel", "2"]],
+                         ids=["tile-dp", "band-parallel"])
+def test_bench_torchrun_gloo_two_ranks(extra):
     """bench.py under torch.distributed.run with 2 CPU ranks (gloo)."""
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--size", "96", "--n-train", "40", "--device", "cpu"]
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--size", "96", "--n-train", "40", "--device", "cpu"] + extra
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     import json
@@ -119,3 +121,64 @@ def test_bench_torchrun_gloo_two_ranks():
     assert len(lines) == 1
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["config"]["finite"]
+
+
+def _bp_worker(rank, world, port, B, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import kafka_inferenceengine_amd as k
+    from kafka_inferenceengine_amd.parallel import Comm, StripPartition
+
+    torch.set_num_threads(1)
+    comm = Comm.from_env(device="cpu", band_parallel=B)
+    try:
+        q.put(_bp_run(k, comm, StripPartition))
+    finally:
+        comm.destroy()
+
+
+def _bp_run(k, comm, StripPartition):
+    mask = np.ones((20, 18), bool)
+    mask[3:6, 2:9] = False
+    part = StripPartition(mask, comm.rank, comm.world)
+    obs = k.SyntheticS2Observations(mask, n_bands=5, n_train=24, device="cpu", stream=False, n_pool=2,
+                                    partition=part, field_cell=6, seed=4)
+    prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
+    kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
+                        state_propagation=None, prior=prior, device="cpu", comm=comm, partition=part,
+                        config=k.EngineConfig(gp_split="never"))
+    grid = [obs.dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in obs.dates[:2]]
+    st = kf.run(grid, kf.state_from_prior(prior), None, None)
+    g = comm.ranks[comm.rank] if comm.band is None else comm.band.ranks[comm.band.rank]
+    return (g, part.offset, st.x.numpy().copy(), [h["gn_iterations"] for h in kf.history],
+            kf.last_status.numpy().copy())
+
+
+@pytest.mark.parametrize("world,B", [(2, 2), (4, 2)], ids=["1strip-x-2bands", "2strips-x-2bands"])
+def test_band_parallel_equals_single_rank(world, B):
+    """Band-parallel (TP-like) decomposition: bands split over the ranks of a
+    strip, normal equations all-reduced (C5) — same result as one rank."""
+    import kafka_inferenceengine_amd as k
+    from kafka_inferenceengine_amd.parallel import Comm, StripPartition
+
+    ref = _bp_run(k, Comm.single("cpu"), StripPartition)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bp_worker, args=(r, world, port, B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    S = world // B
+    for s in range(S):
+        members = res[s * B:(s + 1) * B]
+        for m in members[1:]:      # every member of a band group holds the identical state
+            assert np.array_equal(m[2], members[0][2]) and np.array_equal(m[4], members[0][4])
+    x = np.concatenate([res[s * B][2] for s in range(S)], 1)
+    st = np.concatenate([res[s * B][4][:res[s * B][2].shape[1]] for s in range(S)])
+    assert np.allclose(x, ref[2], rtol=1e-4, atol=1e-5)
+    assert all(r[3] == ref[3] for r in res)
+    assert np.array_equal(st, ref[4][:ref[2].shape[1]])
