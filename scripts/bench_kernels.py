@@ -52,12 +52,15 @@ def main():
                 times[v].append(s.elapsed_time(e))
             outs[v] = xo.clone()
     ref = outs[variants[0]]
+    # GP point evaluations per launch: valid (unmasked) pixel-bands x training points
+    pts = sum(int((d.decode()[1] > 0).sum().item()) for _, d in bands) * a.n_train
     res = {}
     for v in variants:
         t = np.array(times[v])
         res[v] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
+                  "gpoints_per_s": round(pts / (np.median(t) * 1e-3) / 1e9, 1),
                   "max_abs_diff_vs_first": float((outs[v] - ref).abs().max())}
-    print(json.dumps({"size": a.size, "N": N, "n_train": a.n_train, "variants": res}))
+    print(json.dumps({"size": a.size, "N": N, "n_train": a.n_train, "points": pts, "variants": res}))
 
 
 if __name__ == "__main__":
