@@ -187,4 +187,4 @@ def test_fused_propagation_device(cuda, mode, blend, quirk, pmask):
     for (x1, a1, s1), (x2, a2, s2), (x3, a3, s3) in zip(ref, fused, host):
         assert np.array_equal(s1, s2)
         assert close(x2, x1, 1e-4) and close(a2, a1, 1e-5)
-        assert close(x2, x3) and close(a2, a3, 1e-5)
+        assert close(x2, x3) and close(a2, a3, 1e-4)
