@@ -280,7 +280,47 @@ KF_HD float gp_rec(const KF_CONST_AS float* r, int R, int i, int f) {
   return r[((int64_t)(i >> 1) * R + f) * 2 + (i & 1)];
 }
 
-template <int NP, int D, int UNR = 4>
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef float kf_f2 __attribute__((ext_vector_type(2)));
+
+// Streams the band's training-point pairs (s_load into SGPRs) and accumulates
+// S0 = sum alpha k and S_d = sum alpha t_d k, two points per v_pk_fma_f32.
+// ADDC: exponent = L + c + B.x (c the per-pixel -0.5 log2e sum lambda x^2);
+// without it the exponent is L + B.x and the caller rescales by 2^c.
+template <int D, int UNR, bool ADDC>
+__device__ __forceinline__ void gp_pairs(const KF_CONST_AS kf_f2* __restrict__ r2, int T2, const kf_f2 (&xv)[D],
+                                         kf_f2 cv, kf_f2& S0v, kf_f2 (&Sv)[D]) {
+  constexpr int R = 2 * D + 2;
+#pragma unroll UNR
+  for (int i = 0; i < T2; ++i) {
+    const KF_CONST_AS kf_f2* __restrict__ ri = r2 + (int64_t)i * R;
+    kf_f2 e;
+    if constexpr (ADDC) {
+      e = ri[0] + cv;
+#pragma unroll
+      for (int d = 0; d < D; ++d) e = __builtin_elementwise_fma(ri[1 + d], xv[d], e);
+    } else {
+      e = __builtin_elementwise_fma(ri[1], xv[0], ri[0]);
+#pragma unroll
+      for (int d = 1; d < D; ++d) e = __builtin_elementwise_fma(ri[1 + d], xv[d], e);
+    }
+    kf_f2 k;
+    k.x = kexp2(e.x);
+    k.y = kexp2(e.y);
+    S0v = __builtin_elementwise_fma(ri[1 + D], k, S0v);
+#pragma unroll
+    for (int d = 0; d < D; ++d) Sv[d] = __builtin_elementwise_fma(ri[2 + D + d], k, Sv[d]);
+  }
+}
+#endif
+
+// FOLD: when every lane of the wave has -c <= GP_FOLD_MAX the per-point "+ c"
+// is dropped from the exponent (one packed op of D + 2 per point pair) and the
+// sums are rescaled by 2^c once; exponents then grow by at most GP_FOLD_MAX,
+// i.e. <= ~1e-6 relative error in k.  Otherwise the wave takes the exact loop.
+constexpr float GP_FOLD_MAX = 16.f;
+
+template <int NP, int D, int UNR = 4, bool FOLD = false>
 KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&h)[NP]) {
   float xi[D];
   float c = 0.f;
@@ -293,25 +333,23 @@ KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&
   float S0, S[D];
   constexpr int R = 2 * D + 2;
 #if defined(__HIP_DEVICE_COMPILE__)
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  const KF_CONST_AS f2* __restrict__ r2 = (const KF_CONST_AS f2*)cptr(bd.gp);
+  const KF_CONST_AS kf_f2* __restrict__ r2 = (const KF_CONST_AS kf_f2*)cptr(bd.gp);
   const int T2 = bd.T >> 1;
-  f2 S0v = {0.f, 0.f}, Sv[D], xv[D];
-  const f2 cv = {c, c};
+  kf_f2 S0v = {0.f, 0.f}, Sv[D], xv[D];
+  const kf_f2 cv = {c, c};
 #pragma unroll
-  for (int d = 0; d < D; ++d) { Sv[d] = f2{0.f, 0.f}; xv[d] = f2{xi[d], xi[d]}; }
-#pragma unroll UNR
-  for (int i = 0; i < T2; ++i) {
-    const KF_CONST_AS f2* __restrict__ ri = r2 + (int64_t)i * R;
-    f2 e = ri[0] + cv;
+  for (int d = 0; d < D; ++d) { Sv[d] = kf_f2{0.f, 0.f}; xv[d] = kf_f2{xi[d], xi[d]}; }
+  bool folded = false;
+  if constexpr (FOLD) folded = __all(c >= -GP_FOLD_MAX);
+  if (folded)
+    gp_pairs<D, UNR, false>(r2, T2, xv, cv, S0v, Sv);
+  else
+    gp_pairs<D, UNR, true>(r2, T2, xv, cv, S0v, Sv);
+  if (folded) {
+    const float sc = kexp2(c);
+    S0v *= sc;
 #pragma unroll
-    for (int d = 0; d < D; ++d) e = __builtin_elementwise_fma(ri[1 + d], xv[d], e);
-    f2 k;
-    k.x = kexp2(e.x);
-    k.y = kexp2(e.y);
-    S0v = __builtin_elementwise_fma(ri[1 + D], k, S0v);
-#pragma unroll
-    for (int d = 0; d < D; ++d) Sv[d] = __builtin_elementwise_fma(ri[2 + D + d], k, Sv[d]);
+    for (int d = 0; d < D; ++d) Sv[d] *= sc;
   }
   S0 = S0v.x + S0v.y;
 #pragma unroll
@@ -560,7 +598,7 @@ KF_HD void pixel_propagate(const PropArgs& a, int64_t p) {
 // Returns (x_a - x0)^2 summed over parameters.
 // FD > 0: fast path where every band is a GP with FD inputs and FOBS encoding
 // (the compiler then drops the SAR/linear/precomputed code and its registers).
-template <int NP, int FD = 0, int FOBS = 0, int UNR = 4>
+template <int NP, int FD = 0, int FOBS = 0, int UNR = 4, bool FOLD = false>
 KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a.ld;
@@ -606,7 +644,7 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
     float H0, h[NP];
     bool ok;
     if constexpr (FD > 0) {
-      gp_eval<NP, FD, UNR>(bd, x0, H0, h);
+      gp_eval<NP, FD, UNR, FOLD>(bd, x0, H0, h);
       ok = finitef(H0);
 #pragma unroll
       for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);

@@ -37,12 +37,12 @@ __device__ __forceinline__ void block_partial(double v, double* partials) {
   }
 }
 
-template <int NP, int FD = 0, int FOBS = 0, int UNR = 4>
+template <int NP, int FD = 0, int FOBS = 0, int UNR = 4, bool FOLD = false>
 __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
-    acc += (double)pixel_analysis<NP, FD, FOBS, UNR>(a, p);
+    acc += (double)pixel_analysis<NP, FD, FOBS, UNR, FOLD>(a, p);
   if (a.partials) block_partial(acc, a.partials);
 }
 
@@ -237,15 +237,13 @@ static inline int grid_for(int64_t N, int max_blocks) {
 
 template <int NP, int FD>
 static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
+  // variant (A/B tuning, scripts/bench_kernels.py): 0 unroll-4 pairs (default),
+  // 1 unroll-4 + folded exponent, 2 unroll-8
   if (a.fast_obs == OBS_DN16) {
     if (a.variant == 1)
-      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 1>), dim3(grid), dim3(BLOCK), 0, s, a);
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 4, true>), dim3(grid), dim3(BLOCK), 0, s, a);
     else if (a.variant == 2)
-      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 4>), dim3(grid), dim3(BLOCK), 0, s, a);
-    else if (a.variant == 3)
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 8>), dim3(grid), dim3(BLOCK), 0, s, a);
-    else if (a.variant == 4)
-      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 16>), dim3(grid), dim3(BLOCK), 0, s, a);
     else
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
   } else if (a.fast_obs == OBS_F32) {
