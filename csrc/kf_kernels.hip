@@ -186,12 +186,21 @@ __global__ __launch_bounds__(BLOCK) void gather_kernel(const T* src, const int64
   }
 }
 
-__global__ void reduce_partials_kernel(const double* partials, int n, double* out) {
-  // one wave, fixed order: lane-strided sums then a fixed shuffle tree
+constexpr int RED_BLOCK = 1024;
+__global__ __launch_bounds__(RED_BLOCK) void reduce_partials_kernel(const double* partials, int n, double* out) {
+  // one workgroup, fixed order (bit-reproducible): thread-strided sums, a fixed
+  // shuffle tree per wave, then the 16 wave sums in wave order
+  __shared__ double red[RED_BLOCK / 64];
   double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += 64) s += partials[i];
+  for (int i = threadIdx.x; i < n; i += RED_BLOCK) s += partials[i];
   s = wave_sum(s);
-  if (threadIdx.x == 0) out[0] = s;
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < RED_BLOCK / 64; ++w) t += red[w];
+    out[0] = t;
+  }
 }
 
 // K7: nearest LUT entry (utils.py:225-234); LUT staged in LDS.
@@ -303,7 +312,14 @@ static void l_unpack(const float* x, const float* a, int64_t N, int64_t ld, cons
   hipLaunchKernelGGL(unpack_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, x, a, N, ld, idx, mean, unc, plane);
 }
 
-int dev_grid(int64_t N) { return grid_for(N, KF_MAX_BLOCKS); }
+// Grid cap for the per-pixel kernels (one f64 partial per workgroup).  The
+// default keeps grid-stride loops; raising it to >= N/256 gives one pixel per
+// thread so workgroups start and finish at different times and their memory
+// phases overlap other workgroups' compute.
+static int g_max_blocks = KF_MAX_BLOCKS;
+void set_max_blocks(int n) { g_max_blocks = n > 0 ? n : KF_MAX_BLOCKS; }
+int get_max_blocks() { return g_max_blocks; }
+int dev_grid(int64_t N) { return grid_for(N, g_max_blocks); }
 
 bool gp_operator_supported(int np, int d) {
   return (np == 10 && (d == 10 || d == 4)) || (np == 7 && (d == 7 || d == 4)) || (np == d && np >= 2 && np <= 4);
@@ -359,7 +375,7 @@ hipError_t dev_unpack(int np, const float* x, const float* a, int64_t N, int64_t
   return hipGetLastError();
 }
 hipError_t dev_reduce(const double* partials, int n, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(64), 0, s, partials, n, out);
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(RED_BLOCK), 0, s, partials, n, out);
   return hipGetLastError();
 }
 hipError_t dev_gather(int elem_bytes, const void* src, const int64_t* idx, void* dst, int64_t n, int rows,

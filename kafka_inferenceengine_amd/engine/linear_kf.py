@@ -543,6 +543,9 @@ class LinearKalman:
         n_iter = 1
         len_x = float(n * self.n_total)
         while True:
+            # the analysis precision is only needed from the iteration that can
+            # end the loop on: skip its 4*ntri B/px store before min_iterations
+            A_keep = P_out if n_iter >= cfg.min_iterations else None
             if precomp:
                 pre = self._precompute_host(specs, dbs, x_prev)
                 table = build_table(specs, dbs, n, self._cache, self.device, h0_outs, pre)
@@ -554,14 +557,14 @@ class LinearKalman:
                     elif cfg.spatial_gamma > 0:
                         self._regularised_iteration(table, x_prev, fc, x_new, P_out, status)
                     elif bp:
-                        self._band_parallel_iteration(table, x_prev, fc, x_new, P_out, status)
+                        self._band_parallel_iteration(table, x_prev, fc, x_new, A_keep, status)
                     elif split is not None:
-                        self._split_iteration(split, x_prev, fc, x_new, P_out, status)
+                        self._split_iteration(split, x_prev, fc, x_new, A_keep, status)
                     elif prop is not None:
-                        K.analysis(n, table, x_prev, None, None, x_new, P_out, None, status, self._partials, N=N,
+                        K.analysis(n, table, x_prev, None, None, x_new, A_keep, None, status, self._partials, N=N,
                                    prop=prop)
                     else:
-                        K.analysis(n, table, x_prev, fc.x, fc.P, x_new, P_out, None, status, self._partials, N=N)
+                        K.analysis(n, table, x_prev, fc.x, fc.P, x_new, A_keep, None, status, self._partials, N=N)
                     K.reduce_partials(self._partials, self._red)
                 else:
                     self._red.zero_()

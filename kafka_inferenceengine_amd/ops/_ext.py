@@ -20,6 +20,15 @@ except ImportError as e:  # pragma: no cover - exercised only when unbuilt
     _err = e
 
 
+def _apply_env(m):
+    """KAFKA_MAX_BLOCKS: grid cap of the per-pixel kernels (tuning / A-B)."""
+    if m is not None and os.environ.get("KAFKA_MAX_BLOCKS") and hasattr(m, "set_max_blocks"):
+        m.set_max_blocks(int(os.environ["KAFKA_MAX_BLOCKS"]))
+
+
+_apply_env(ext)
+
+
 def require_ext():
     if ext is None:
         raise RuntimeError(
@@ -44,4 +53,5 @@ def ensure_built(verbose: bool = False):
 
     ext = importlib.import_module("kafka_inferenceengine_amd._kafka_hip")
     _err = None
+    _apply_env(ext)
     return ext

@@ -36,16 +36,24 @@ def main():
     Pf = torch.tensor(pack_matrix(Pi), dtype=torch.float32, device=dev)[:, None].expand(28, N).contiguous()
     xo = torch.empty_like(xf)
     ao = torch.empty_like(Pf)
-    part = K.partials_buffer(N, dev)
-    variants = a.variants.split(",")
+    variants = a.variants.split(",")   # "V" or "V@MAXBLOCKS" (grid cap; 0 = default)
+    ext = K.ext()
+    default_cap = ext.get_max_blocks()
+    parts = {}
+    for v in variants:
+        cap = int(v.split("@")[1]) if "@" in v else 0
+        ext.set_max_blocks(cap or default_cap)
+        parts[v] = K.partials_buffer(N, dev)
     times = {v: [] for v in variants}
     outs = {}
     for r in range(a.rounds + 1):
         for v in variants:
+            vv, cap = (v.split("@") + ["0"])[:2]
+            ext.set_max_blocks(int(cap) or default_cap)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            K.analysis(7, tab, xf, xf, Pf, xo, ao, None, None, part, fast=(v != "g"),
-                       variant=0 if v == "g" else int(v))
+            K.analysis(7, tab, xf, xf, Pf, xo, ao, None, None, parts[v], fast=(vv != "g"),
+                       variant=0 if vv == "g" else int(vv))
             e.record()
             e.synchronize()
             if r:
