@@ -137,6 +137,23 @@ KF_HD float kexp2(float x) {
 
 KF_HD bool finitef(float v) { return v - v == 0.f; }
 
+// Hardware reciprocal / reciprocal square root (1 ulp) instead of the ~10-
+// instruction IEEE division expansion; the per-pixel solves are f32 anyway.
+KF_HD float kf_rcp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcpf(x);
+#else
+  return 1.f / x;
+#endif
+}
+KF_HD float kf_rsqrt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rsqf(x);
+#else
+  return 1.f / sqrtf(x);
+#endif
+}
+
 // Wave-uniform read-only data (band descriptors, GP training records) is read
 // through the constant address space so hipcc emits scalar s_load/s_buffer
 // loads into SGPRs (one fetch per wave, no VGPRs, no vector-memory traffic).
@@ -161,6 +178,8 @@ KF_HD const KF_CONST_AS T* opaque(const KF_CONST_AS T* p) {
 }
 
 // In-place packed Cholesky A = U^T U (U upper, stored in A's packed slots).
+// Convention: the diagonal slots hold 1 / U_jj (what the solves multiply by);
+// only chol_solve / chol_inverse read a factor.
 template <int NP>
 KF_HD bool chol_packed(float (&A)[ntri(NP)]) {
   bool ok = true;
@@ -171,9 +190,8 @@ KF_HD bool chol_packed(float (&A)[ntri(NP)]) {
     for (int k = 0; k < j; ++k) s = fmaf(-A[tri(NP, k, j)], A[tri(NP, k, j)], s);
     ok = ok && (s > 0.f) && finitef(s);
     s = s > 0.f ? s : 1.f;
-    const float r = sqrtf(s);
-    const float inv = 1.f / r;
-    A[tri(NP, j, j)] = r;
+    const float inv = kf_rsqrt(s);
+    A[tri(NP, j, j)] = inv;
 #pragma unroll
     for (int i = j + 1; i < NP; ++i) {
       float t = A[tri(NP, j, i)];
@@ -193,14 +211,14 @@ KF_HD void chol_solve(const float (&U)[ntri(NP)], float (&b)[NP]) {
     float t = b[i];
 #pragma unroll
     for (int k = 0; k < i; ++k) t = fmaf(-U[tri(NP, k, i)], b[k], t);
-    b[i] = t / U[tri(NP, i, i)];
+    b[i] = t * U[tri(NP, i, i)];
   }
 #pragma unroll
   for (int i = NP - 1; i >= 0; --i) {  // U x = z
     float t = b[i];
 #pragma unroll
     for (int k = i + 1; k < NP; ++k) t = fmaf(-U[tri(NP, i, k)], b[k], t);
-    b[i] = t / U[tri(NP, i, i)];
+    b[i] = t * U[tri(NP, i, i)];
   }
 }
 
@@ -245,7 +263,7 @@ KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y, float& w) {
     const uint16_t dn = bd.dn[p];
     y = (float)dn * bd.scale;
     float sig = fmaxf(bd.rel_unc * y, bd.unc_floor);
-    w = (dn > 0 && sig > 0.f) ? 1.f / (sig * sig) : 0.f;
+    w = (dn > 0 && sig > 0.f) ? kf_rcp(sig * sig) : 0.f;
     if (dn == 0) y = 0.f;
   } else if (FOBS == OBS_F32 || (FOBS == 0 && bd.obs == OBS_F32)) {
     y = bd.y[p];
@@ -471,7 +489,7 @@ KF_HD void forecast_partial(const KF_CONST_AS PropArgs* a, int64_t p, float (&xf
     if ((a->prop_mask >> j) & 1u) {
       const float q = a->q_pix ? a->q_pix[j * ld + p] : a->q[j];
       xf[j] = a->m[j] * a->x_a[j * ld + p];
-      P[tri(NP, j, j)] = 1.f / (1.f / a->p_a[tri(NP, j, j) * ld + p] + q);
+      P[tri(NP, j, j)] = kf_rcp(kf_rcp(a->p_a[tri(NP, j, j) * ld + p]) + q);
     }
   }
 }

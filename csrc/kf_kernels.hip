@@ -247,12 +247,14 @@ static inline int grid_for(int64_t N, int max_blocks) {
 template <int NP, int FD>
 static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
   // variant (A/B tuning, scripts/bench_kernels.py): 0 unroll-4 pairs (default),
-  // 1 unroll-4 + folded exponent, 2 unroll-8
+  // 1 unroll-4 + folded exponent, 2 unroll-8, 3 unroll-3
   if (a.fast_obs == OBS_DN16) {
     if (a.variant == 1)
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 4, true>), dim3(grid), dim3(BLOCK), 0, s, a);
     else if (a.variant == 2)
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 8>), dim3(grid), dim3(BLOCK), 0, s, a);
+    else if (a.variant == 3)
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 3>), dim3(grid), dim3(BLOCK), 0, s, a);
     else
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
   } else if (a.fast_obs == OBS_F32) {
