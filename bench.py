@@ -194,6 +194,10 @@ def main():
         prof.__exit__(None, None, None)
         prof.export_chrome_trace(a.profile)
     ok = bool(torch.isfinite(state.x[:, :state.N]).all().item())
+    # numerical health: pixels whose solve fell back to the forecast (should be ~0)
+    st_last = getattr(kf, "last_status", None)
+    fallback = 0.0 if st_last is None or not state.N else \
+        float(((st_last[:state.N] & 16) > 0).float().mean().item())
     value = float(part.N_total) * a.steps / elapsed
     if g_rank == 0:
         gn = [h.get("gn_iterations") for h in kf.history[a.warmup:]]
@@ -210,7 +214,7 @@ def main():
                "config": {"name": a.config, "model": c["model"], "tile": f"{H}x{W}", "active_pixels": part.N_total,
                           "global_batch": part.N_total, "seq_len": 1,
                           "gp_train_points": a.n_train or c.get("n_train"), "parallelism": f"tile-dp{world}" + (f" x band-tp{B}" if B > 1 else ""),
-                          "gn_iterations": gn, "finite": ok, "ingest_bytes_per_step": ingest,
+                          "gn_iterations": gn, "finite": ok, "fallback_frac": round(fallback, 6), "ingest_bytes_per_step": ingest,
                           "baseline_updates_per_s": c["baseline"]}}
         print(json.dumps(rec), flush=True)
     comm.destroy()

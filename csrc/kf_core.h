@@ -135,7 +135,9 @@ KF_HD float kexp2(float x) {
 #endif
 }
 
-KF_HD bool finitef(float v) { return v - v == 0.f; }
+// (not `v - v == 0`: with FP contraction the compiler rewrites a product's
+// `v - v` into fma(a, b, -a*b), the product's rounding error, which is != 0)
+KF_HD bool finitef(float v) { return __builtin_isfinite(v); }
 
 // Hardware reciprocal / reciprocal square root (1 ulp) instead of the ~10-
 // instruction IEEE division expansion; the per-pixel solves are f32 anyway.

@@ -121,6 +121,7 @@ def test_bench_torchrun_gloo_two_ranks(extra):
     assert len(lines) == 1
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["config"]["finite"]
+    assert rec["config"]["fallback_frac"] < 0.01
 
 
 def _bp_worker(rank, world, port, B, q):
