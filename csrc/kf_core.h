@@ -523,7 +523,7 @@ KF_HD uint8_t forecast_pixel(const PropArgs& a, int64_t p, float (&xf)[NP], floa
         xf[j] = pj ? a.m[j] * a.x_a[j * ld + p] : a.reset_mean[j];
         if (pj) {
           const float pa = a.p_a[tri(NP, j, j) * ld + p];
-          P[tri(NP, j, j)] = 1.f / (1.f / pa + q[j]);
+          P[tri(NP, j, j)] = kf_rcp(kf_rcp(pa) + q[j]);   // same rounding as forecast_partial
         }
       }
     } break;
