@@ -340,8 +340,28 @@ __device__ __forceinline__ void gp_pairs(const KF_CONST_AS kf_f2* __restrict__ r
 // i.e. <= ~1e-6 relative error in k.  Otherwise the wave takes the exact loop.
 constexpr float GP_FOLD_MAX = 16.f;
 
-template <int NP, int D, int UNR = 4, bool FOLD = false>
-KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&h)[NP]) {
+// f = offset + S0,  df/dx_d = -lambda_d (x_d S0 - S_d), scattered to the state.
+template <int NP, int D, typename F, typename I>
+KF_HD void gp_epilogue(float offset, const F& coef, const I& map, const float (&xi)[D], float S0,
+                       const float (&S)[D], float& H0, float (&h)[NP]) {
+  H0 = offset + S0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) h[j] = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const float g = -coef[d] * fmaf(xi[d], S0, -S[d]);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) h[j] += (map[d] == j) ? g : 0.f;
+  }
+}
+
+// RELOAD + bdp (device fast paths): the descriptor's table entry; its epilogue fields
+// are then re-read after the record stream through an opaque pointer instead
+// of being kept live in SGPRs across it (which spills them to VGPR lanes:
+// ~270 fewer v_readlane/v_writelane per pixel in analysis_kernel<7,4,DN16>).
+template <int NP, int D, int UNR = 4, bool FOLD = false, bool RELOAD = false>
+KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&h)[NP],
+                   const BandDesc* bdp = nullptr) {
   float xi[D];
   float c = 0.f;
 #pragma unroll
@@ -393,15 +413,14 @@ KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&
 #pragma unroll
   for (int d = 0; d < D; ++d) S[d] = Sa[0][d] + Sa[1][d];
 #endif
-  H0 = bd.offset + S0;
-#pragma unroll
-  for (int j = 0; j < NP; ++j) h[j] = 0.f;
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    const float g = -bd.coef[d] * fmaf(xi[d], S0, -S[d]);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) h[j] += (bd.map[d] == j) ? g : 0.f;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (RELOAD) {
+    const KF_CONST_AS BandDesc* q = opaque(cptr(bdp));
+    gp_epilogue<NP, D>(q->offset, q->coef, q->map, xi, S0, S, H0, h);
+    return;
   }
+#endif
+  gp_epilogue<NP, D>(bd.offset, bd.coef, bd.map, xi, S0, S, H0, h);
 }
 
 // Water Cloud Model (sar_forward_model.py:13-106), analytic gradient.
@@ -611,6 +630,58 @@ KF_HD void pixel_propagate(const PropArgs& a, int64_t p) {
   if (a.status) a.status[p] |= st;
 }
 
+// K1 epilogue: store (A, b) if requested, factor and solve, health fallback
+// to the forecast, store x and status; returns |x - x0|^2.  AP is a host or
+// constant-address-space pointer to the launch arguments.
+template <int NP, typename AP>
+KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[NP], const float (&x0)[NP],
+                              uint8_t st) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a->ld;
+  if (a->a_out) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = A[t];
+  }
+  if (a->b_out) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) a->b_out[j * ld + p] = b[j];
+  }
+  float dn = 0.f;
+  if (a->solve) {
+    const bool spd = chol_packed<NP>(A);
+    chol_solve<NP>(A, b);
+    bool fin = true;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) fin = fin && finitef(b[j]);
+    if (!spd || !fin) {
+      // Health fallback: keep the forecast (prior) for this pixel.
+      st |= (!spd ? ST_NONSPD : 0) | (!fin ? ST_NONFINITE : 0) | ST_FALLBACK;
+      if (a->prop) {
+        forecast_partial<NP>(opaque(cptr(a->prop)), p, b, A);   // rare path: recompute instead of keeping it live
+        if (a->a_out) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = A[t];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NP; ++j) b[j] = a->x_f[j * ld + p];
+        if (a->a_out) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = a->pf_inv[t * ld + p];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      a->x_out[j * ld + p] = b[j];
+      const float d = b[j] - x0[j];
+      dn = fmaf(d, d, dn);
+    }
+  }
+  if (a->status) a->status[p] = st;
+  return dn;
+}
+
 // ---------------------------------------------------------------------------
 // K1: fused Gauss-Newton analysis for one pixel (information form).
 //   A = P_f^-1 + sum_b w_b h_b h_b^T,  b = P_f^-1 x_f + sum_b w_b h_b y'_b,
@@ -664,14 +735,22 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
     float H0, h[NP];
     bool ok;
     if constexpr (FD > 0) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      gp_eval<NP, FD, UNR, FOLD, true>(bd, x0, H0, h, a.bands + bi);
+#else
       gp_eval<NP, FD, UNR, FOLD>(bd, x0, H0, h);
+#endif
       ok = finitef(H0);
 #pragma unroll
       for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);
     } else {
       ok = eval_operator<NP>(bd, p, ld, x0, H0, h);
     }
-    if (bd.h0_out) bd.h0_out[p] = H0;
+    float* h0o = bd.h0_out;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (FD > 0) h0o = opaque(cptr(a.bands + bi))->h0_out;   // not live across the GP loop
+#endif
+    if (h0o) h0o[p] = H0;
     if (!ok) { st |= ST_BAD_OP; continue; }
     ++nobs;
     float yp = y - H0;
@@ -687,48 +766,17 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
     }
   }
   if (nobs == 0) st |= ST_NO_OBS;
-  if (a.a_out) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = A[t];
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (FD > 0) {
+    // fast kernels: re-read the launch arguments from the kernarg segment
+    // through an opaque pointer, so they are not pinned in SGPRs across the
+    // band / record loops above (analysis_kernel passes them at offset 0)
+    const KF_CONST_AS AnalysisArgs* ka =
+        opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
+    return analysis_epilogue<NP>(ka, p, A, b, x0, st);
   }
-  if (a.b_out) {
-#pragma unroll
-    for (int j = 0; j < NP; ++j) a.b_out[j * ld + p] = b[j];
-  }
-  float dn = 0.f;
-  if (a.solve) {
-    const bool spd = chol_packed<NP>(A);
-    chol_solve<NP>(A, b);
-    bool fin = true;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) fin = fin && finitef(b[j]);
-    if (!spd || !fin) {
-      // Health fallback: keep the forecast (prior) for this pixel.
-      st |= (!spd ? ST_NONSPD : 0) | (!fin ? ST_NONFINITE : 0) | ST_FALLBACK;
-      if (a.prop) {
-        forecast_partial<NP>(opaque(cptr(a.prop)), p, b, A);   // rare path: recompute instead of keeping it live
-        if (a.a_out) {
-#pragma unroll
-          for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = A[t];
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < NP; ++j) b[j] = a.x_f[j * ld + p];
-        if (a.a_out) {
-#pragma unroll
-          for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = a.pf_inv[t * ld + p];
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      a.x_out[j * ld + p] = b[j];
-      const float d = b[j] - x0[j];
-      dn = fmaf(d, d, dn);
-    }
-  }
-  if (a.status) a.status[p] = st;
-  return dn;
+#endif
+  return analysis_epilogue<NP>(&a, p, A, b, x0, st);
 }
 
 // Packed SPD inverse (covariance <-> precision conversion).
