@@ -157,6 +157,7 @@ PYBIND11_MODULE(_kafka_hip, m) {
   m.def("grid", [](int64_t N) { return dev_grid(N); });
   m.def("set_max_blocks", [](int n) { set_max_blocks(n); });
   m.def("get_max_blocks", []() { return get_max_blocks(); });
+  m.def("set_gp_unroll", [](int n) { set_gp_unroll(n); });
 
   m.def("analysis", [](int np, const AnalysisArgs& a, int grid, bool device, uintptr_t stream) {
     if (device) check_hip(dev_analysis(np, a, grid, (hipStream_t)stream), "analysis");

@@ -36,6 +36,7 @@ constexpr float LOG2_10 = 3.321928094887362f;
 constexpr float DEG2RAD = 0.017453292519943295f;
 
 KF_HD constexpr int ntri(int n) { return n * (n + 1) / 2; }
+constexpr int FD_PRECOMP = -1;    // AnalysisArgs.fast_d: all bands OP_PRECOMP
 // packed upper triangle, row-major: (0,0) (0,1) .. (0,n-1) (1,1) ..
 KF_HD constexpr int tri(int n, int i, int j) { return i * n - (i * (i - 1)) / 2 + (j - i); }
 template <int NP> KF_HD constexpr int sym(int i, int j) { return i <= j ? tri(NP, i, j) : tri(NP, j, i); }
@@ -260,28 +261,33 @@ KF_HD float bf16_to_f32(uint16_t b) {
 // observation decode: returns weight w (inverse variance, 0 when masked) and y
 // FOBS != 0 compiles a single encoding (fast-path kernels).
 template <int FOBS = 0>
-KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y, float& w) {
+KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y_out, float& w_out) {
+  // locals, assigned once at the end: conditional stores through the output
+  // references made the compiler spill (y, w) to scratch in generic kernels
+  float y = 0.f, w = 0.f;
   if (FOBS == OBS_DN16 || (FOBS == 0 && bd.obs == OBS_DN16)) {
     const uint16_t dn = bd.dn[p];
-    y = (float)dn * bd.scale;
-    float sig = fmaxf(bd.rel_unc * y, bd.unc_floor);
-    w = (dn > 0 && sig > 0.f) ? kf_rcp(sig * sig) : 0.f;
-    if (dn == 0) y = 0.f;
-  } else if (FOBS == OBS_F32 || (FOBS == 0 && bd.obs == OBS_F32)) {
-    y = bd.y[p];
-    w = bd.w[p];
-    if (bd.mask && !bd.mask[p]) w = 0.f;
-    if (!(w > 0.f) || !finitef(w) || !finitef(y)) { w = 0.f; y = 0.f; }
-  } else if (FOBS == OBS_BF16 || (FOBS == 0 && bd.obs == OBS_BF16)) {
-    // bf16 (y, w) pairs: half the ingest bytes of f32; math stays f32
-    y = bf16_to_f32(reinterpret_cast<const uint16_t*>(bd.y)[p]);
-    w = bf16_to_f32(reinterpret_cast<const uint16_t*>(bd.w)[p]);
-    if (bd.mask && !bd.mask[p]) w = 0.f;
-    if (!(w > 0.f) || !finitef(w) || !finitef(y)) { w = 0.f; y = 0.f; }
-  } else {
-    y = 0.f;
-    w = 0.f;
+    const float yd = (float)dn * bd.scale;
+    const float sig = fmaxf(bd.rel_unc * yd, bd.unc_floor);
+    const bool ok = dn > 0 && sig > 0.f;
+    w = ok ? kf_rcp(sig * sig) : 0.f;
+    y = dn > 0 ? yd : 0.f;
+  } else if (FOBS == OBS_F32 || FOBS == OBS_BF16 || (FOBS == 0 && (bd.obs == OBS_F32 || bd.obs == OBS_BF16))) {
+    float yv, wv;
+    if (FOBS == OBS_F32 || (FOBS == 0 && bd.obs == OBS_F32)) {
+      yv = bd.y[p];
+      wv = bd.w[p];
+    } else {
+      // bf16 (y, w) pairs: half the ingest bytes of f32; math stays f32
+      yv = bf16_to_f32(reinterpret_cast<const uint16_t*>(bd.y)[p]);
+      wv = bf16_to_f32(reinterpret_cast<const uint16_t*>(bd.w)[p]);
+    }
+    const bool keep = (!bd.mask || bd.mask[p]) && (wv > 0.f) && finitef(wv) && finitef(yv);
+    y = keep ? yv : 0.f;
+    w = keep ? wv : 0.f;
   }
+  y_out = y;
+  w_out = w;
 }
 
 // ---------------------------------------------------------------------------
@@ -688,7 +694,8 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
 //   y'_b = y_b + h_b . x0 - H0_b,      x_a = A^-1 b
 // Returns (x_a - x0)^2 summed over parameters.
 // FD > 0: fast path where every band is a GP with FD inputs and FOBS encoding
-// (the compiler then drops the SAR/linear/precomputed code and its registers).
+// (the compiler then drops the SAR/linear/precomputed code and its registers);
+// FD == FD_PRECOMP: every band has a precomputed operator (split GP path).
 template <int NP, int FD = 0, int FOBS = 0, int UNR = 4, bool FOLD = false>
 KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
   constexpr int NT = ntri(NP);
@@ -743,6 +750,15 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
       ok = finitef(H0);
 #pragma unroll
       for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);
+    } else if constexpr (FD == FD_PRECOMP) {
+      // precomputed operator (split GP path / host factories): H0, h from HBM
+      H0 = bd.pre_h0[p];
+      ok = finitef(H0);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        h[j] = bd.pre_h[j * bd.pre_ld + p];
+        ok = ok && finitef(h[j]);
+      }
     } else {
       ok = eval_operator<NP>(bd, p, ld, x0, H0, h);
     }
@@ -767,7 +783,7 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
   }
   if (nobs == 0) st |= ST_NO_OBS;
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (FD > 0) {
+  if constexpr (FD != 0) {
     // fast kernels: re-read the launch arguments from the kernarg segment
     // through an opaque pointer, so they are not pinned in SGPRs across the
     // band / record loops above (analysis_kernel passes them at offset 0)

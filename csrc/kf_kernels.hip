@@ -107,7 +107,7 @@ __global__ __launch_bounds__(BLOCK) void operator_kernel(const BandDesc* bands, 
 // runs at high occupancy; used for large input counts (PROSAIL D=10) and many
 // bands (multi-sensor), followed by the OP_PRECOMP analysis kernel.  Pixels
 // whose observation is masked skip the GP (wave-level skip under clouds).
-template <int NP, int D>
+template <int NP, int D, int UNR>
 __global__ __launch_bounds__(BLOCK) void gp_operator_kernel(const BandDesc* bands, int nb, const float* x,
                                                            int64_t N, int64_t ld, float* h0, float* h,
                                                            int64_t ldh) {
@@ -122,7 +122,9 @@ __global__ __launch_bounds__(BLOCK) void gp_operator_kernel(const BandDesc* band
 #pragma unroll
       for (int j = 0; j < NP; ++j) hv[j] = 0.f;
       decode_obs(bd, p, y, w);
-      if (w > 0.f) gp_eval<NP, D>(bd, xv, H0, hv);
+      // RELOAD: the descriptor's epilogue fields are re-read after the record
+      // stream (61 instead of 91 VGPRs, 26 instead of 233 SGPR spills at D=10)
+      if (w > 0.f) gp_eval<NP, D, UNR, false, true>(bd, xv, H0, hv, bands + b);
       h0[b * ldh + p] = H0;
 #pragma unroll
       for (int j = 0; j < NP; ++j) h[((int64_t)b * NP + j) * ldh + p] = hv[j];
@@ -247,13 +249,13 @@ static inline int grid_for(int64_t N, int max_blocks) {
 template <int NP, int FD>
 static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
   // variant (A/B tuning, scripts/bench_kernels.py): 0 unroll-4 pairs (default),
-  // 1 unroll-4 + folded exponent, 2 unroll-8, 3 unroll-3
+  // 1 unroll-4 + folded exponent, 2 unroll-8, 3 unroll-3 (GP fast paths only)
   if (a.fast_obs == OBS_DN16) {
-    if (a.variant == 1)
+    if (FD > 0 && a.variant == 1)
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 4, true>), dim3(grid), dim3(BLOCK), 0, s, a);
-    else if (a.variant == 2)
+    else if (FD > 0 && a.variant == 2)
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 8>), dim3(grid), dim3(BLOCK), 0, s, a);
-    else if (a.variant == 3)
+    else if (FD > 0 && a.variant == 3)
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 3>), dim3(grid), dim3(BLOCK), 0, s, a);
     else
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
@@ -279,6 +281,9 @@ static void l_analysis(const AnalysisArgs& a, int grid, hipStream_t s) {
     } else if constexpr (NP <= 4) {
       if (a.fast_d == NP) done = l_analysis_fast<NP, NP>(a, grid, s);
     }
+  }
+  else if (a.fast_d == FD_PRECOMP) {
+    done = l_analysis_fast<NP, FD_PRECOMP>(a, grid, s);
   }
   if (!done) hipLaunchKernelGGL(analysis_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
 }
@@ -320,6 +325,8 @@ static void l_unpack(const float* x, const float* a, int64_t N, int64_t ld, cons
 // phases overlap other workgroups' compute.
 static int g_max_blocks = KF_MAX_BLOCKS;
 void set_max_blocks(int n) { g_max_blocks = n > 0 ? n : KF_MAX_BLOCKS; }
+static int g_gp_unroll = 4;
+void set_gp_unroll(int n) { g_gp_unroll = n; }
 int get_max_blocks() { return g_max_blocks; }
 int dev_grid(int64_t N) { return grid_for(N, g_max_blocks); }
 
@@ -355,11 +362,16 @@ hipError_t dev_operator(int np, const BandDesc* b, int band, const float* x, int
 hipError_t dev_gp_operator(int np, int d, const BandDesc* b, int nb, const float* x, int64_t N, int64_t ld,
                            float* h0, float* h, int64_t ldh, hipStream_t s) {
   const int g = grid_for(N, KF_MAX_BLOCKS);
-#define KF_GPOP(NP_, D_)                                                                                  \
-  if (np == NP_ && d == D_) {                                                                            \
-    hipLaunchKernelGGL((gp_operator_kernel<NP_, D_>), dim3(g), dim3(BLOCK), 0, s, b, nb, x, N, ld, h0, h, \
-                       ldh);                                                                             \
-    return hipGetLastError();                                                                            \
+  // record-stream unroll: 4 pairs by default, 2 selectable (set_gp_unroll) for A/B
+#define KF_GPOP(NP_, D_)                                                                                     \
+  if (np == NP_ && d == D_) {                                                                               \
+    if (g_gp_unroll == 2)                                                                                   \
+      hipLaunchKernelGGL((gp_operator_kernel<NP_, D_, 2>), dim3(g), dim3(BLOCK), 0, s, b, nb, x, N, ld, h0, \
+                         h, ldh);                                                                           \
+    else                                                                                                    \
+      hipLaunchKernelGGL((gp_operator_kernel<NP_, D_, 4>), dim3(g), dim3(BLOCK), 0, s, b, nb, x, N, ld, h0, \
+                         h, ldh);                                                                           \
+    return hipGetLastError();                                                                               \
   }
   KF_GPOP(10, 10) KF_GPOP(10, 4) KF_GPOP(7, 7) KF_GPOP(7, 4) KF_GPOP(4, 4) KF_GPOP(3, 3) KF_GPOP(2, 2)
 #undef KF_GPOP

@@ -15,6 +15,7 @@ namespace kf {
 
 int dev_grid(int64_t N);
 void set_max_blocks(int n);
+void set_gp_unroll(int n);
 int get_max_blocks();
 hipError_t dev_analysis(int np, const AnalysisArgs& a, int grid, hipStream_t s);
 hipError_t dev_gain(int np, const GainArgs& a, int grid, hipStream_t s);

@@ -21,9 +21,14 @@ except ImportError as e:  # pragma: no cover - exercised only when unbuilt
 
 
 def _apply_env(m):
-    """KAFKA_MAX_BLOCKS: grid cap of the per-pixel kernels (tuning / A-B)."""
-    if m is not None and os.environ.get("KAFKA_MAX_BLOCKS") and hasattr(m, "set_max_blocks"):
+    """Tuning / A-B knobs: KAFKA_MAX_BLOCKS (grid cap of the per-pixel kernels),
+    KAFKA_GP_UNROLL (record-stream unroll of the split GP operator kernel)."""
+    if m is None:
+        return
+    if os.environ.get("KAFKA_MAX_BLOCKS") and hasattr(m, "set_max_blocks"):
         m.set_max_blocks(int(os.environ["KAFKA_MAX_BLOCKS"]))
+    if os.environ.get("KAFKA_GP_UNROLL") and hasattr(m, "set_gp_unroll"):
+        m.set_gp_unroll(int(os.environ["KAFKA_GP_UNROLL"]))
 
 
 _apply_env(ext)

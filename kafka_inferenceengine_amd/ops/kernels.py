@@ -90,7 +90,11 @@ class BandTable:
         return int(self.buf.data_ptr())
 
 
+OP_PRECOMP = 0
 OP_GP = 2
+
+
+FD_PRECOMP = -1   # kf_core.h: fast analysis kernel for all-precomputed operators
 
 
 def make_band_table(descs: list, device, keepalive=()) -> BandTable:
@@ -98,11 +102,14 @@ def make_band_table(descs: list, device, keepalive=()) -> BandTable:
     cpu = torch.frombuffer(bytearray(raw), dtype=torch.uint8) if raw else torch.zeros(8, dtype=torch.uint8)
     buf = cpu.to(device) if torch.device(device).type == "cuda" else cpu.clone()
     fast_d = fast_obs = 0
+    obs = {d.obs for d in descs}
+    uniform_obs = len(obs) == 1 and next(iter(obs)) in (OBS_F32, OBS_DN16)
     if descs and all(d.op == OP_GP for d in descs):
         ds = {d.d for d in descs}
-        obs = {d.obs for d in descs}
-        if len(ds) == 1 and len(obs) == 1 and next(iter(obs)) in (OBS_F32, OBS_DN16):
+        if len(ds) == 1 and uniform_obs:
             fast_d, fast_obs = next(iter(ds)), next(iter(obs))
+    elif descs and uniform_obs and all(d.op == OP_PRECOMP for d in descs):
+        fast_d, fast_obs = FD_PRECOMP, next(iter(obs))
     return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs)
 
 
