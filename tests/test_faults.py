@@ -74,3 +74,84 @@ def test_nonspd_forecast_falls_back_per_pixel():
     assert torch.equal(xo[:, :6], x[:, :6])
     assert not torch.any(st[6:] & K.ST_FALLBACK)
     assert torch.isfinite(xo).all()
+
+
+# ----------------------------------------------------------- rank failure
+def _rank_worker(rank, world, port, ckdir, die_at, q):
+    import os
+    import torch.distributed as dist
+
+    from kafka_inferenceengine_amd.parallel import Comm, StripPartition
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=dt.timedelta(seconds=60))
+    try:
+        mask = np.ones((24, 16), bool)
+        part = StripPartition(mask, rank, world)
+        obs = k.SyntheticBHRObservations(mask, n_train=30, device="cpu", stream=False, n_pool=2, partition=part,
+                                         field_cell=6, seed=9)
+        kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS,
+                            device="cpu", comm=Comm(rank, world, "cpu"), partition=part,
+                            config=k.EngineConfig(checkpoint_dir=ckdir, checkpoint_every=1 if ckdir else 0))
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(6)]
+        if die_at is not None and rank == 1:
+            step = kf.step
+            count = [0]
+
+            def dying_step(*a, **kw):
+                count[0] += 1
+                if count[0] == die_at:
+                    os._exit(17)          # the rank disappears mid-run (no cleanup)
+                return step(*a, **kw)
+            kf.step = dying_step
+        resume = k.CheckpointManager.latest(ckdir) if (ckdir and die_at is None) else None
+        try:
+            start = None if resume else kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask))
+            st = kf.run(grid, start, None, None, resume_from=resume)
+            q.put((rank, "ok", st.x.numpy().copy()))
+        except Exception as e:  # the survivor sees the failed peer as a collective error
+            q.put((rank, "error", type(e).__name__))
+    finally:
+        try:
+            dist.destroy_process_group()
+        except Exception:
+            pass
+
+
+def _launch(world, ckdir, die_at):
+    import socket
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, ckdir, die_at, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    expected = world - (1 if die_at is not None else 0)
+    res = [q.get(timeout=240) for _ in range(expected)]
+    for p in procs:
+        p.join(timeout=120)
+    return sorted(res, key=lambda t: t[0]), [p.exitcode for p in procs]
+
+
+def test_rank_failure_detected_and_resumed_from_checkpoint(tmp_path):
+    """a rank dies mid-run -> the survivor's collective fails
+    (no hang), the job restarts from the last per-timestep checkpoint and ends
+    on the same state as an uninterrupted run."""
+    ref, codes = _launch(2, None, None)
+    assert codes == [0, 0] and all(r[1] == "ok" for r in ref)
+    ck = str(tmp_path / "ck")
+    res, codes = _launch(2, ck, die_at=4)
+    assert codes[1] == 17
+    assert res[0][1] == "error"
+    assert k.CheckpointManager.latest(ck) is not None
+    res, codes = _launch(2, ck, None)
+    assert codes == [0, 0]
+    for (r0, s0, x0), (r1, s1, x1) in zip(ref, res):
+        assert s1 == "ok" and np.allclose(x0, x1, rtol=1e-6, atol=1e-7)

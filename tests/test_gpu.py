@@ -188,3 +188,19 @@ def test_fused_propagation_device(cuda, mode, blend, quirk, pmask):
         assert np.array_equal(s1, s2)
         assert close(x2, x1, 1e-4) and close(a2, a1, 1e-5)
         assert close(x2, x3) and close(a2, a3, 1e-4)
+
+
+def test_gpu_runs_are_bit_reproducible(cuda):
+    """SURVEY.md §5.2 deterministic-reduction mode: fixed-order f64 partials,
+    no atomics -> two runs give bit-identical states and norms."""
+    mask = np.ones((64, 48), bool)
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(4)]
+    outs = []
+    for _ in range(2):
+        obs = k.SyntheticBHRObservations(mask, n_train=100, device=cuda, stream=True, n_pool=3, field_cell=8)
+        kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device=cuda)
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
+        outs.append((st.x.cpu(), st.P.cpu(), [r["norms"] for r in kf.metrics.records if r.get("event") == "date"]))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
