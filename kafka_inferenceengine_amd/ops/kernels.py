@@ -10,6 +10,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import os
+
 import numpy as np
 import torch
 
@@ -95,6 +97,8 @@ OP_GP = 2
 
 
 FD_PRECOMP = -1   # kf_core.h: fast analysis kernel for all-precomputed operators
+# analysis fast-kernel variant (kf_kernels.hip:l_analysis_fast); env override for A/B runs
+DEFAULT_VARIANT = int(os.environ.get("KAFKA_ANALYSIS_VARIANT", "0"))
 
 
 def make_band_table(descs: list, device, keepalive=()) -> BandTable:
@@ -135,7 +139,7 @@ def gp_operator_supported(n_params, d) -> bool:
 
 
 def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=None, b_out=None, status=None,
-             partials=None, N=None, solve=True, fast=True, variant=0, a_in=None, b_in=None, prop=None):
+             partials=None, N=None, solve=True, fast=True, variant=None, a_in=None, b_in=None, prop=None):
     """K1 fused Gauss-Newton analysis (information form).
 
     ``prop`` (from :func:`prop_args`) fuses the propagation: the forecast is
@@ -170,7 +174,7 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     a = ext().AnalysisArgs()
     a.N, a.ld, a.n_bands, a.solve = N, ld, bands.n, int(bool(solve))
     a.fast_d, a.fast_obs = (bands.fast_d, bands.fast_obs) if fast else (0, 0)
-    a.variant = int(variant)
+    a.variant = DEFAULT_VARIANT if variant is None else int(variant)
     a.bands = bands.ptr
     a.x_prev, a.x_f, a.pf_inv = _ptr(x_prev), _ptr(x_f), _ptr(pf_inv)
     a.x_out, a.a_out, a.b_out = _ptr(x_out), _ptr(a_out), _ptr(b_out)
