@@ -46,62 +46,6 @@ __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
   if (a.partials) block_partial(acc, a.partials);
 }
 
-// Cloud-compacted variant: a workgroup takes chunks of CK*256 consecutive
-// pixels, ranks them "any valid observation" first (ballot + popcount per
-// wave, wave offsets through LDS) and runs the analysis over that order, so
-// the GP loop's waves are (nearly) fully populated instead of carrying the
-// masked lanes of partially cloudy waves; cloudy pixels follow in waves that
-// skip every band.  Deterministic: the order depends only on the data.
-constexpr int CK = 8;
-template <int NP, int FD, int FOBS, int UNR = 4>
-__global__ __launch_bounds__(BLOCK) void analysis_compact_kernel(AnalysisArgs a) {
-  constexpr int SLOTS = CK * (BLOCK / 64);   // 64-pixel groups per chunk, in pixel order
-  __shared__ int32_t order[BLOCK * CK];
-  __shared__ int slot_valid[SLOTS];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint64_t below = lane ? ((~0ull) >> (64 - lane)) : 0ull;
-  double acc = 0.0;
-  for (int64_t base = (int64_t)blockIdx.x * BLOCK * CK; base < a.N; base += (int64_t)gridDim.x * BLOCK * CK) {
-    const int n = (int)((a.N - base < BLOCK * CK) ? (a.N - base) : BLOCK * CK);
-    uint64_t mask[CK];
-#pragma unroll
-    for (int k = 0; k < CK; ++k) {
-      const int i = k * BLOCK + threadIdx.x;   // slot k * 4 + wid, lane
-      bool v = false;
-      if (i < n) {
-        for (int bi = 0; bi < a.n_bands; ++bi) {
-          const BandDesc bd = cptr(a.bands)[bi];
-          float y, w;
-          decode_obs<FOBS>(bd, base + i, y, w);
-          v = v || (w > 0.f);
-        }
-      }
-      mask[k] = __ballot(v);
-      if (lane == 0) slot_valid[k * (BLOCK / 64) + wid] = __popcll(mask[k]);
-    }
-    __syncthreads();
-    int nvalid = 0;
-    for (int s = 0; s < SLOTS; ++s) nvalid += slot_valid[s];
-#pragma unroll
-    for (int k = 0; k < CK; ++k) {
-      const int slot = k * (BLOCK / 64) + wid;
-      const int i = slot * 64 + lane;
-      int off = 0;                                   // valid pixels in earlier slots
-      for (int s = 0; s < slot; ++s) off += slot_valid[s];
-      const int r = __popcll(mask[k] & below);       // valid lanes below in this slot
-      if (i < n) {
-        if ((mask[k] >> lane) & 1ull) order[off + r] = i;
-        else order[nvalid + (slot * 64 - off) + (lane - r)] = i;
-      }
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j < n; j += BLOCK)
-      acc += (double)pixel_analysis<NP, FD, FOBS, UNR>(a, base + order[j]);
-    __syncthreads();
-  }
-  if (a.partials) block_partial(acc, a.partials);
-}
-
 template <int NP>
 __global__ __launch_bounds__(BLOCK) void gain_kernel(GainArgs a) {
   double acc = 0.0;
@@ -313,8 +257,6 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 8>), dim3(grid), dim3(BLOCK), 0, s, a);
     else if (FD > 0 && a.variant == 3)
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 3>), dim3(grid), dim3(BLOCK), 0, s, a);
-    else if (FD > 0 && a.variant == 4)
-      hipLaunchKernelGGL((analysis_compact_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
     else
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
   } else if (a.fast_obs == OBS_F32) {
