@@ -101,24 +101,42 @@ __global__ __launch_bounds__(256) void gp_mfma(const float* __restrict__ aop, co
 #pragma unroll
       for (int m = 0; m < NV; ++m) acc[cb][m] = 0.f;
     const int ntile = T / 16;
-    for (int t = 0; t < ntile; ++t) {
-      const float a0 = aop[(t * 2 + 0) * 64 + lane];
-      const float a1 = aop[(t * 2 + 1) * 64 + lane];
-      f4 v[NV];
+    // software pipeline: operands of tile t+1 are loaded while tile t computes;
+    // all 8 MFMAs of a tile are issued before their results are consumed
+    float a0 = aop[0 * 64 + lane], a1 = aop[1 * 64 + lane];
+    f4 v[NV];
 #pragma unroll
-      for (int m = 0; m < NV; ++m) v[m] = *(const f4*)(vop + (t * NV + m) * 16 + 4 * g);
+    for (int m = 0; m < NV; ++m) v[m] = *(const f4*)(vop + m * 16 + 4 * g);
+    for (int t = 0; t < ntile; ++t) {
+      f4 e[4];
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
-        f4 e = {0.f, 0.f, 0.f, 0.f};
-        e = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bop[cb][0], e, 0, 0, 0);
-        e = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bop[cb][1], e, 0, 0, 0);
+        e[cb] = f4{0.f, 0.f, 0.f, 0.f};
+        e[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bop[cb][0], e[cb], 0, 0, 0);
+      }
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) e[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bop[cb][1], e[cb], 0, 0, 0);
+      f4 vn[NV];
+      float a0n = 0.f, a1n = 0.f;
+      if (t + 1 < ntile) {
+        a0n = aop[((t + 1) * 2 + 0) * 64 + lane];
+        a1n = aop[((t + 1) * 2 + 1) * 64 + lane];
+#pragma unroll
+        for (int m = 0; m < NV; ++m) vn[m] = *(const f4*)(vop + ((t + 1) * NV + m) * 16 + 4 * g);
+      }
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float k = __builtin_amdgcn_exp2f(e[r]);
+          const float k = __builtin_amdgcn_exp2f(e[cb][r]);
 #pragma unroll
           for (int m = 0; m < NV; ++m) acc[cb][m] = fmaf(v[m][r], k, acc[cb][m]);
         }
       }
+      a0 = a0n;
+      a1 = a1n;
+#pragma unroll
+      for (int m = 0; m < NV; ++m) v[m] = vn[m];
     }
     // butterfly over the 4 lane groups, then lane l keeps block cb = g (its own pixel)
     float res[NV];
