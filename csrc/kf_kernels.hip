@@ -46,53 +46,6 @@ __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
   if (a.partials) block_partial(acc, a.partials);
 }
 
-// Wave-compacted variant: each wave owns runs of KW*64 consecutive pixels,
-// tests which have any valid observation (ballot + mbcnt), writes the run's
-// pixel order "valid first" into its own LDS slice (no workgroup barrier) and
-// then analyses 64 of them per pass, so partially clouded 64-pixel groups no
-// longer carry idle lanes through the GP loop.  Deterministic (data-defined order).
-constexpr int KW = 4;
-template <int NP, int FD, int FOBS, int UNR = 4>
-__global__ __launch_bounds__(BLOCK) void analysis_wave_compact_kernel(AnalysisArgs a) {
-  __shared__ int32_t order[BLOCK / 64][64 * KW];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint64_t below = lane ? ((~0ull) >> (64 - lane)) : 0ull;
-  int32_t* ord = order[wid];
-  double acc = 0.0;
-  const int64_t run = 64 * KW;
-  for (int64_t base = ((int64_t)blockIdx.x * (BLOCK / 64) + wid) * run; base < a.N;
-       base += (int64_t)gridDim.x * (BLOCK / 64) * run) {
-    const int n = (int)((a.N - base < run) ? (a.N - base) : run);
-    int nv = 0;
-#pragma unroll
-    for (int k = 0; k < KW; ++k) {
-      const int i = k * 64 + lane;
-      bool v = false;
-      if (i < n) {
-        for (int bi = 0; bi < a.n_bands; ++bi) {
-          const BandDesc bd = cptr(a.bands)[bi];
-          float y, w;
-          decode_obs<FOBS>(bd, base + i, y, w);
-          v = v || (w > 0.f);
-        }
-      }
-      const uint64_t m = __ballot(v);
-      const int r = __popcll(m & below);
-      if (i < n) {
-        if (v) ord[nv + r] = i;
-        else ord[n - 1 - (i - nv - r)] = i;   // invalid pixels fill from the end
-      }
-      nv += __popcll(m);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int j = lane; j < n; j += 64) acc += (double)pixel_analysis<NP, FD, FOBS, UNR>(a, base + ord[j]);
-    __builtin_amdgcn_wave_barrier();
-  }
-  if (a.partials) block_partial(acc, a.partials);
-}
-
 template <int NP>
 __global__ __launch_bounds__(BLOCK) void gain_kernel(GainArgs a) {
   double acc = 0.0;
@@ -304,8 +257,6 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 8>), dim3(grid), dim3(BLOCK), 0, s, a);
     else if (FD > 0 && a.variant == 3)
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 3>), dim3(grid), dim3(BLOCK), 0, s, a);
-    else if (FD > 0 && a.variant == 4)
-      hipLaunchKernelGGL((analysis_wave_compact_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
     else
       hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
   } else if (a.fast_obs == OBS_F32) {

@@ -206,21 +206,3 @@ def test_gpu_runs_are_bit_reproducible(cuda):
     assert outs[0][2] == outs[1][2]
 
 
-
-def test_wave_compacted_analysis_equals_default(cuda):
-    """analysis_wave_compact_kernel (variant 4): same per-pixel results as the
-    grid-stride kernel, pixels only visited in a different order."""
-    prob = C.tip_problem(N=50003, dn16=True, seed=21, mask_frac=0.3)
-    tab = C.table(prob, cuda)
-    outs = []
-    for variant in (0, 4):
-        xo = torch.zeros((7, prob["N"]), device=cuda)
-        ao = torch.zeros((28, prob["N"]), device=cuda)
-        st = torch.zeros(prob["N"], dtype=torch.uint8, device=cuda)
-        part = K.partials_buffer(prob["N"], cuda)
-        K.analysis(7, tab, C.soa(prob["x"], cuda), C.soa(prob["xf"], cuda), C.packed(prob["Pf"], cuda), xo, ao,
-                   None, st, part, variant=variant)
-        outs.append((xo.cpu(), ao.cpu(), st.cpu(), float(K.reduce_partials(part).cpu())))
-    (x0, a0, s0, r0), (x1, a1, s1, r1) = outs
-    assert torch.equal(x0, x1) and torch.equal(a0, a1) and torch.equal(s0, s1)
-    assert abs(r0 - r1) <= 1e-9 * abs(r0)
