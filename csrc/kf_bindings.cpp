@@ -97,7 +97,11 @@ PYBIND11_MODULE(_kafka_hip, m) {
       .PTR_FIELD(AnalysisArgs, b_in, const float*)
       .PTR_FIELD(AnalysisArgs, status, uint8_t*)
       .PTR_FIELD(AnalysisArgs, partials, double*)
-      .PTR_FIELD(AnalysisArgs, prop, const PropArgs*);
+      .PTR_FIELD(AnalysisArgs, prop, const PropArgs*)
+      .PTR_FIELD(AnalysisArgs, out_mean, float*)
+      .PTR_FIELD(AnalysisArgs, out_unc, float*)
+      .PTR_FIELD(AnalysisArgs, out_idx, const int64_t*)
+      .def_readwrite("out_plane", &AnalysisArgs::out_plane);
 
   py::class_<GainArgs>(m, "GainArgs")
       .def(py::init([]() { GainArgs a; memset(&a, 0, sizeof(a)); return a; }))

@@ -115,6 +115,10 @@ struct AnalysisArgs {
   uint8_t* status;       // per-pixel flags (may be null)
   double* partials;      // per-block sum (x_out - x_prev)^2
   const PropArgs* prop;  // fused propagation (device copy; x_f / pf_inv unused, x_prev null = linearise at the forecast)
+  float* out_mean;       // fused output (DeviceOutput): x and 1/sqrt(diag A) into [NP][out_plane] rasters
+  float* out_unc;
+  const int64_t* out_idx;  // raster position of each pixel (null: identity)
+  int64_t out_plane;
 };
 
 
@@ -654,6 +658,9 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
   }
   float dn = 0.f;
   if (a->solve) {
+    float dA[NP];   // analysis precision diagonal (output uncertainty) before the in-place factorisation
+#pragma unroll
+    for (int j = 0; j < NP; ++j) dA[j] = A[tri(NP, j, j)];
     const bool spd = chol_packed<NP>(A);
     chol_solve<NP>(A, b);
     bool fin = true;
@@ -664,17 +671,17 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
       st |= (!spd ? ST_NONSPD : 0) | (!fin ? ST_NONFINITE : 0) | ST_FALLBACK;
       if (a->prop) {
         forecast_partial<NP>(opaque(cptr(a->prop)), p, b, A);   // rare path: recompute instead of keeping it live
-        if (a->a_out) {
-#pragma unroll
-          for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = A[t];
-        }
       } else {
 #pragma unroll
         for (int j = 0; j < NP; ++j) b[j] = a->x_f[j * ld + p];
-        if (a->a_out) {
 #pragma unroll
-          for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = a->pf_inv[t * ld + p];
-        }
+        for (int t = 0; t < NT; ++t) A[t] = a->pf_inv[t * ld + p];
+      }
+#pragma unroll
+      for (int j = 0; j < NP; ++j) dA[j] = A[tri(NP, j, j)];
+      if (a->a_out) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = A[t];
       }
     }
 #pragma unroll
@@ -682,6 +689,16 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
       a->x_out[j * ld + p] = b[j];
       const float d = b[j] - x0[j];
       dn = fmaf(d, d, dn);
+    }
+    if (a->out_mean) {
+      // fused output dump: the unpack pass's work without re-reading x and A
+      const int64_t r = a->out_idx ? a->out_idx[p] : p;
+      const int64_t pl = a->out_plane;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        a->out_mean[j * pl + r] = b[j];
+        a->out_unc[j * pl + r] = kf_rsqrt(dA[j]);
+      }
     }
   }
   if (a->status) a->status[p] = st;

@@ -132,7 +132,7 @@ static int h_unpack(const float* x, const float* a, int64_t N, int64_t ld, const
     const int64_t r = idx ? idx[p] : p;
     for (int j = 0; j < NP; ++j) {
       if (mean) mean[j * plane + r] = x[j * ld + p];
-      if (unc) unc[j * plane + r] = 1.f / sqrtf(a[tri(NP, j, j) * ld + p]);
+      if (unc) unc[j * plane + r] = kf_rsqrt(a[tri(NP, j, j) * ld + p]);
     }
   }
   return 0;

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(BLOCK) void unpack_kernel(const float* x, const flo
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
       if (mean) mean[j * plane + r] = x[j * ld + p];
-      if (unc) unc[j * plane + r] = 1.f / sqrtf(a[tri(NP, j, j) * ld + p]);
+      if (unc) unc[j * plane + r] = kf_rsqrt(a[tri(NP, j, j) * ld + p]);
     }
   }
 }

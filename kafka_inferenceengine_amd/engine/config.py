@@ -43,6 +43,7 @@ class EngineConfig:
     device: str | None = None                 # 'cuda', 'cuda:1', 'cpu' (default: cuda if present)
     prefetch: bool = True                     # overlap next date's ingest with compute
     fuse_propagation: bool = True             # evaluate the forecast inside the analysis kernel
+    fuse_output: bool = True                  # device outputs written by the final analysis iteration
     return_innovations: bool = False
     metrics_path: str | None = None           # JSONL metrics (per date / timestep)
     checkpoint_dir: str | None = None

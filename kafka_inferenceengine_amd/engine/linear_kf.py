@@ -100,6 +100,7 @@ class LinearKalman:
         self.metrics = MetricsLogger(self.config.metrics_path, rank=self.comm.rank)
         self.timer = PhaseTimer(self.device, sync=self.config.sync_timing)
         self._reg = None
+        self._output_written = None
         band = getattr(self.comm, "band", None)
         self.band_comm = band if (band is not None and band.world > 1) else None
         self._bp_buf = None
@@ -542,10 +543,17 @@ class LinearKalman:
         norms = []
         n_iter = 1
         len_x = float(n * self.n_total)
+        # fused output: an output with device rasters is written by the analysis
+        # kernel itself in every iteration that can end the loop (the last one wins)
+        plain = not (gain or precomp or split or bp or cfg.spatial_gamma > 0 or cfg.hessian_correction)
+        out_t = None
+        if plain and N and cfg.fuse_output and hasattr(self.output, "device_targets"):
+            out_t = self.output.device_targets(self, self.device)
         while True:
             # the analysis precision is only needed from the iteration that can
             # end the loop on: skip its 4*ntri B/px store before min_iterations
             A_keep = P_out if n_iter >= cfg.min_iterations else None
+            out_now = out_t if n_iter >= cfg.min_iterations else None
             if precomp:
                 pre = self._precompute_host(specs, dbs, x_prev)
                 table = build_table(specs, dbs, n, self._cache, self.device, h0_outs, pre)
@@ -562,9 +570,10 @@ class LinearKalman:
                         self._split_iteration(split, x_prev, fc, x_new, A_keep, status)
                     elif prop is not None:
                         K.analysis(n, table, x_prev, None, None, x_new, A_keep, None, status, self._partials, N=N,
-                                   prop=prop)
+                                   prop=prop, out=out_now)
                     else:
-                        K.analysis(n, table, x_prev, fc.x, fc.P, x_new, A_keep, None, status, self._partials, N=N)
+                        K.analysis(n, table, x_prev, fc.x, fc.P, x_new, A_keep, None, status, self._partials, N=N,
+                                   out=out_now)
                     K.reduce_partials(self._partials, self._red)
                 else:
                     self._red.zero_()
@@ -584,6 +593,7 @@ class LinearKalman:
         if ld != x_prev.shape[1]:
             raise RuntimeError("leading dimension changed")
         state = KFState(x_prev, P_out, COVARIANCE if gain else PRECISION, N)
+        self._output_written = state if out_t is not None else None
         if cfg.hessian_correction and not gain and N:
             with self.timer.phase("hessian"):
                 K.hessian(n, table, state.x, state.P, N=N)
@@ -780,6 +790,9 @@ class LinearKalman:
         if self.output is None:
             return
         with self.timer.phase("output"):
+            if getattr(self, "_output_written", None) is state:
+                self.output.mark_written(timestep, state, self)   # written by the analysis kernel
+                return
             if hasattr(self.output, "dump_state"):
                 self.output.dump_state(timestep, state, self)
                 return

@@ -167,22 +167,37 @@ class DeviceOutput:
         self.timestep = None
         self.history = {}
 
-    def dump_state(self, timestep, state, engine):
+    def _ensure(self, engine, dev):
         part = engine.partition
         n = engine.n_params
         H, W = part.strip_shape
-        dev = state.x.device
         if self.mean is None or self.mean.device != dev:
             self.mean = torch.zeros((n, H * W), dtype=torch.float32, device=dev)
             self.unc = torch.zeros((n, H * W), dtype=torch.float32, device=dev)
-            self._idx = torch.from_numpy(part.local_idx).to(dev)
+            idx = np.asarray(part.local_idx, dtype=np.int64)
+            if idx.size and (idx.min() < 0 or idx.max() >= H * W):
+                raise ValueError("partition raster index outside the strip")
+            self._idx = torch.from_numpy(idx).to(dev)
             self._identity = part.N == H * W
-        prec = engine._as_kind(state, "precision")
-        if state.N:
-            K.unpack(n, prec.x, prec.P, self.mean, self.unc, idx=None if self._identity else self._idx, N=state.N)
+
+    def device_targets(self, engine, dev):
+        """(mean, unc, idx) rasters the analysis kernel can write directly
+        (fused output, AnalysisArgs.out_*); followed by ``mark_written``."""
+        self._ensure(engine, dev)
+        return self.mean, self.unc, None if self._identity else self._idx
+
+    def mark_written(self, timestep, state, engine):
         self.timestep = timestep
         if self.keep_history:
             self.history[timestep] = (self.mean.clone(), self.unc.clone())
+
+    def dump_state(self, timestep, state, engine):
+        n = engine.n_params
+        self._ensure(engine, state.x.device)
+        prec = engine._as_kind(state, "precision")
+        if state.N:
+            K.unpack(n, prec.x, prec.P, self.mean, self.unc, idx=None if self._identity else self._idx, N=state.N)
+        self.mark_written(timestep, state, engine)
 
     def to_host(self, shape=None):
         n = self.mean.shape[0]

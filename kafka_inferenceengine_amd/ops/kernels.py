@@ -139,13 +139,18 @@ def gp_operator_supported(n_params, d) -> bool:
 
 
 def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=None, b_out=None, status=None,
-             partials=None, N=None, solve=True, fast=True, variant=None, a_in=None, b_in=None, prop=None):
+             partials=None, N=None, solve=True, fast=True, variant=None, a_in=None, b_in=None, prop=None,
+             out=None):
     """K1 fused Gauss-Newton analysis (information form).
 
     ``prop`` (from :func:`prop_args`) fuses the propagation: the forecast is
     computed per pixel from the previous analysis inside the kernel and
     ``x_f``/``pf_inv`` must be None; ``x_prev=None`` then linearises at the
-    forecast (first Gauss-Newton iteration)."""
+    forecast (first Gauss-Newton iteration).
+
+    ``out = (mean, unc, idx)`` additionally writes x and 1/sqrt(diag A) into
+    output rasters ``[n_params, plane]`` at raster positions ``idx`` (int64 [N],
+    None = identity) — the unpack pass fused into the final iteration."""
     check_np(n_params)
     ref = next(t for t in (x_prev, x_f, x_out, a_out) if t is not None)
     N = int(ref.shape[1] if N is None else N)
@@ -186,6 +191,20 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     a.status, a.partials = _ptr(status), _ptr(partials)
     if prop is not None:
         a.prop = _ptr(prop.device_copy())
+    if out is not None:
+        mean, unc, idx = out
+        if not solve:
+            raise ValueError("fused output needs solve=True")
+        plane = mean.shape[1]
+        for t, nm in ((mean, "out mean"), (unc, "out unc")):
+            _check_soa(t, n_params, 0, nm, device=dev)
+            if t.shape[1] != plane:
+                raise ValueError("out mean / unc planes differ")
+        if idx is not None:
+            _check_vec(idx, N, "out idx", torch.int64, dev)
+        elif plane < N:
+            raise ValueError("identity output needs plane >= N")
+        a.out_mean, a.out_unc, a.out_idx, a.out_plane = _ptr(mean), _ptr(unc), _ptr(idx), plane
     grid = grid_for(N)
     ext().analysis(n_params, a, grid, _dev(ref), _stream(ref))
     return partials

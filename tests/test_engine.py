@@ -220,3 +220,21 @@ def test_fused_propagation_engine_equals_materialized(with_prior):
     assert ia == ib
     assert torch.allclose(a.x, b.x, rtol=1e-6, atol=1e-7)
     assert torch.allclose(a.P, b.P, rtol=1e-6, atol=1e-6)
+
+
+def test_fused_output_equals_unpack():
+    """EngineConfig.fuse_output: DeviceOutput rasters written by the final
+    analysis iteration equal the separate unpack pass."""
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=6)
+    grid = _grid(4)
+    res = []
+    for fuse in (False, True):
+        out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
+        kf = _engine(mask, obs, Q, out=out, fuse_output=fuse)
+        kf.run(grid, x0, None, Pinv)
+        res.append(out)
+    a, b = res
+    assert sorted(a.history) == sorted(b.history) and len(a.history) == 3
+    for t in a.history:
+        assert torch.allclose(a.history[t][0], b.history[t][0], rtol=1e-6, atol=1e-7)
+        assert torch.allclose(a.history[t][1], b.history[t][1], rtol=1e-5, atol=1e-7)

@@ -206,3 +206,20 @@ def test_gpu_runs_are_bit_reproducible(cuda):
     assert outs[0][2] == outs[1][2]
 
 
+
+
+def test_fused_output_gpu(cuda):
+    mask = np.ones((40, 36), bool)
+    mask[3:9, 2:20] = False
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(4)]
+    outs = []
+    for fuse in (False, True):
+        obs = k.SyntheticBHRObservations(mask, n_train=80, device=cuda, stream=False, n_pool=2, field_cell=8)
+        out = k.DeviceOutput(k.TIP_PARAMETERS)
+        kf = k.LinearKalman(obs, out, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device=cuda,
+                            config=k.EngineConfig(fuse_output=fuse))
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
+        outs.append((out.mean.cpu(), out.unc.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-6)
