@@ -212,6 +212,8 @@ class LinearKalman:
             if ckpt is not None and self.config.checkpoint_every and (step_i + 1) % self.config.checkpoint_every == 0:
                 ckpt.save(timestep, analysis)
         self.final_state = analysis
+        if self.metrics.enabled:
+            self.metrics_summary()
         return analysis
 
     def step(self, timestep, locate_times, state: KFState, advance: bool = True, all_dates=None) -> KFState:
@@ -396,8 +398,54 @@ class LinearKalman:
             info["norms"].append(res.norms[-1] if res.norms else None)
             rec = {"event": "date", "date": step.isoformat(), "n_iter": res.n_iter, "norms": res.norms,
                    "wall_s": time.perf_counter() - t0, "phases_ms": self.timer.snapshot()}
+            if self.metrics.enabled:
+                rec.update(self._health_metrics(rec["wall_s"]))
             self.metrics.log(rec)
         return forecast, info
+
+    def _health_metrics(self, wall_s: float) -> dict:
+        """Per-date structured metrics: rank-local pixel updates/s,
+        per-pixel status counts (masked, fallback, non-SPD, bad operator) and
+        host-to-device ingest bytes.  One device reduction + sync, only when
+        metrics are enabled."""
+        out = {"n_pixels_local": self.N, "pixel_updates_per_s_local": self.N / max(wall_s, 1e-9)}
+        st = getattr(self, "last_status", None)
+        if st is not None and self.N:
+            s = st[:self.N]
+            bits = torch.stack([(s & b) > 0 for b in (K.ST_NO_OBS, K.ST_FALLBACK, K.ST_NONSPD, K.ST_NONFINITE,
+                                                      K.ST_BAD_OP)]).sum(1).cpu().tolist()
+            out["status"] = dict(zip(("no_obs", "fallback", "non_spd", "non_finite", "bad_operator"), bits))
+            out["masked_fraction"] = bits[0] / self.N
+        if hasattr(self.observations, "ingest_bytes"):
+            total = int(self.observations.ingest_bytes())
+            out["h2d_bytes"] = total - getattr(self, "_h2d_seen", 0)
+            self._h2d_seen = total
+        return out
+
+    def metrics_summary(self) -> dict | None:
+        """Aggregate this run's per-date metrics over every rank onto rank 0
+        (written next to the JSONL as ``*.summary.json``); None on other ranks."""
+        dates = [r for r in self.metrics.records if r.get("event") == "date"]
+        mine = {"rank": self.comm.rank, "n_pixels": self.N, "n_dates": len(dates),
+                "wall_s": sum(r["wall_s"] for r in dates),
+                "gn_iterations": [r["n_iter"] for r in dates],
+                "phases_ms": {}, "status": {}, "h2d_bytes": sum(r.get("h2d_bytes", 0) for r in dates)}
+        for r in dates:
+            for k2, v in r.get("phases_ms", {}).items():
+                mine["phases_ms"][k2] = mine["phases_ms"].get(k2, 0.0) + v
+            for k2, v in r.get("status", {}).items():
+                mine["status"][k2] = mine["status"].get(k2, 0) + v
+        per_rank = self.comm.gather_object(mine)
+        if per_rank is None:
+            return None
+        summary = {"ranks": per_rank, "n_pixels": sum(p["n_pixels"] for p in per_rank),
+                   "n_dates": max(p["n_dates"] for p in per_rank),
+                   "wall_s_max": max(p["wall_s"] for p in per_rank),
+                   "h2d_bytes": sum(p["h2d_bytes"] for p in per_rank)}
+        if summary["wall_s_max"] > 0:
+            summary["pixel_updates_per_s"] = summary["n_pixels"] * summary["n_dates"] / summary["wall_s_max"]
+        self.metrics.write_summary(summary)
+        return summary
 
     # ----------------------------------------------------- observations
     def _device_bands(self, date):

@@ -162,6 +162,15 @@ class Comm:
             for r in dist.batch_isend_irecv(ops):
                 r.wait()
 
+    def gather_object(self, obj):
+        """Gather a small picklable object (metrics) from every rank onto rank 0
+        (list in rank order there, None elsewhere).  Objects are this process's own."""
+        if not self.distributed:
+            return [obj]
+        out = [None] * self.world if self.rank == 0 else None
+        dist.gather_object(obj, out, dst=self.ranks[0], group=self.group)
+        return out if self.rank == 0 else None
+
     def gather_to_root(self, t: torch.Tensor, sizes: list[int]):
         """C3: gather variable-length pixel blocks [rows, n_i] onto rank 0."""
         if not self.distributed:

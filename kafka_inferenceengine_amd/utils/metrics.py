@@ -1,7 +1,9 @@
 """Metrics and timers.
 
 * ``MetricsLogger`` — structured JSONL per date / timestep (GN iterations,
-  convergence norms, per-phase ms, wall time), one file per rank.
+  convergence norms, per-phase ms, wall time, pixel updates/s, per-pixel status
+  counts, ingest bytes), one file per rank, plus a rank-0 summary aggregated
+  over the ranks (``LinearKalman.metrics_summary``).
 * ``PhaseTimer`` — hipEvent-based (``torch.cuda.Event``) per-phase timing on
   the compute stream; host clock on CPU.  Non-synchronising by default: the
   event pairs are resolved lazily in ``snapshot()``.
@@ -26,6 +28,16 @@ class MetricsLogger:
             self.path = f"{root}.rank{rank}{ext or '.jsonl'}" if rank else str(path)
             os.makedirs(os.path.dirname(os.path.abspath(self.path)), exist_ok=True)
         self.rank = rank
+
+    @property
+    def enabled(self) -> bool:
+        return self.path is not None
+
+    def write_summary(self, summary: dict):
+        if self.path:
+            root, _ = os.path.splitext(self.path)
+            with open(root + ".summary.json", "w") as f:
+                json.dump(summary, f, indent=1, default=str)
 
     def log(self, rec: dict):
         rec = {"rank": self.rank, "t": time.time(), **rec}

@@ -183,3 +183,13 @@ def test_band_parallel_equals_single_rank(world, B):
     assert np.allclose(x, ref[2], rtol=1e-4, atol=1e-5)
     assert all(r[3] == ref[3] for r in res)
     assert np.array_equal(st, ref[4][:ref[2].shape[1]])
+
+
+def test_metrics_summary_aggregates_ranks(tmp_path):
+    import json
+    path = str(tmp_path / "m.jsonl")
+    _gather(2, {"metrics_path": path})
+    summary = json.load(open(tmp_path / "m.summary.json"))
+    assert [r["rank"] for r in summary["ranks"]] == [0, 1]
+    assert summary["n_pixels"] == sum(r["n_pixels"] for r in summary["ranks"])
+    assert os.path.exists(str(tmp_path / "m.rank1.jsonl"))

@@ -238,3 +238,18 @@ def test_fused_output_equals_unpack():
     for t in a.history:
         assert torch.allclose(a.history[t][0], b.history[t][0], rtol=1e-6, atol=1e-7)
         assert torch.allclose(a.history[t][1], b.history[t][1], rtol=1e-5, atol=1e-7)
+
+
+def test_structured_metrics_and_summary(tmp_path):
+    import json
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=7)
+    path = tmp_path / "m.jsonl"
+    kf = _engine(mask, obs, Q, metrics_path=str(path))
+    kf.run(_grid(4), x0, None, Pinv)
+    recs = [json.loads(line) for line in open(path)]
+    dates = [r for r in recs if r["event"] == "date"]
+    assert dates and all("status" in r and "pixel_updates_per_s_local" in r and "phases_ms" in r for r in dates)
+    assert all(0.0 <= r["masked_fraction"] <= 1.0 for r in dates)
+    summary = json.load(open(tmp_path / "m.summary.json"))
+    assert summary["n_pixels"] == kf.n_total and summary["pixel_updates_per_s"] > 0
+    assert len(summary["ranks"]) == 1 and summary["ranks"][0]["n_dates"] == len(dates)
