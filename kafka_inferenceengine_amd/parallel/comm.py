@@ -60,7 +60,9 @@ class Comm:
                 device = torch.device("cpu")
         device = torch.device(device)
         if not dist.is_initialized():
-            backend = backend or ("nccl" if device.type == "cuda" else "gloo")
+            # KAFKA_DIST_BACKEND: rehearsal override (e.g. gloo for several ranks on
+            # one GPU); production is RCCL ("nccl") for device tensors
+            backend = backend or os.environ.get("KAFKA_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
             kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
             if backend == "nccl":
                 kw["device_id"] = device
@@ -125,7 +127,7 @@ class Comm:
     def barrier(self):
         """Barrier over every rank of the job (strips and band groups)."""
         if self.distributed:
-            if self.device.type == "cuda":
+            if self.device.type == "cuda" and dist.get_backend(self.group) == "nccl":
                 dist.barrier(group=self.group, device_ids=[self.device.index])
             else:
                 dist.barrier(group=self.group)
