@@ -42,6 +42,7 @@ class EngineConfig:
     # runtime
     device: str | None = None                 # 'cuda', 'cuda:1', 'cpu' (default: cuda if present)
     prefetch: bool = True                     # overlap next date's ingest with compute
+    lookahead: bool = True                    # prepare the next date's bands under the last GN iteration
     fuse_propagation: bool = True             # evaluate the forecast inside the analysis kernel
     fuse_output: bool = True                  # device outputs written by the final analysis iteration
     return_innovations: bool = False
@@ -49,6 +50,7 @@ class EngineConfig:
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0                 # timesteps between checkpoints (0: off)
     comm_timeout_s: float = 600.0
+    phase_timing: bool = False                # per-phase hipEvent timers without metrics_path
     sync_timing: bool = False                 # device-synchronising per-phase timers
     extra: dict = field(default_factory=dict)
 

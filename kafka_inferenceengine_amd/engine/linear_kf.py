@@ -96,9 +96,15 @@ class LinearKalman:
         self.previous_state = None
         self._cache = RecordCache()
         self._partials = K.partials_buffer(max(self.N, 1), self.device)
-        self._red = torch.zeros(1, dtype=torch.float64, device=self.device)
+        # one reduction slot per GN iteration: norms of iterations that cannot end
+        # the loop (n_iter < min_iterations) are read after the loop, not waited on
+        self._red_hist = torch.zeros(self.config.max_iterations + 2, dtype=torch.float64, device=self.device)
+        self._red = self._red_hist[:1]
         self.metrics = MetricsLogger(self.config.metrics_path, rank=self.comm.rank)
-        self.timer = PhaseTimer(self.device, sync=self.config.sync_timing)
+        self.timer = PhaseTimer(self.device, sync=self.config.sync_timing,
+                                enabled=self.metrics.enabled or self.config.phase_timing)
+        self._lookahead_fn = None       # host prep of the next date, run under the last GN iteration
+        self._prepared = None           # (date, bands, table) made by it
         self._reg = None
         self._output_written = None
         band = getattr(self.comm, "band", None)
@@ -387,12 +393,19 @@ class LinearKalman:
             if self.config.band_sequential:
                 res = self._assimilate_sequential(step, self._materialize(forecast))
             else:
-                bands = self._device_bands(step)
-                if self.config.prefetch and hasattr(self.observations, "prefetch"):
-                    nxt = [d for d in upcoming if d > step]
-                    if nxt:
-                        self.observations.prefetch(nxt[0])
-                res = self.do_all_bands_state(step, bands, forecast)
+                prep = self._prepared
+                self._prepared = None
+                bands = prep[1] if (prep is not None and prep[0] == step) else self._device_bands(step)
+                nxt = [d for d in upcoming if d > step]
+                if nxt and self.config.prefetch and hasattr(self.observations, "prefetch"):
+                    self.observations.prefetch(nxt[0])
+                if nxt and self.config.lookahead:
+                    self._lookahead_fn = lambda d=nxt[0]: self._prepare_date(d)
+                try:
+                    res = self.do_all_bands_state(step, bands, forecast,
+                                                  table=prep[2] if (prep is not None and prep[1] is bands) else None)
+                finally:
+                    self._lookahead_fn = None
             forecast = res.state
             info["gn_iterations"].append(res.n_iter)
             info["norms"].append(res.norms[-1] if res.norms else None)
@@ -402,6 +415,21 @@ class LinearKalman:
                 rec.update(self._health_metrics(rec["wall_s"]))
             self.metrics.log(rec)
         return forecast, info
+
+    def _prepare_date(self, date):
+        """Lookahead: acquire the next date's device bands and build its band
+        table while the current date's last Gauss-Newton iteration runs (the
+        host work otherwise sits between two dates with the GPU idle).  Only the
+        fused single-kernel path reuses the table; the bands serve every path."""
+        bands = self._device_bands(date)
+        table = None
+        specs = [sp for sp, _ in bands]
+        cfg = self.config
+        if not (cfg.return_innovations or cfg.analysis_form == "gain" or cfg.spatial_gamma > 0 or
+                self.band_comm is not None or any(sp.kind == OP_PRECOMP for sp in specs)) and \
+                self._split_plan_kind(specs) is None:
+            table = build_table(specs, [d for _, d in bands], self.n_params, self._cache, self.device, None)
+        self._prepared = (date, bands, table)
 
     def _health_metrics(self, wall_s: float) -> dict:
         """Per-date structured metrics: rank-local pixel updates/s,
@@ -552,7 +580,8 @@ class LinearKalman:
         inn = np.hstack([i.cpu().numpy() for i in res.innovations]) if res.innovations else None
         return (x, None, P, inn) if res.state.kind == PRECISION else (x, P, None, inn)
 
-    def do_all_bands_state(self, timestep, bands, forecast: KFState, innovations=None) -> AssimilationResult:
+    def do_all_bands_state(self, timestep, bands, forecast: KFState, innovations=None,
+                           table=None) -> AssimilationResult:
         """Gauss-Newton loop on device (linear_kf.py:245-307)."""
         cfg = self.config
         n = self.n_params
@@ -568,7 +597,10 @@ class LinearKalman:
         if bp and (gain or cfg.spatial_gamma > 0 or cfg.hessian_correction):
             raise ValueError("band_parallel runs the information form without regulariser / Hessian correction")
         split = None if (precomp or gain or bp or cfg.spatial_gamma > 0) else self._split_plan(specs, dbs, h0_outs)
-        table = None if (precomp or split) else build_table(specs, dbs, n, self._cache, self.device, h0_outs)
+        if precomp or split:
+            table = None
+        elif table is None or h0_outs is not None:
+            table = build_table(specs, dbs, n, self._cache, self.device, h0_outs)
         prop = None
         if isinstance(forecast, LazyForecast) and not (gain or precomp or split or bp or cfg.spatial_gamma > 0) \
                 and N:
@@ -589,6 +621,7 @@ class LinearKalman:
             P_out = torch.empty_like(fc.P)
         status = torch.zeros(max(N, 1), dtype=torch.uint8, device=self.device)
         norms = []
+        deferred = []
         n_iter = 1
         len_x = float(n * self.n_total)
         # fused output: an output with device rasters is written by the analysis
@@ -622,16 +655,30 @@ class LinearKalman:
                     else:
                         K.analysis(n, table, x_prev, fc.x, fc.P, x_new, A_keep, None, status, self._partials, N=N,
                                    out=out_now)
-                    K.reduce_partials(self._partials, self._red)
+            red = self._red_hist[min(n_iter, self._red_hist.numel() - 1):][:1]
+            with self.timer.phase("analysis"):
+                if N:
+                    K.reduce_partials(self._partials, red)
                 else:
-                    self._red.zero_()
+                    red.zero_()
             with self.timer.phase("converge"):
-                total = self.comm.sum_f64(self._red)
-            convergence_norm = float(np.sqrt(max(total, 0.0)) / len_x)
-            norms.append(convergence_norm)
-            LOG.info("Band {:d}, Iteration # {:d}, convergence norm: {:g}".format(len(bands) - 1, n_iter,
-                                                                                 convergence_norm))
+                pend = self.comm.sum_f64_async(red)
             x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
+            if n_iter < cfg.min_iterations:
+                # this iteration cannot end the loop (n_iter <= max_iterations too):
+                # queue the next one without waiting for the norm
+                deferred.append((n_iter, pend))
+                n_iter += 1
+                continue
+            if self._lookahead_fn is not None:
+                # host preparation of the next date runs under this iteration's kernels
+                self._lookahead_fn()
+                self._lookahead_fn = None
+            for it, pd in deferred:
+                norms.append(self._log_norm(pd.result(), len_x, len(bands), it))
+            deferred = []
+            convergence_norm = self._log_norm(pend.result(), len_x, len(bands), n_iter)
+            norms.append(convergence_norm)
             if convergence_norm < cfg.convergence_tolerance and n_iter >= cfg.min_iterations:
                 break
             if n_iter > cfg.max_iterations:
@@ -656,9 +703,17 @@ class LinearKalman:
                 inn.append(torch.where(w > 0, y - h0[:N], torch.zeros_like(y)))
         return AssimilationResult(state, n_iter, norms, inn)
 
+    @staticmethod
+    def _log_norm(total: float, len_x: float, n_bands: int, n_iter: int) -> float:
+        """convergence_norm = ||x_a - x_prev||_2 / len(x_a) (linear_kf.py:293-296)."""
+        convergence_norm = float(np.sqrt(max(total, 0.0)) / len_x)
+        LOG.info("Band {:d}, Iteration # {:d}, convergence norm: {:g}".format(n_bands - 1, n_iter,
+                                                                             convergence_norm))
+        return convergence_norm
+
     # ------------------------------------------------ split GP operator path
-    def _split_plan(self, specs, dbs, h0_outs):
-        """Band chunks for the split path, or None for the fused kernel."""
+    def _split_plan_kind(self, specs):
+        """GP input count d when these bands take the split path, else None."""
         from ..models.operators import OP_GP
         cfg = self.config
         if cfg.gp_split == "never" or not specs or any(s.kind != OP_GP for s in specs):
@@ -672,6 +727,14 @@ class LinearKalman:
             return None
         if cfg.gp_split == "auto" and d < cfg.gp_split_min_d and len(specs) < cfg.gp_split_min_bands:
             return None
+        return d
+
+    def _split_plan(self, specs, dbs, h0_outs):
+        """Band chunks for the split path, or None for the fused kernel."""
+        d = self._split_plan_kind(specs)
+        if d is None:
+            return None
+        cfg = self.config
         n, N = self.n_params, self.N
         C = max(1, min(int(cfg.band_chunk), len(specs)))
         ldh = max(N, 1)

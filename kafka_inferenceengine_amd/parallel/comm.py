@@ -28,6 +28,20 @@ import torch
 import torch.distributed as dist
 
 
+class PendingSum:
+    """Deferred C1 result (``Comm.sum_f64_async``)."""
+
+    def __init__(self, vals: torch.Tensor, n: int):
+        self.vals = vals
+        self.n = n
+
+    def result(self) -> float:
+        total = 0.0
+        for v in self.vals.cpu().tolist():  # fixed rank order
+            total += v
+        return total
+
+
 class Comm:
     def __init__(self, rank: int = 0, world: int = 1, device=None, group=None, ranks=None, band=None):
         self.rank = rank
@@ -100,6 +114,18 @@ class Comm:
         for v in vals:  # fixed rank order
             total += v
         return total
+
+    def sum_f64_async(self, local: torch.Tensor) -> "PendingSum":
+        """C1 without a host wait: the all-gather is queued on the stream (RCCL)
+        and ``.result()`` reads the rank values and sums them in rank order.
+        ``local`` must not be overwritten before ``result()`` (it is gathered
+        from the device later on a single rank)."""
+        if not self.distributed:
+            return PendingSum(local.reshape(1), 1)
+        local = local.reshape(1).to(torch.float64)
+        out = torch.empty((self.world, 1), dtype=torch.float64, device=local.device)
+        dist.all_gather(list(out.unbind(0)), local, group=self.group)
+        return PendingSum(out.reshape(-1), self.world)
 
     def sum_int(self, v: int) -> int:
         if not self.distributed:
