@@ -169,6 +169,7 @@ def main():
     steps = list(iterate_time_grid(grid, dates))
     prof = None
     first = True
+    msgs = []   # per-step lines of the timed steps are printed after the timed region
     for i, (t, loc, is_first) in enumerate(steps[:a.warmup + a.steps]):
         if i == a.warmup:
             comm.barrier()
@@ -184,12 +185,18 @@ def main():
         first = False
         if dev.type == "cuda" and i < a.warmup:
             torch.cuda.synchronize()
-        log(f"step {i}{' (warmup)' if i < a.warmup else ''} {(time.perf_counter() - t0) * 1e3:.1f} ms "
-            f"gn_iters={kf.history[-1].get('gn_iterations')}")
+        msgs.append(f"step {i}{' (warmup)' if i < a.warmup else ''} {(time.perf_counter() - t0) * 1e3:.1f} ms "
+                    f"gn_iters={kf.history[-1].get('gn_iterations')}")
+        if i < a.warmup:
+            for m in msgs:
+                log(m)
+            msgs = []
     comm.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     elapsed = comm.max_float(time.perf_counter() - t_start)
+    for m in msgs:
+        log(m)
     if prof is not None:
         prof.__exit__(None, None, None)
         prof.export_chrome_trace(a.profile)

@@ -101,10 +101,22 @@ FD_PRECOMP = -1   # kf_core.h: fast analysis kernel for all-precomputed operator
 DEFAULT_VARIANT = int(os.environ.get("KAFKA_ANALYSIS_VARIANT", "0"))
 
 
+def small_h2d(cpu: torch.Tensor, device) -> torch.Tensor:
+    """Copy a small host buffer (descriptor table, launch arguments) to the
+    device without blocking the host: staged in pinned memory (torch's caching
+    host allocator keeps the block until the copy has run) and queued on the
+    current stream.  A pageable ``.to(device)`` would wait for every kernel
+    already queued, which stalls the host's preparation of the next launch."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return cpu.clone()
+    return cpu.pin_memory().to(device, non_blocking=True)
+
+
 def make_band_table(descs: list, device, keepalive=()) -> BandTable:
     raw = ext().pack_band_descs(descs)
     cpu = torch.frombuffer(bytearray(raw), dtype=torch.uint8) if raw else torch.zeros(8, dtype=torch.uint8)
-    buf = cpu.to(device) if torch.device(device).type == "cuda" else cpu.clone()
+    buf = small_h2d(cpu, device)
     fast_d = fast_obs = 0
     obs = {d.obs for d in descs}
     uniform_obs = len(obs) == 1 and next(iter(obs)) in (OBS_F32, OBS_DN16)
@@ -322,7 +334,7 @@ class PropHandle:
         """The PropArgs bytes on the device (read by the kernel through s_load)."""
         if self._buf is None:
             raw = torch.frombuffer(bytearray(ext().pack_prop_args(self.args)), dtype=torch.uint8)
-            self._buf = raw.to(self.device, copy=True)
+            self._buf = small_h2d(raw, self.device)
         return self._buf
 
 
