@@ -51,6 +51,7 @@ PYBIND11_MODULE(_kafka_hip, m) {
       .def_readwrite("obs", &BandDesc::obs)
       .def_readwrite("d", &BandDesc::d)
       .def_readwrite("T", &BandDesc::T)
+      .def_readwrite("Tp", &BandDesc::Tp)
       .ARR_FIELD(BandDesc, map, int32_t)
       .def_readwrite("scale", &BandDesc::scale)
       .def_readwrite("rel_unc", &BandDesc::rel_unc)

@@ -31,6 +31,7 @@ namespace kf {
 constexpr int MAX_D = 16;         // max mapped inputs per band / max state size
 constexpr int MAX_NT = 136;       // ntri(16)
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
 constexpr float LN10 = 2.302585092994046f;
 constexpr float LOG2_10 = 3.321928094887362f;
 constexpr float DEG2RAD = 0.017453292519943295f;
@@ -61,11 +62,12 @@ enum StatusBits : uint8_t {
 // host by kf_bindings (pack_band_descs) so the C++ layout is authoritative.
 struct BandDesc {
   int32_t op, obs, d, T;
+  int32_t Tp, pad_;            // GP: the first Tp record pairs carry alpha > 0, the rest alpha < 0
   int32_t map[MAX_D];          // state index feeding input d of the operator
   float scale, rel_unc, unc_floor, offset;
   float coef[MAX_D];           // LINEAR: c_j per state j; GP: lambda_d; SAR: A,B,C,D,E,theta
   float center[MAX_D];         // GP input centre (training mean), subtracted in-kernel
-  const float* gp;             // GP records [T][2d+2]: L, B[d], alpha, (alpha*t)[d]
+  const float* gp;             // GP records [T/2][d+1][2]: L + log2|alpha|, B[d] (models/gp.py)
   const float* y;              // OBS_F32 observation
   const float* w;              // OBS_F32 inverse variance (weight)
   const uint8_t* mask;         // optional validity
@@ -299,13 +301,21 @@ KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y_out, float& w_out)
 
 // RBF (ARD) Gaussian-process emulator, inputs centred on the training mean:
 //   f(x) = offset + sum_i alpha_i s exp(-1/2 sum_d lambda_d (x_d - t_id)^2)
-// records (host-built, models/gp.py): L_i = log2(s) - 1/2 log2e sum lambda t^2,
-// B_id = log2e lambda_d t_id, alpha_i, alpha_i t_id  (t centred), stored as
-// training-point PAIRS, field-major: rec[pair][field][2] (T padded to even
-// with alpha = 0).  On gfx950 one pair is one v_pk_fma_f32 per field with the
-// pair's two values as one 64-bit SGPR operand: the exponent and the five
-// weighted sums run at the packed-f32 rate (2 points per lane per issue).
-// Replaces gp.predict + the lil_matrix scatter of utils.py:181-219.
+// Records (host-built, models/gp.py): per training point
+//   L'_i = log2(s |alpha_i|) - 1/2 log2e sum_d lambda_d t_id^2,  B_id = log2e lambda_d t_id
+// (t centred), so that with c = -1/2 log2e sum lambda x^2 (per pixel)
+//   m_i = 2^(L'_i + c + B_i.x) = |alpha_i| k_i,
+//   S0 = sum sgn(alpha_i) m_i = f - offset,
+//   S'_d = sum sgn(alpha_i) m_i B_id = log2e lambda_d sum alpha_i k_i t_id,
+//   df/dx_d = -lambda_d (x_d S0 - sum alpha k t_d) = -lambda_d x_d S0 + ln2 S'_d.
+// B doubles as the exponent and the gradient weight, so a point costs D + 1
+// record floats instead of 2D + 2 (alpha and alpha*t are folded away).  Points
+// are grouped by the sign of alpha (first Tp pairs positive; each group padded
+// to a pair with L' = -1e30, i.e. m = 0) and the sums are negated between the
+// groups.  Stored as PAIRS, field-major: rec[pair][field][2]; on gfx950 one
+// pair is one v_pk_fma_f32 per field with the pair as one 64-bit SGPR operand
+// (2 points per lane per issue).  Replaces gp.predict + the lil_matrix scatter
+// of utils.py:181-219.
 KF_HD float gp_rec(const KF_CONST_AS float* r, int R, int i, int f) {
   return r[((int64_t)(i >> 1) * R + f) * 2 + (i & 1)];
 }
@@ -313,14 +323,13 @@ KF_HD float gp_rec(const KF_CONST_AS float* r, int R, int i, int f) {
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef float kf_f2 __attribute__((ext_vector_type(2)));
 
-// Streams the band's training-point pairs (s_load into SGPRs) and accumulates
-// S0 = sum alpha k and S_d = sum alpha t_d k, two points per v_pk_fma_f32.
-// ADDC: exponent = L + c + B.x (c the per-pixel -0.5 log2e sum lambda x^2);
-// without it the exponent is L + B.x and the caller rescales by 2^c.
+// Streams training-point pairs (s_load into SGPRs) and accumulates S0 += m and
+// S'_d += B_d m, two points per v_pk_fma_f32.
+// ADDC: exponent = L' + c + B.x; without it L' + B.x and the caller rescales by 2^c.
 template <int D, int UNR, bool ADDC>
 __device__ __forceinline__ void gp_pairs(const KF_CONST_AS kf_f2* __restrict__ r2, int T2, const kf_f2 (&xv)[D],
                                          kf_f2 cv, kf_f2& S0v, kf_f2 (&Sv)[D]) {
-  constexpr int R = 2 * D + 2;
+  constexpr int R = D + 1;
 #pragma unroll UNR
   for (int i = 0; i < T2; ++i) {
     const KF_CONST_AS kf_f2* __restrict__ ri = r2 + (int64_t)i * R;
@@ -334,13 +343,27 @@ __device__ __forceinline__ void gp_pairs(const KF_CONST_AS kf_f2* __restrict__ r
 #pragma unroll
       for (int d = 1; d < D; ++d) e = __builtin_elementwise_fma(ri[1 + d], xv[d], e);
     }
-    kf_f2 k;
-    k.x = kexp2(e.x);
-    k.y = kexp2(e.y);
-    S0v = __builtin_elementwise_fma(ri[1 + D], k, S0v);
+    kf_f2 m;
+    m.x = kexp2(e.x);
+    m.y = kexp2(e.y);
+    S0v += m;
 #pragma unroll
-    for (int d = 0; d < D; ++d) Sv[d] = __builtin_elementwise_fma(ri[2 + D + d], k, Sv[d]);
+    for (int d = 0; d < D; ++d) Sv[d] = __builtin_elementwise_fma(ri[1 + d], m, Sv[d]);
   }
+}
+
+// Both sign groups: S = S(alpha > 0) - S(alpha < 0).
+template <int D, int UNR, bool ADDC>
+__device__ __forceinline__ void gp_signed_pairs(const KF_CONST_AS kf_f2* __restrict__ r2, int T2, int Tp,
+                                                const kf_f2 (&xv)[D], kf_f2 cv, kf_f2& S0v, kf_f2 (&Sv)[D]) {
+  gp_pairs<D, UNR, ADDC>(r2, Tp, xv, cv, S0v, Sv);
+  S0v = -S0v;
+#pragma unroll
+  for (int d = 0; d < D; ++d) Sv[d] = -Sv[d];
+  gp_pairs<D, UNR, ADDC>(r2 + (int64_t)Tp * (D + 1), T2 - Tp, xv, cv, S0v, Sv);
+  S0v = -S0v;
+#pragma unroll
+  for (int d = 0; d < D; ++d) Sv[d] = -Sv[d];
 }
 #endif
 
@@ -350,7 +373,7 @@ __device__ __forceinline__ void gp_pairs(const KF_CONST_AS kf_f2* __restrict__ r
 // i.e. <= ~1e-6 relative error in k.  Otherwise the wave takes the exact loop.
 constexpr float GP_FOLD_MAX = 16.f;
 
-// f = offset + S0,  df/dx_d = -lambda_d (x_d S0 - S_d), scattered to the state.
+// f = offset + S0,  df/dx_d = -lambda_d x_d S0 + ln2 S'_d, scattered to the state.
 template <int NP, int D, typename F, typename I>
 KF_HD void gp_epilogue(float offset, const F& coef, const I& map, const float (&xi)[D], float S0,
                        const float (&S)[D], float& H0, float (&h)[NP]) {
@@ -359,7 +382,7 @@ KF_HD void gp_epilogue(float offset, const F& coef, const I& map, const float (&
   for (int j = 0; j < NP; ++j) h[j] = 0.f;
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    const float g = -coef[d] * fmaf(xi[d], S0, -S[d]);
+    const float g = fmaf(-coef[d] * xi[d], S0, LN2 * S[d]);
 #pragma unroll
     for (int j = 0; j < NP; ++j) h[j] += (map[d] == j) ? g : 0.f;
   }
@@ -381,10 +404,11 @@ KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&
   }
   c *= -0.5f * LOG2E;
   float S0, S[D];
-  constexpr int R = 2 * D + 2;
+  constexpr int R = D + 1;
 #if defined(__HIP_DEVICE_COMPILE__)
   const KF_CONST_AS kf_f2* __restrict__ r2 = (const KF_CONST_AS kf_f2*)cptr(bd.gp);
   const int T2 = bd.T >> 1;
+  const int Tp = bd.Tp;
   kf_f2 S0v = {0.f, 0.f}, Sv[D], xv[D];
   const kf_f2 cv = {c, c};
 #pragma unroll
@@ -392,9 +416,9 @@ KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&
   bool folded = false;
   if constexpr (FOLD) folded = __all(c >= -GP_FOLD_MAX);
   if (folded)
-    gp_pairs<D, UNR, false>(r2, T2, xv, cv, S0v, Sv);
+    gp_signed_pairs<D, UNR, false>(r2, T2, Tp, xv, cv, S0v, Sv);
   else
-    gp_pairs<D, UNR, true>(r2, T2, xv, cv, S0v, Sv);
+    gp_signed_pairs<D, UNR, true>(r2, T2, Tp, xv, cv, S0v, Sv);
   if (folded) {
     const float sc = kexp2(c);
     S0v *= sc;
@@ -414,10 +438,10 @@ KF_HD void gp_eval(const BandDesc& bd, const float (&x)[NP], float& H0, float (&
     float e = gp_rec(r, R, i, 0) + c;
 #pragma unroll
     for (int d = 0; d < D; ++d) e = fmaf(gp_rec(r, R, i, 1 + d), xi[d], e);
-    const float k = kexp2(e);
-    S0a[l] = fmaf(gp_rec(r, R, i, 1 + D), k, S0a[l]);
+    const float m = ((i >> 1) < bd.Tp) ? kexp2(e) : -kexp2(e);
+    S0a[l] += m;
 #pragma unroll
-    for (int d = 0; d < D; ++d) Sa[l][d] = fmaf(gp_rec(r, R, i, 2 + D + d), k, Sa[l][d]);
+    for (int d = 0; d < D; ++d) Sa[l][d] = fmaf(gp_rec(r, R, i, 1 + d), m, Sa[l][d]);
   }
   S0 = S0a[0] + S0a[1];
 #pragma unroll
@@ -986,14 +1010,14 @@ KF_HD void gp_hessian(const BandDesc& bd, const float (&x)[NP], float& f, float 
   for (int d = 0; d < D; ++d) S[d] = 0.f;
 #pragma unroll
   for (int t = 0; t < ntri(D); ++t) S2[t] = 0.f;
-  constexpr int R = 2 * D + 2;
+  constexpr int R = D + 1;
   const KF_CONST_AS float* rr = cptr(bd.gp);
   for (int i = 0; i < bd.T; ++i) {
     float e = gp_rec(rr, R, i, 0) + c;
 #pragma unroll
     for (int d = 0; d < D; ++d) e = fmaf(gp_rec(rr, R, i, 1 + d), xi[d], e);
-    const float k = kexp2(e);
-    const float ak = gp_rec(rr, R, i, 1 + D) * k;
+    const float m = kexp2(e);                       // |alpha_i| k_i
+    const float ak = ((i >> 1) < bd.Tp) ? m : -m;   // alpha_i k_i
     S0 += ak;
     float t[D];
 #pragma unroll

@@ -98,9 +98,11 @@ def band_desc(spec: OperatorSpec, obs: DeviceBand | None, n_params: int, cache: 
         if spec.d > 12 or spec.d > n_params:
             raise ValueError(f"GP with {spec.d} inputs exceeds the compiled limit for n_params={n_params}")
         rec = cache.get(spec, device)
-        if rec.dim() != 3 or rec.shape[1] != 2 * spec.d + 2 or rec.shape[2] != 2:
-            raise ValueError(f"GP records must be [T/2, 2d+2, 2], got {tuple(rec.shape)}")
-        d.d, d.T = spec.d, 2 * int(rec.shape[0])
+        if rec.dim() != 3 or rec.shape[1] != spec.d + 1 or rec.shape[2] != 2:
+            raise ValueError(f"GP records must be [T/2, d+1, 2], got {tuple(rec.shape)}")
+        if not 0 <= int(spec.gp_pos_pairs) <= int(rec.shape[0]):
+            raise ValueError(f"gp_pos_pairs={spec.gp_pos_pairs} outside [0, {rec.shape[0]}]")
+        d.d, d.T, d.Tp = spec.d, 2 * int(rec.shape[0]), int(spec.gp_pos_pairs)
         d.gp = rec.data_ptr()
         keep.append(rec)
     elif spec.kind == OP_SAR:

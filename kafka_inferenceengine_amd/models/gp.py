@@ -80,20 +80,36 @@ class GaussianProcessEmulator:
 
     def records(self) -> np.ndarray:
         """float32 kernel records, training-point pairs field-major:
-        [ceil(T/2), 2D+2, 2] with fields L, B[D], alpha, alpha*t[D] (inputs
-        centred); an odd T is padded with an alpha = 0 point."""
+        [T2, D+1, 2] with fields L' = log2(s |alpha|) - 1/2 log2e sum lambda t^2
+        and B = log2e lambda t (inputs centred).  Points with alpha > 0 come
+        first (``n_pos_pairs`` pairs), then alpha < 0; each group is padded to
+        an even count with an L' = -1e30 point (contributes 0); alpha = 0 points
+        are dropped.  See ``csrc/kf_core.h`` (gp_pairs) for the algebra."""
         if self._records is None:
             c = self.center()
             t = self.inputs - c[None, :]
             L = np.log2(self.signal) - 0.5 * LOG2E * (t * t * self.lam[None, :]).sum(1)
             B = LOG2E * self.lam[None, :] * t
-            at = self.alpha[:, None] * t
-            rec = np.concatenate([L[:, None], B, self.alpha[:, None], at], axis=1)   # [T, R]
-            if rec.shape[0] % 2:
-                rec = np.concatenate([rec, np.zeros((1, rec.shape[1]))], axis=0)
-            pairs = rec.reshape(-1, 2, rec.shape[1]).transpose(0, 2, 1)           # [T2, R, 2]
+            groups = []
+            for sel in (self.alpha > 0, self.alpha < 0):
+                Lg = L[sel] + np.log2(np.abs(self.alpha[sel]))
+                rec = np.concatenate([Lg[:, None], B[sel]], axis=1)          # [Tg, D+1]
+                if rec.shape[0] % 2:
+                    pad = np.zeros((1, rec.shape[1]))
+                    pad[0, 0] = -1e30   # 2^(-1e30 + ...) = 0
+                    rec = np.concatenate([rec, pad], axis=0)
+                groups.append(rec.reshape(-1, 2, rec.shape[1]).transpose(0, 2, 1))   # [Tg/2, D+1, 2]
+            self._n_pos_pairs = int(groups[0].shape[0])
+            pairs = np.concatenate(groups, axis=0) if (groups[0].size + groups[1].size) else \
+                np.zeros((0, self.n_inputs + 1, 2))
             self._records = np.ascontiguousarray(pairs.astype(np.float32))
         return self._records
+
+    @property
+    def n_pos_pairs(self) -> int:
+        """Leading record pairs with alpha > 0 (``BandDesc.Tp``)."""
+        self.records()
+        return self._n_pos_pairs
 
     @property
     def n_records(self) -> int:

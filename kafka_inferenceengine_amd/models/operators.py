@@ -45,9 +45,10 @@ class OperatorSpec:
     coef: list = field(default_factory=list)
     center: list = field(default_factory=list)
     offset: float = 0.0
-    records: np.ndarray | None = None     # GP training records [T, 2D+2]
+    records: np.ndarray | None = None     # GP training records [T/2, D+1, 2] (models/gp.py)
     aux: np.ndarray | None = None         # per active pixel auxiliary (SAR theta)
     emulator: object = None
+    gp_pos_pairs: int = 0                 # leading record pairs with alpha > 0
 
     @property
     def d(self) -> int:
@@ -72,7 +73,7 @@ def gp_spec(emulator: GaussianProcessEmulator, state_map) -> OperatorSpec:
     if emulator.n_inputs != len(state_map):
         raise ValueError(f"emulator has {emulator.n_inputs} inputs but state map has {len(state_map)}")
     return OperatorSpec(OP_GP, state_map, list(map(float, emulator.lam)), list(map(float, emulator.center())),
-                        float(emulator.mean), emulator.records(), None, emulator)
+                        float(emulator.mean), emulator.records(), None, emulator, emulator.n_pos_pairs)
 
 
 # ---------------------------------------------------------------- helpers

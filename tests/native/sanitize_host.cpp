@@ -38,18 +38,16 @@ bool all_finite(const std::vector<float>& v) {
   return true;
 }
 
-// GP records, pair layout [T/2][2D+2][2] (models/gp.py: records()).
+// GP records, pair layout [T/2][D+1][2] (models/gp.py: records()): L', B[D];
+// the first half of the pairs is the alpha > 0 group (BandDesc.Tp = T/4).
 std::vector<float> gp_records(int D, int T) {
-  const int R = 2 * D + 2;
-  std::vector<float> r((size_t)T * R);
+  const int R = D + 1;
+  std::vector<float> r((size_t)T / 2 * R * 2);
   for (int i = 0; i < T; ++i) {
     const float t_scale = 0.3f;
     for (int f = 0; f < R; ++f) {
-      float v;
-      if (f == 0) v = unif(-2.f, 0.f);                       // L
-      else if (f <= D) v = unif(-1.f, 1.f) * t_scale;        // B
-      else if (f == D + 1) v = unif(-0.05f, 0.05f);          // alpha
-      else v = unif(-0.02f, 0.02f);                          // alpha * t
+      const float v = (f == 0) ? unif(-6.f, -3.f)                 // L' = L + log2|alpha|
+                               : unif(-1.f, 1.f) * t_scale;      // B
       r[((size_t)(i >> 1) * R + f) * 2 + (i & 1)] = v;
     }
   }
@@ -95,6 +93,7 @@ int main() {
     bd.obs = OBS_DN16;
     bd.d = D;
     bd.T = T;
+    bd.Tp = T / 4;
     const int mp[2][4] = {{0, 1, 6, 2}, {3, 4, 6, 5}};
     for (int d = 0; d < D; ++d) {
       bd.map[d] = mp[b][d];
