@@ -64,14 +64,21 @@ def build(cfg_name, a, mask, part, dev, comm):
     c = CONFIGS[cfg_name]
     n_dates = a.warmup + a.steps + 1
     seed = 0
+    over = {}
+    for kv in getattr(a, "set", None) or []:        # --set field=value (EngineConfig A/B knobs)
+        key, val = kv.split("=", 1)
+        over[key] = type(getattr(k.EngineConfig(), key))(val) if not isinstance(getattr(k.EngineConfig(), key), bool) \
+            else val.lower() in ("1", "true", "yes")
+
+    def mkcfg(**kw):
+        return k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel, **{**kw, **over})
     if cfg_name in ("tip7", "spatial"):
         dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(n_dates)]
         obs = k.SyntheticBHRObservations(mask, dates=dates, n_train=a.n_train or c["n_train"], partition=part,
                                          device=dev, n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=seed)
-        cfg = k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel)
+        cfg = mkcfg()
         if cfg_name == "spatial":
-            cfg = k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel, spatial_gamma=c["gamma"], spatial_params=[6],
-                                 jacobi_sweeps=c["sweeps"])
+            cfg = mkcfg(spatial_gamma=c["gamma"], spatial_params=[6], jacobi_sweeps=c["sweeps"])
         kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_nonlinear_observation_operator,
                             k.TIP_PARAMETERS, state_propagation=k.propagate_information_filter_LAI, config=cfg,
                             comm=comm, partition=part)
@@ -83,7 +90,7 @@ def build(cfg_name, a, mask, part, dev, comm):
                                               stream=True, cloud_fraction=a.cloud, seed=seed)
         kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_linear_observation_operator,
                             k.TIP_PARAMETERS, state_propagation=k.propagate_information_filter_LAI,
-                            config=k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel), comm=comm, partition=part)
+                            config=mkcfg(), comm=comm, partition=part)
         kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
         state = kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask))
     else:
@@ -102,7 +109,7 @@ def build(cfg_name, a, mask, part, dev, comm):
         prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
         kf = k.LinearKalman(obs, k.DeviceOutput(k.SAIL_PARAMETERS), mask, k.create_prosail_observation_operator,
                             k.SAIL_PARAMETERS, state_propagation=None, prior=prior,
-                            config=k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel), comm=comm, partition=part)
+                            config=mkcfg(), comm=comm, partition=part)
         state = kf.state_from_prior(prior)
     return obs, kf, state, dates
 
@@ -122,6 +129,8 @@ def main():
     ap.add_argument("--profile", default=None, help="write a torch.profiler chrome trace here (rank 0)")
     ap.add_argument("--watchdog", type=float, default=0, help="dump Python stacks every N s (hang triage)")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
+                    help="override an EngineConfig field (A/B runs), e.g. --set gp_split=never")
     ap.add_argument("--band-parallel", type=int, default=1,
                     help="ranks per band group (strips x band groups; multi-band configs)")
     a = ap.parse_args()

@@ -33,9 +33,12 @@ class EngineConfig:
     # GP operator placement: fused into the analysis kernel, or "split" (high-
     # occupancy operator kernel -> HBM -> analysis over band chunks)
     gp_split: str = "auto"                    # 'auto' | 'always' | 'never'
-    gp_split_min_d: int = 7                   # auto: split when a GP band has >= this many inputs
-    gp_split_min_bands: int = 13              # auto: ... or when a date has >= this many GP bands
-    band_chunk: int = 10                      # bands per operator/accumulation chunk in split mode
+    # auto: split when a GP band has >= gp_split_min_d inputs or a date has >= gp_split_min_bands
+    # GP bands.  Measured (profiles/r1_v8_split_vs_fused.log, compact records): PROSAIL 10 bands
+    # x D=10 fused 300 ms vs split 306 ms/step; 34 bands split (one chunk) 133 vs fused 142 ms.
+    gp_split_min_d: int = 99
+    gp_split_min_bands: int = 13
+    band_chunk: int = 0                       # bands per split chunk; 0 = as many as fit in half the free HBM
     # band-parallel (TP-like) decomposition: ranks = strips x band_parallel;
     # the B ranks of a strip split the bands and all-reduce the normal equations
     band_parallel: int = 1

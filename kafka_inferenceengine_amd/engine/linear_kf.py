@@ -105,6 +105,7 @@ class LinearKalman:
                                 enabled=self.metrics.enabled or self.config.phase_timing)
         self._lookahead_fn = None       # host prep of the next date, run under the last GN iteration
         self._prepared = None           # (date, bands, table) made by it
+        self._split_chunk = {}          # split path: bands per chunk, per band count
         self._reg = None
         self._output_written = None
         band = getattr(self.comm, "band", None)
@@ -736,7 +737,23 @@ class LinearKalman:
             return None
         cfg = self.config
         n, N = self.n_params, self.N
-        C = max(1, min(int(cfg.band_chunk), len(specs)))
+        C = int(cfg.band_chunk)
+        if C <= 0:
+            # as many bands per chunk as fit in the free HBM (h0 + h: 4 (1 + n) B/px/band) after
+            # the iteration's own state buffers (x_prev, x_new, P_out, the forecast and the (A, b)
+            # accumulators of a multi-chunk plan) and 2 GiB of slack: one chunk = one operator
+            # pass and no (A, b) round trip.  Sized once per band count (later dates see the
+            # allocator's cached blocks as used).
+            C = self._split_chunk.get(len(specs))
+            if C is None:
+                C = 10
+                if self.device.type == "cuda":
+                    free, _ = torch.cuda.mem_get_info(self.device)
+                    nt = ntri(n)
+                    reserve = 4 * max(N, 1) * (4 * n + 2 * nt + 2 * (nt + n)) + (2 << 30)
+                    C = max(1, int((free - reserve) // (4 * (1 + n) * max(N, 1))))
+                self._split_chunk[len(specs)] = C
+        C = max(1, min(C, len(specs)))
         ldh = max(N, 1)
         h0_buf = torch.empty((C, ldh), dtype=torch.float32, device=self.device)
         h_buf = torch.empty((C * n, ldh), dtype=torch.float32, device=self.device)
