@@ -35,6 +35,11 @@ static std::vector<A> get_arr(const A (&src)[N]) { return std::vector<A>(src, sr
 #define PTR_FIELD(cls, name, T)                                                                     \
   def_property(#name, [](const cls& s) { return (uintptr_t)s.name; },                              \
                [](cls& s, uintptr_t v) { s.name = reinterpret_cast<T>(v); })
+#define GEO_FIELDS(cls, g)                                                                          \
+  def_property("geo_w", [](const cls& s) { return s.g.w; }, [](cls& s, int64_t v) { s.g.w = v; })        \
+      .def_property("geo_n_up", [](const cls& s) { return s.g.n_up; }, [](cls& s, int64_t v) { s.g.n_up = v; }) \
+      .def_property("geo_h", [](const cls& s) { return s.g.h; }, [](cls& s, int32_t v) { s.g.h = v; })   \
+      .def_property("geo_halo", [](const cls& s) { return s.g.halo; }, [](cls& s, int32_t v) { s.g.halo = v; })
 #define ARR_FIELD(cls, name, T)                                                                     \
   def_property(#name, [](const cls& s) { return get_arr(s.name); },                                \
                [](cls& s, const std::vector<T>& v) { set_arr(s.name, v, #name); })
@@ -102,7 +107,13 @@ PYBIND11_MODULE(_kafka_hip, m) {
       .PTR_FIELD(AnalysisArgs, out_mean, float*)
       .PTR_FIELD(AnalysisArgs, out_unc, float*)
       .PTR_FIELD(AnalysisArgs, out_idx, const int64_t*)
-      .def_readwrite("out_plane", &AnalysisArgs::out_plane);
+      .def_readwrite("out_plane", &AnalysisArgs::out_plane)
+      .def_readwrite("reg_gamma", &AnalysisArgs::reg_gamma)
+      .def_readwrite("reg_mask", &AnalysisArgs::reg_mask)
+      .PTR_FIELD(AnalysisArgs, reg_nbr, const int32_t*)
+      .PTR_FIELD(AnalysisArgs, reg_v, float*)
+      .PTR_FIELD(AnalysisArgs, x0_out, float*)
+      .GEO_FIELDS(AnalysisArgs, reg_geo);
 
   py::class_<GainArgs>(m, "GainArgs")
       .def(py::init([]() { GainArgs a; memset(&a, 0, sizeof(a)); return a; }))
@@ -133,7 +144,13 @@ PYBIND11_MODULE(_kafka_hip, m) {
       .PTR_FIELD(JacobiArgs, x_ref, const float*)
       .PTR_FIELD(JacobiArgs, x_out, float*)
       .PTR_FIELD(JacobiArgs, a_out, float*)
-      .PTR_FIELD(JacobiArgs, partials, double*);
+      .PTR_FIELD(JacobiArgs, partials, double*)
+      .def_readwrite("mode", &JacobiArgs::mode)
+      .def_readwrite("k", &JacobiArgs::k)
+      .PTR_FIELD(JacobiArgs, u, const float*)
+      .PTR_FIELD(JacobiArgs, v, float*)
+      .PTR_FIELD(JacobiArgs, z_out, float*)
+      .GEO_FIELDS(JacobiArgs, geo);
 
   py::class_<PropArgs>(m, "PropArgs")
       .def(py::init([]() { PropArgs a; memset(&a, 0, sizeof(a)); return a; }))

@@ -99,6 +99,26 @@ struct PropArgs {
   uint8_t* status;
 };
 
+// Dense row-strip geometry (every pixel of the strip and of the halo rows
+// active): neighbours and degrees follow from the pixel index, no [4][N]
+// table read.  Local pixel p = r * w + c; halo-up pixel of column c at N + c,
+// halo-down at N + n_up + c (parallel/partition.py:neighbour_table layout).
+struct StripGeo {
+  int64_t w, n_up;       // w = 0: not dense, use the neighbour table
+  int32_t h, halo;       // rows; bit 0: halo row above, bit 1: halo row below
+};
+
+KF_HD int32_t geo_neighbour(const StripGeo& g, int64_t N, int64_t p, int k) {
+  const uint32_t w = (uint32_t)g.w;
+  const uint32_t r = (uint32_t)p / w, c = (uint32_t)p - r * w;
+  switch (k) {
+    case 0: return r > 0 ? (int32_t)(p - w) : ((g.halo & 1) ? (int32_t)(N + c) : -1);
+    case 1: return r + 1 < (uint32_t)g.h ? (int32_t)(p + w) : ((g.halo & 2) ? (int32_t)(N + g.n_up + c) : -1);
+    case 2: return c > 0 ? (int32_t)(p - 1) : -1;
+    default: return c + 1 < w ? (int32_t)(p + 1) : -1;
+  }
+}
+
 struct AnalysisArgs {
   int64_t N, ld;
   int32_t n_bands, solve;
@@ -121,6 +141,15 @@ struct AnalysisArgs {
   float* out_unc;
   const int64_t* out_idx;  // raster position of each pixel (null: identity)
   int64_t out_plane;
+  // K9 regulariser prepare fused into the epilogue (reg_v non-null): A_reg = A +
+  // g deg E_R -> a_out, u = A_reg^-1 b -> x_out, V = A_reg^-1 E_R -> reg_v [k*NP][ld];
+  // no convergence partial (the JACOBI_FINISH pass computes it)
+  float reg_gamma;
+  uint32_t reg_mask;
+  const int32_t* reg_nbr;  // [4][N] neighbour table (degrees) unless reg_geo.w > 0
+  float* reg_v;
+  float* x0_out;           // the linearisation point (the fused forecast when x_prev is null)
+  StripGeo reg_geo;
 };
 
 
@@ -672,6 +701,47 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
                               uint8_t st) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a->ld;
+  if (a->x0_out) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) a->x0_out[j * ld + p] = x0[j];
+  }
+  if (a->reg_v) {
+    int deg = 0;
+    if (a->reg_geo.w > 0) {
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) deg += geo_neighbour(a->reg_geo, a->N, p, q4) >= 0 ? 1 : 0;
+    } else {
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) deg += a->reg_nbr[q4 * a->N + p] >= 0 ? 1 : 0;
+    }
+    const float gd = a->reg_gamma * (float)deg;
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+      if ((a->reg_mask >> j) & 1u) A[tri(NP, j, j)] += gd;
+    if (a->a_out) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = A[t];
+    }
+    if (!chol_packed<NP>(A)) st |= ST_NONSPD;
+    chol_solve<NP>(A, b);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) a->x_out[j * ld + p] = b[j];
+    int c = 0;
+#pragma unroll
+    for (int r = 0; r < NP; ++r) {
+      if ((a->reg_mask >> r) & 1u) {
+        float e[NP];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) e[j] = (j == r) ? 1.f : 0.f;
+        chol_solve<NP>(A, e);
+#pragma unroll
+        for (int j = 0; j < NP; ++j) a->reg_v[((int64_t)c * NP + j) * ld + p] = e[j];
+        ++c;
+      }
+    }
+    if (a->status) a->status[p] = st;
+    return 0.f;
+  }
   if (a->a_out) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = A[t];
@@ -945,10 +1015,139 @@ struct JacobiArgs {
   float* x_out;          // [NP][ld]
   float* a_out;          // optional: regularised precision written back
   double* partials;
+  // Affine form of the same sweeps (JACOBI_PREPARE / _SWEEP / _FINISH): with
+  // A_reg = A + g deg E_R factored once per GN iteration, u = A_reg^-1 b and
+  // V = A_reg^-1 E_R (NP x k), a sweep is x = u + g V s(x_R), s = sum of the
+  // neighbours' regularised components, so only the k regularised fields z
+  // are iterated (and exchanged); the full state is formed once at the end.
+  int32_t mode, k;
+  const float* u;        // [NP][ld]    A_reg^-1 b            (SWEEP, FINISH)
+  float* v;              // [k*NP][ld]  column c of V = A_reg^-1 e_{R_c} (PREPARE writes)
+  float* z_out;          // [k][ld_ext] regularised components (SWEEP writes the local part)
+  StripGeo geo;          // dense strip: neighbours from the index (nbr unused)
 };
+
+template <typename JA>
+KF_HD int32_t jacobi_neighbour(const JA& a, int64_t p, int k) {
+  return a.geo.w > 0 ? geo_neighbour(a.geo, a.N, p, k) : a.nbr[k * a.N + p];
+}
+
+constexpr int JACOBI_CLASSIC = 0, JACOBI_PREPARE = 1, JACOBI_SWEEP = 2, JACOBI_FINISH = 3;
+
+// neighbour sums of the k fields of an extended array (x_ext rows 0..k-1)
+template <int NP>
+KF_HD void reg_neighbour_sums(const JacobiArgs& a, int64_t p, float (&s)[NP], int& deg) {
+#pragma unroll
+  for (int c = 0; c < NP; ++c) s[c] = 0.f;
+  deg = 0;
+#pragma unroll
+  for (int q4 = 0; q4 < 4; ++q4) {
+    const int32_t q = jacobi_neighbour(a, p, q4);
+    if (q >= 0) {
+      ++deg;
+#pragma unroll
+      for (int c = 0; c < NP; ++c)
+        if (c < a.k) s[c] += a.x_ext[c * a.ld_ext + q];
+    }
+  }
+}
+
+template <int NP>
+KF_HD float pixel_reg_prepare(const JacobiArgs& a, int64_t p) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a.ld;
+  float A[NT], b[NP];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) A[t] = a.a_in[t * ld + p];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) b[j] = a.b_in[j * ld + p];
+  int deg = 0;
+#pragma unroll
+  for (int q4 = 0; q4 < 4; ++q4) deg += jacobi_neighbour(a, p, q4) >= 0 ? 1 : 0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j)
+    if ((a.reg_mask >> j) & 1u) A[tri(NP, j, j)] += a.gamma * (float)deg;
+  if (a.a_out) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = A[t];
+  }
+  chol_packed<NP>(A);
+  chol_solve<NP>(A, b);
+#pragma unroll
+  for (int j = 0; j < NP; ++j) a.x_out[j * ld + p] = b[j];
+  int c = 0;
+#pragma unroll
+  for (int r = 0; r < NP; ++r) {
+    if ((a.reg_mask >> r) & 1u) {
+      float e[NP];
+#pragma unroll
+      for (int j = 0; j < NP; ++j) e[j] = (j == r) ? 1.f : 0.f;
+      chol_solve<NP>(A, e);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) a.v[((int64_t)c * NP + j) * ld + p] = e[j];
+      ++c;
+    }
+  }
+  return 0.f;
+}
+
+template <int NP>
+KF_HD float pixel_reg_sweep(const JacobiArgs& a, int64_t p) {
+  const int64_t ld = a.ld;
+  float s[NP];
+  int deg;
+  reg_neighbour_sums<NP>(a, p, s, deg);
+  int r = 0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    if ((a.reg_mask >> j) & 1u) {
+      float z = 0.f;
+#pragma unroll
+      for (int c = 0; c < NP; ++c)
+        if (c < a.k) z = fmaf(a.v[((int64_t)c * NP + j) * ld + p], s[c], z);
+      a.z_out[r * a.ld_ext + p] = fmaf(a.gamma, z, a.u[j * ld + p]);
+      ++r;
+    }
+  }
+  return 0.f;
+}
+
+template <int NP>
+KF_HD float pixel_reg_finish(const JacobiArgs& a, int64_t p) {
+  const int64_t ld = a.ld;
+  float s[NP];
+  int deg;
+  reg_neighbour_sums<NP>(a, p, s, deg);
+  float dn = 0.f;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    float z = 0.f;
+#pragma unroll
+    for (int c = 0; c < NP; ++c)
+      if (c < a.k) z = fmaf(a.v[((int64_t)c * NP + j) * ld + p], s[c], z);
+    const float x = fmaf(a.gamma, z, a.u[j * ld + p]);
+    a.x_out[j * ld + p] = x;
+    const float d = x - a.x_ref[j * ld + p];
+    dn = fmaf(d, d, dn);
+  }
+  return dn;
+}
+
+template <int NP>
+KF_HD float pixel_jacobi_classic(const JacobiArgs& a, int64_t p);
 
 template <int NP>
 KF_HD float pixel_jacobi(const JacobiArgs& a, int64_t p) {
+  switch (a.mode) {
+    case JACOBI_PREPARE: return pixel_reg_prepare<NP>(a, p);
+    case JACOBI_SWEEP: return pixel_reg_sweep<NP>(a, p);
+    case JACOBI_FINISH: return pixel_reg_finish<NP>(a, p);
+    default: return pixel_jacobi_classic<NP>(a, p);
+  }
+}
+
+template <int NP>
+KF_HD float pixel_jacobi_classic(const JacobiArgs& a, int64_t p) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a.ld;
   float A[NT], b[NP];
@@ -962,7 +1161,7 @@ KF_HD float pixel_jacobi(const JacobiArgs& a, int64_t p) {
   for (int j = 0; j < NP; ++j) sx[j] = 0.f;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int32_t q = a.nbr[k * a.N + p];
+    const int32_t q = jacobi_neighbour(a, p, k);
     if (q >= 0) {
       ++deg;
 #pragma unroll

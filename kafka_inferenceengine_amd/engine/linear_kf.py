@@ -107,6 +107,8 @@ class LinearKalman:
         self._prepared = None           # (date, bands, table) made by it
         self._split_chunk = {}          # split path: bands per chunk, per band count
         self._reg = None
+        self._reg_uv = None             # affine regulariser: u = A_reg^-1 b, V = A_reg^-1 E_R, x0
+        self._reg_geo = None
         self._output_written = None
         band = getattr(self.comm, "band", None)
         self.band_comm = band if (band is not None and band.world > 1) else None
@@ -603,8 +605,7 @@ class LinearKalman:
         elif table is None or h0_outs is not None:
             table = build_table(specs, dbs, n, self._cache, self.device, h0_outs)
         prop = None
-        if isinstance(forecast, LazyForecast) and not (gain or precomp or split or bp or cfg.spatial_gamma > 0) \
-                and N:
+        if isinstance(forecast, LazyForecast) and not (gain or precomp or split or bp) and N:
             # fused propagation: the kernel computes the forecast per pixel from
             # the previous analysis; the first iteration linearises at it
             prop = forecast.handle()
@@ -645,7 +646,7 @@ class LinearKalman:
                         K.gain(n, table, x_prev, fc.x, fc.P, x_new, P_out, status, self._partials, N=N,
                                joseph=cfg.joseph)
                     elif cfg.spatial_gamma > 0:
-                        self._regularised_iteration(table, x_prev, fc, x_new, P_out, status)
+                        self._regularised_iteration(table, x_prev, fc, x_new, P_out, status, prop)
                     elif bp:
                         self._band_parallel_iteration(table, x_prev, fc, x_new, A_keep, status)
                     elif split is not None:
@@ -789,29 +790,51 @@ class LinearKalman:
                            a_in=a_in, b_in=b_in)
                 prev = (A_c, b_c)
 
-    def _regularised_iteration(self, table, x_prev, fc: KFState, x_out, A_out, status):
-        """Assemble (A, b) with the fused kernel, then block-Jacobi sweeps of the
-        GMRF smoother with halo exchange between sweeps (K9 + C2)."""
+    def _regularised_iteration(self, table, x_prev, fc: KFState | None, x_out, A_out, status, prop=None):
+        """GMRF spatial prior (K9 + C2), affine block-Jacobi form (kf_core.h):
+        the analysis kernel assembles (A, b) and, instead of solving, factors
+        A_reg = A + g deg E_R once and writes u = A_reg^-1 b and V = A_reg^-1 E_R;
+        each sweep then iterates only the k regularised fields z <- u_R + g V_RR
+        s(z) (s: neighbour sums, halo rows exchanged by C2), and the last one forms
+        x = u + g V s(z) with the convergence partials.  Identical to ``sweeps``
+        block-Jacobi sweeps of (A_reg) x = b + g E_R sum_q x_q.  The analysis
+        precision includes the smoother's diagonal.  With ``prop`` the forecast
+        is fused as in the plain path (first iteration: x0 = forecast, written
+        for the norm and the first sweep)."""
         from ..parallel.halo import HaloExchanger
 
         if self._reg is None:
             self._reg = HaloExchanger(self.partition, self.comm, self.n_params, self.device,
                                       self.config.spatial_params)
-        reg = self._reg
+            self._reg_geo = self.partition.dense_geometry()
+        reg, geo = self._reg, self._reg_geo
         n, N = self.n_params, self.N
-        b = torch.empty_like(fc.x)
-        K.analysis(n, table, x_prev, fc.x, fc.P, None, A_out, b, status, None, N=N, solve=False)
-        x_cur = x_prev
+        gamma = self.config.spatial_gamma
         sweeps = max(1, int(self.config.jacobi_sweeps))
-        for s in range(sweeps):
-            x_ext = reg.extend(x_cur)
-            last = s == sweeps - 1
-            dst = x_out if last else reg.scratch(x_cur)
-            K.jacobi(n, A_out, b, x_ext, reg.nbr, x_prev, dst, self.config.spatial_gamma, reg.reg_mask, N,
-                     a_out=None, partials=self._partials if last else None)
-            x_cur = dst
-        # analysis precision includes the smoother's diagonal contribution
-        reg.add_regulariser_diagonal(A_out, self.config.spatial_gamma)
+        rows = reg.reg_rows()
+        fx, fP = (fc.x, fc.P) if fc is not None else (None, None)
+        if not rows:   # nothing regularised: plain analysis
+            K.analysis(n, table, x_prev, fx, fP, x_out, A_out, None, status, self._partials, N=N, prop=prop)
+            return
+        k = len(rows)
+        ld = x_out.shape[1]
+        if self._reg_uv is None or self._reg_uv[0].shape[1] != ld or self._reg_uv[1].shape[0] != k * n:
+            self._reg_uv = tuple(torch.empty((r, ld), dtype=torch.float32, device=self.device)
+                                 for r in (n, k * n, n))
+        u, v, x0_buf = self._reg_uv
+        x_ref = x_prev if x_prev is not None else x0_buf
+        K.analysis(n, table, x_prev, fx, fP, u, A_out, None, status, None, N=N, prop=prop,
+                   reg=dict(gamma=gamma, mask=reg.reg_mask, v_out=v, nbr=None if geo else reg.nbr, geo=geo),
+                   x0_out=None if x_prev is not None else x0_buf)
+        nbr = None if geo else reg.nbr
+        z = reg.z_buffers(k)
+        z[0][:, :N].copy_(x_ref[rows, :N])
+        cur = reg.fill_halo(z[0])
+        for _ in range(sweeps - 1):
+            nxt = z[1] if cur is z[0] else z[0]
+            K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo)
+            cur = reg.fill_halo(nxt)
+        K.reg_finish(n, u, v, cur, nbr, x_ref, x_out, gamma, reg.reg_mask, N, partials=self._partials, geo=geo)
 
     # ------------------------------------------------ band-parallel (TP-like)
     def _band_parallel_iteration(self, table, x_prev, fc: KFState, x_out, A_out, status):

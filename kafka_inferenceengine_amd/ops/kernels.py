@@ -152,7 +152,7 @@ def gp_operator_supported(n_params, d) -> bool:
 
 def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=None, b_out=None, status=None,
              partials=None, N=None, solve=True, fast=True, variant=None, a_in=None, b_in=None, prop=None,
-             out=None):
+             out=None, reg=None, x0_out=None):
     """K1 fused Gauss-Newton analysis (information form).
 
     ``prop`` (from :func:`prop_args`) fuses the propagation: the forecast is
@@ -162,7 +162,12 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
 
     ``out = (mean, unc, idx)`` additionally writes x and 1/sqrt(diag A) into
     output rasters ``[n_params, plane]`` at raster positions ``idx`` (int64 [N],
-    None = identity) — the unpack pass fused into the final iteration."""
+    None = identity) — the unpack pass fused into the final iteration.
+
+    ``reg = dict(gamma, mask, v_out, nbr=None, geo=None)`` replaces the solve by
+    the K9 regulariser prepare (kf_core.h): a_out <- A + g deg E_R, x_out <- u =
+    A_reg^-1 b, v_out [k*n, ld] <- A_reg^-1 E_R; no partials.  ``x0_out``
+    receives the linearisation point (the fused forecast when x_prev is None)."""
     check_np(n_params)
     ref = next(t for t in (x_prev, x_f, x_out, a_out) if t is not None)
     N = int(ref.shape[1] if N is None else N)
@@ -217,6 +222,28 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
         elif plane < N:
             raise ValueError("identity output needs plane >= N")
         a.out_mean, a.out_unc, a.out_idx, a.out_plane = _ptr(mean), _ptr(unc), _ptr(idx), plane
+    if x0_out is not None:
+        _check_soa(x0_out, n_params, N, "x0_out", device=dev)
+        if x0_out.shape[1] != ld:
+            raise ValueError("x0_out must share the leading dimension")
+        a.x0_out = _ptr(x0_out)
+    if reg is not None:
+        k = bin(int(reg["mask"])).count("1")
+        v_out = reg["v_out"]
+        _check_soa(v_out, k * n_params, N, "reg v_out", device=dev)
+        if x_out is None or v_out.shape[1] != ld or k == 0:
+            raise ValueError("regulariser prepare needs x_out (u), v_out [k*n, ld] and a non-empty mask")
+        _check_nbr(reg.get("nbr"), N, reg.get("geo"))
+        if partials is not None or out is not None:
+            raise ValueError("regulariser prepare produces no partials / output")
+        a.reg_gamma, a.reg_mask = float(reg["gamma"]), int(reg["mask"])
+        a.reg_nbr, a.reg_v = _ptr(reg.get("nbr")), _ptr(v_out)
+        geo = reg.get("geo")
+        if geo is not None:
+            if geo["w"] <= 0 or geo["h"] * geo["w"] != N:
+                raise ValueError(f"dense geometry {geo} does not cover N={N} pixels")
+            a.geo_w, a.geo_h, a.geo_halo, a.geo_n_up = int(geo["w"]), int(geo["h"]), int(geo["halo"]), \
+                int(geo["n_up"])
     grid = grid_for(N)
     ext().analysis(n_params, a, grid, _dev(ref), _stream(ref))
     return partials
@@ -242,7 +269,8 @@ def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out, status=None
     return partials
 
 
-def jacobi(n_params, a_in, b_in, x_ext, nbr, x_ref, x_out, gamma, reg_mask, N, a_out=None, partials=None):
+def jacobi(n_params, a_in, b_in, x_ext, nbr, x_ref, x_out, gamma, reg_mask, N, a_out=None, partials=None,
+           geo=None):
     """K9 block-Jacobi sweep of the GMRF spatial regulariser."""
     check_np(n_params)
     dev = a_in.device
@@ -251,14 +279,103 @@ def jacobi(n_params, a_in, b_in, x_ext, nbr, x_ref, x_out, gamma, reg_mask, N, a
     _check_soa(x_ref, n_params, N, "x_ref", device=dev)
     _check_soa(x_out, n_params, N, "x_out", device=dev)
     _check_soa(x_ext, n_params, N, "x_ext", device=dev)
-    if nbr.dtype != torch.int32 or nbr.shape != (4, N) or not nbr.is_contiguous():
-        raise ValueError("nbr must be contiguous int32 [4, N]")
+    _check_nbr(nbr, N, geo)
     a = ext().JacobiArgs()
+    _set_geo(a, geo, N)
     a.N, a.ld, a.ld_ext = N, a_in.shape[1], x_ext.shape[1]
     a.gamma, a.reg_mask = float(gamma), int(reg_mask)
     a.a_in, a.b_in, a.x_ext, a.nbr, a.x_ref, a.x_out = map(_ptr, (a_in, b_in, x_ext, nbr, x_ref, x_out))
     a.a_out, a.partials = _ptr(a_out), _ptr(partials)
     ext().jacobi(n_params, a, grid_for(N), _dev(a_in), _stream(a_in))
+    return partials
+
+
+JACOBI_PREPARE, JACOBI_SWEEP, JACOBI_FINISH = 1, 2, 3
+
+
+def _set_geo(a, geo, N, prefix="geo"):
+    """Dense strip geometry (StripPartition.dense_geometry) into an args struct."""
+    if geo is None:
+        return
+    if geo["w"] <= 0 or geo["h"] * geo["w"] != N:
+        raise ValueError(f"dense geometry {geo} does not cover N={N} pixels")
+    a.geo_w, a.geo_h, a.geo_halo, a.geo_n_up = int(geo["w"]), int(geo["h"]), int(geo["halo"]), int(geo["n_up"])
+
+
+def _check_nbr(nbr, N, geo):
+    if geo is not None and nbr is None:
+        return
+    if nbr is None or nbr.dtype != torch.int32 or nbr.shape != (4, N) or not nbr.is_contiguous():
+        raise ValueError("nbr must be contiguous int32 [4, N] (or pass the dense geometry)")
+
+
+def _reg_args(n_params, mode, N, ld, gamma, reg_mask, nbr, geo=None):
+    _check_nbr(nbr, N, geo)
+    a = ext().JacobiArgs()
+    a.N, a.ld = N, ld
+    a.gamma, a.reg_mask = float(gamma), int(reg_mask)
+    a.mode, a.k = mode, bin(int(reg_mask)).count("1")
+    a.nbr = _ptr(nbr)
+    _set_geo(a, geo, N)
+    return a
+
+
+def reg_prepare(n_params, a_in, b_in, nbr, u_out, v_out, gamma, reg_mask, N, a_out=None, geo=None):
+    """K9 affine form, once per GN iteration: A_reg = A + g deg E_R (written to
+    ``a_out``, may alias ``a_in``), u = A_reg^-1 b, V = A_reg^-1 E_R ([k*n, ld])."""
+    check_np(n_params)
+    dev = a_in.device
+    k = bin(int(reg_mask)).count("1")
+    _check_soa(a_in, ntri(n_params), N, "a_in", device=dev)
+    _check_soa(b_in, n_params, N, "b_in", device=dev)
+    _check_soa(u_out, n_params, N, "u_out", device=dev)
+    _check_soa(v_out, k * n_params, N, "v_out", device=dev)
+    _check_soa(a_out, ntri(n_params), N, "a_out", device=dev)
+    ld = a_in.shape[1]
+    for t in (b_in, u_out, v_out, a_out):
+        if t is not None and t.shape[1] != ld:
+            raise ValueError("all SoA operands must share the leading dimension")
+    a = _reg_args(n_params, JACOBI_PREPARE, N, ld, gamma, reg_mask, nbr, geo)
+    a.a_in, a.b_in, a.x_out, a.v, a.a_out = map(_ptr, (a_in, b_in, u_out, v_out, a_out))
+    ext().jacobi(n_params, a, grid_for(N), _dev(a_in), _stream(a_in))
+
+
+def reg_sweep(n_params, u, v, z_ext, nbr, z_out, gamma, reg_mask, N, geo=None):
+    """K9 affine sweep of the k regularised fields: z_out[:, :N] = u_R + g V_RR s(z_ext)."""
+    check_np(n_params)
+    dev = u.device
+    k = bin(int(reg_mask)).count("1")
+    _check_soa(u, n_params, N, "u", device=dev)
+    _check_soa(v, k * n_params, N, "v", device=dev)
+    _check_soa(z_ext, k, N, "z_ext", device=dev)
+    _check_soa(z_out, k, N, "z_out", device=dev)
+    if z_out.shape[1] != z_ext.shape[1] or v.shape[1] != u.shape[1]:
+        raise ValueError("z_out must share z_ext's leading dimension and v u's")
+    a = _reg_args(n_params, JACOBI_SWEEP, N, u.shape[1], gamma, reg_mask, nbr, geo)
+    a.ld_ext = z_ext.shape[1]
+    a.u, a.v, a.x_ext, a.z_out = map(_ptr, (u, v, z_ext, z_out))
+    ext().jacobi(n_params, a, grid_for(N), _dev(u), _stream(u))
+
+
+def reg_finish(n_params, u, v, z_ext, nbr, x_ref, x_out, gamma, reg_mask, N, partials=None, geo=None):
+    """K9 affine form, last sweep: x = u + g V s(z_ext) for every parameter, with
+    the convergence partials of (x - x_ref)."""
+    check_np(n_params)
+    dev = u.device
+    k = bin(int(reg_mask)).count("1")
+    _check_soa(u, n_params, N, "u", device=dev)
+    _check_soa(v, k * n_params, N, "v", device=dev)
+    _check_soa(z_ext, k, N, "z_ext", device=dev)
+    _check_soa(x_ref, n_params, N, "x_ref", device=dev)
+    _check_soa(x_out, n_params, N, "x_out", device=dev)
+    ld = u.shape[1]
+    for t in (v, x_ref, x_out):
+        if t.shape[1] != ld:
+            raise ValueError("all SoA operands must share the leading dimension")
+    a = _reg_args(n_params, JACOBI_FINISH, N, ld, gamma, reg_mask, nbr, geo)
+    a.ld_ext = z_ext.shape[1]
+    a.u, a.v, a.x_ext, a.x_ref, a.x_out, a.partials = map(_ptr, (u, v, z_ext, x_ref, x_out, partials))
+    ext().jacobi(n_params, a, grid_for(N), _dev(u), _stream(u))
     return partials
 
 

@@ -90,6 +90,17 @@ class StripPartition:
         return {"send_up": send_up.astype(np.int64), "send_down": last.astype(np.int64), "n_up": n_up,
                 "n_down": n_down}
 
+    def dense_geometry(self):
+        """``{"w", "h", "halo", "n_up"}`` when the strip and its halo rows are fully
+        active (the kernels then derive neighbours from the pixel index instead of
+        reading the [4, N] table — kf_core.h:StripGeo), else None."""
+        H, W = self.shape
+        lo, hi = max(self.r0 - 1, 0), min(self.r1 + 1, H)
+        if self.N == 0 or not self.state_mask[lo:hi].all() or self.N >= 2 ** 31:
+            return None
+        halo = (1 if self.r0 > 0 else 0) | (2 if self.r1 < H else 0)
+        return {"w": W, "h": self.r1 - self.r0, "halo": halo, "n_up": W if self.r0 > 0 else 0}
+
     def neighbour_table(self) -> np.ndarray:
         """int32 [4, N]: index of the up/down/left/right active neighbour in the
         extended state (local 0..N-1, halo-up N.., halo-down N+n_up..), -1 if none."""

@@ -223,3 +223,9 @@ def test_fused_output_gpu(cuda):
         outs.append((out.mean.cpu(), out.unc.cpu()))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-6)
+
+
+@pytest.mark.parametrize("regmask", [0b1000000, 0b1000101])
+def test_affine_jacobi_equals_classic_gpu(cuda, regmask):
+    from test_kernels import affine_vs_classic_jacobi
+    affine_vs_classic_jacobi(cuda, regmask=regmask)

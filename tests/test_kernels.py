@@ -296,3 +296,85 @@ def test_fused_propagation_equals_materialized(mode, blend, quirk, pmask):
 def test_heavy_propagation_is_not_fused(mode, blend):
     with pytest.raises(ValueError, match="fused"):
         C.fused_vs_materialized("cpu", mode, blend, N=64)
+
+
+def affine_vs_classic_jacobi(device, n=7, regmask=0b1000100, sweeps=4, seed=9):
+    """The affine regulariser (prepare once, iterate the k regularised fields,
+    finish) equals ``sweeps`` classic block-Jacobi sweeps, and writes A + g deg E_R."""
+    from kafka_inferenceengine_amd.parallel import StripPartition
+    rng = np.random.default_rng(seed)
+    mask = rng.random((14, 11)) > 0.15
+    part = StripPartition(mask)
+    N = part.N
+    A = C.spd_blocks(rng, N, n)
+    b = rng.normal(size=(N, n))
+    x0 = rng.normal(size=(N, n))
+    nbr = torch.from_numpy(part.neighbour_table()).to(device)
+    gamma = 2.5
+    Ad, bd, xd = C.packed(A, device), C.soa(b, device), C.soa(x0, device)
+    # classic: every sweep re-factors A + g deg E_R
+    cur = xd.clone()
+    for _ in range(sweeps):
+        nxt = torch.zeros_like(cur)
+        K.jacobi(n, Ad, bd, cur, nbr, xd, nxt, gamma, regmask, N)
+        cur = nxt
+    ref = cur.cpu().numpy()
+    # affine
+    rows = [j for j in range(n) if (regmask >> j) & 1]
+    k = len(rows)
+    u = torch.zeros((n, N), device=device)
+    v = torch.zeros((k * n, N), device=device)
+    A2 = Ad.clone()
+    K.reg_prepare(n, A2, bd, nbr, u, v, gamma, regmask, N, a_out=A2)
+    z = [xd[rows].clone().contiguous(), torch.zeros((k, N), device=device)]
+    c = 0
+    for _ in range(sweeps - 1):
+        K.reg_sweep(n, u, v, z[c], nbr, z[1 - c], gamma, regmask, N)
+        c = 1 - c
+    out = torch.zeros((n, N), device=device)
+    part_buf = K.partials_buffer(N, device)
+    K.reg_finish(n, u, v, z[c], nbr, xd, out, gamma, regmask, N, partials=part_buf)
+    got = out.cpu().numpy()
+    assert np.allclose(got, ref, rtol=1e-4, atol=1e-5), float(np.abs(got - ref).max())
+    norm = float(K.reduce_partials(part_buf).cpu()[0])
+    assert np.isclose(norm, float(((got - x0.T) ** 2).sum()), rtol=1e-4)
+    deg = (nbr >= 0).sum(0).cpu().numpy()
+    Areg = unpack_blocks(A2.cpu().numpy(), n)
+    for j in rows:
+        assert np.allclose(Areg[:, j, j], A[:, j, j] + gamma * deg, rtol=1e-5)
+
+
+@pytest.mark.parametrize("regmask", [0b1000000, 0b1000101])
+def test_affine_jacobi_equals_classic(regmask):
+    affine_vs_classic_jacobi("cpu", regmask=regmask)
+
+
+def test_dense_geometry_equals_neighbour_table():
+    """Index-derived neighbours (kf_core.h:StripGeo) reproduce the table for
+    dense strips of a 3-rank partition (halo above, below, both)."""
+    from kafka_inferenceengine_amd.parallel import StripPartition
+    rng = np.random.default_rng(3)
+    mask = np.ones((15, 7), bool)
+    n, regmask, gamma = 4, 0b0110, 1.7
+    for rank in range(3):
+        part = StripPartition(mask, rank, 3)
+        geo = part.dense_geometry()
+        assert geo is not None
+        N = part.N
+        lay = part.halo_layout()
+        cols = N + lay["n_up"] + lay["n_down"]
+        u = torch.from_numpy(rng.normal(size=(n, N)).astype(np.float32))
+        v = torch.from_numpy(rng.normal(size=(2 * n, N)).astype(np.float32))
+        z = torch.from_numpy(rng.normal(size=(2, cols)).astype(np.float32))
+        nbr = torch.from_numpy(part.neighbour_table())
+        outs = []
+        for g, t in ((geo, None), (None, nbr)):
+            zo = torch.zeros((2, cols))
+            K.reg_sweep(n, u, v, z, t, zo, gamma, regmask, N, geo=g)
+            xo = torch.zeros((n, N))
+            K.reg_finish(n, u, v, z, t, u, xo, gamma, regmask, N, geo=g)
+            outs.append((zo, xo))
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    holes = mask.copy()
+    holes[7, 3] = False
+    assert StripPartition(holes, 1, 3).dense_geometry() is None
