@@ -69,7 +69,17 @@ class LinearOperator:
 
 
 def gp_spec(emulator: GaussianProcessEmulator, state_map) -> OperatorSpec:
+    """Device operator description of a GP band (memoised per emulator and state
+    map: the engine asks for it on every observation date)."""
     state_map = [int(i) for i in state_map]
+    cache = emulator.__dict__.setdefault("_spec_cache", {})
+    key = tuple(state_map)
+    if key not in cache:
+        cache[key] = _gp_spec(emulator, state_map)
+    return cache[key]
+
+
+def _gp_spec(emulator: GaussianProcessEmulator, state_map) -> OperatorSpec:
     if emulator.n_inputs != len(state_map):
         raise ValueError(f"emulator has {emulator.n_inputs} inputs but state map has {len(state_map)}")
     return OperatorSpec(OP_GP, state_map, list(map(float, emulator.lam)), list(map(float, emulator.center())),
