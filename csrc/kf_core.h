@@ -38,6 +38,7 @@ constexpr float DEG2RAD = 0.017453292519943295f;
 
 KF_HD constexpr int ntri(int n) { return n * (n + 1) / 2; }
 constexpr int FD_PRECOMP = -1;    // AnalysisArgs.fast_d: all bands OP_PRECOMP
+constexpr int FD_LINEAR = -2;     // AnalysisArgs.fast_d: all bands OP_LINEAR (identity / selection)
 // packed upper triangle, row-major: (0,0) (0,1) .. (0,n-1) (1,1) ..
 KF_HD constexpr int tri(int n, int i, int j) { return i * n - (i * (i - 1)) / 2 + (j - i); }
 template <int NP> KF_HD constexpr int sym(int i, int j) { return i <= j ? tri(NP, i, j) : tri(NP, j, i); }
@@ -870,6 +871,13 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
         h[j] = bd.pre_h[j * bd.pre_ld + p];
         ok = ok && finitef(h[j]);
       }
+    } else if constexpr (FD == FD_LINEAR) {
+      // linear / identity operator (utils.py:119-126, fixed): h = c, H0 = offset + c . x0
+      float t = bd.offset;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) { h[j] = bd.coef[j]; t = fmaf(h[j], x0[j], t); }
+      H0 = t;
+      ok = finitef(H0);
     } else {
       ok = eval_operator<NP>(bd, p, ld, x0, H0, h);
     }

@@ -1,0 +1,261 @@
+// kf_device.h — gfx950 (MI355X) kernel templates for the KaFKA engine, shared by
+// the translation units kf_kernels.hip, kf_analysis7.hip and kf_analysis10.hip
+// (split so the heavy analysis instantiations compile in parallel, _build.py).
+//
+// Design: every matrix the reference builds is block
+// diagonal with n_p x n_p per-pixel blocks, so the whole Gauss-Newton
+// analysis (operator + Jacobian, normal equations, Cholesky, convergence
+// partial) is one pixel per lane, SoA layout ([param][pixel], coalesced
+// 256-B wave loads), grid-stride over pixels, 256-thread workgroups
+// (4 wave64 per workgroup).  GP training records are wave-uniform and are
+// read through the scalar path (s_load) so they cost no VGPRs/LDS traffic.
+// Deterministic reductions: per-block f64 partials, summed in fixed order
+// by reduce_partials_kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "kf_core.h"
+#include "kf_launch.h"
+
+namespace kf {
+
+constexpr int BLOCK = 256;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ void block_partial(double v, double* partials) {
+  __shared__ double red[BLOCK / 64];
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < BLOCK / 64; ++i) s += red[i];
+    partials[blockIdx.x] = s;
+  }
+}
+
+template <int NP, int FD = 0, int FOBS = 0, int UNR = 4, bool FOLD = false>
+__global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
+    acc += (double)pixel_analysis<NP, FD, FOBS, UNR, FOLD>(a, p);
+  if (a.partials) block_partial(acc, a.partials);
+}
+
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void gain_kernel(GainArgs a) {
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
+    acc += (double)pixel_gain<NP>(a, p);
+  if (a.partials) block_partial(acc, a.partials);
+}
+
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void jacobi_kernel(JacobiArgs a) {
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
+    acc += (double)pixel_jacobi<NP>(a, p);
+  if (a.partials) block_partial(acc, a.partials);
+}
+
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void propagate_kernel(PropArgs a) {
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
+    pixel_propagate<NP>(a, p);
+}
+
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void invert_kernel(const float* src, float* dst, int64_t N, int64_t ld,
+                                                      uint8_t* status) {
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
+    const bool ok = pixel_invert<NP>(src, dst, ld, p);
+    if (status && !ok) status[p] |= ST_NONSPD;
+  }
+}
+
+// Standalone operator evaluation (H0 and Jacobian rows) for one band.
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void operator_kernel(const BandDesc* bands, int band, const float* x,
+                                                        int64_t N, int64_t ld, float* h0, float* h,
+                                                        int64_t h_ld, uint8_t* ok_out) {
+  const BandDesc bd = cptr(bands)[band];
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
+    float xv[NP], hv[NP], H0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) xv[j] = x[j * ld + p];
+    const bool ok = eval_operator<NP>(bd, p, ld, xv, H0, hv);
+    h0[p] = H0;
+    if (h) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) h[j * h_ld + p] = hv[j];
+    }
+    if (ok_out) ok_out[p] = ok ? 1 : 0;
+  }
+}
+
+// K2 split path: GP emulator value + Jacobian for a chunk of bands into HBM
+// (h0[b][p], h[b*NP+j][p]).  Without the analysis' packed A/b in registers it
+// runs at high occupancy; used for large input counts (PROSAIL D=10) and many
+// bands (multi-sensor), followed by the OP_PRECOMP analysis kernel.  Pixels
+// whose observation is masked skip the GP (wave-level skip under clouds).
+template <int NP, int D, int UNR>
+__global__ __launch_bounds__(BLOCK) void gp_operator_kernel(const BandDesc* bands, int nb, const float* x,
+                                                           int64_t N, int64_t ld, float* h0, float* h,
+                                                           int64_t ldh) {
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
+    float xv[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) xv[j] = x[j * ld + p];
+    for (int b = 0; b < nb; ++b) {
+      const BandDesc bd = cptr(bands)[b];
+      float y, w, H0 = 0.f, hv[NP];
+#pragma unroll
+      for (int j = 0; j < NP; ++j) hv[j] = 0.f;
+      decode_obs(bd, p, y, w);
+      // RELOAD: the descriptor's epilogue fields are re-read after the record
+      // stream (61 instead of 91 VGPRs, 26 instead of 233 SGPR spills at D=10)
+      if (w > 0.f) gp_eval<NP, D, UNR, false, true>(bd, xv, H0, hv, bands + b);
+      h0[b * ldh + p] = H0;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) h[((int64_t)b * NP + j) * ldh + p] = hv[j];
+    }
+  }
+}
+
+// K6 Hessian correction: A -= w (y - H0(x)) d2f/dx2 for every GP band.
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void hessian_kernel(const BandDesc* bands, int n_bands, const float* x,
+                                                       float* a, int64_t N, int64_t ld) {
+  constexpr int NT = ntri(NP);
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
+    float xv[NP], acc[NT];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) xv[j] = x[j * ld + p];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = 0.f;
+    for (int bi = 0; bi < n_bands; ++bi) {
+      const BandDesc bd = cptr(bands)[bi];
+      if (bd.op != OP_GP) continue;
+      float y, w;
+      decode_obs(bd, p, y, w);
+      if (!(w > 0.f)) continue;
+      float f, Hs[NT];
+      if (!gp_hessian_dispatch<NP>(bd, xv, f, Hs)) continue;
+      const float s = w * (y - f);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = fmaf(s, Hs[t], acc[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) a[t * ld + p] -= acc[t];
+  }
+}
+
+// Output unpack (observations.py:374-376, 392-393): mean and 1/sqrt(diag(P^-1))
+// scattered onto the raster; idx==nullptr means the identity map.
+template <int NP>
+__global__ __launch_bounds__(BLOCK) void unpack_kernel(const float* x, const float* a, int64_t N, int64_t ld,
+                                                      const int64_t* idx, float* mean, float* unc,
+                                                      int64_t plane) {
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
+    const int64_t r = idx ? idx[p] : p;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      if (mean) mean[j * plane + r] = x[j * ld + p];
+      if (unc) unc[j * plane + r] = kf_rsqrt(a[tri(NP, j, j) * ld + p]);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(BLOCK) void gather_kernel(const T* src, const int64_t* idx, T* dst, int64_t n,
+                                                      int rows, int64_t src_ld, int64_t dst_ld) {
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < n; p += stride) {
+    const int64_t s = idx[p];
+    for (int r = 0; r < rows; ++r) dst[r * dst_ld + p] = src[r * src_ld + s];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+inline int grid_for(int64_t N, int max_blocks) {
+  int64_t g = (N + BLOCK - 1) / BLOCK;
+  if (g > max_blocks) g = max_blocks;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+#define KF_NP_SWITCH(np, FN, ...)                 \
+  switch (np) {                                   \
+    case 1: FN<1>(__VA_ARGS__); break;            \
+    case 2: FN<2>(__VA_ARGS__); break;            \
+    case 3: FN<3>(__VA_ARGS__); break;            \
+    case 4: FN<4>(__VA_ARGS__); break;            \
+    case 7: FN<7>(__VA_ARGS__); break;            \
+    case 10: FN<10>(__VA_ARGS__); break;          \
+    default: return hipErrorInvalidValue;         \
+  }
+
+template <int NP, int FD>
+static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
+  // variant (A/B tuning, scripts/bench_kernels.py): 0 unroll-4 pairs (default),
+  // 1 unroll-4 + folded exponent, 2 unroll-8, 3 unroll-3 (GP fast paths only)
+  if (a.fast_obs == OBS_DN16) {
+    if (FD > 0 && a.variant == 1)
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 4, true>), dim3(grid), dim3(BLOCK), 0, s, a);
+    else if (FD > 0 && a.variant == 2)
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 8>), dim3(grid), dim3(BLOCK), 0, s, a);
+    else if (FD > 0 && a.variant == 3)
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 3>), dim3(grid), dim3(BLOCK), 0, s, a);
+    else
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
+  } else if (a.fast_obs == OBS_F32) {
+    hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_F32>), dim3(grid), dim3(BLOCK), 0, s, a);
+  } else if constexpr (FD <= 0) {
+    // bf16 (y, w) observations: precomputed / linear operators only
+    if (a.fast_obs != OBS_BF16) return false;
+    hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_BF16>), dim3(grid), dim3(BLOCK), 0, s, a);
+  } else {
+    return false;
+  }
+  return true;
+}
+
+// Fast-path instantiations: JRC-TIP (7 params, 4-input band GPs), PROSAIL
+// (10 params, full-state GPs) and full-state GPs for small states.
+template <int NP>
+static void l_analysis(const AnalysisArgs& a, int grid, hipStream_t s) {
+  bool done = false;
+  if (a.fast_d > 0) {
+    if constexpr (NP == 7) {
+      if (a.fast_d == 4) done = l_analysis_fast<7, 4>(a, grid, s);
+      else if (a.fast_d == 7) done = l_analysis_fast<7, 7>(a, grid, s);
+    } else if constexpr (NP == 10) {
+      if (a.fast_d == 10) done = l_analysis_fast<10, 10>(a, grid, s);
+    } else if constexpr (NP <= 4) {
+      if (a.fast_d == NP) done = l_analysis_fast<NP, NP>(a, grid, s);
+    }
+  }
+  else if (a.fast_d == FD_PRECOMP) {
+    done = l_analysis_fast<NP, FD_PRECOMP>(a, grid, s);
+  } else if (a.fast_d == FD_LINEAR) {
+    done = l_analysis_fast<NP, FD_LINEAR>(a, grid, s);
+  }
+  if (!done) hipLaunchKernelGGL(analysis_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
+}
+}  // namespace kf

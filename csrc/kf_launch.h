@@ -1,4 +1,5 @@
-// kf_launch.h — launcher entry points (device: kf_kernels.hip, host: kf_host.cpp).
+// kf_launch.h — launcher entry points (device: kf_kernels.hip + kf_analysis{7,10}.hip,
+// host: kf_host.cpp).
 #pragma once
 #include <stdint.h>
 #include "kf_core.h"
@@ -20,6 +21,8 @@ void set_max_blocks(int n);
 void set_gp_unroll(int n);
 int get_max_blocks();
 hipError_t dev_analysis(int np, const AnalysisArgs& a, int grid, hipStream_t s);
+hipError_t dev_analysis_np7(const AnalysisArgs& a, int grid, hipStream_t s);
+hipError_t dev_analysis_np10(const AnalysisArgs& a, int grid, hipStream_t s);
 hipError_t dev_gain(int np, const GainArgs& a, int grid, hipStream_t s);
 hipError_t dev_jacobi(int np, const JacobiArgs& a, int grid, hipStream_t s);
 hipError_t dev_propagate(int np, const PropArgs& a, hipStream_t s);

@@ -27,7 +27,10 @@ ARCH = os.environ.get("KAFKA_OFFLOAD_ARCH", "gfx950")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 EXT_PATH = PKG_DIR / f"_kafka_hip{EXT_SUFFIX}"
 
-HEADERS = ["kf_core.h", "kf_launch.h", "kf_stream.h"]
+HEADERS = ["kf_core.h", "kf_launch.h", "kf_stream.h", "kf_device.h"]
+# device translation units (compiled concurrently: the NP = 7 / 10 analysis
+# instantiations dominate the build)
+HIP_SOURCES = ["kf_kernels.hip", "kf_analysis7.hip", "kf_analysis10.hip"]
 
 
 def _pybind_includes() -> list[str]:
@@ -60,34 +63,43 @@ def _run(cmd: list[str], verbose: bool) -> None:
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
+    from concurrent.futures import ThreadPoolExecutor
+
     BUILD.mkdir(parents=True, exist_ok=True)
     hdrs = [CSRC / h for h in HEADERS]
     common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}"]
     hip_defs = ["-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}"]
     hipcc = _hipcc()
-    objs = []
+    jobs, objs = [], []
 
-    # 1. device kernels (gfx950 code objects embedded in the host object)
-    src, obj = CSRC / "kf_kernels.hip", BUILD / "kf_kernels.o"
-    if force or _stale(obj, [src] + hdrs):
-        _run([hipcc, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics", "-c", str(src), "-o", str(obj)],
-             verbose)
-    objs.append(obj)
+    # 1. device kernels (gfx950 code objects embedded in the host objects)
+    for name in HIP_SOURCES:
+        src, obj = CSRC / name, BUILD / (Path(name).stem + ".o")
+        if force or _stale(obj, [src] + hdrs):
+            jobs.append([hipcc, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics", "-c", str(src), "-o",
+                         str(obj)])
+        objs.append(obj)
 
     # 2. host runner of the same per-pixel code (g++, OpenMP)
     src, obj = CSRC / "kf_host.cpp", BUILD / "kf_host.o"
     if force or _stale(obj, [src] + hdrs):
-        _run(["g++", *common, *hip_defs, "-fopenmp", "-mavx2", "-mfma", "-ffp-contract=fast", "-c", str(src),
-              "-o", str(obj)], verbose)
+        jobs.append(["g++", *common, *hip_defs, "-fopenmp", "-mavx2", "-mfma", "-ffp-contract=fast", "-c", str(src),
+                     "-o", str(obj)])
     objs.append(obj)
 
     # 3. bindings + ingest runtime (host code, HIP runtime API)
     for name in ("kf_bindings.cpp", "kf_stream.cpp"):
         src, obj = CSRC / name, BUILD / (Path(name).stem + ".o")
         if force or _stale(obj, [src] + hdrs):
-            _run(["g++", *common, *hip_defs, *_pybind_includes(), "-fvisibility=hidden", "-c", str(src), "-o",
-                  str(obj)], verbose)
+            jobs.append(["g++", *common, *hip_defs, *_pybind_includes(), "-fvisibility=hidden", "-c", str(src),
+                         "-o", str(obj)])
         objs.append(obj)
+
+    if jobs:
+        workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+        with ThreadPoolExecutor(workers) as pool:
+            for f in [pool.submit(_run, cmd, verbose) for cmd in jobs]:
+                f.result()
 
     if force or _stale(EXT_PATH, objs):
         _run([hipcc, "-shared", "-fPIC", *map(str, objs), "-o", str(EXT_PATH), "-lgomp", "-lpthread",

@@ -93,10 +93,12 @@ class BandTable:
 
 
 OP_PRECOMP = 0
+OP_LINEAR = 1
 OP_GP = 2
 
 
 FD_PRECOMP = -1   # kf_core.h: fast analysis kernel for all-precomputed operators
+FD_LINEAR = -2    # kf_core.h: fast analysis kernel for all-linear (identity/selection) operators
 # analysis fast-kernel variant (kf_kernels.hip:l_analysis_fast); env override for A/B runs
 DEFAULT_VARIANT = int(os.environ.get("KAFKA_ANALYSIS_VARIANT", "0"))
 
@@ -119,13 +121,15 @@ def make_band_table(descs: list, device, keepalive=()) -> BandTable:
     buf = small_h2d(cpu, device)
     fast_d = fast_obs = 0
     obs = {d.obs for d in descs}
-    uniform_obs = len(obs) == 1 and next(iter(obs)) in (OBS_F32, OBS_DN16)
+    one_obs = next(iter(obs)) if len(obs) == 1 else None
     if descs and all(d.op == OP_GP for d in descs):
         ds = {d.d for d in descs}
-        if len(ds) == 1 and uniform_obs:
-            fast_d, fast_obs = next(iter(ds)), next(iter(obs))
-    elif descs and uniform_obs and all(d.op == OP_PRECOMP for d in descs):
-        fast_d, fast_obs = FD_PRECOMP, next(iter(obs))
+        if len(ds) == 1 and one_obs in (OBS_F32, OBS_DN16):
+            fast_d, fast_obs = next(iter(ds)), one_obs
+    elif descs and one_obs in (OBS_F32, OBS_DN16, OBS_BF16) and all(d.op == OP_PRECOMP for d in descs):
+        fast_d, fast_obs = FD_PRECOMP, one_obs
+    elif descs and one_obs in (OBS_F32, OBS_DN16, OBS_BF16) and all(d.op == OP_LINEAR for d in descs):
+        fast_d, fast_obs = FD_LINEAR, one_obs
     return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs)
 
 

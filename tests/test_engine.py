@@ -253,3 +253,27 @@ def test_structured_metrics_and_summary(tmp_path):
     summary = json.load(open(tmp_path / "m.summary.json"))
     assert summary["n_pixels"] == kf.n_total and summary["pixel_updates_per_s"] > 0
     assert len(summary["ranks"]) == 1 and summary["ranks"][0]["n_dates"] == len(dates)
+
+
+def test_identity_operator_engine_matches_oracle():
+    """BASELINE config 2 semantics: 7 direct (identity) observations of the TIP
+    state, bf16 (y, w) ingest, LAI propagator — engine (host runner) vs the
+    float64 oracle driving the reference-API linear operator factory."""
+    mask = np.ones((16, 12), bool)
+    mask[:2, :3] = False
+    obs = k.SyntheticIdentityObservations(mask, device="cpu", stream=False, n_pool=4, field_cell=8)
+    prior = k.JRCPrior(k.TIP_PARAMETERS, mask)
+    x0, Pinv = prior.process_prior(None)
+    Q = np.zeros_like(x0)
+    Q[6::7] = 0.04
+    grid = _grid(4)
+    kf = k.LinearKalman(obs, None, mask, k.create_linear_observation_operator, k.TIP_PARAMETERS,
+                        state_propagation=k.propagate_information_filter_LAI, device="cpu")
+    kf.set_trajectory_model()
+    kf.set_trajectory_uncertainty(Q)
+    st = kf.run(grid, x0, None, Pinv)
+    xr, Pr, iters = oracle_run(obs, mask, k.create_linear_observation_operator, 7, grid, x0, Pinv,
+                               propagator=k.propagate_information_filter_LAI, Q=Q)
+    _compare(st, xr, Pr)
+    # several observation dates per 16-day step (the source observes every 5 days)
+    assert [n for r in kf.history for n in r.get("gn_iterations", [])] == iters

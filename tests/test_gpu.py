@@ -229,3 +229,20 @@ def test_fused_output_gpu(cuda):
 def test_affine_jacobi_equals_classic_gpu(cuda, regmask):
     from test_kernels import affine_vs_classic_jacobi
     affine_vs_classic_jacobi(cuda, regmask=regmask)
+
+
+def test_identity_linear_fast_path_gpu_matches_cpu(cuda):
+    """The all-linear bf16 analysis kernel (FD_LINEAR, OBS_BF16) on the device
+    vs the generic host runner."""
+    mask = np.ones((40, 36), bool)
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(4)]
+    outs = []
+    for dev in (cuda, "cpu"):
+        obs = k.SyntheticIdentityObservations(mask, device=dev, stream=False, n_pool=3, field_cell=8)
+        kf = k.LinearKalman(obs, None, mask, k.create_linear_observation_operator, k.TIP_PARAMETERS, device=dev,
+                            state_propagation=k.propagate_information_filter_LAI)
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
+        outs.append((st.x.cpu(), st.P.cpu(), [h.get("gn_iterations") for h in kf.history]))
+    assert outs[0][2] == outs[1][2]
+    assert close(outs[0][0], outs[1][0], 1e-4) and close(outs[0][1], outs[1][1], 1e-4, floor=1.0)
