@@ -1,6 +1,6 @@
 """Minimal GeoTIFF writer/reader (GDAL is not available in this stack).
 
-Writes single-band rasters (float32 / uint8 / uint16 / int16 / float64) as
+Writes single- or multi-band (planar, ``(bands, H, W)``) rasters (float32 / uint8 / uint16 / int16 / float64) as
 classic or BigTIFF, striped, uncompressed or DEFLATE (the reference writes
 DEFLATE/BIGTIFF/TILED Float32, ``observations.py:366-371``), with GeoTIFF
 georeferencing: ModelPixelScale (33550), ModelTiepoint (33922), a
@@ -27,25 +27,28 @@ _TFMT = {1: "B", 2: "c", 3: "H", 4: "I", 11: "f", 12: "d", 16: "Q"}
 def write_tiff(path, array, geotransform=None, projection: str | None = None, compress: str | None = "deflate",
                rows_per_strip: int = 64, bigtiff: bool | None = None, nodata=None):
     a = np.ascontiguousarray(np.asarray(array))
-    if a.ndim != 2:
-        raise ValueError("write_tiff writes single-band 2-D rasters")
+    if a.ndim not in (2, 3):
+        raise ValueError("write_tiff writes 2-D rasters or (bands, H, W) stacks")
     if a.dtype == np.bool_:
         a = a.astype(np.uint8)
     if a.dtype not in _DT:
         raise TypeError(f"unsupported dtype {a.dtype}")
     fmt_code, bits = _DT[a.dtype]
     a = a.astype(a.dtype.newbyteorder("<"), copy=False)
-    H, W = a.shape
+    planes = a[None] if a.ndim == 2 else a
+    nb, H, W = planes.shape
     rps = max(1, min(rows_per_strip, H))
     strips = []
-    for r in range(0, H, rps):
-        raw = a[r:r + rps].tobytes()
-        strips.append(zlib.compress(raw, 6) if compress == "deflate" else raw)
+    for plane in planes:     # PlanarConfiguration 2: all strips of band 0, then band 1, ...
+        for r in range(0, H, rps):
+            raw = plane[r:r + rps].tobytes()
+            strips.append(zlib.compress(raw, 6) if compress == "deflate" else raw)
     total = sum(len(s) for s in strips)
     if bigtiff is None:
         bigtiff = total > 3_500_000_000
-    tags = [(256, LONG, [W]), (257, LONG, [H]), (258, SHORT, [bits]), (259, SHORT, [8 if compress == "deflate" else 1]),
-            (262, SHORT, [1]), (277, SHORT, [1]), (278, LONG, [rps]), (284, SHORT, [1]), (339, SHORT, [fmt_code])]
+    tags = [(256, LONG, [W]), (257, LONG, [H]), (258, SHORT, [bits] * nb),
+            (259, SHORT, [8 if compress == "deflate" else 1]), (262, SHORT, [1]), (277, SHORT, [nb]),
+            (278, LONG, [rps]), (284, SHORT, [2 if nb > 1 else 1]), (339, SHORT, [fmt_code] * nb)]
     if geotransform is not None:
         gt = [float(v) for v in geotransform]
         tags.append((33550, DOUBLE, [gt[1], -gt[5], 0.0]))
@@ -150,8 +153,16 @@ def read_tiff(path):
         elif comp != 1:
             raise ValueError(f"unsupported TIFF compression {comp}")
         out += chunk
-    arr = np.frombuffer(bytes(out[:W * H * dtype.itemsize]), dtype=dtype).reshape(H, W)
-    info = {"shape": (H, W)}
+    nb = tags.get(277, [1])[0]
+    planar = tags.get(284, [1])[0]
+    arr = np.frombuffer(bytes(out[:nb * W * H * dtype.itemsize]), dtype=dtype)
+    if nb == 1:
+        arr = arr.reshape(H, W)
+    elif planar == 2:
+        arr = arr.reshape(nb, H, W)
+    else:                    # chunky (pixel-interleaved) -> (bands, H, W)
+        arr = arr.reshape(H, W, nb).transpose(2, 0, 1).copy()
+    info = {"shape": (H, W), "bands": nb}
     if 33550 in tags and 33922 in tags:
         sx, sy = tags[33550][0], tags[33550][1]
         tp = tags[33922]

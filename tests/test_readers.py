@@ -132,3 +132,104 @@ def test_ross_li_kernels_nadir():
     assert np.isclose(k0, 1.0)
     assert np.isclose(kv, -np.pi / 4 + np.pi / 4, atol=1e-12) or np.isfinite(kv)
     assert np.isfinite(kg)
+
+
+# ---------------------------------------------------------------- footprints
+REF_TIF = "/root/reference/Barrax_pivots.tif"
+REF_JSON = "/root/reference/Barrax_pivots.json"
+
+
+def test_utm_roundtrip_and_crs_parsing():
+    from kafka_inferenceengine_amd.input_output import geo
+    lon, lat = np.array([-2.1, -3.0, 0.5]), np.array([39.05, 41.2, 38.0])
+    e, n = geo.lonlat_to_utm(lon, lat, 30)
+    lo2, la2 = geo.utm_to_lonlat(e, n, 30)
+    assert np.allclose(lo2, lon, atol=1e-8) and np.allclose(la2, lat, atol=1e-8)
+    # central meridian of zone 30 is -3 deg: easting 500 km exactly, northing = k0 * meridian arc
+    e0, _ = geo.lonlat_to_utm(-3.0, 40.0, 30)
+    assert abs(e0 - 500000.0) < 1e-6
+    assert geo.parse_crs("urn:ogc:def:crs:EPSG::32630") == geo.CRS("utm", 30, True)
+    assert geo.parse_crs("WGS 84 / UTM zone 30N|WGS 84") == geo.CRS("utm", 30, True)
+    assert geo.parse_crs(32731) == geo.CRS("utm", 31, False)
+    assert geo.parse_crs("EPSG:4326") == geo.WGS84
+
+
+def test_rasterized_pivots_reproduce_reference_mask():
+    """The drivers' cutline mask: the 5 pivot polygons of Barrax_pivots.json
+    rasterised on the grid of Barrax_pivots.tif give exactly its 13,027 pixels."""
+    if not (os.path.exists(REF_TIF) and os.path.exists(REF_JSON)):
+        return
+    m, info = k.read_tiff(REF_TIF)
+    polys = k.read_geojson_polygons(REF_JSON)
+    assert len(polys) == 5
+    r = k.rasterize_polygons(polys, info["geotransform"], info["shape"], info["projection"])
+    assert np.array_equal(r, m > 0)
+
+
+def test_raster_extent_feature_and_overlap(tmp_path):
+    if not (os.path.exists(REF_TIF) and os.path.exists(REF_JSON)):
+        return
+    ext = k.raster_extent_feature(REF_TIF)
+    x0, y0, x1, y1 = ext.bounds()
+    assert -2.12 < x0 < x1 < -2.08 and 39.04 < y0 < y1 < 39.07       # Barrax, Spain
+    assert all(k.find_overlap_raster_feature(REF_TIF, p) for p in k.read_geojson_polygons(REF_JSON))
+    assert not k.find_overlap_raster_feature(REF_TIF, k.Polygon([[0, 0], [1, 0], [1, 1], [0, 1]], 4326))
+    # a polygon containing the whole raster (no edge crossings) still intersects
+    big = k.Polygon([[-3, 38], [-1, 38], [-1, 40], [-3, 40]], "EPSG:4326")
+    assert k.find_overlap_raster_feature(REF_TIF, big)
+
+
+# ---------------------------------------------------------------- MODIS
+def test_mod09_reader_npz(tmp_path):
+    rng = np.random.default_rng(3)
+    f = tmp_path / "MOD09GA.A2017001.h17v05.npz"
+    sds = {f"sur_refl_b0{b}_1": rng.integers(0, 5000, (8, 8)).astype(np.int16) for b in range(1, 8)}
+    qa = np.full((4, 4), 8, np.uint16)
+    qa[0, 0] = 9                                      # not in the QA whitelist
+    sds.update(state_1km_1=qa, SolarZenith_1=np.full((4, 4), 3000), SolarAzimuth_1=np.full((4, 4), 1000),
+               SensorZenith_1=np.full((4, 4), 1500), SensorAzimuth_1=np.full((4, 4), 4000))
+    np.savez(f, **sds)
+    d = dt.datetime(2017, 1, 1)
+    obs = k.MOD09_ObservationsKernels([d], [str(f)])
+    r = obs.get_band_data(d, 2)
+    assert np.allclose(r.reflectance, sds["sur_refl_b02_1"] / 1e4)
+    assert r.mask.shape == (8, 8) and not r.mask[:2, :2].any() and r.mask[2:, :].all()
+    assert np.allclose(r.uncertainty, 0.015) and np.allclose(r.raa, 30.0) and np.allclose(r.sza, 30.0)
+    _, kv, kg = S.ross_li_kernels(15.0, 30.0, 30.0)
+    assert np.allclose(r.obs_op.Ross, kv) and np.allclose(r.obs_op.Li, kg)
+    # kernels are reciprocal in (sza, vza) and vanish at nadir/nadir
+    _, kv2, kg2 = S.ross_li_kernels(30.0, 15.0, 30.0)
+    assert np.isclose(kv, kv2) and np.isclose(kg, kg2)
+    _, kv0, kg0 = S.ross_li_kernels(0.0, 0.0, 0.0)
+    assert abs(kv0) < 1e-12 and abs(kg0) < 1e-12
+    assert obs.get_band_data(dt.datetime(2018, 1, 1), 1) is None
+    with np.testing.assert_raises(IOError):
+        k.MOD09_ObservationsKernels([d], ["x.hdf"]).get_band_data(d, 1)
+
+
+def test_synergy_kernels_broadband(tmp_path):
+    from kafka_inferenceengine_amd.input_output import modis as M
+    shape = (5, 4)
+    rng = np.random.default_rng(4)
+    K = {}
+    for day in (10, 40):
+        stem = tmp_path / f"Synergy.A2017{day:03d}.h17v05"
+        for b in range(7):
+            K[(day, b)] = rng.uniform(0.0, 0.3, (3, *shape)).astype(np.float32)
+            k.write_tiff(f"{stem}_b{b}_kernel_weights.tif", K[(day, b)])
+        m = np.ones(shape, np.uint8)
+        m[0, 0] = 0
+        k.write_tiff(f"{stem}mask.tif", m)
+    start = dt.datetime(2017, 1, 5)
+    obs = k.SynergyKernels(str(tmp_path), "h17v05", start)
+    assert sorted(obs.dates) == [dt.datetime(2017, 1, 10), dt.datetime(2017, 2, 9)]
+    assert k.SynergyKernels(str(tmp_path), "h17v05", start, reference_quirks=True).dates == []
+    d = dt.datetime(2017, 1, 10)
+    for band, (coef, off) in enumerate(((M.TO_VIS, M.A_TO_VIS), (M.TO_NIR, M.A_TO_NIR))):
+        r = obs.get_band_data(d, band)
+        bhr = np.array([np.tensordot(M.TO_BHR, K[(10, b)].astype(np.float64), 1) for b in range(7)])
+        want = np.tensordot(coef, bhr, 1) + off
+        assert not r.mask[0, 0] and r.mask.sum() == shape[0] * shape[1] - 1
+        assert np.allclose(r.observations[r.mask], want[r.mask])
+        w = r.uncertainty.diagonal().reshape(shape)
+        assert w[0, 0] == 0 and np.allclose(w[1:, 1:], 1 / np.maximum(2.5e-3, 0.05 * np.abs(want[1:, 1:])) ** 2)
