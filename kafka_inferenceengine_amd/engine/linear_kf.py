@@ -150,6 +150,12 @@ class LinearKalman:
     def _plotter_iteration_end(self, plot_obj, x, P, innovation, mask):
         pass
 
+    def _get_observations_timestep(self, timestep, band=None):
+        """Override point (reference ``linear_kf.py:148-169``, unused by ``run``):
+        ``(observations, uncertainty, mask, metadata, emulator)`` of one band."""
+        data = self.observations.get_band_data(timestep, band)
+        return data.observations, data.uncertainty, data.mask, data.metadata, data.emulator
+
     # ------------------------------------------------------ conversion
     def initial_state(self, x_forecast, P_forecast=None, P_forecast_inverse=None) -> KFState:
         """Reference inputs (interleaved x over ALL active pixels, block-diagonal
