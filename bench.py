@@ -190,7 +190,11 @@ def main():
                                                           torch.profiler.ProfilerActivity.CUDA])
                 prof.__enter__()
         t0 = time.perf_counter()
-        state = kf.step(t, loc, state, advance=not first, all_dates=dates)
+        # the next step's first GN iteration may be queued inside this one
+        # (EngineConfig.speculate) -- never across the timed-region boundaries
+        j = i + 1
+        nxt = steps[j][:2] if (j < a.warmup + a.steps and j != a.warmup) else None
+        state = kf.step(t, loc, state, advance=not first, all_dates=dates, next_step=nxt)
         first = False
         if dev.type == "cuda" and i < a.warmup:
             torch.cuda.synchronize()

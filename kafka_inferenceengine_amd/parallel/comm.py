@@ -32,12 +32,24 @@ class PendingSum:
     """Deferred C1 result (``Comm.sum_f64_async``)."""
 
     def __init__(self, vals: torch.Tensor, n: int):
-        self.vals = vals
         self.n = n
+        self.event = None
+        if vals.is_cuda:
+            # async copy into pinned memory + an event: result() waits for THIS
+            # value only, not for work queued on the stream after it (the next
+            # step's speculatively queued iteration)
+            self.vals = torch.empty(vals.shape, dtype=vals.dtype, pin_memory=True)
+            self.vals.copy_(vals, non_blocking=True)
+            self.event = torch.cuda.Event()
+            self.event.record(torch.cuda.current_stream(vals.device))
+        else:
+            self.vals = vals
 
     def result(self) -> float:
+        if self.event is not None:
+            self.event.synchronize()
         total = 0.0
-        for v in self.vals.cpu().tolist():  # fixed rank order
+        for v in self.vals.tolist():  # fixed rank order
             total += v
         return total
 
@@ -118,8 +130,8 @@ class Comm:
     def sum_f64_async(self, local: torch.Tensor) -> "PendingSum":
         """C1 without a host wait: the all-gather is queued on the stream (RCCL)
         and ``.result()`` reads the rank values and sums them in rank order.
-        ``local`` must not be overwritten before ``result()`` (it is gathered
-        from the device later on a single rank)."""
+        The values are copied to pinned host memory in stream order right away,
+        so ``local`` may be overwritten by later queued work."""
         if not self.distributed:
             return PendingSum(local.reshape(1), 1)
         local = local.reshape(1).to(torch.float64)

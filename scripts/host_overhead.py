@@ -43,15 +43,15 @@ def run(sl):
 
 
 run(steps[:3])
-torch.cuda.synchronize()
+torch.cuda.synchronize() if dev.type == "cuda" else None
 t0 = time.perf_counter()
 run(steps[3:3 + a0.steps])
-torch.cuda.synchronize()
+torch.cuda.synchronize() if dev.type == "cuda" else None
 print(f"host+device ms/step at {a0.size}^2: {(time.perf_counter() - t0) * 1e3 / a0.steps:.3f}")
 prof = cProfile.Profile()
 prof.enable()
 run(steps[3 + a0.steps:3 + 2 * a0.steps])
-torch.cuda.synchronize()
+torch.cuda.synchronize() if dev.type == "cuda" else None
 prof.disable()
 st = pstats.Stats(prof)
 st.sort_stats("cumulative").print_stats(45)

@@ -277,3 +277,30 @@ def test_identity_operator_engine_matches_oracle():
     _compare(st, xr, Pr)
     # several observation dates per 16-day step (the source observes every 5 days)
     assert [n for r in kf.history for n in r.get("gn_iterations", [])] == iters
+
+
+@pytest.mark.parametrize("tol", [1e-3, 1e-9])
+def test_speculative_next_step_equals_sequential(tol):
+    """EngineConfig.speculate: the next step's first GN iteration queued before
+    the convergence read-back gives the same run; with a tolerance that forces
+    extra iterations the queued iteration is dropped (and the predictor stops
+    queueing)."""
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=7)
+    grid = _grid(6)
+    res = []
+    for spec in (False, True):
+        out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
+        kf = _engine(mask, obs, Q, out=out, speculate=spec, convergence_tolerance=tol, max_iterations=4)
+        st = kf.run(grid, x0, None, Pinv)
+        res.append((st, out, [h["gn_iterations"] for h in kf.history], [h["norms"] for h in kf.history],
+                    dict(kf.spec_stats)))
+    (a, oa, ia, na, sa), (b, ob, ib, nb, sb) = res
+    assert ia == ib and na == nb
+    assert torch.equal(a.x, b.x) and torch.equal(a.P, b.P)
+    for t in oa.history:
+        assert torch.equal(oa.history[t][0], ob.history[t][0])
+    assert sa == {"queued": 0, "adopted": 0}
+    if tol == 1e-3:
+        assert sb["queued"] >= sb["adopted"] >= len(grid) - 3
+    else:
+        assert sb["adopted"] == 0 and sb["queued"] <= 1
