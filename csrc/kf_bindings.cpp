@@ -44,7 +44,10 @@ static std::vector<A> get_arr(const A (&src)[N]) { return std::vector<A>(src, sr
   def_property(#name, [](const cls& s) { return get_arr(s.name); },                                \
                [](cls& s, const std::vector<T>& v) { set_arr(s.name, v, #name); })
 
-PYBIND11_MODULE(_kafka_hip, m) {
+#ifndef KF_MODULE_NAME
+#define KF_MODULE_NAME _kafka_hip
+#endif
+PYBIND11_MODULE(KF_MODULE_NAME, m) {
   m.doc() = "KaFKA MI355X kernels (gfx950) + host runner of the same per-pixel code";
   m.attr("MAX_D") = MAX_D;
   m.attr("MAX_BLOCKS") = KF_MAX_BLOCKS;

@@ -26,6 +26,35 @@
 #define KF_HD inline __attribute__((always_inline))
 #endif
 
+// KF_CHECKED (debug build, `_build.py --checked` -> module _kafka_hip_checked,
+// selected with KAFKA_CHECKED=1): index assertions on the gather / scatter /
+// neighbour paths (SURVEY.md §5.2 "explicit bounds assertions in the debug
+// build").  A failed check prints the condition and traps (device) or aborts
+// (host runner); the release build compiles them away.
+#ifdef KF_CHECKED
+#include <stdio.h>
+#include <stdlib.h>
+#if defined(__HIPCC__)
+#define KF_DCHECK(c)                                                          \
+  do {                                                                        \
+    if (!(c)) {                                                               \
+      printf("KF_DCHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c);        \
+      __builtin_trap();                                                       \
+    }                                                                         \
+  } while (0)
+#else
+#define KF_DCHECK(c)                                                          \
+  do {                                                                        \
+    if (!(c)) {                                                               \
+      fprintf(stderr, "KF_DCHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      abort();                                                                \
+    }                                                                         \
+  } while (0)
+#endif
+#else
+#define KF_DCHECK(c) ((void)0)
+#endif
+
 namespace kf {
 
 constexpr int MAX_D = 16;         // max mapped inputs per band / max state size
@@ -1037,7 +1066,9 @@ struct JacobiArgs {
 
 template <typename JA>
 KF_HD int32_t jacobi_neighbour(const JA& a, int64_t p, int k) {
-  return a.geo.w > 0 ? geo_neighbour(a.geo, a.N, p, k) : a.nbr[k * a.N + p];
+  const int32_t q = a.geo.w > 0 ? geo_neighbour(a.geo, a.N, p, k) : a.nbr[k * a.N + p];
+  KF_DCHECK(q >= -1 && q < a.ld_ext);
+  return q;
 }
 
 constexpr int JACOBI_CLASSIC = 0, JACOBI_PREPARE = 1, JACOBI_SWEEP = 2, JACOBI_FINISH = 3;

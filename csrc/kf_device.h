@@ -173,6 +173,7 @@ __global__ __launch_bounds__(BLOCK) void unpack_kernel(const float* x, const flo
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < N; p += stride) {
     const int64_t r = idx ? idx[p] : p;
+    KF_DCHECK(r >= 0 && r < plane);
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
       if (mean) mean[j * plane + r] = x[j * ld + p];
@@ -187,6 +188,7 @@ __global__ __launch_bounds__(BLOCK) void gather_kernel(const T* src, const int64
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < n; p += stride) {
     const int64_t s = idx[p];
+    KF_DCHECK(s >= 0 && s < src_ld);
     for (int r = 0; r < rows; ++r) dst[r * dst_ld + p] = src[r * src_ld + s];
   }
 }

@@ -6,7 +6,12 @@ file so it travels with the repository snapshot to the GPU box.  No hipify,
 no JIT cache: the object files live under ``build/`` and are rebuilt only
 when a source is newer.
 
-Usage: ``python -m kafka_inferenceengine_amd._build [--force] [--verbose]``.
+Usage: ``python -m kafka_inferenceengine_amd._build [--force] [--verbose] [--checked]``.
+
+``--checked`` builds the debug variant ``_kafka_hip_checked`` (``-DKF_CHECKED``:
+device/host index assertions, csrc/kf_core.h ``KF_DCHECK``) into its own build
+directory; ``KAFKA_CHECKED=1`` makes ``ops/_ext.py`` load it instead of the release
+module.
 """
 from __future__ import annotations
 
@@ -26,6 +31,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("KAFKA_OFFLOAD_ARCH", "gfx950")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 EXT_PATH = PKG_DIR / f"_kafka_hip{EXT_SUFFIX}"
+CHECKED_EXT_PATH = PKG_DIR / f"_kafka_hip_checked{EXT_SUFFIX}"
 
 HEADERS = ["kf_core.h", "kf_launch.h", "kf_stream.h", "kf_device.h"]
 # device translation units (compiled concurrently: the NP = 7 / 10 analysis
@@ -62,26 +68,30 @@ def _run(cmd: list[str], verbose: bool) -> None:
         raise RuntimeError(f"build step failed ({r.returncode}): {' '.join(cmd)}\n{msg[-8000:]}")
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
+def build(force: bool = False, verbose: bool = False, checked: bool = False) -> Path:
     from concurrent.futures import ThreadPoolExecutor
 
-    BUILD.mkdir(parents=True, exist_ok=True)
+    build_dir = BUILD.with_name("kafka_hip_checked") if checked else BUILD
+    ext_path = CHECKED_EXT_PATH if checked else EXT_PATH
+    build_dir.mkdir(parents=True, exist_ok=True)
     hdrs = [CSRC / h for h in HEADERS]
     common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}"]
+    if checked:
+        common += ["-DKF_CHECKED", "-DKF_MODULE_NAME=_kafka_hip_checked"]
     hip_defs = ["-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}"]
     hipcc = _hipcc()
     jobs, objs = [], []
 
     # 1. device kernels (gfx950 code objects embedded in the host objects)
     for name in HIP_SOURCES:
-        src, obj = CSRC / name, BUILD / (Path(name).stem + ".o")
+        src, obj = CSRC / name, build_dir / (Path(name).stem + ".o")
         if force or _stale(obj, [src] + hdrs):
             jobs.append([hipcc, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics", "-c", str(src), "-o",
                          str(obj)])
         objs.append(obj)
 
     # 2. host runner of the same per-pixel code (g++, OpenMP)
-    src, obj = CSRC / "kf_host.cpp", BUILD / "kf_host.o"
+    src, obj = CSRC / "kf_host.cpp", build_dir / "kf_host.o"
     if force or _stale(obj, [src] + hdrs):
         jobs.append(["g++", *common, *hip_defs, "-fopenmp", "-mavx2", "-mfma", "-ffp-contract=fast", "-c", str(src),
                      "-o", str(obj)])
@@ -89,7 +99,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
 
     # 3. bindings + ingest runtime (host code, HIP runtime API)
     for name in ("kf_bindings.cpp", "kf_stream.cpp"):
-        src, obj = CSRC / name, BUILD / (Path(name).stem + ".o")
+        src, obj = CSRC / name, build_dir / (Path(name).stem + ".o")
         if force or _stale(obj, [src] + hdrs):
             jobs.append(["g++", *common, *hip_defs, *_pybind_includes(), "-fvisibility=hidden", "-c", str(src),
                          "-o", str(obj)])
@@ -101,18 +111,19 @@ def build(force: bool = False, verbose: bool = False) -> Path:
             for f in [pool.submit(_run, cmd, verbose) for cmd in jobs]:
                 f.result()
 
-    if force or _stale(EXT_PATH, objs):
-        _run([hipcc, "-shared", "-fPIC", *map(str, objs), "-o", str(EXT_PATH), "-lgomp", "-lpthread",
+    if force or _stale(ext_path, objs):
+        _run([hipcc, "-shared", "-fPIC", *map(str, objs), "-o", str(ext_path), "-lgomp", "-lpthread",
               f"-L{ROCM / 'lib'}", "-lamdhip64"], verbose)
-    return EXT_PATH
+    return ext_path
 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--checked", action="store_true", help="debug build with index assertions")
     a = ap.parse_args()
-    p = build(force=a.force, verbose=a.verbose)
+    p = build(force=a.force, verbose=a.verbose, checked=a.checked)
     print(f"built {p}")
 
 

@@ -13,8 +13,12 @@ import os
 import torch  # noqa: F401  (must precede the extension import)
 
 _err = None
+CHECKED = os.environ.get("KAFKA_CHECKED", "0") not in ("", "0")
 try:
-    from .. import _kafka_hip as ext  # type: ignore
+    if CHECKED:  # debug build with index assertions (_build.py --checked)
+        from .. import _kafka_hip_checked as ext  # type: ignore
+    else:
+        from .. import _kafka_hip as ext  # type: ignore
 except ImportError as e:  # pragma: no cover - exercised only when unbuilt
     ext = None
     _err = e
@@ -53,10 +57,10 @@ def ensure_built(verbose: bool = False):
         return ext
     from .. import _build
 
-    _build.build(verbose=verbose)
+    _build.build(verbose=verbose, checked=CHECKED)
     import importlib
 
-    ext = importlib.import_module("kafka_inferenceengine_amd._kafka_hip")
+    ext = importlib.import_module("kafka_inferenceengine_amd._kafka_hip" + ("_checked" if CHECKED else ""))
     _err = None
     _apply_env(ext)
     return ext

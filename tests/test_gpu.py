@@ -246,3 +246,23 @@ def test_identity_linear_fast_path_gpu_matches_cpu(cuda):
         outs.append((st.x.cpu(), st.P.cpu(), [h.get("gn_iterations") for h in kf.history]))
     assert outs[0][2] == outs[1][2]
     assert close(outs[0][0], outs[1][0], 1e-4) and close(outs[0][1], outs[1][1], 1e-4, floor=1.0)
+
+
+def test_checked_build_smoke_on_device(cuda):
+    """The debug variant (KF_CHECKED index assertions in the gfx950 kernels) runs the
+    smoke step on the GPU without a failed check."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from kafka_inferenceengine_amd import _build
+
+    if not _build.CHECKED_EXT_PATH.exists():
+        pytest.skip("checked variant not built")
+    root = str(Path(__file__).resolve().parents[1])
+    env = dict(os.environ, KAFKA_CHECKED="1")
+    r = subprocess.run([sys.executable, "-c", "import __graft_entry__ as g; g.smoke()"], env=env, cwd=root,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "smoke ok" in r.stdout and "_kafka_hip_checked" in r.stdout, r.stdout[-2000:]

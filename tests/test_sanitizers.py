@@ -24,3 +24,53 @@ def test_host_runner_under_asan_ubsan(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert "sanitize_host ok" in r.stdout
+
+
+_CHECKED_SCRIPT = r"""
+import sys, numpy as np, torch
+from kafka_inferenceengine_amd.ops import _ext, kernels as K
+assert _ext.CHECKED and _ext.ext is not None and _ext.ext.__name__.endswith("_kafka_hip_checked")
+N, n = 16, 4
+rng = np.random.default_rng(0)
+L = rng.normal(size=(N, n, n)) * 0.1
+A = np.einsum("pij,pkj->pik", L, L) + np.eye(n)
+iu = np.triu_indices(n)
+a = torch.tensor(A[:, iu[0], iu[1]].T.copy(), dtype=torch.float32)
+b = torch.randn(n, N); x = torch.randn(n, N); out = torch.zeros(n, N)
+nbr = torch.full((4, N), -1, dtype=torch.int32)
+nbr[0, 1:] = torch.arange(N - 1, dtype=torch.int32)
+if sys.argv[1] == "bad":
+    nbr[1, 3] = N + 5          # neighbour index past x_ext
+K.jacobi(n, a, b, x, nbr, x, out, 2.0, 0b1111, N)
+assert torch.isfinite(out).all()
+print("ok")
+"""
+
+
+def test_checked_build_traps_out_of_range_neighbour(tmp_path):
+    """Debug build (``_build.py --checked``): KF_DCHECK index
+    assertions are live in the host runner of the same per-pixel code and abort
+    on an out-of-range neighbour; valid input runs unchanged."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    import pytest
+
+    from kafka_inferenceengine_amd import _build
+
+    if not _build.CHECKED_EXT_PATH.exists():
+        pytest.skip("checked variant not built (python -m kafka_inferenceengine_amd._build --checked)")
+    script = tmp_path / "checked.py"
+    script.write_text(_CHECKED_SCRIPT)
+    env = dict(os.environ, KAFKA_CHECKED="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    root = str(Path(__file__).resolve().parents[1])
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    good = subprocess.run([sys.executable, str(script), "good"], env=env, capture_output=True, text=True,
+                          timeout=300, cwd=root)
+    assert good.returncode == 0 and "ok" in good.stdout, good.stderr[-2000:]
+    bad = subprocess.run([sys.executable, str(script), "bad"], env=env, capture_output=True, text=True,
+                         timeout=300, cwd=root)
+    assert bad.returncode != 0
+    assert "KF_DCHECK failed" in bad.stderr and "ld_ext" in bad.stderr, bad.stderr[-2000:]
