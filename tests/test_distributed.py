@@ -94,6 +94,19 @@ def test_two_ranks_equal_one_rank(cfg):
     assert [len(a) for a in n1[0]] == [len(a) for a in n2[0]]
 
 
+def test_four_ranks_regularised_halo_equal_one_rank():
+    """Interior strips (ranks 1 and 2) exchange halos with BOTH neighbours, which
+    world_size 2 never exercises (C2 up and down in the same Jacobi sweep)."""
+    cfg = {"spatial_gamma": 30.0, "spatial_params": [6], "jacobi_sweeps": 5}
+    x1, P1, n1 = _gather(1, cfg)
+    x4, P4, n4 = _gather(4, cfg)
+    assert x1.shape == x4.shape
+    assert np.allclose(x1, x4, rtol=1e-5, atol=1e-6)
+    assert np.allclose(P1, P4, rtol=1e-5, atol=1e-3)
+    assert all(n == n4[0] for n in n4[1:])
+    assert [len(a) for a in n1[0]] == [len(a) for a in n4[0]]
+
+
 def test_strip_partition_balances_active_pixels():
     from kafka_inferenceengine_amd.parallel import StripPartition
     rng = np.random.default_rng(0)
