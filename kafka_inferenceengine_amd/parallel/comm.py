@@ -187,6 +187,18 @@ class Comm:
         boundary rows.  Empty tensors are skipped consistently on both sides."""
         if not self.distributed:
             return
+        dev = next((t for t in (send_up, send_down, recv_up, recv_down) if t is not None and t.numel()), None)
+        if dev is not None and dev.is_cuda and dist.get_backend(self.group) != "nccl":
+            # gloo P2P has no device-stream ordering (one-GPU rehearsals): stage
+            # through host memory so the sends see the finished pack kernels and
+            # the device sees the received rows in stream order.
+            h = [None if t is None else t.cpu() for t in (send_up, send_down)]
+            r = [None if t is None else torch.empty(t.shape, dtype=t.dtype) for t in (recv_up, recv_down)]
+            self.exchange_halo(h[0], h[1], r[0], r[1])
+            for dst, src in ((recv_up, r[0]), (recv_down, r[1])):
+                if dst is not None and dst.numel():
+                    dst.copy_(src)
+            return
         ops = []
         if self.rank > 0:
             if send_up is not None and send_up.numel():
