@@ -227,6 +227,9 @@ class Comm:
         """C3: gather variable-length pixel blocks [rows, n_i] onto rank 0."""
         if not self.distributed:
             return t
+        if t.is_cuda and dist.get_backend(self.group) != "nccl":  # gloo gather is host-only
+            out = self.gather_to_root(t.cpu(), sizes)
+            return None if out is None else out.to(t.device)
         rows = t.shape[0]
         maxn = max(sizes)
         pad = torch.zeros((rows, maxn), dtype=t.dtype, device=t.device)
