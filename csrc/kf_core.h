@@ -752,8 +752,32 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
 #pragma unroll
       for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = A[t];
     }
-    if (!chol_packed<NP>(A)) st |= ST_NONSPD;
+    const bool spd = chol_packed<NP>(A);
     chol_solve<NP>(A, b);
+    bool fin = true;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) fin = fin && finitef(b[j]);
+    // Health fallback (same rule as the plain path below): a non-SPD or
+    // non-finite pixel keeps its forecast and is decoupled (V = 0, so the
+    // sweeps give x = u = x_f and only finite values reach its neighbours
+    // and, through fill_halo, the adjacent ranks).
+    const bool bad = !spd || !fin;
+    if (bad) {
+      st |= (!spd ? ST_NONSPD : 0) | (!fin ? ST_NONFINITE : 0) | ST_FALLBACK;
+      float Af[NT];
+      if (a->prop) {
+        forecast_partial<NP>(opaque(cptr(a->prop)), p, b, Af);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NP; ++j) b[j] = a->x_f[j * ld + p];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) Af[t] = a->pf_inv[t * ld + p];
+      }
+      if (a->a_out) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = Af[t];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NP; ++j) a->x_out[j * ld + p] = b[j];
     int c = 0;
@@ -765,7 +789,7 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
         for (int j = 0; j < NP; ++j) e[j] = (j == r) ? 1.f : 0.f;
         chol_solve<NP>(A, e);
 #pragma unroll
-        for (int j = 0; j < NP; ++j) a->reg_v[((int64_t)c * NP + j) * ld + p] = e[j];
+        for (int j = 0; j < NP; ++j) a->reg_v[((int64_t)c * NP + j) * ld + p] = bad ? 0.f : e[j];
         ++c;
       }
     }
@@ -1110,10 +1134,15 @@ KF_HD float pixel_reg_prepare(const JacobiArgs& a, int64_t p) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = A[t];
   }
-  chol_packed<NP>(A);
+  const bool spd = chol_packed<NP>(A);
   chol_solve<NP>(A, b);
+  bool bad = !spd;
 #pragma unroll
-  for (int j = 0; j < NP; ++j) a.x_out[j * ld + p] = b[j];
+  for (int j = 0; j < NP; ++j) bad = bad || !finitef(b[j]);
+  // unhealthy pixel: decoupled (V = 0) at the reference point (x_ref when
+  // given, else 0), so no non-finite value enters the neighbour sums
+#pragma unroll
+  for (int j = 0; j < NP; ++j) a.x_out[j * ld + p] = bad ? (a.x_ref ? a.x_ref[j * ld + p] : 0.f) : b[j];
   int c = 0;
 #pragma unroll
   for (int r = 0; r < NP; ++r) {
@@ -1123,7 +1152,7 @@ KF_HD float pixel_reg_prepare(const JacobiArgs& a, int64_t p) {
       for (int j = 0; j < NP; ++j) e[j] = (j == r) ? 1.f : 0.f;
       chol_solve<NP>(A, e);
 #pragma unroll
-      for (int j = 0; j < NP; ++j) a.v[((int64_t)c * NP + j) * ld + p] = e[j];
+      for (int j = 0; j < NP; ++j) a.v[((int64_t)c * NP + j) * ld + p] = bad ? 0.f : e[j];
       ++c;
     }
   }

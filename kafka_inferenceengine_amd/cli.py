@@ -98,7 +98,11 @@ def _build(args, comm):
 def cmd_run(args):
     from .parallel import Comm
 
-    comm = Comm.from_env(device=args.device, band_parallel=getattr(args, "band_parallel", None) or 1)
+    import kafka_inferenceengine_amd as k
+
+    cfg = k.EngineConfig.from_args(args)
+    comm = Comm.from_env(device=args.device, band_parallel=getattr(args, "band_parallel", None) or 1,
+                         timeout_s=cfg.comm_timeout_s)
     if not comm.distributed and comm.band is None:
         import torch
         dev = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
@@ -107,7 +111,7 @@ def cmd_run(args):
     start = None
     if args.resume:
         from .input_output.checkpoint import CheckpointManager
-        path = CheckpointManager.latest(args.resume) if not args.resume.endswith("manifest.json") else args.resume
+        path = CheckpointManager.resolve(args.resume)
         state = kf.run(grid, None, None, None, resume_from=path)
     else:
         start = kf.state_from_prior(prior)

@@ -234,7 +234,11 @@ class LinearKalman:
             analysis = self.step(timestep, locate_times, analysis if advance else forecast, advance, all_dates,
                                  next_step=nxt)
             if ckpt is not None and self.config.checkpoint_every and (step_i + 1) % self.config.checkpoint_every == 0:
-                ckpt.save(timestep, analysis)
+                with self.timer.phase("checkpoint"):
+                    ckpt.save(timestep, analysis)
+        if ckpt is not None:
+            with self.timer.phase("checkpoint"):
+                ckpt.finish()
         self.final_state = analysis
         if self.metrics.enabled:
             self.metrics_summary()
@@ -398,12 +402,13 @@ class LinearKalman:
         else:
             qv = np.tile(self._q, self.N)
         Q = sp.diags(qv).tocsr()
+        kw = dict(prior=self.prior, date=date, state_propagator=self._state_propagator)
+        if self._advance is propagate_and_blend_prior:
+            kw["reference_quirks"] = bool(self.config.reference_quirks)   # same blend as the device path
         if analysis.kind == PRECISION:
-            xf, Pf, Pfi = self._advance(x, None, P.tocsr(), M, Q, prior=self.prior, date=date,
-                                        state_propagator=self._state_propagator)
+            xf, Pf, Pfi = self._advance(x, None, P.tocsr(), M, Q, **kw)
         else:
-            xf, Pf, Pfi = self._advance(x, P.tocsr(), None, M, Q, prior=self.prior, date=date,
-                                        state_propagator=self._state_propagator)
+            xf, Pf, Pfi = self._advance(x, P.tocsr(), None, M, Q, **kw)
         if xf is None:
             return analysis
         if Pfi is not None:

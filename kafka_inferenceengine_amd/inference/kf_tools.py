@@ -52,10 +52,6 @@ def _diag(m, n_total=None):
     return np.diag(m) if m.ndim == 2 else m
 
 
-def _n_params_of(x, block_hint=None):
-    return block_hint
-
-
 def _apply_M(M_matrix, x):
     if M_matrix is None:
         return np.asarray(x) * 1.0
@@ -107,15 +103,19 @@ def _guess_block(m, size):
 
 
 def propagate_and_blend_prior(x_analysis, P_analysis, P_analysis_inverse, M_matrix, Q_matrix,
-                              prior=None, state_propagator=None, date=None):
-    """Propagator then prior blend (kf_tools.py:136-171)."""
+                              prior=None, state_propagator=None, date=None, reference_quirks: bool = True):
+    """Propagator then prior blend (kf_tools.py:136-171).  ``reference_quirks``
+    selects the reference's swapped blend (default, the reference API) or the
+    Gaussian product; ``LinearKalman`` passes its ``EngineConfig.reference_quirks``
+    so host and device blends agree."""
     if state_propagator is not None:
         x_forecast, P_forecast, P_forecast_inverse = state_propagator(
             x_analysis, P_analysis, P_analysis_inverse, M_matrix, Q_matrix)
     if prior is not None:
         prior_mean, prior_cov_inverse = prior.process_prior(date, inv_cov=True)
     if prior is not None and state_propagator is not None:
-        x_combined, combined_cov_inv = blend_prior(prior_mean, prior_cov_inverse, x_forecast, P_forecast_inverse)
+        x_combined, combined_cov_inv = blend_prior(prior_mean, prior_cov_inverse, x_forecast, P_forecast_inverse,
+                                                   quirk=reference_quirks)
         return x_combined, None, combined_cov_inv
     elif prior is not None:
         return prior_mean, None, prior_cov_inverse

@@ -36,31 +36,98 @@ class CheckpointManager:
         self.root = Path(root)
         self.engine = engine
         self.root.mkdir(parents=True, exist_ok=True)
+        self._side = None       # D2H side stream
+        self._pinned = None     # reused pinned host buffers (x, P)
+        self._thread = None     # background file writer
+        self._pending = None    # (dir, timestep, kind) awaiting commit
+        self.last_enqueue_s = 0.0
+        self.last_commit_wait_s = 0.0
 
     def path_for(self, timestep) -> Path:
         return self.root / timestep.strftime("A%Y%j")
 
-    def save(self, timestep, state: KFState) -> Path:
+    def save(self, timestep, state: KFState, block: bool = False) -> Path:
+        """Checkpoint ``state`` at ``timestep``.  Device states are snapshotted
+        with one device-to-device copy on the compute stream (milliseconds), then
+        copied to reused pinned host buffers on a side stream and written by a
+        background thread, so the next time step runs under the write.  The
+        checkpoint is committed (barrier, rank 0 writes ``manifest.json``,
+        barrier) by the next ``save`` or by :meth:`finish`; ``latest`` only sees
+        committed checkpoints.  With band-parallel groups only band slot 0 of
+        each strip writes (every member holds the same state)."""
+        import threading
+        import time
+
+        self.finish()
+        e = self.engine
+        d = self.path_for(timestep)
+        t0 = time.perf_counter()
+        writer = e.band_comm is None or e.band_comm.rank == 0
+        if writer:
+            d.mkdir(parents=True, exist_ok=True)
+            r = e.comm.rank
+            N = state.N
+            if state.x.is_cuda:
+                cur = torch.cuda.current_stream(state.x.device)
+                snap = (state.x[:, :N].clone(), state.P[:, :N].clone())   # compute stream, HBM copy
+                if self._side is None:
+                    self._side = torch.cuda.Stream(state.x.device)
+                if self._pinned is None or any(p.shape != s.shape for p, s in zip(self._pinned, snap)):
+                    self._pinned = tuple(torch.empty(s.shape, dtype=s.dtype, pin_memory=True) for s in snap)
+                ev = torch.cuda.Event()
+                self._side.wait_stream(cur)
+                with torch.cuda.stream(self._side):
+                    for h, s in zip(self._pinned, snap):
+                        h.copy_(s, non_blocking=True)
+                    ev.record(self._side)
+                host = self._pinned
+            else:
+                snap, ev = None, None
+                host = (state.x[:, :N].detach().clone(), state.P[:, :N].detach().clone())
+
+            def write(host=host, ev=ev, snap=snap):
+                if ev is not None:
+                    ev.synchronize()
+                for tag, h in zip(("x", "P"), host):
+                    _atomic_write(d / f"state.rank{r}.{tag}.f32", np.ascontiguousarray(h.numpy(), dtype="<f4"))
+                if r == 0:
+                    _atomic_write(d / "state_mask.u8", np.packbits(e.partition.state_mask.ravel()).tobytes())
+                del snap
+
+            if block or snap is None:
+                write()
+            else:
+                self._thread = threading.Thread(target=write, name="kafka-ckpt", daemon=True)
+                self._thread.start()
+        self._pending = (d, timestep, state.kind)
+        self.last_enqueue_s = time.perf_counter() - t0
+        if block:
+            self.finish()
+        return d
+
+    def finish(self):
+        """Wait for the pending checkpoint's files and commit its manifest."""
+        if self._pending is None:
+            return
+        import time
+
+        t0 = time.perf_counter()
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        d, timestep, kind = self._pending
+        self._pending = None
         e = self.engine
         part = e.partition
-        d = self.path_for(timestep)
-        d.mkdir(parents=True, exist_ok=True)
-        r = e.comm.rank
-        x = state.x[:, :state.N].detach().cpu().numpy().astype("<f4")
-        P = state.P[:, :state.N].detach().cpu().numpy().astype("<f4")
-        _atomic_write(d / f"state.rank{r}.x.f32", x.tobytes())
-        _atomic_write(d / f"state.rank{r}.P.f32", P.tobytes())
-        if r == 0:
-            _atomic_write(d / "state_mask.u8", np.packbits(part.state_mask.ravel()).tobytes())
         e.comm.barrier()
-        if r == 0:
+        if e.comm.rank == 0 and (e.band_comm is None or e.band_comm.rank == 0):
             man = {"format": FORMAT, "version": VERSION, "n_params": e.n_params,
                    "parameters": e.parameters_list, "shape": list(part.shape), "timestep": timestep.isoformat(),
-                   "kind": state.kind, "dtype": "float32", "world": e.comm.world, "bounds": part.bounds,
+                   "kind": kind, "dtype": "float32", "world": e.comm.world, "bounds": part.bounds,
                    "counts": part.counts, "layout": {"x": "soa[n_p,N]", "P": "packed_upper_rowmajor[ntri,N]"}}
             _atomic_write(d / "manifest.json", json.dumps(man, indent=1).encode())
         e.comm.barrier()
-        return d
+        self.last_commit_wait_s = time.perf_counter() - t0
 
     @staticmethod
     def read_manifest(path) -> dict:
@@ -105,13 +172,29 @@ class CheckpointManager:
         return st, dt.datetime.fromisoformat(man["timestep"])
 
     @staticmethod
+    def resolve(path) -> Path:
+        """A checkpoint directory from ``path``: a ``manifest.json`` file (its
+        directory), a checkpoint directory, or a checkpoint root (its latest
+        committed checkpoint).  Raises FileNotFoundError when there is none."""
+        p = Path(path)
+        if p.is_file() and p.name == "manifest.json":
+            return p.parent
+        if (p / "manifest.json").is_file():
+            return p
+        last = CheckpointManager.latest(p) if p.is_dir() else None
+        if last is None:
+            raise FileNotFoundError(f"no committed checkpoint (manifest.json) at or under {path}")
+        return last
+
+    @staticmethod
     def latest(root):
         root = Path(root)
         cands = sorted(p for p in root.glob("A*") if (p / "manifest.json").exists())
         return cands[-1] if cands else None
 
 
-def _atomic_write(path: Path, data: bytes):
+def _atomic_write(path: Path, data):
+    """Write ``data`` (bytes or any contiguous buffer) to ``path`` via a tmp file."""
     tmp = path.with_suffix(path.suffix + ".tmp")
     with open(tmp, "wb") as f:
         f.write(data)

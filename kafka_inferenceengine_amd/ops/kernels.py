@@ -324,9 +324,10 @@ def _reg_args(n_params, mode, N, ld, gamma, reg_mask, nbr, geo=None):
     return a
 
 
-def reg_prepare(n_params, a_in, b_in, nbr, u_out, v_out, gamma, reg_mask, N, a_out=None, geo=None):
+def reg_prepare(n_params, a_in, b_in, nbr, u_out, v_out, gamma, reg_mask, N, a_out=None, geo=None, x_ref=None):
     """K9 affine form, once per GN iteration: A_reg = A + g deg E_R (written to
-    ``a_out``, may alias ``a_in``), u = A_reg^-1 b, V = A_reg^-1 E_R ([k*n, ld])."""
+    ``a_out``, may alias ``a_in``), u = A_reg^-1 b, V = A_reg^-1 E_R ([k*n, ld]).
+    A non-SPD / non-finite pixel gets V = 0 and u = ``x_ref`` (0 without it)."""
     check_np(n_params)
     dev = a_in.device
     k = bin(int(reg_mask)).count("1")
@@ -339,8 +340,13 @@ def reg_prepare(n_params, a_in, b_in, nbr, u_out, v_out, gamma, reg_mask, N, a_o
     for t in (b_in, u_out, v_out, a_out):
         if t is not None and t.shape[1] != ld:
             raise ValueError("all SoA operands must share the leading dimension")
+    if x_ref is not None:
+        _check_soa(x_ref, n_params, N, "x_ref", device=dev)
+        if x_ref.shape[1] != ld:
+            raise ValueError("all SoA operands must share the leading dimension")
     a = _reg_args(n_params, JACOBI_PREPARE, N, ld, gamma, reg_mask, nbr, geo)
     a.a_in, a.b_in, a.x_out, a.v, a.a_out = map(_ptr, (a_in, b_in, u_out, v_out, a_out))
+    a.x_ref = _ptr(x_ref)
     ext().jacobi(n_params, a, grid_for(N), _dev(a_in), _stream(a_in))
 
 

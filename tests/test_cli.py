@@ -26,6 +26,21 @@ def test_cli_run_bhr_and_resume(tmp_path):
     out = _run("run", "--sensor", "bhr", "--size", "24", "20", "--steps", "6", "--n-train", "40", "--device", "cpu",
                "--resume", str(tmp_path / "ck"))
     assert json.loads(out.strip().splitlines()[-1])["timesteps"] == 2
+    # an explicit checkpoint directory and its manifest.json resume the same way
+    ck = sorted(p for p in (tmp_path / "ck").iterdir() if (p / "manifest.json").exists())
+    for target in (ck[1], ck[1] / "manifest.json"):
+        out = _run("run", "--sensor", "bhr", "--size", "24", "20", "--steps", "4", "--n-train", "40", "--device",
+                   "cpu", "--resume", str(target))
+        assert json.loads(out.strip().splitlines()[-1])["timesteps"] == 2
+
+
+def test_cli_resume_without_checkpoint_fails_clearly(tmp_path):
+    (tmp_path / "empty").mkdir()
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-m", "kafka_inferenceengine_amd", "run", "--sensor", "bhr", "--size", "8",
+                        "8", "--steps", "2", "--n-train", "20", "--device", "cpu", "--resume",
+                        str(tmp_path / "empty")], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode != 0 and "no committed checkpoint" in r.stderr
 
 
 def test_cli_chunks_matches_reference_golden():

@@ -207,3 +207,54 @@ def test_metrics_summary_aggregates_ranks(tmp_path):
     assert [r["rank"] for r in summary["ranks"]] == [0, 1]
     assert summary["n_pixels"] == sum(r["n_pixels"] for r in summary["ranks"])
     assert os.path.exists(str(tmp_path / "m.rank1.jsonl"))
+
+
+def _bp_ck_worker(rank, world, port, B, ckdir, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import kafka_inferenceengine_amd as k
+    from kafka_inferenceengine_amd.parallel import Comm, StripPartition
+
+    torch.set_num_threads(1)
+    comm = Comm.from_env(device="cpu", band_parallel=B)
+    try:
+        mask = np.ones((12, 10), bool)
+        part = StripPartition(mask, comm.rank, comm.world)
+        obs = k.SyntheticS2Observations(mask, n_bands=4, n_train=20, device="cpu", stream=False, n_pool=2,
+                                        partition=part, field_cell=5, seed=2)
+        prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
+        kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
+                            state_propagation=None, prior=prior, device="cpu", comm=comm, partition=part,
+                            config=k.EngineConfig(gp_split="never", checkpoint_dir=ckdir, checkpoint_every=1))
+        grid = [obs.dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in obs.dates[:3]]
+        st = kf.run(grid, kf.state_from_prior(prior), None, None)
+        q.put((comm.band.rank if comm.band is not None else 0, st.x.numpy().copy()))
+    finally:
+        comm.destroy()
+
+
+def test_band_parallel_checkpoint_single_writer(tmp_path):
+    """with band groups every member holds the same strip state, so
+    only band slot 0 writes; a checkpoint per timestep is committed and loads
+    back to the final state."""
+    import kafka_inferenceengine_amd as k
+
+    ck = str(tmp_path / "ck")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bp_ck_worker, args=(r, 2, port, 2, ck, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dirs = sorted(p for p in os.listdir(ck))
+    assert len(dirs) == 3
+    for d in dirs:
+        files = sorted(os.listdir(os.path.join(ck, d)))
+        assert files == ["manifest.json", "state.rank0.P.f32", "state.rank0.x.f32", "state_mask.u8"], files
+    last = k.CheckpointManager.resolve(ck)
+    x = np.fromfile(last / "state.rank0.x.f32", dtype="<f4").reshape(10, -1)
+    assert np.array_equal(x, res[0][1][:, :x.shape[1]])

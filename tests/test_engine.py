@@ -304,3 +304,37 @@ def test_speculative_next_step_equals_sequential(tol):
         assert sb["queued"] >= sb["adopted"] >= len(grid) - 3
     else:
         assert sb["adopted"] == 0 and sb["queued"] <= 1
+
+
+class _HostOnlyPrior:
+    """A reference-style prior object: only ``process_prior`` (no device fast path)."""
+
+    def __init__(self, inner):
+        self.inner = inner
+
+    def process_prior(self, date, inv_cov=True):
+        return self.inner.process_prior(date, inv_cov=inv_cov)
+
+
+@pytest.mark.parametrize("quirks", [False, True], ids=["gaussian-product", "reference-swap"])
+def test_prior_blend_same_on_host_and_device_paths(quirks):
+    """EngineConfig.reference_quirks drives both the device blend (K5) and the
+    host ``propagate_and_blend_prior`` used for reference prior objects."""
+    import datetime as dt
+    import kafka_inferenceengine_amd as k
+
+    mask = np.ones((6, 5), bool)
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(4)]
+    out = []
+    for wrap in (False, True):
+        obs = k.SyntheticBHRObservations(mask, n_train=30, device="cpu", stream=False, n_pool=2, seed=5)
+        prior = k.JRCPrior(k.TIP_PARAMETERS, mask)
+        kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS,
+                            state_propagation=k.propagate_information_filter_LAI,
+                            prior=_HostOnlyPrior(prior) if wrap else prior, device="cpu",
+                            config=k.EngineConfig(reference_quirks=quirks))
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        x0, Pinv = prior.process_prior(None)
+        st = kf.run(grid, x0, None, Pinv)
+        out.append(st.x[:, :st.N].numpy().copy())
+    assert np.allclose(out[0], out[1], rtol=1e-4, atol=1e-5)

@@ -32,15 +32,20 @@ class NaNInjected:
         return r._replace(observations=obs, uncertainty=unc.tocsr())
 
 
-def test_nan_tile_is_contained_and_flagged():
+import pytest
+
+
+@pytest.mark.parametrize("gamma", [0.0, 2.0], ids=["plain", "spatial"])
+def test_nan_tile_is_contained_and_flagged(gamma):
     mask = np.ones((16, 12), bool)
     src = k.SyntheticBHRObservations(mask, n_train=40, device="cpu", stream=False, n_pool=2, field_cell=4)
     bad = NaNInjected(src, slice(2, 5), slice(3, 7))
     grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(3)]
     res = []
     for obs in (src, bad):
+        cfg = k.EngineConfig(spatial_gamma=gamma, spatial_params=[6], jacobi_sweeps=3)
         kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS,
-                            device="cpu")
+                            device="cpu", config=cfg)
         kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
         st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
         res.append((st.x.clone(), kf.last_status.clone()))
@@ -50,8 +55,15 @@ def test_nan_tile_is_contained_and_flagged():
     img[2:5, 3:7] = True
     inside = torch.from_numpy(img.ravel())
     assert torch.all((sb[inside] & K.ST_NO_OBS) > 0)       # corrupted pixels saw no valid observation
-    # pixels outside the tile: identical physics, only the global norm could differ
-    assert torch.allclose(xa[:, ~inside], xb[:, ~inside], rtol=1e-5, atol=1e-6)
+    if gamma == 0.0:
+        # pixels outside the tile: identical physics, only the global norm could differ
+        assert torch.allclose(xa[:, ~inside], xb[:, ~inside], rtol=1e-5, atol=1e-6)
+    else:
+        # coupled: far from the tile (> 3 sweeps of 4-neighbour influence) nothing changes
+        far = np.ones(mask.shape, bool)
+        far[0:9, 0:11] = False
+        far = torch.from_numpy(far.ravel())
+        assert torch.allclose(xa[:, far], xb[:, far], rtol=1e-3, atol=1e-4)
 
 
 def test_nonspd_forecast_falls_back_per_pixel():
@@ -74,6 +86,36 @@ def test_nonspd_forecast_falls_back_per_pixel():
     assert torch.equal(xo[:, :6], x[:, :6])
     assert not torch.any(st[6:] & K.ST_FALLBACK)
     assert torch.isfinite(xo).all()
+
+
+def test_nonspd_forecast_falls_back_in_spatial_epilogue():
+    """The regularised (reg_v) epilogue: non-SPD / NaN pixels keep the forecast,
+    are decoupled (V = 0) and nothing non-finite reaches the sweeps."""
+    n, H, W = 7, 4, 16
+    N = H * W
+    mu, _, Pi = k.tip_prior()
+    from kafka_inferenceengine_amd.utils.blocks import pack_matrix, ntri
+    x = torch.tensor(np.tile(mu[:, None], (1, N)), dtype=torch.float32)
+    P = torch.tensor(np.tile(pack_matrix(Pi)[:, None], (1, N)), dtype=torch.float32)
+    P[:, :5] = torch.tensor(pack_matrix(-np.eye(7)), dtype=torch.float32)[:, None]
+    P[:, 5] = float("nan")
+    y = torch.full((N,), 0.1)
+    w = torch.zeros(N)
+    spec = k.models.operators._linear_device_spec(n, None, None, 0)
+    from kafka_inferenceengine_amd.engine.bands import RecordCache, build_table
+    tab = build_table([spec], [DeviceBand(K.OBS_F32, y=y, w=w)], n, RecordCache(), "cpu")
+    u, ao = torch.zeros_like(x), torch.zeros_like(P)
+    v = torch.full((n, N), 7.0)
+    st = torch.zeros(N, dtype=torch.uint8)
+    geo = {"w": W, "h": H, "halo": 0, "n_up": 0}
+    K.analysis(n, tab, x, x, P, u, ao, None, st, None, N=N,
+               reg=dict(gamma=2.0, mask=1 << 6, v_out=v, nbr=None, geo=geo))
+    assert torch.all(st[:6] & K.ST_FALLBACK) and not torch.any(st[6:] & K.ST_FALLBACK)
+    assert torch.equal(u[:, :6], x[:, :6])
+    assert torch.all(v[:, :6] == 0) and torch.isfinite(v).all() and torch.isfinite(u).all()
+    keep = torch.ones(N, dtype=torch.bool)
+    keep[5] = False            # its forecast precision is NaN, and the fallback keeps the forecast
+    assert torch.isfinite(ao[:, keep]).all()
 
 
 # ----------------------------------------------------------- rank failure
