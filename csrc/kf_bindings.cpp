@@ -76,7 +76,10 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(BandDesc, pre_h0, const float*)
       .PTR_FIELD(BandDesc, pre_h, const float*)
       .PTR_FIELD(BandDesc, h0_out, float*)
-      .def_readwrite("pre_ld", &BandDesc::pre_ld);
+      .def_readwrite("pre_ld", &BandDesc::pre_ld)
+      .def_readwrite("gpm_nchunk", &BandDesc::gpm_nchunk)
+      .def_readwrite("gpm_scale", &BandDesc::gpm_scale)
+      .PTR_FIELD(BandDesc, gpm, const void*);
 
   m.def("pack_band_descs", [](const std::vector<BandDesc>& v) {
     return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(BandDesc));
@@ -95,6 +98,7 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .def_readwrite("fast_d", &AnalysisArgs::fast_d)
       .def_readwrite("fast_obs", &AnalysisArgs::fast_obs)
       .def_readwrite("variant", &AnalysisArgs::variant)
+      .def_readwrite("gpm_frags", &AnalysisArgs::gpm_frags)
       .PTR_FIELD(AnalysisArgs, bands, const BandDesc*)
       .PTR_FIELD(AnalysisArgs, x_prev, const float*)
       .PTR_FIELD(AnalysisArgs, x_f, const float*)

@@ -92,7 +92,8 @@ enum StatusBits : uint8_t {
 // host by kf_bindings (pack_band_descs) so the C++ layout is authoritative.
 struct BandDesc {
   int32_t op, obs, d, T;
-  int32_t Tp, pad_;            // GP: the first Tp record pairs carry alpha > 0, the rest alpha < 0
+  int32_t Tp;                  // GP: the first Tp record pairs carry alpha > 0, the rest alpha < 0
+  int32_t gpm_nchunk;          // GP on MFMA: 32-point chunks of the split-f16 table (0: VALU path only)
   int32_t map[MAX_D];          // state index feeding input d of the operator
   float scale, rel_unc, unc_floor, offset;
   float coef[MAX_D];           // LINEAR: c_j per state j; GP: lambda_d; SAR: A,B,C,D,E,theta
@@ -107,6 +108,9 @@ struct BandDesc {
   const float* pre_h;          // OP_PRECOMP h [NP][ld]
   float* h0_out;               // optional diagnostics: H0 at the linearisation point
   int64_t pre_ld;              // leading dim of pre_h
+  const void* gpm;             // GP split-f16 MFMA fragments (kf_gp_mfma.h, models/gp.py:mfma_tables)
+  float gpm_scale;             // 2^sigma: undoes the f16-range shift folded into the table's L'
+  int32_t pad_;
 };
 
 struct PropArgs {
@@ -154,7 +158,7 @@ struct AnalysisArgs {
   int32_t n_bands, solve;
   int32_t fast_d, fast_obs;  // host hint: all bands GP with fast_d inputs, one encoding (0: generic)
   int32_t variant;           // kernel variant selector (tuning; 0 = default)
-  int32_t pad1;
+  int32_t gpm_frags;         // > 0: every band has an MFMA table, fragments of all bands (LDS / 16 B)
   const BandDesc* bands;
   const float* x_prev;   // [NP][ld] linearisation point
   const float* x_f;      // [NP][ld] forecast mean

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include "kf_core.h"
 #include "kf_launch.h"
+#include "kf_gp_mfma.h"
 
 namespace kf {
 
@@ -47,6 +48,37 @@ __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
   for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
     acc += (double)pixel_analysis<NP, FD, FOBS, UNR, FOLD>(a, p);
   if (a.partials) block_partial(acc, a.partials);
+}
+
+// K1 with the GP on the matrix cores (kf_gp_mfma.h).  Every band's split-f16
+// table is staged in LDS once per workgroup (a.gpm_frags x 16 B of dynamic
+// LDS), then each wave walks 64-pixel tiles grid-stride.
+template <int NP, int D, int FOBS, int BPP>
+__global__ __launch_bounds__(BLOCK) void analysis_mfma_kernel(AnalysisArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  extern __shared__ kf_h8 gpm_lds[];
+  {
+    int off = 0;
+    for (int bi = 0; bi < a.n_bands; ++bi) {
+      const KF_CONST_AS BandDesc* bd = cptr(a.bands) + bi;
+      const int n = bd->gpm_nchunk * gpm_frags_per_chunk(D);
+      const kf_h8* src = (const kf_h8*)bd->gpm;
+      for (int i = threadIdx.x; i < n; i += BLOCK) gpm_lds[off + i] = src[i];
+      off += n;
+    }
+  }
+  __syncthreads();
+  double acc = 0.0;
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t base = (int64_t)blockIdx.x * BLOCK + (threadIdx.x - lane); base < a.N; base += stride) {
+    const int64_t p = base + lane;
+    const bool act = p < a.N;
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, BPP>(a, act ? p : a.N - 1, act, gpm_lds);
+    acc += act ? (double)dn : 0.0;
+  }
+  if (a.partials) block_partial(acc, a.partials);
+#endif
 }
 
 template <int NP>
@@ -213,8 +245,42 @@ inline int grid_for(int64_t N, int max_blocks) {
     default: return hipErrorInvalidValue;         \
   }
 
+// dynamic LDS above the 64 KiB default (tables of several bands, up to the
+// 160 KiB of a gfx950 CU)
+template <typename K>
+static void gpm_lds_attr(K kernel, size_t bytes) {
+  if (bytes > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+}
+
 template <int NP, int FD>
 static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
+  // GP on the matrix cores when the host attached split-f16 tables to every band
+  // (variant 4 forces the VALU record loop, for A/B)
+  if constexpr (FD > 0 && FD <= GPM_MAX_D) {
+    if (a.gpm_frags > 0 && a.variant != 4) {
+      // variant 5: one 32-pixel column block per pass (A/B against the default 2)
+      const size_t lds = (size_t)a.gpm_frags * sizeof(kf_h8);
+#define KF_MFMA_LAUNCH(OBS_)                                                                               \
+  if (a.variant == 5) {                                                                                    \
+    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, 1>, lds);                                              \
+    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, 1>), dim3(grid), dim3(BLOCK), lds, s, a);      \
+  } else {                                                                                                 \
+    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, 2>, lds);                                              \
+    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, 2>), dim3(grid), dim3(BLOCK), lds, s, a);      \
+  }
+      if (a.fast_obs == OBS_DN16) {
+        KF_MFMA_LAUNCH(OBS_DN16)
+      } else if (a.fast_obs == OBS_F32) {
+        KF_MFMA_LAUNCH(OBS_F32)
+      } else {
+        return false;
+      }
+#undef KF_MFMA_LAUNCH
+      return true;
+    }
+  }
   // variant (A/B tuning, scripts/bench_kernels.py): 0 unroll-4 pairs (default),
   // 1 unroll-4 + folded exponent, 2 unroll-8, 3 unroll-3 (GP fast paths only)
   if (a.fast_obs == OBS_DN16) {

@@ -1,0 +1,289 @@
+// kf_gp_mfma.h — GP emulator operator + Jacobian on the gfx950 matrix cores.
+//
+// The GP sums of kf_core.h (gp_eval) for a wave's 64 pixels are two GEMMs
+// over the T training points (replaces utils.py:181-219 + gp.predict):
+//   E[i][p]  = L'_i + c_p + sum_d B_id x_pd                    (exponent, K = D)
+//   m[i][p]  = 2^E[i][p]                                        (v_exp_f32)
+//   S[f][p]  = sum_i A[f][i] m[i][p],  A = [sgn_i; sgn_i B_i]   (K = T)
+// Both run on v_mfma_f32_32x32x16_f16 with split-f16 operands (v = hi + lo,
+// hi = f16(v), lo = f16(v - hi); products hi.hi + hi.lo + lo.hi accumulated in
+// f32): 22 significant bits per operand, as accurate as the f32 VALU loop it
+// replaces (scripts/sim_gp_mfma_precision.py).  The exponent comes out of the
+// accumulator in f32; only v_exp and the hi/lo split of m stay on the VALU.
+//
+// Layout (lane l, h = l >> 5, col = l & 31; fragment element j = K index 8h + j
+// of a 16-wide K step; C row of accumulator register r = (r&3) + 8(r>>2) + 4h):
+//   exponent  A rows = 32 training points, B cols = 32 pixels, K slots
+//             [Bh(D) | Bl(D) | Bh(D) | L'h | L'l | 1 | 1 | 0..] x
+//             [xh(D) | xh(D) | xl(D) | 1   | 1   | ch | cl | 0..]   (ceil((3D+4)/16) K steps)
+//             -> lane l holds E of pixel col at points (r&3) + 8(r>>2) + 4h, r = 0..15
+//   sums      A rows = fields (S0, S'_1..S'_D; rows > D unused), B cols = 32 pixels,
+//             two K = 16 halves q: K slot 8h + j <-> point (j&3) + 4h + 8(j>>2) + 16q,
+//             i.e. exactly accumulator registers 8q .. 8q+7 of the exponent MFMA.
+// Host tables (models/gp.py: mfma_tables), per 32-point chunk: the exponent A
+// fragments of every lane, then for q = 0, 1 the hi and lo sums A fragments of
+// the lanes with row <= D.  A band's table is staged in LDS once per
+// workgroup.  m is kept <= 2^14 (f16 range) by a per-band power-of-two shift
+// folded into L' and undone on S (BandDesc.gpm_scale).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "kf_core.h"
+
+namespace kf {
+
+typedef _Float16 kf_h8 __attribute__((ext_vector_type(8)));
+typedef float kf_f16v __attribute__((ext_vector_type(16)));
+typedef uint32_t kf_u4 __attribute__((ext_vector_type(4)));
+typedef __fp16 kf_hp2 __attribute__((ext_vector_type(2)));
+
+// exponent K steps of 16 slots (3D + 4 used)
+KF_HD constexpr int gpm_k_steps(int D) { return (3 * D + 4 + 15) / 16; }
+// sums fragments per (q, hi/lo): lanes with row <= D in both K halves
+KF_HD constexpr int gpm_sum_lanes(int D) { return 2 * (D + 1); }
+// 16-byte fragments per 32-point chunk
+KF_HD constexpr int gpm_frags_per_chunk(int D) { return 64 * gpm_k_steps(D) + 4 * gpm_sum_lanes(D); }
+constexpr int GPM_MAX_D = 10;
+
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint32_t gpm_pack(_Float16 a, _Float16 b) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+
+// K slot k of the exponent B operand
+template <int D>
+__device__ __forceinline__ _Float16 gpm_xslot(int k, const _Float16 (&xh)[D], const _Float16 (&xl)[D],
+                                              _Float16 ch, _Float16 cl) {
+  if (k < D) return xh[k];
+  if (k < 2 * D) return xh[k - D];
+  if (k < 3 * D) return xl[k - 2 * D];
+  if (k < 3 * D + 2) return (_Float16)1.f;
+  if (k == 3 * D + 2) return ch;
+  if (k == 3 * D + 3) return cl;
+  return (_Float16)0.f;
+}
+
+template <int D>
+__device__ __forceinline__ kf_u4 gpm_xfrag(int k0, const _Float16 (&xh)[D], const _Float16 (&xl)[D], _Float16 ch,
+                                           _Float16 cl) {
+  kf_u4 v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    v[q] = gpm_pack(gpm_xslot<D>(k0 + 2 * q, xh, xl, ch, cl), gpm_xslot<D>(k0 + 2 * q + 1, xh, xl, ch, cl));
+  return v;
+}
+
+__device__ __forceinline__ void gpm_split16(float v, _Float16& h, _Float16& l) {
+  h = (_Float16)v;
+  l = (_Float16)(v - (float)h);
+}
+
+// Exponent B operands (all K steps) of column block `blk` (pixels 32 blk ..
+// 32 blk + 31 of the wave).
+template <int D>
+__device__ __forceinline__ void gpm_operand(const float (&xi)[D], float c, int blk,
+                                            kf_h8 (&xb)[gpm_k_steps(D)]) {
+  const int lane = threadIdx.x & 63;
+  const int src = 32 * blk + (lane & 31);
+  _Float16 xh[D], xl[D], ch, cl;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    // clamp: f16 range (a state that far out has k = 0 anyway through c)
+    gpm_split16(fminf(fmaxf(__shfl(xi[d], src, 64), -6.0e4f), 6.0e4f), xh[d], xl[d]);
+  }
+  gpm_split16(fmaxf(__shfl(c, src, 64), -6.0e4f), ch, cl);
+  const bool h1 = lane >= 32;
+#pragma unroll
+  for (int kk = 0; kk < gpm_k_steps(D); ++kk) {
+    const kf_u4 f0 = gpm_xfrag<D>(16 * kk, xh, xl, ch, cl), f1 = gpm_xfrag<D>(16 * kk + 8, xh, xl, ch, cl);
+    xb[kk] = __builtin_bit_cast(kf_h8, h1 ? f1 : f0);
+  }
+}
+
+// m = 2^e for 8 accumulator registers, split into f16 hi (round toward zero)
+// and lo = f16(m - hi).
+__device__ __forceinline__ void gpm_exp_split(const kf_f16v& e, int r0, kf_h8& mh, kf_h8& ml) {
+  kf_u4 hv, lv;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float m0 = kexp2(e[r0 + 2 * q]), m1 = kexp2(e[r0 + 2 * q + 1]);
+    const kf_hp2 h = __builtin_amdgcn_cvt_pkrtz(m0, m1);
+    hv[q] = __builtin_bit_cast(uint32_t, h);
+    // lo of both halves with two mixed-precision FMAs (-hi * 1 + m): v_fma_mix
+    // reads hi as f16 straight from the packed register
+    uint32_t l;
+    asm volatile("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(hv[q]), "v"(m0));
+    asm volatile("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hv[q]), "v"(m1));
+    lv[q] = l;
+  }
+  mh = __builtin_bit_cast(kf_h8, hv);
+  ml = __builtin_bit_cast(kf_h8, lv);
+}
+
+// Wave-cooperative GP sums for the 64 pixels of the wave (lane = pixel).
+// tab: the band's fragments (LDS), nchunk 32-point chunks.  Returns the lane's
+// S[0] = sum sgn m, S[1 + d] = sum sgn m B_d, unscaled.  Every lane of the wave
+// must call it (MFMA); lanes without an observation pass any finite x.
+// BPP = column blocks (of 32 pixels) per pass sharing each chunk's A fragments.
+template <int D, int BPP = 2>
+__device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, int nchunk, const float (&xi)[D],
+                                             float c, float (&S)[D + 1]) {
+  static_assert(D >= 1 && D <= GPM_MAX_D, "GP input count for the matrix-core path");
+  static_assert(BPP == 1 || BPP == 2, "column blocks per pass");
+  constexpr int NK = gpm_k_steps(D), NLS = gpm_sum_lanes(D), FPC = gpm_frags_per_chunk(D);
+  const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+  // sums fragment of this lane; rows > D read fragment 0: finite values that
+  // only reach accumulator rows nobody reads (no exec-mask branch, no zeroing)
+  const int is = 64 * NK + (col <= D ? h * (D + 1) + col : 0);
+  const kf_f16v zero = {};
+#pragma unroll
+  for (int f = 0; f <= D; ++f) S[f] = 0.f;
+  for (int pass = 0; pass < 2 / BPP; ++pass) {
+    kf_h8 xb[BPP][NK];
+    kf_f16v acc[BPP];
+#pragma unroll
+    for (int i = 0; i < BPP; ++i) {
+      gpm_operand<D>(xi, c, pass * BPP + i, xb[i]);
+      acc[i] = zero;
+    }
+    // (a software-pipelined order -- next chunk's exponent MFMAs between the two
+    // K halves -- removes the s_nop padding but measured 4-7 % slower: more
+    // VGPRs, fewer waves; the other waves already fill the MFMA latency)
+    for (int ch = 0; ch < nchunk; ++ch) {
+      const kf_h8* t = tab + ch * FPC;
+      kf_h8 ea[NK], sa[2][2];
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) ea[kk] = t[64 * kk + lane];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        sa[q][0] = t[is + (2 * q) * NLS];
+        sa[q][1] = t[is + (2 * q + 1) * NLS];
+      }
+#pragma unroll
+      for (int i = 0; i < BPP; ++i) {
+        kf_f16v e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[0], xb[i][0], zero, 0, 0, 0);
+#pragma unroll
+        for (int kk = 1; kk < NK; ++kk) e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[kk], xb[i][kk], e, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          kf_h8 mh, ml;
+          gpm_exp_split(e, 8 * q, mh, ml);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][0], mh, acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][0], ml, acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][1], mh, acc[i], 0, 0, 0);
+        }
+      }
+    }
+    // field f sits in register (f&3) + 4(f>>3) of lanes h = (f>>2)&1 for pixel
+    // 32 blk + col; bring fields 0..D of the lane's own pixel (blk = h) home.
+#pragma unroll
+    for (int i = 0; i < BPP; ++i) {
+#pragma unroll
+      for (int f = 0; f <= D; ++f) {
+        const float v = __shfl(acc[i][(f & 3) + 4 * (f >> 3)], 32 * ((f >> 2) & 1) + col, 64);
+        S[f] = h == pass * BPP + i ? v : S[f];
+      }
+    }
+  }
+}
+#endif
+
+}  // namespace kf
+
+namespace kf {
+#if defined(__HIP_DEVICE_COMPILE__)
+// K1 on the matrix cores: pixel_analysis (kf_core.h) with lane = pixel and the
+// GP sums of every band evaluated wave-cooperatively by gp_mfma_sums.  All 64
+// lanes run the band loop (act = false for the tail lanes past N: clamped
+// reads, no stores); the GP is skipped only when no lane of the wave has an
+// observation of the band (wave-level cloud skip).
+template <int NP, int D, int FOBS, int BPP = 2>
+__device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
+                                                     const kf_h8* lds) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a.ld;
+  float x0[NP], A[NT], b[NP];
+  uint8_t st = 0;
+  if (a.x_prev) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
+  }
+  if (a.prop) {
+    float xf[NP];
+    forecast_partial<NP>(opaque(cptr(a.prop)), p, xf, A);
+    symv<NP>(A, xf, b);
+    if (!a.x_prev) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) x0[j] = xf[j];
+    }
+  } else if (a.a_in) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) A[t] = a.a_in[t * ld + p];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) b[j] = a.b_in[j * ld + p];
+  } else {
+    float xf[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) xf[j] = a.x_f[j * ld + p];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) A[t] = a.pf_inv[t * ld + p];
+    symv<NP>(A, xf, b);
+  }
+  int nobs = 0;
+  int off = 0;
+  for (int bi = 0; bi < a.n_bands; ++bi) {
+    const KF_CONST_AS BandDesc* bdp = cptr(a.bands) + bi;
+    float y, w;
+    decode_obs<FOBS>(*bdp, p, y, w);
+    const bool use = act && (w > 0.f);
+    float H0 = 0.f, h[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) h[j] = 0.f;
+    bool ok = false;
+    const int nch = bdp->gpm_nchunk;
+    if (__any(use)) {
+      float xi[D], c = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        xi[d] = gather_state<NP>(x0, bdp->map[d]) - bdp->center[d];
+        c = fmaf(bdp->coef[d] * xi[d], xi[d], c);
+      }
+      c *= -0.5f * LOG2E;
+      float S[D + 1];
+      gp_mfma_sums<D, BPP>(lds + off, nch, xi, c, S);
+      const KF_CONST_AS BandDesc* q = opaque(bdp);   // epilogue fields: not live across the chunk loop
+      const float sc = q->gpm_scale;
+      float Sd[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) Sd[d] = S[1 + d] * sc;
+      gp_epilogue<NP, D>(q->offset, q->coef, q->map, xi, S[0] * sc, Sd, H0, h);
+      ok = finitef(H0);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);
+    }
+    off += nch * gpm_frags_per_chunk(D);
+    float* h0o = opaque(bdp)->h0_out;
+    if (act && h0o) h0o[p] = use ? H0 : 0.f;
+    if (use && !ok) st |= ST_BAD_OP;
+    if (use && ok) {
+      ++nobs;
+      float yp = y - H0;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) yp = fmaf(h[j], x0[j], yp);
+      const float wy = w * yp;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const float wh = w * h[i];
+        b[i] = fmaf(h[i], wy, b[i]);
+#pragma unroll
+        for (int j = i; j < NP; ++j) A[tri(NP, i, j)] = fmaf(wh, h[j], A[tri(NP, i, j)]);
+      }
+    }
+  }
+  if (nobs == 0) st |= ST_NO_OBS;
+  if (!act) return 0.f;
+  const KF_CONST_AS AnalysisArgs* ka =
+      opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
+  return analysis_epilogue<NP>(ka, p, A, b, x0, st);
+}
+#endif
+}  // namespace kf

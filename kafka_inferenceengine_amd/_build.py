@@ -33,7 +33,7 @@ EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 EXT_PATH = PKG_DIR / f"_kafka_hip{EXT_SUFFIX}"
 CHECKED_EXT_PATH = PKG_DIR / f"_kafka_hip_checked{EXT_SUFFIX}"
 
-HEADERS = ["kf_core.h", "kf_launch.h", "kf_stream.h", "kf_device.h"]
+HEADERS = ["kf_core.h", "kf_launch.h", "kf_stream.h", "kf_device.h", "kf_gp_mfma.h"]
 # device translation units (compiled concurrently: the NP = 7 / 10 analysis
 # instantiations dominate the build)
 HIP_SOURCES = ["kf_kernels.hip", "kf_analysis7.hip", "kf_analysis10.hip"]
@@ -86,8 +86,9 @@ def build(force: bool = False, verbose: bool = False, checked: bool = False) -> 
     for name in HIP_SOURCES:
         src, obj = CSRC / name, build_dir / (Path(name).stem + ".o")
         if force or _stale(obj, [src] + hdrs):
-            jobs.append([hipcc, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics", "-c", str(src), "-o",
-                         str(obj)])
+            # MFMA results straight into VGPRs (no v_accvgpr_read per exponent in kf_gp_mfma.h)
+            jobs.append([hipcc, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics", "-mllvm",
+                         "-amdgpu-mfma-vgpr-form", "-c", str(src), "-o", str(obj)])
         objs.append(obj)
 
     # 2. host runner of the same per-pixel code (g++, OpenMP)

@@ -9,11 +9,13 @@ with ``w`` the inverse variance (the reference's ``uncertainty``).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
 import torch
 
+from ..models.gp import mfma_tables
 from ..models.operators import OP_GP, OP_LINEAR, OP_PRECOMP, OP_SAR, OperatorSpec
 from ..ops import kernels as K
 
@@ -66,10 +68,30 @@ class DeviceBand:
 
 
 class RecordCache:
-    """Uploads GP training records once per (emulator, device)."""
+    """Uploads GP training records (and their split-f16 MFMA tables) once per
+    (emulator, device)."""
 
     def __init__(self):
         self._c = {}
+        self._m = {}
+
+    def get_mfma(self, spec: OperatorSpec, device):
+        """(table tensor, n_chunks, scale) of the matrix-core GP path, or None
+        (disabled with KAFKA_GP_MFMA=0, D > 10, or values outside f16 range)."""
+        if os.environ.get("KAFKA_GP_MFMA", "1") == "0":
+            return None
+        key = (id(spec.emulator) if spec.emulator is not None else id(spec.records), str(device))
+        hit = self._m.get(key)
+        if hit is None:
+            built = mfma_tables(spec.records, spec.gp_pos_pairs, spec.coef)
+            if built is None:
+                hit = (None, spec.records)
+            else:
+                tab, nch, scale = built
+                t = torch.from_numpy(np.ascontiguousarray(tab).view(np.int16)).to(device)
+                hit = ((t, nch, scale), spec.records)
+            self._m[key] = hit
+        return hit[0]
 
     def get(self, spec: OperatorSpec, device) -> torch.Tensor:
         key = (id(spec.emulator) if spec.emulator is not None else id(spec.records), str(device))
@@ -105,6 +127,10 @@ def band_desc(spec: OperatorSpec, obs: DeviceBand | None, n_params: int, cache: 
         d.d, d.T, d.Tp = spec.d, 2 * int(rec.shape[0]), int(spec.gp_pos_pairs)
         d.gp = rec.data_ptr()
         keep.append(rec)
+        mt = cache.get_mfma(spec, device)
+        if mt is not None:
+            d.gpm, d.gpm_nchunk, d.gpm_scale = mt[0].data_ptr(), int(mt[1]), float(mt[2])
+            keep.append(mt[0])
     elif spec.kind == OP_SAR:
         d.d, d.T = 2, 0
     elif spec.kind == OP_LINEAR:

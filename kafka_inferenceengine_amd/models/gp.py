@@ -146,6 +146,141 @@ class GaussianProcessEmulator:
 
 
 # --------------------------------------------------------------------------
+# split-f16 MFMA tables (csrc/kf_gp_mfma.h)
+
+GPM_MAX_D = 10
+GPM_M_LOG2 = 14          # m = 2^E is kept <= 2^14 (f16 max 65504)
+_F16_SAFE = 6.0e4
+
+
+def gpm_k_steps(d: int) -> int:
+    """16-slot K steps of the exponent MFMA (3d + 4 slots used)."""
+    return (3 * d + 4 + 15) // 16
+
+
+def gpm_sum_lanes(d: int) -> int:
+    return 2 * (d + 1)
+
+
+def gpm_frags_per_chunk(d: int) -> int:
+    return 64 * gpm_k_steps(d) + 4 * gpm_sum_lanes(d)
+
+
+def _split16(v):
+    hi = np.asarray(v, dtype=np.float64).astype(np.float16)
+    lo = (v - hi.astype(np.float64)).astype(np.float16)
+    return hi, lo
+
+
+def _sum_points():
+    """[q, h, j] -> point of the chunk in K slot 8h + j of sums half q (the
+    exponent MFMA's accumulator registers 8q..8q+7, csrc/kf_gp_mfma.h)."""
+    q, h, j = np.meshgrid(np.arange(2), np.arange(2), np.arange(8), indexing="ij")
+    return (j & 3) + 4 * h + 8 * (j >> 2) + 16 * q
+
+
+def mfma_tables(records, n_pos_pairs: int, lam):
+    """Operand fragments of the matrix-core GP (``csrc/kf_gp_mfma.h``) from the
+    packed VALU records (``GaussianProcessEmulator.records``), so any
+    ``OperatorSpec`` with records gets them.
+
+    Returns ``(table, n_chunks, scale)``: ``table`` is float16 ``[n_chunks,
+    frags_per_chunk, 8]``; per 32-point chunk the exponent A fragments of all
+    64 lanes for each 16-slot K step (rows = points, slots ``[Bh | Bl | Bh |
+    L'h | L'l | 1 | 1]``), then for each K half q the hi and lo sums A
+    fragments (rows = ``sgn``, ``sgn B_d``) of the lanes with row <= D.
+    ``scale = 2^sigma`` undoes the shift that keeps every m below 2^14.  None
+    when the values do not fit f16."""
+    rec = np.asarray(records, dtype=np.float64)
+    if rec.ndim != 3 or rec.shape[2] != 2:
+        raise ValueError("records must be [T/2, D+1, 2]")
+    D = rec.shape[1] - 1
+    if not 1 <= D <= GPM_MAX_D:
+        return None
+    pts = rec.transpose(0, 2, 1).reshape(-1, D + 1)          # point-major [T, D+1]: L', B
+    sgn = np.where(np.arange(pts.shape[0]) < 2 * int(n_pos_pairs), 1.0, -1.0)
+    keep = pts[:, 0] > -1e29                                  # drop the pair padding (m = 0)
+    pts, sgn = pts[keep], sgn[keep]
+    L, B = pts[:, 0], pts[:, 1:]
+    lam = np.asarray(lam, dtype=np.float64)[:D]
+    # log2 m = L' + c + B.x <= L' + max_x (c + B.x) = L' + 1/2 sum_d B_d^2 / (log2e lambda_d)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        q = np.where(lam[None, :] > 0, B * B / (LOG2E * lam[None, :]), 0.0)
+    bound = L + 0.5 * q.sum(1)
+    sigma = float(np.ceil(bound.max()) - GPM_M_LOG2) if bound.size else 0.0
+    Ls = L - sigma
+    if B.size and (np.abs(B).max() > _F16_SAFE or np.abs(Ls).max() > _F16_SAFE):
+        return None
+    T = pts.shape[0]
+    nch = max(1, -(-T // 32))
+    Tpad = 32 * nch
+    NK = gpm_k_steps(D)
+    Bh, Bl = _split16(B)
+    Lh, Ll = _split16(Ls)
+    kexp = np.zeros((Tpad, 16 * NK), dtype=np.float16)        # exponent A rows (pad rows 0: m = 2^c, A = 0)
+    kexp[:T, 0:D], kexp[:T, D:2 * D], kexp[:T, 2 * D:3 * D] = Bh, Bl, Bh
+    kexp[:T, 3 * D], kexp[:T, 3 * D + 1] = Lh, Ll
+    kexp[:T, 3 * D + 2] = kexp[:T, 3 * D + 3] = 1.0
+    A = np.zeros((D + 1, Tpad))
+    A[0, :T] = sgn
+    A[1:, :T] = (sgn[:, None] * B).T
+    Ah, Al = _split16(A)
+    NLS = gpm_sum_lanes(D)
+    lane = np.arange(64)
+    j = np.arange(8)
+    sp = _sum_points()                                        # [q, h, j]
+    hh = np.repeat(np.arange(2), D + 1)                       # compact lane h (D+1) + row
+    row = np.tile(np.arange(D + 1), 2)
+    out = np.zeros((nch, gpm_frags_per_chunk(D), 8), dtype=np.float16)
+    for ch in range(nch):
+        for kk in range(NK):
+            out[ch, 64 * kk:64 * (kk + 1)] = kexp[ch * 32 + (lane & 31)[:, None], 16 * kk + 8 * (lane >> 5)[:, None] + j]
+        base = 64 * NK
+        for qq in range(2):
+            pt = ch * 32 + sp[qq][hh]                         # [NLS, 8]
+            out[ch, base + 2 * qq * NLS:base + (2 * qq + 1) * NLS] = Ah[row[:, None], pt]
+            out[ch, base + (2 * qq + 1) * NLS:base + (2 * qq + 2) * NLS] = Al[row[:, None], pt]
+    return out, nch, float(2.0 ** sigma)
+
+
+def mfma_emulate(table, n_chunks: int, scale: float, D: int, xi, c):
+    """NumPy model of ``gp_mfma_sums`` read straight from the fragment table:
+    ``S [n, D+1]`` (S0, S'_d, scaled) for centred inputs ``xi [n, D]`` and
+    exponent constants ``c [n]``; f16 operand splits, exact products, float64
+    sums (the device accumulates in f32 and rounds hi toward zero)."""
+    xi = np.asarray(xi, dtype=np.float64)
+    NK, NLS = gpm_k_steps(D), gpm_sum_lanes(D)
+    tab = np.asarray(table, dtype=np.float16).reshape(n_chunks, gpm_frags_per_chunk(D), 8).astype(np.float64)
+    xh, xl = _split16(xi)
+    ch_, cl_ = _split16(np.asarray(c, dtype=np.float64))
+    xs = np.zeros((xi.shape[0], 16 * NK))
+    xs[:, 0:D], xs[:, D:2 * D], xs[:, 2 * D:3 * D] = xh, xh, xl
+    xs[:, 3 * D] = xs[:, 3 * D + 1] = 1.0
+    xs[:, 3 * D + 2], xs[:, 3 * D + 3] = ch_, cl_
+    lane = np.arange(64)
+    j = np.arange(8)
+    sp = _sum_points()
+    hh = np.repeat(np.arange(2), D + 1)
+    row = np.tile(np.arange(D + 1), 2)
+    S = np.zeros((xi.shape[0], D + 1))
+    for ch in range(n_chunks):
+        kexp = np.zeros((32, 16 * NK))
+        for kk in range(NK):
+            kexp[(lane & 31)[:, None], 16 * kk + 8 * (lane >> 5)[:, None] + j] = tab[ch, 64 * kk:64 * (kk + 1)]
+        e = (xs @ kexp.T).astype(np.float32)                   # [n, 32 points]
+        A = np.zeros((2, D + 1, 32))
+        base = 64 * NK
+        for qq in range(2):
+            for s in range(2):
+                A[s][row[:, None], sp[qq][hh]] = tab[ch, base + (2 * qq + s) * NLS:base + (2 * qq + s + 1) * NLS]
+        m = np.exp2(e).astype(np.float32)
+        mh = m.astype(np.float16).astype(np.float64)
+        ml = (m - mh).astype(np.float16).astype(np.float64)
+        S += mh @ A[0].T + ml @ A[0].T + mh @ A[1].T
+    return S * scale
+
+
+# --------------------------------------------------------------------------
 # synthetic targets ("random-init" physics stand-ins)
 
 def tip_bhr_target(band: int):

@@ -15,6 +15,7 @@ import os
 import numpy as np
 import torch
 
+from ..models.gp import gpm_frags_per_chunk
 from ..utils.blocks import ntri
 from . import _ext
 
@@ -86,6 +87,7 @@ class BandTable:
     keepalive: tuple
     fast_d: int = 0
     fast_obs: int = 0
+    gpm_frags: int = 0      # > 0: GP on the matrix cores, LDS fragments of all bands (kf_gp_mfma.h)
 
     @property
     def ptr(self) -> int:
@@ -96,6 +98,9 @@ OP_PRECOMP = 0
 OP_LINEAR = 1
 OP_GP = 2
 
+
+# LDS budget of the matrix-core GP analysis (every band's table staged per workgroup)
+GPM_MAX_LDS = 160 * 1024
 
 FD_PRECOMP = -1   # kf_core.h: fast analysis kernel for all-precomputed operators
 FD_LINEAR = -2    # kf_core.h: fast analysis kernel for all-linear (identity/selection) operators
@@ -130,7 +135,12 @@ def make_band_table(descs: list, device, keepalive=()) -> BandTable:
         fast_d, fast_obs = FD_PRECOMP, one_obs
     elif descs and one_obs in (OBS_F32, OBS_DN16, OBS_BF16) and all(d.op == OP_LINEAR for d in descs):
         fast_d, fast_obs = FD_LINEAR, one_obs
-    return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs)
+    gpm_frags = 0
+    if fast_d > 0 and all(d.gpm_nchunk > 0 for d in descs):
+        gpm_frags = sum(d.gpm_nchunk for d in descs) * gpm_frags_per_chunk(fast_d)
+        if gpm_frags * 16 > GPM_MAX_LDS:
+            gpm_frags = 0
+    return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs, gpm_frags)
 
 
 # ------------------------------------------------------------------ ops
@@ -201,6 +211,7 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     a.N, a.ld, a.n_bands, a.solve = N, ld, bands.n, int(bool(solve))
     a.fast_d, a.fast_obs = (bands.fast_d, bands.fast_obs) if fast else (0, 0)
     a.variant = DEFAULT_VARIANT if variant is None else int(variant)
+    a.gpm_frags = bands.gpm_frags if fast else 0
     a.bands = bands.ptr
     a.x_prev, a.x_f, a.pf_inv = _ptr(x_prev), _ptr(x_f), _ptr(pf_inv)
     a.x_out, a.a_out, a.b_out = _ptr(x_out), _ptr(a_out), _ptr(b_out)

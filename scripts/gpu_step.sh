@@ -1,0 +1,40 @@
+#!/bin/bash
+# One GPU call = a list of named steps, each under its own time limit, stopping at
+# the first failure (gpurun rules: no retries, nothing after a fault/timeout).
+#   bash scripts/gpu_step.sh tests[:FILTER] mfma_ab bench[:ARGS] prof[:ARGS] pmc:COUNTERS ...
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" && mkdir -p gpurun_out
+export PYTHONPATH="$R${PYTHONPATH:+:$PYTHONPATH}"
+stop() { echo "!! step $1 rc=$2"; exit "$2"; }
+for step in "$@"; do
+  name=${step%%:*}; arg=""; [ "$name" != "$step" ] && arg=${step#*:}
+  case $name in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${arg:+-k "$arg"} \
+        > gpurun_out/gpu_tests.log 2>&1 || { rc=$?; tail -40 gpurun_out/gpu_tests.log; stop tests $rc; }
+      tail -3 gpurun_out/gpu_tests.log ;;
+    smoke)
+      timeout -k 10 300 python -u __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 || { rc=$?; tail -20 gpurun_out/smoke.log; stop smoke $rc; }
+      tail -1 gpurun_out/smoke.log ;;
+    ab)
+      timeout -k 10 400 python -u scripts/bench_kernels.py $arg > gpurun_out/ab.log 2>&1 || { rc=$?; tail -20 gpurun_out/ab.log; stop ab $rc; }
+      tail -5 gpurun_out/ab.log ;;
+    bench)
+      timeout -k 10 600 python -u bench.py $arg > gpurun_out/bench.log 2>&1 || { rc=$?; tail -20 gpurun_out/bench.log; stop bench $rc; }
+      tail -1 gpurun_out/bench.log ;;
+    prof)
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run \
+        --output-format csv -- python "$R/bench.py" --steps 4 --warmup 1 $arg > "$R/gpurun_out/prof.log" 2>&1 ) \
+        || { rc=$?; tail -20 gpurun_out/prof.log; stop prof $rc; }
+      echo prof-done ;;
+    pmc)
+      # pmc:V/C1,C2,...  (V = analysis variant, one counter pass per step)
+      v=${arg%%/*}; ctrs=${arg#*/}; tag=${PMC_TAG:-pmc}_v${v}_$(echo "$ctrs" | md5sum | cut -c1-6)
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc ${ctrs//,/ } -d "$R/gpurun_out/pmc" -o "$tag" \
+        --output-format csv -- python "$R/scripts/bench_kernels.py" --rounds 1 --variants $v > "$R/gpurun_out/pmc.log" 2>&1 ) \
+        || { rc=$?; tail -20 gpurun_out/pmc.log; stop pmc $rc; }
+      echo pmc-done ;;
+    *) echo "unknown step $name"; exit 2 ;;
+  esac
+done

@@ -25,7 +25,7 @@ def close(a, b, tol=1e-3, floor=0.05):
     return float(((a - b).abs() / scale).max()) < tol
 
 
-def _analysis(prob, device):
+def _analysis(prob, device, variant=None):
     N, n = prob["N"], prob["n"]
     tab = C.table(prob, device)
     xo = torch.zeros((n, N), device=device)
@@ -33,7 +33,7 @@ def _analysis(prob, device):
     st = torch.zeros(N, dtype=torch.uint8, device=device)
     part = K.partials_buffer(N, device)
     K.analysis(n, tab, C.soa(prob["x"], device), C.soa(prob["xf"], device), C.packed(prob["Pf"], device), xo, ao,
-               None, st, part)
+               None, st, part, variant=variant)
     red = K.reduce_partials(part)
     return xo.cpu(), ao.cpu(), st.cpu(), float(red.cpu().item())
 
@@ -45,8 +45,10 @@ def test_native_extension_is_loaded(cuda):
 
 @pytest.mark.parametrize("dn16", [False, True])
 def test_analysis_device_vs_host_and_oracle(cuda, dn16):
+    """VALU record loop (variant 4) vs the host runner of the same source, and
+    the default matrix-core GP (kf_gp_mfma.h) vs the float64 oracle."""
     prob = C.tip_problem(N=20000, dn16=dn16, seed=11)
-    xd, ad, sd, rd = _analysis(prob, cuda)
+    xd, ad, sd, rd = _analysis(prob, cuda, variant=4)
     xh, ah, sh, rh = _analysis(prob, "cpu")
     assert torch.equal(sd, sh)
     assert close(xd, xh)
@@ -54,6 +56,17 @@ def test_analysis_device_vs_host_and_oracle(cuda, dn16):
     assert abs(rd - rh) / rh < 1e-4
     xr, Ar = analysis_blocks(prob["x"], prob["xf"], prob["Pf"], C.oracle_bands(prob, prob["x"]))
     assert np.max(np.abs(xd.numpy().T - xr) / (np.abs(xr) + 0.05)) < 2e-3
+    xm, am, sm, rm = _analysis(prob, cuda)
+    assert torch.equal(sm, sh)
+    assert np.max(np.abs(xm.numpy().T - xr) / (np.abs(xr) + 0.05)) < 2e-3
+    # A against the oracle, entries scaled by sqrt(A_ii A_jj); the f32 VALU path
+    # on the host is the yardstick (both f32 Jacobians of cancelling GP sums)
+    d = np.sqrt(np.einsum("nii->ni", Ar))
+    norm = d[:, :, None] * d[:, None, :]
+    err_m = np.max(np.abs(unpack_blocks(am.numpy(), 7) - Ar) / norm)
+    err_h = np.max(np.abs(unpack_blocks(ah.numpy(), 7) - Ar) / norm)
+    assert err_m < max(2e-4, 1.5 * err_h), (err_m, err_h)
+    assert abs(rm - rh) / rh < 1e-2
 
 
 def test_propagate_and_invert_device(cuda):
