@@ -13,6 +13,9 @@
 
 namespace py = pybind11;
 using namespace kf;
+namespace kf {
+void bind_tiff(py::module_& m);   // kf_tiff.cpp
+}
 
 template <typename T>
 static T* P(uintptr_t v) { return reinterpret_cast<T*>(v); }
@@ -153,6 +156,8 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(JacobiArgs, a_out, float*)
       .PTR_FIELD(JacobiArgs, partials, double*)
       .def_readwrite("mode", &JacobiArgs::mode)
+      .def_readwrite("p0", &JacobiArgs::p0)
+      .def_readwrite("pn", &JacobiArgs::pn)
       .def_readwrite("k", &JacobiArgs::k)
       .PTR_FIELD(JacobiArgs, u, const float*)
       .PTR_FIELD(JacobiArgs, v, float*)
@@ -255,4 +260,5 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
   });
 
   bind_stream(m);
+  bind_tiff(m);
 }

@@ -158,7 +158,7 @@ struct AnalysisArgs {
   int32_t n_bands, solve;
   int32_t fast_d, fast_obs;  // host hint: all bands GP with fast_d inputs, one encoding (0: generic)
   int32_t variant;           // kernel variant selector (tuning; 0 = default)
-  int32_t gpm_frags;         // > 0: every band has an MFMA table, fragments of all bands (LDS / 16 B)
+  int32_t gpm_frags;         // > 0: every band has an MFMA table; LDS fragments (16 B) of all bands + 1 zero
   const BandDesc* bands;
   const float* x_prev;   // [NP][ld] linearisation point
   const float* x_f;      // [NP][ld] forecast mean
@@ -596,20 +596,30 @@ KF_HD bool eval_operator(const BandDesc& bd, int64_t p, int64_t ld, const float 
 //   xf_j = m_j x_a,j (propagated) | mu_j (reset)
 //   Pf   = C^-1 with diag_j = 1 / (1 / P_a,jj + q_j) for propagated j.
 template <int NP>
-KF_HD void forecast_partial(const KF_CONST_AS PropArgs* a, int64_t p, float (&xf)[NP], float (&P)[ntri(NP)]) {
-  constexpr int NT = ntri(NP);
+KF_HD void forecast_partial_mean(const KF_CONST_AS PropArgs* a, int64_t p, float (&xf)[NP]) {
+#pragma unroll
+  for (int j = 0; j < NP; ++j)
+    xf[j] = ((a->prop_mask >> j) & 1u) ? a->m[j] * a->x_a[j * a->ld + p] : a->reset_mean[j];
+}
+
+template <int NP>
+KF_HD void forecast_partial_precision(const KF_CONST_AS PropArgs* a, int64_t p, float (&P)[ntri(NP)]) {
   const int64_t ld = a->ld;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) P[t] = a->reset_cinv[t];
+  for (int t = 0; t < ntri(NP); ++t) P[t] = a->reset_cinv[t];
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
-    xf[j] = a->reset_mean[j];
     if ((a->prop_mask >> j) & 1u) {
       const float q = a->q_pix ? a->q_pix[j * ld + p] : a->q[j];
-      xf[j] = a->m[j] * a->x_a[j * ld + p];
       P[tri(NP, j, j)] = kf_rcp(kf_rcp(a->p_a[tri(NP, j, j) * ld + p]) + q);
     }
   }
+}
+
+template <int NP>
+KF_HD void forecast_partial(const KF_CONST_AS PropArgs* a, int64_t p, float (&xf)[NP], float (&P)[ntri(NP)]) {
+  forecast_partial_precision<NP>(a, p, P);
+  forecast_partial_mean<NP>(a, p, xf);
 }
 
 // forecast_pixel computes the forecast (xf, P) of pixel p without storing it;
@@ -1090,6 +1100,7 @@ struct JacobiArgs {
   float* v;              // [k*NP][ld]  column c of V = A_reg^-1 e_{R_c} (PREPARE writes)
   float* z_out;          // [k][ld_ext] regularised components (SWEEP writes the local part)
   StripGeo geo;          // dense strip: neighbours from the index (nbr unused)
+  int64_t p0, pn;        // pixel range [p0, p0 + pn) of this launch (pn = 0: all N); C2 overlap
 };
 
 template <typename JA>

@@ -27,8 +27,9 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+template <int BS = BLOCK>
 __device__ __forceinline__ void block_partial(double v, double* partials) {
-  __shared__ double red[BLOCK / 64];
+  __shared__ double red[BS / 64];
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (lane == 0) red[wid] = v;
@@ -36,7 +37,7 @@ __device__ __forceinline__ void block_partial(double v, double* partials) {
   if (threadIdx.x == 0) {
     double s = 0.0;
 #pragma unroll
-    for (int i = 0; i < BLOCK / 64; ++i) s += red[i];
+    for (int i = 0; i < BS / 64; ++i) s += red[i];
     partials[blockIdx.x] = s;
   }
 }
@@ -52,9 +53,12 @@ __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
 
 // K1 with the GP on the matrix cores (kf_gp_mfma.h).  Every band's split-f16
 // table is staged in LDS once per workgroup (a.gpm_frags x 16 B of dynamic
-// LDS), then each wave walks 64-pixel tiles grid-stride.
-template <int NP, int D, int FOBS, int BPP>
-__global__ __launch_bounds__(BLOCK) void analysis_mfma_kernel(AnalysisArgs a) {
+// LDS), then each wave walks 64-pixel tiles grid-stride.  BS = 512 with
+// MINW = 4 waves per SIMD (<= 128 VGPRs, 2 workgroups per CU for two bands'
+// tables) lets the HBM phases (state loads, result stores) of some waves run
+// under the record loops of others; BS = 256 gives 3 waves per SIMD.
+template <int NP, int D, int FOBS, int BPP, int BS = BLOCK, int MINW = 1, int NBM = 2>
+__global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   extern __shared__ kf_h8 gpm_lds[];
   {
@@ -63,21 +67,22 @@ __global__ __launch_bounds__(BLOCK) void analysis_mfma_kernel(AnalysisArgs a) {
       const KF_CONST_AS BandDesc* bd = cptr(a.bands) + bi;
       const int n = bd->gpm_nchunk * gpm_frags_per_chunk(D);
       const kf_h8* src = (const kf_h8*)bd->gpm;
-      for (int i = threadIdx.x; i < n; i += BLOCK) gpm_lds[off + i] = src[i];
+      for (int i = threadIdx.x; i < n; i += BS) gpm_lds[off + i] = src[i];
       off += n;
     }
+    if (threadIdx.x == 0) gpm_lds[a.gpm_frags - 1] = kf_h8{};   // shared zero fragment
   }
   __syncthreads();
   double acc = 0.0;
   const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * BLOCK;
-  for (int64_t base = (int64_t)blockIdx.x * BLOCK + (threadIdx.x - lane); base < a.N; base += stride) {
+  const int64_t stride = (int64_t)gridDim.x * BS;
+  for (int64_t base = (int64_t)blockIdx.x * BS + (threadIdx.x - lane); base < a.N; base += stride) {
     const int64_t p = base + lane;
     const bool act = p < a.N;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, BPP>(a, act ? p : a.N - 1, act, gpm_lds);
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, BPP, NBM>(a, act ? p : a.N - 1, act, gpm_lds);
     acc += act ? (double)dn : 0.0;
   }
-  if (a.partials) block_partial(acc, a.partials);
+  if (a.partials) block_partial<BS>(acc, a.partials);
 #endif
 }
 
@@ -94,8 +99,9 @@ template <int NP>
 __global__ __launch_bounds__(BLOCK) void jacobi_kernel(JacobiArgs a) {
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
-  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
-    acc += (double)pixel_jacobi<NP>(a, p);
+  const int64_t n = a.pn > 0 ? a.pn : a.N;
+  for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride)
+    acc += (double)pixel_jacobi<NP>(a, a.p0 + i);
   if (a.partials) block_partial(acc, a.partials);
 }
 
@@ -259,17 +265,19 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
   // GP on the matrix cores when the host attached split-f16 tables to every band
   // (variant 4 forces the VALU record loop, for A/B)
   if constexpr (FD > 0 && FD <= GPM_MAX_D) {
-    if (a.gpm_frags > 0 && a.variant != 4) {
-      // variant 5: one 32-pixel column block per pass (A/B against the default 2)
+    if (a.gpm_frags > 0 && a.variant != 4 && a.n_bands <= GPM_MAX_BANDS) {
+      // variant 5 (A/B): one 32-pixel column block per pass
       const size_t lds = (size_t)a.gpm_frags * sizeof(kf_h8);
-#define KF_MFMA_LAUNCH(OBS_)                                                                               \
-  if (a.variant == 5) {                                                                                    \
-    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, 1>, lds);                                              \
-    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, 1>), dim3(grid), dim3(BLOCK), lds, s, a);      \
-  } else {                                                                                                 \
-    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, 2>, lds);                                              \
-    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, 2>), dim3(grid), dim3(BLOCK), lds, s, a);      \
+#define KF_MFMA_GO(OBS_, BPP_, BS_, MINW_, NBM_)                                                             \
+  {                                                                                                          \
+    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, BPP_, BS_, MINW_, NBM_>, lds);                          \
+    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, BPP_, BS_, MINW_, NBM_>), dim3(grid), dim3(BS_), \
+                       lds, s, a);                                                                           \
   }
+#define KF_MFMA_LAUNCH(OBS_)                                                                                 \
+  if (a.n_bands > 2) KF_MFMA_GO(OBS_, 2, BLOCK, 1, GPM_MAX_BANDS)                                          \
+  else if (a.variant == 5) KF_MFMA_GO(OBS_, 1, BLOCK, 1, 2)                                                  \
+  else KF_MFMA_GO(OBS_, 2, BLOCK, 1, 2)
       if (a.fast_obs == OBS_DN16) {
         KF_MFMA_LAUNCH(OBS_DN16)
       } else if (a.fast_obs == OBS_F32) {
@@ -278,6 +286,7 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
         return false;
       }
 #undef KF_MFMA_LAUNCH
+#undef KF_MFMA_GO
       return true;
     }
   }

@@ -43,6 +43,8 @@ KF_HD constexpr int gpm_sum_lanes(int D) { return 2 * (D + 1); }
 // 16-byte fragments per 32-point chunk
 KF_HD constexpr int gpm_frags_per_chunk(int D) { return 64 * gpm_k_steps(D) + 4 * gpm_sum_lanes(D); }
 constexpr int GPM_MAX_D = 10;
+// bands whose sums are held across the record loops (larger tables fall back to VALU)
+constexpr int GPM_MAX_BANDS = 4;
 
 #if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ uint32_t gpm_pack(_Float16 a, _Float16 b) {
@@ -72,6 +74,16 @@ __device__ __forceinline__ kf_u4 gpm_xfrag(int k0, const _Float16 (&xh)[D], cons
   return v;
 }
 
+// x of lane l ^ 32 (v_permlane32_swap: a VALU op, no LDS round trip; the
+// compiler pads its VALU-write hazard itself).  Call it unconditionally from
+// every lane and select afterwards: under a divergent branch the swap would
+// read inactive partner lanes (fetch-inactive is also set for safety).
+__device__ __forceinline__ float gpm_partner32(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, true, false);
+  return __builtin_bit_cast(float, (threadIdx.x & 32) ? r[0] : r[1]);
+}
+
 __device__ __forceinline__ void gpm_split16(float v, _Float16& h, _Float16& l) {
   h = (_Float16)v;
   l = (_Float16)(v - (float)h);
@@ -82,16 +94,20 @@ __device__ __forceinline__ void gpm_split16(float v, _Float16& h, _Float16& l) {
 template <int D>
 __device__ __forceinline__ void gpm_operand(const float (&xi)[D], float c, int blk,
                                             kf_h8 (&xb)[gpm_k_steps(D)]) {
-  const int lane = threadIdx.x & 63;
-  const int src = 32 * blk + (lane & 31);
+  // column col of block blk is pixel 32 blk + col: this lane's own pixel when
+  // its half h equals blk, else the pixel of lane l ^ 32
+  const bool h1 = (threadIdx.x & 32) != 0;
+  const bool own = (h1 ? 1 : 0) == blk;
   _Float16 xh[D], xl[D], ch, cl;
 #pragma unroll
   for (int d = 0; d < D; ++d) {
+    const float pv = gpm_partner32(xi[d]);
+    const float v = own ? xi[d] : pv;
     // clamp: f16 range (a state that far out has k = 0 anyway through c)
-    gpm_split16(fminf(fmaxf(__shfl(xi[d], src, 64), -6.0e4f), 6.0e4f), xh[d], xl[d]);
+    gpm_split16(fminf(fmaxf(v, -6.0e4f), 6.0e4f), xh[d], xl[d]);
   }
-  gpm_split16(fmaxf(__shfl(c, src, 64), -6.0e4f), ch, cl);
-  const bool h1 = lane >= 32;
+  const float pc = gpm_partner32(c);
+  gpm_split16(fmaxf(own ? c : pc, -6.0e4f), ch, cl);
 #pragma unroll
   for (int kk = 0; kk < gpm_k_steps(D); ++kk) {
     const kf_u4 f0 = gpm_xfrag<D>(16 * kk, xh, xl, ch, cl), f1 = gpm_xfrag<D>(16 * kk + 8, xh, xl, ch, cl);
@@ -103,17 +119,30 @@ __device__ __forceinline__ void gpm_operand(const float (&xi)[D], float c, int b
 // and lo = f16(m - hi).
 __device__ __forceinline__ void gpm_exp_split(const kf_f16v& e, int r0, kf_h8& mh, kf_h8& ml) {
   kf_u4 hv, lv;
+  // two pairs at a time: both low halves, then both high halves (no
+  // back-to-back partial writes of one register, which cost an s_nop)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float m0 = kexp2(e[r0 + 2 * q]), m1 = kexp2(e[r0 + 2 * q + 1]);
-    const kf_hp2 h = __builtin_amdgcn_cvt_pkrtz(m0, m1);
-    hv[q] = __builtin_bit_cast(uint32_t, h);
-    // lo of both halves with two mixed-precision FMAs (-hi * 1 + m): v_fma_mix
-    // reads hi as f16 straight from the packed register
-    uint32_t l;
-    asm volatile("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(hv[q]), "v"(m0));
-    asm volatile("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hv[q]), "v"(m1));
-    lv[q] = l;
+  for (int q = 0; q < 4; q += 2) {
+    float m[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m[j] = kexp2(e[r0 + 2 * q + j]);
+    hv[q] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(m[0], m[1]));
+    hv[q + 1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(m[2], m[3]));
+    // lo = f16(m - hi) with mixed-precision FMAs (-hi * 1 + m): v_fma_mix reads
+    // hi as f16 straight from the packed register
+    asm volatile("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lv[q]) : "v"(hv[q]), "v"(m[0]));
+    asm volatile("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lv[q + 1]) : "v"(hv[q + 1]), "v"(m[2]));
+    asm volatile("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                 : "+v"(lv[q]) : "v"(hv[q]), "v"(m[1]));
+    if (q == 0) {
+      asm volatile("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                   : "+v"(lv[q + 1]) : "v"(hv[q + 1]), "v"(m[3]));
+    } else {
+      // last writer of the MFMA B operand ml: VALU write -> MFMA SrcB read needs
+      // 2 wait states, and hipcc pads only one after an asm statement
+      asm volatile("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\ts_nop 1"
+                   : "+v"(lv[q + 1]) : "v"(hv[q + 1]), "v"(m[3]));
+    }
   }
   mh = __builtin_bit_cast(kf_h8, hv);
   ml = __builtin_bit_cast(kf_h8, lv);
@@ -125,15 +154,18 @@ __device__ __forceinline__ void gpm_exp_split(const kf_f16v& e, int r0, kf_h8& m
 // must call it (MFMA); lanes without an observation pass any finite x.
 // BPP = column blocks (of 32 pixels) per pass sharing each chunk's A fragments.
 template <int D, int BPP = 2>
-__device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, int nchunk, const float (&xi)[D],
-                                             float c, float (&S)[D + 1]) {
+__device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, const kf_h8* __restrict__ zf, int nchunk,
+                                             const float (&xi)[D], float c, float (&S)[D + 1]) {
   static_assert(D >= 1 && D <= GPM_MAX_D, "GP input count for the matrix-core path");
   static_assert(BPP == 1 || BPP == 2, "column blocks per pass");
   constexpr int NK = gpm_k_steps(D), NLS = gpm_sum_lanes(D), FPC = gpm_frags_per_chunk(D);
   const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
-  // sums fragment of this lane; rows > D read fragment 0: finite values that
-  // only reach accumulator rows nobody reads (no exec-mask branch, no zeroing)
-  const int is = 64 * NK + (col <= D ? h * (D + 1) + col : 0);
+  // sums fragments of this lane; rows > D read the shared zero fragment zf
+  // (stride 0): no exec-mask branch, and zero rows keep the matrix cores'
+  // switching energy (and so the DVFS clock penalty) down
+  const bool ls = col <= D;
+  const kf_h8* sp = ls ? tab + 64 * NK + h * (D + 1) + col : zf;
+  const int sstep = ls ? FPC : 0, soff = ls ? NLS : 0;
   const kf_f16v zero = {};
 #pragma unroll
   for (int f = 0; f <= D; ++f) S[f] = 0.f;
@@ -153,34 +185,38 @@ __device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, int 
       kf_h8 ea[NK], sa[2][2];
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) ea[kk] = t[64 * kk + lane];
+      const kf_h8* st = sp + ch * sstep;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        sa[q][0] = t[is + (2 * q) * NLS];
-        sa[q][1] = t[is + (2 * q + 1) * NLS];
+        sa[q][0] = st[(2 * q) * soff];
+        sa[q][1] = st[(2 * q + 1) * soff];
       }
 #pragma unroll
       for (int i = 0; i < BPP; ++i) {
         kf_f16v e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[0], xb[i][0], zero, 0, 0, 0);
 #pragma unroll
         for (int kk = 1; kk < NK; ++kk) e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[kk], xb[i][kk], e, 0, 0, 0);
+        kf_h8 mh[2], ml[2];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          kf_h8 mh, ml;
-          gpm_exp_split(e, 8 * q, mh, ml);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][0], mh, acc[i], 0, 0, 0);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][0], ml, acc[i], 0, 0, 0);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][1], mh, acc[i], 0, 0, 0);
+          gpm_exp_split(e, 8 * q, mh[q], ml[q]);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][0], mh[q], acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][0], ml[q], acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][1], mh[q], acc[i], 0, 0, 0);
         }
       }
     }
-    // field f sits in register (f&3) + 4(f>>3) of lanes h = (f>>2)&1 for pixel
-    // 32 blk + col; bring fields 0..D of the lane's own pixel (blk = h) home.
+    // field f of pixel 32 blk + col sits in register (f&3) + 4(f>>3) of lane
+    // 32 ((f>>2)&1) + col: the lane itself or its partner l ^ 32
 #pragma unroll
     for (int i = 0; i < BPP; ++i) {
+      const int blk = pass * BPP + i;
 #pragma unroll
       for (int f = 0; f <= D; ++f) {
-        const float v = __shfl(acc[i][(f & 3) + 4 * (f >> 3)], 32 * ((f >> 2) & 1) + col, 64);
-        S[f] = h == pass * BPP + i ? v : S[f];
+        const float mine = acc[i][(f & 3) + 4 * (f >> 3)];
+        const float theirs = gpm_partner32(mine);
+        const float v = (((f >> 2) & 1) == h) ? mine : theirs;
+        S[f] = h == blk ? v : S[f];
       }
     }
   }
@@ -196,7 +232,12 @@ namespace kf {
 // lanes run the band loop (act = false for the tail lanes past N: clamped
 // reads, no stores); the GP is skipped only when no lane of the wave has an
 // observation of the band (wave-level cloud skip).
-template <int NP, int D, int FOBS, int BPP = 2>
+// (A two-phase variant -- every band's GP sums first, the forecast precision
+// and normal equations afterwards, 8 fewer VGPRs -- gave intermittently wrong
+// pixels on some waves under full occupancy on MI355X while this order never
+// did (scripts/debug_mfma_tiles.py, r2 bisect); tests/test_gpu_mfma.py
+// ::test_gp_mfma_realistic_tile_matches_valu guards it.)
+template <int NP, int D, int FOBS, int BPP = 2, int NBM = 2>
 __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
                                                      const kf_h8* lds) {
   constexpr int NT = ntri(NP);
@@ -249,7 +290,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
       }
       c *= -0.5f * LOG2E;
       float S[D + 1];
-      gp_mfma_sums<D, BPP>(lds + off, nch, xi, c, S);
+      gp_mfma_sums<D, BPP>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
       const KF_CONST_AS BandDesc* q = opaque(bdp);   // epilogue fields: not live across the chunk loop
       const float sc = q->gpm_scale;
       float Sd[D];

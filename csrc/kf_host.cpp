@@ -47,7 +47,7 @@ static int h_gain(const GainArgs& a, int grid) {
 }
 template <int NP>
 static int h_jacobi(const JacobiArgs& a, int grid) {
-  grid_stride(a.N, grid, a.partials, [&](int64_t p) { return pixel_jacobi<NP>(a, p); });
+  grid_stride(a.pn > 0 ? a.pn : a.N, grid, a.partials, [&](int64_t i) { return pixel_jacobi<NP>(a, a.p0 + i); });
   return 0;
 }
 template <int NP>

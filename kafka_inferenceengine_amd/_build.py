@@ -99,7 +99,7 @@ def build(force: bool = False, verbose: bool = False, checked: bool = False) -> 
     objs.append(obj)
 
     # 3. bindings + ingest runtime (host code, HIP runtime API)
-    for name in ("kf_bindings.cpp", "kf_stream.cpp"):
+    for name in ("kf_bindings.cpp", "kf_stream.cpp", "kf_tiff.cpp"):
         src, obj = CSRC / name, build_dir / (Path(name).stem + ".o")
         if force or _stale(obj, [src] + hdrs):
             jobs.append(["g++", *common, *hip_defs, *_pybind_includes(), "-fvisibility=hidden", "-c", str(src),
@@ -113,7 +113,7 @@ def build(force: bool = False, verbose: bool = False, checked: bool = False) -> 
                 f.result()
 
     if force or _stale(ext_path, objs):
-        _run([hipcc, "-shared", "-fPIC", *map(str, objs), "-o", str(ext_path), "-lgomp", "-lpthread",
+        _run([hipcc, "-shared", "-fPIC", *map(str, objs), "-o", str(ext_path), "-lgomp", "-lpthread", "-lz",
               f"-L{ROCM / 'lib'}", "-lamdhip64"], verbose)
     return ext_path
 

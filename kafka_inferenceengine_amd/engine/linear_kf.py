@@ -116,6 +116,7 @@ class LinearKalman:
         self._reg = None
         self._reg_uv = None             # affine regulariser: u = A_reg^-1 b, V = A_reg^-1 E_R, x0
         self._reg_geo = None
+        self.reg_overlapped_sweeps = 0    # C2 sweeps whose halo exchange ran under the interior rows
         self._output_written = None
         band = getattr(self.comm, "band", None)
         self.band_comm = band if (band is not None and band.world > 1) else None
@@ -928,10 +929,26 @@ class LinearKalman:
         z = reg.z_buffers(k)
         z[0][:, :N].copy_(x_ref[rows, :N])
         cur = reg.fill_halo(z[0])
+        # C2 overlap on dense strips: the rows the neighbours need first, their
+        # exchange posted, then the interior while the rows are on the wire
+        w = geo["w"] if geo else 0
+        overlap = self.comm.distributed and w > 0 and N > 2 * w
         for _ in range(sweeps - 1):
             nxt = z[1] if cur is z[0] else z[0]
-            K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo)
-            cur = reg.fill_halo(nxt)
+            if overlap:
+                with self.timer.phase("reg_boundary"):
+                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(0, w))
+                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(N - w, w))
+                with self.timer.phase("halo"):
+                    pend = reg.start_fill(nxt)
+                with self.timer.phase("reg_interior"):
+                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(w, N - 2 * w))
+                with self.timer.phase("halo"):
+                    cur = reg.finish_fill(pend, nxt)
+                self.reg_overlapped_sweeps += 1
+            else:
+                K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo)
+                cur = reg.fill_halo(nxt)
         K.reg_finish(n, u, v, cur, nbr, x_ref, x_out, gamma, reg.reg_mask, N, partials=self._partials, geo=geo)
 
     # ------------------------------------------------ band-parallel (TP-like)

@@ -1,4 +1,11 @@
-"""Minimal GeoTIFF writer/reader (GDAL is not available in this stack).
+"""GeoTIFF writer/reader (GDAL is not available in this stack).
+
+The hot paths are native (``csrc/kf_tiff.cpp``, thread-pool DEFLATE of tiles /
+strips straight into or out of caller buffers): ``write_tiff`` writes tiled
+DEFLATE GeoTIFFs with EPSG GeoKeys, ``read_tiff`` / ``read_tiff_window`` decode
+strips or tiles in parallel.  The pure-Python codec below is the fallback for
+layouts the native reader does not take (big-endian, pixel-interleaved) and
+for builds without the extension.
 
 Writes single- or multi-band (planar, ``(bands, H, W)``) rasters (float32 / uint8 / uint16 / int16 / float64) as
 classic or BigTIFF, striped, uncompressed or DEFLATE (the reference writes
@@ -10,6 +17,8 @@ striped files of the reference (e.g. ``Barrax_pivots.tif``).
 """
 from __future__ import annotations
 
+import os
+import re
 import struct
 import zlib
 
@@ -24,8 +33,62 @@ _TSIZE = {1: 1, 2: 1, 3: 2, 4: 4, 5: 8, 11: 4, 12: 8, 16: 8}
 _TFMT = {1: "B", 2: "c", 3: "H", 4: "I", 11: "f", 12: "d", 16: "Q"}
 
 
+_NATIVE_FMT = {np.dtype("uint8"): (8, 1), np.dtype("uint16"): (16, 1), np.dtype("int16"): (16, 2),
+               np.dtype("int32"): (32, 2), np.dtype("uint32"): (32, 1), np.dtype("float32"): (32, 3),
+               np.dtype("float64"): (64, 3)}
+
+
+def _native():
+    try:
+        from ..ops._ext import ext
+    except Exception:  # pragma: no cover
+        return None
+    return ext if (ext is not None and hasattr(ext, "tiff_write")) else None
+
+
+def _threads() -> int:
+    return max(1, min(int(os.environ.get("KAFKA_IO_THREADS", "0")) or (os.cpu_count() or 4), 64))
+
+
+def epsg_of(projection) -> int:
+    """EPSG code of a projection given as an int, ``"EPSG:32630"`` or a WKT
+    with an ``AUTHORITY["EPSG", "..."]`` (the outermost, i.e. last, one); 0 if
+    none is found."""
+    if projection is None:
+        return 0
+    if isinstance(projection, (int, np.integer)):
+        return int(projection)
+    s = str(projection)
+    m = re.findall(r'AUTHORITY\["EPSG",\s*"?(\d+)"?\]', s) or re.findall(r"EPSG:(\d+)", s)
+    return int(m[-1]) if m else 0
+
+
 def write_tiff(path, array, geotransform=None, projection: str | None = None, compress: str | None = "deflate",
-               rows_per_strip: int = 64, bigtiff: bool | None = None, nodata=None):
+               rows_per_strip: int = 64, bigtiff: bool | None = None, nodata=None, tile: int | None = 256,
+               level: int = 6, threads: int | None = None):
+    """Write a 2-D raster or a (bands, H, W) stack.  Native path: tiled
+    (``tile`` px) DEFLATE, parallel compression, EPSG GeoKeys from
+    ``projection``; ``tile=None`` (or no extension) writes the striped Python
+    layout."""
+    a = np.ascontiguousarray(np.asarray(array))
+    if a.dtype == np.bool_:
+        a = a.astype(np.uint8)
+    E = _native() if tile else None
+    if E is not None and a.ndim in (2, 3) and a.dtype in _NATIVE_FMT and a.dtype.byteorder in ("=", "<", "|"):
+        planes = a[None] if a.ndim == 2 else a
+        nb, H, W = planes.shape
+        bits, fmt = _NATIVE_FMT[a.dtype]
+        gt = [float(v) for v in geotransform] if geotransform is not None else []
+        big = -1 if bigtiff is None else int(bool(bigtiff))
+        E.tiff_write(str(path), planes.ctypes.data, nb, H, W, bits, fmt, int(tile),
+                     level if compress == "deflate" else 0, threads or _threads(), gt, epsg_of(projection),
+                     "" if projection is None else str(projection), "" if nodata is None else str(nodata), big)
+        return
+    _write_tiff_py(path, a, geotransform, projection, compress, rows_per_strip, bigtiff, nodata)
+
+
+def _write_tiff_py(path, array, geotransform=None, projection: str | None = None, compress: str | None = "deflate",
+                   rows_per_strip: int = 64, bigtiff: bool | None = None, nodata=None):
     a = np.ascontiguousarray(np.asarray(array))
     if a.ndim not in (2, 3):
         raise ValueError("write_tiff writes 2-D rasters or (bands, H, W) stacks")
@@ -106,8 +169,79 @@ def write_tiff(path, array, geotransform=None, projection: str | None = None, co
         f.write(ext)
 
 
+def _geo_from_native(info) -> dict:
+    out = {"shape": (int(info["height"]), int(info["width"])), "bands": int(info["bands"])}
+    sc, tp = info["pixel_scale"], info["tiepoint"]
+    if len(sc) >= 2 and len(tp) >= 5:
+        out["geotransform"] = [tp[3] - tp[0] * sc[0], sc[0], 0.0, tp[4] + tp[1] * sc[1], 0.0, -sc[1]]
+    if info["geo_ascii"]:
+        out["projection"] = info["geo_ascii"].rstrip("|")
+    keys = list(info["geokeys"])
+    for i in range(4, len(keys) - 3, 4):
+        if keys[i] in (3072, 2048) and keys[i + 1] == 0:
+            out["epsg"] = int(keys[i + 3])
+    if info["nodata"]:
+        out["nodata"] = info["nodata"]
+    return out
+
+
+_NP_OF = {(8, 1): "u1", (16, 1): "u2", (16, 2): "i2", (32, 1): "u4", (32, 2): "i4", (32, 3): "f4", (64, 3): "f8"}
+
+
+def tiff_info(path) -> dict:
+    """Header of a GeoTIFF (native parser): size, bands, layout, georeferencing."""
+    E = _native()
+    if E is None:
+        return read_tiff(path)[1]
+    info = E.tiff_info(str(path))
+    out = _geo_from_native(info)
+    out.update({k: info[k] for k in ("bits", "sample_format", "compression", "predictor", "tiled", "tile",
+                                     "rows_per_strip", "bigtiff", "planar")})
+    out["dtype"] = np.dtype(_NP_OF[(int(info["bits"]), int(info["sample_format"]))])
+    return out
+
+
+def read_tiff_window(path, band: int = 0, window=None, out=None, threads: int | None = None):
+    """Decode one band (rows r0:r1, columns c0:c1 of ``window = (r0, r1, c0,
+    c1)``) into ``out`` (a C-contiguous numpy array or a pinned CPU tensor of
+    the raster dtype) with the native thread pool; returns ``out``."""
+    E = _native()
+    info = E.tiff_info(str(path))
+    H, W = int(info["height"]), int(info["width"])
+    r0, r1, c0, c1 = window if window is not None else (0, H, 0, W)
+    dt = np.dtype(_NP_OF[(int(info["bits"]), int(info["sample_format"]))])
+    if out is None:
+        out = np.empty((r1 - r0, c1 - c0), dtype=dt)
+    ptr = out.data_ptr() if hasattr(out, "data_ptr") else out.ctypes.data
+    nbytes = out.numel() * out.element_size() if hasattr(out, "data_ptr") else out.nbytes
+    if nbytes != (r1 - r0) * (c1 - c0) * dt.itemsize:
+        raise ValueError("out does not match the window")
+    E.tiff_read(str(path), int(band), ptr, r0, r1, c0, c1, threads or _threads())
+    return out
+
+
 def read_tiff(path):
     """-> (array, info dict with geotransform/projection)."""
+    E = _native()
+    if E is not None:
+        try:
+            info = E.tiff_info(str(path))
+        except RuntimeError:
+            info = None   # big-endian etc.: Python codec below
+        if info is not None and (int(info["bands"]) == 1 or int(info["planar"]) == 2) and \
+                (int(info["bits"]), int(info["sample_format"])) in _NP_OF and \
+                int(info["compression"]) in (1, 8, 32946):
+            H, W, nb = int(info["height"]), int(info["width"]), int(info["bands"])
+            dt = np.dtype(_NP_OF[(int(info["bits"]), int(info["sample_format"]))])
+            arr = np.empty((nb, H, W), dtype=dt)
+            for b in range(nb):
+                E.tiff_read(str(path), b, arr[b].ctypes.data, 0, H, 0, W, _threads())
+            return (arr[0] if nb == 1 else arr), _geo_from_native(info)
+    return _read_tiff_py(path)
+
+
+def _read_tiff_py(path):
+    """Pure-Python reader (strips, uncompressed / DEFLATE, either byte order)."""
     with open(path, "rb") as f:
         b = f.read()
     bo = "<" if b[:2] == b"II" else ">"

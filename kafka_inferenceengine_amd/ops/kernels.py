@@ -137,7 +137,7 @@ def make_band_table(descs: list, device, keepalive=()) -> BandTable:
         fast_d, fast_obs = FD_LINEAR, one_obs
     gpm_frags = 0
     if fast_d > 0 and all(d.gpm_nchunk > 0 for d in descs):
-        gpm_frags = sum(d.gpm_nchunk for d in descs) * gpm_frags_per_chunk(fast_d)
+        gpm_frags = sum(d.gpm_nchunk for d in descs) * gpm_frags_per_chunk(fast_d) + 1   # + zero fragment
         if gpm_frags * 16 > GPM_MAX_LDS:
             gpm_frags = 0
     return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs, gpm_frags)
@@ -361,8 +361,10 @@ def reg_prepare(n_params, a_in, b_in, nbr, u_out, v_out, gamma, reg_mask, N, a_o
     ext().jacobi(n_params, a, grid_for(N), _dev(a_in), _stream(a_in))
 
 
-def reg_sweep(n_params, u, v, z_ext, nbr, z_out, gamma, reg_mask, N, geo=None):
-    """K9 affine sweep of the k regularised fields: z_out[:, :N] = u_R + g V_RR s(z_ext)."""
+def reg_sweep(n_params, u, v, z_ext, nbr, z_out, gamma, reg_mask, N, geo=None, rows=None):
+    """K9 affine sweep of the k regularised fields: z_out[:, :N] = u_R + g V_RR s(z_ext).
+    ``rows = (p0, n)`` restricts it to local pixels [p0, p0 + n) (C2 overlap: the
+    boundary rows first, then the interior while the halo is in flight)."""
     check_np(n_params)
     dev = u.device
     k = bin(int(reg_mask)).count("1")
@@ -375,7 +377,15 @@ def reg_sweep(n_params, u, v, z_ext, nbr, z_out, gamma, reg_mask, N, geo=None):
     a = _reg_args(n_params, JACOBI_SWEEP, N, u.shape[1], gamma, reg_mask, nbr, geo)
     a.ld_ext = z_ext.shape[1]
     a.u, a.v, a.x_ext, a.z_out = map(_ptr, (u, v, z_ext, z_out))
-    ext().jacobi(n_params, a, grid_for(N), _dev(u), _stream(u))
+    n = N
+    if rows is not None:
+        p0, n = int(rows[0]), int(rows[1])
+        if p0 < 0 or n < 0 or p0 + n > N:
+            raise ValueError(f"sweep rows {rows} outside [0, {N})")
+        if n == 0:
+            return
+        a.p0, a.pn = p0, n
+    ext().jacobi(n_params, a, grid_for(n), _dev(u), _stream(u))
 
 
 def reg_finish(n_params, u, v, z_ext, nbr, x_ref, x_out, gamma, reg_mask, N, partials=None, geo=None):

@@ -54,6 +54,18 @@ class PendingSum:
         return total
 
 
+class PendingP2P:
+    """Posted C2 transfers (``Comm.exchange_halo_async``)."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
+
+
 class Comm:
     def __init__(self, rank: int = 0, world: int = 1, device=None, group=None, ranks=None, band=None):
         self.rank = rank
@@ -183,22 +195,32 @@ class Comm:
 
     def exchange_halo(self, send_up: torch.Tensor | None, send_down: torch.Tensor | None,
                       recv_up: torch.Tensor | None, recv_down: torch.Tensor | None):
-        """C2: send my first rows to rank-1 / last rows to rank+1 and receive their
-        boundary rows.  Empty tensors are skipped consistently on both sides."""
+        """C2 (blocking): send my first rows to rank-1 / last rows to rank+1 and
+        receive their boundary rows.  Empty tensors are skipped consistently on
+        both sides."""
+        self.exchange_halo_async(send_up, send_down, recv_up, recv_down).wait()
+
+    def exchange_halo_async(self, send_up: torch.Tensor | None, send_down: torch.Tensor | None,
+                            recv_up: torch.Tensor | None, recv_down: torch.Tensor | None) -> "PendingP2P":
+        """C2 posted without waiting.  On RCCL the transfers run on the process
+        group's own stream, ordered after the work already queued on the current
+        stream (the pack kernels); ``wait()`` makes the current stream wait for
+        them (no host block), so kernels queued in between overlap the
+        transfer."""
         if not self.distributed:
-            return
+            return PendingP2P([])
         dev = next((t for t in (send_up, send_down, recv_up, recv_down) if t is not None and t.numel()), None)
         if dev is not None and dev.is_cuda and dist.get_backend(self.group) != "nccl":
             # gloo P2P has no device-stream ordering (one-GPU rehearsals): stage
             # through host memory so the sends see the finished pack kernels and
-            # the device sees the received rows in stream order.
+            # the device sees the received rows in stream order (no overlap).
             h = [None if t is None else t.cpu() for t in (send_up, send_down)]
             r = [None if t is None else torch.empty(t.shape, dtype=t.dtype) for t in (recv_up, recv_down)]
             self.exchange_halo(h[0], h[1], r[0], r[1])
             for dst, src in ((recv_up, r[0]), (recv_down, r[1])):
                 if dst is not None and dst.numel():
                     dst.copy_(src)
-            return
+            return PendingP2P([])
         ops = []
         if self.rank > 0:
             if send_up is not None and send_up.numel():
@@ -210,9 +232,7 @@ class Comm:
                 ops.append(dist.P2POp(dist.isend, send_down.contiguous(), self.ranks[self.rank + 1], group=self.group))
             if recv_down is not None and recv_down.numel():
                 ops.append(dist.P2POp(dist.irecv, recv_down, self.ranks[self.rank + 1], group=self.group))
-        if ops:
-            for r in dist.batch_isend_irecv(ops):
-                r.wait()
+        return PendingP2P(dist.batch_isend_irecv(ops) if ops else [])
 
     def gather_object(self, obj):
         """Gather a small picklable object (metrics) from every rank onto rank 0

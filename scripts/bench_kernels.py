@@ -22,7 +22,8 @@ def main():
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--n-train", type=int, default=500)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="g,0,1,2")
+    ap.add_argument("--variants", default="4,0")
+    ap.add_argument("--uniform", action="store_true", help="every pixel at the prior mean (old behaviour)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     mask = np.ones((a.size, a.size), bool)
@@ -31,8 +32,17 @@ def main():
     bands = [(obs.band_specs[b], obs.get_device_band_data(date, b)) for b in range(2)]
     tab = build_table([s for s, _ in bands], [d for _, d in bands], 7, RecordCache(), dev)
     N = obs.N
-    mu, _, Pi = k.tip_prior()
-    xf = torch.tensor(mu, dtype=torch.float32, device=dev)[:, None].expand(7, N).contiguous()
+    mu, P, Pi = k.tip_prior()
+    if a.uniform:
+        xf = torch.tensor(mu, dtype=torch.float32, device=dev)[:, None].expand(7, N).contiguous()
+    else:
+        # per-pixel states spread like a real tile's (a uniform state makes every
+        # column of the MFMA operands identical, which lets the chip clock higher)
+        g = torch.Generator(device=dev).manual_seed(0)
+        sd = torch.tensor(np.sqrt(np.diag(P)) * 0.3, dtype=torch.float32, device=dev)[:, None]
+        xf = torch.tensor(mu, dtype=torch.float32, device=dev)[:, None] + sd * torch.randn(7, N, device=dev,
+                                                                                            generator=g)
+        xf[6].clamp_(0.05, 0.95)
     Pf = torch.tensor(pack_matrix(Pi), dtype=torch.float32, device=dev)[:, None].expand(28, N).contiguous()
     xo = torch.empty_like(xf)
     ao = torch.empty_like(Pf)

@@ -23,12 +23,13 @@ def _free_port():
     return p
 
 
-def _problem(world, rank):
+def _problem(world, rank, dense=False):
     import kafka_inferenceengine_amd as k
     from kafka_inferenceengine_amd.parallel import Comm, StripPartition
 
     mask = np.ones((30, 22), bool)
-    mask[4:9, 3:12] = False
+    if not dense:   # dense strips take the index geometry and the overlapped C2 path
+        mask[4:9, 3:12] = False
     comm = Comm(rank, world, "cpu") if world > 1 else Comm.single("cpu")
     part = StripPartition(mask, rank, world)
     obs = k.SyntheticBHRObservations(mask, n_train=60, device="cpu", stream=True, n_pool=4, partition=part,
@@ -37,7 +38,9 @@ def _problem(world, rank):
 
 
 def _run(world, rank, cfg, out_q):
-    k, mask, comm, part, obs = _problem(world, rank)
+    cfg = dict(cfg)
+    dense = cfg.pop("_dense", False)
+    k, mask, comm, part, obs = _problem(world, rank, dense)
     kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device="cpu",
                         comm=comm, partition=part, config=k.EngineConfig(**cfg))
     kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
@@ -46,7 +49,7 @@ def _run(world, rank, cfg, out_q):
     grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
     st = kf.run(grid, x0, None, Pinv)
     norms = [r["norms"] for r in kf.metrics.records if r.get("event") == "date"]
-    out_q.put((rank, part.offset, st.x.numpy().copy(), st.P.numpy().copy(), norms))
+    out_q.put((rank, part.offset, st.x.numpy().copy(), st.P.numpy().copy(), norms, kf.reg_overlapped_sweeps))
 
 
 def _worker(rank, world, port, cfg, q):
@@ -76,6 +79,7 @@ def _gather(world, cfg):
     res.sort(key=lambda t: t[0])
     x = np.concatenate([r[2] for r in res], 1)
     P = np.concatenate([r[3] for r in res], 1)
+    _gather.overlapped = [r[5] for r in res]
     return x, P, [r[4] for r in res]
 
 
@@ -94,12 +98,17 @@ def test_two_ranks_equal_one_rank(cfg):
     assert [len(a) for a in n1[0]] == [len(a) for a in n2[0]]
 
 
-def test_four_ranks_regularised_halo_equal_one_rank():
+@pytest.mark.parametrize("dense", [False, True], ids=["masked", "dense-overlap"])
+def test_four_ranks_regularised_halo_equal_one_rank(dense):
     """Interior strips (ranks 1 and 2) exchange halos with BOTH neighbours, which
-    world_size 2 never exercises (C2 up and down in the same Jacobi sweep)."""
-    cfg = {"spatial_gamma": 30.0, "spatial_params": [6], "jacobi_sweeps": 5}
+    world_size 2 never exercises (C2 up and down in the same Jacobi sweep).  On a
+    dense tile the sweeps run boundary rows -> posted exchange -> interior rows ->
+    wait (C2 overlap); the result must not change."""
+    cfg = {"spatial_gamma": 30.0, "spatial_params": [6], "jacobi_sweeps": 5, "_dense": dense}
     x1, P1, n1 = _gather(1, cfg)
     x4, P4, n4 = _gather(4, cfg)
+    if dense:
+        assert all(c > 0 for c in _gather.overlapped), _gather.overlapped
     assert x1.shape == x4.shape
     assert np.allclose(x1, x4, rtol=1e-5, atol=1e-6)
     assert np.allclose(P1, P4, rtol=1e-5, atol=1e-3)

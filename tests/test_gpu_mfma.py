@@ -125,3 +125,39 @@ def test_gp_mfma_tail_and_cloud_waves(cuda):
     assert np.all(sm[64 * 3:64 * 5] & K.ST_NO_OBS)
     assert np.max(np.abs(xm - xv) / (np.abs(xv) + 0.05)) < 2e-3
     assert np.all(h0[0][64 * 3:64 * 5] == 0)
+
+
+@pytest.mark.parametrize("cap", [0, 16])
+@pytest.mark.parametrize("variant", [0, 5])
+def test_gp_mfma_realistic_tile_matches_valu(cuda, variant, cap):
+    """A 512^2 synthetic TIP tile with per-pixel states (one and many 64-pixel
+    tiles per wave): every pixel of both matrix-core variants agrees with the
+    VALU loop.  Guards the VALU -> MFMA operand wait states of the inline-asm
+    hi/lo split (a missing pad corrupted a quarter of some waves only)."""
+    from kafka_inferenceengine_amd.utils.blocks import pack_matrix
+    mask = np.ones((512, 512), bool)
+    obs = k.SyntheticBHRObservations(mask, n_train=500, device=cuda, stream=False, n_pool=1)
+    bands = [(obs.band_specs[b], obs.get_device_band_data(obs.dates[0], b)) for b in range(2)]
+    tab = build_table([s for s, _ in bands], [d for _, d in bands], 7, RecordCache(), cuda)
+    N = obs.N
+    mu, P, Pi = k.tip_prior()
+    g = torch.Generator(device=cuda).manual_seed(0)
+    sd = torch.tensor(np.sqrt(np.diag(P)) * 0.3, dtype=torch.float32, device=cuda)[:, None]
+    xf = torch.tensor(mu, dtype=torch.float32, device=cuda)[:, None] + sd * torch.randn(7, N, device=cuda, generator=g)
+    xf[6].clamp_(0.05, 0.95)
+    Pf = torch.tensor(pack_matrix(Pi), dtype=torch.float32, device=cuda)[:, None].expand(28, N).contiguous()
+    ext = K.ext()
+    outs = {}
+    try:
+        ext.set_max_blocks(cap or ext.MAX_BLOCKS)
+        for v in (4, variant):
+            for _ in range(2):   # twice: the corruption was timing dependent
+                xo = torch.zeros_like(xf)
+                K.analysis(7, tab, xf, xf, Pf, xo, torch.zeros_like(Pf), None, None, None, variant=v)
+                outs.setdefault(v, []).append(xo.cpu().numpy())
+    finally:
+        ext.set_max_blocks(ext.MAX_BLOCKS)
+    ref = outs[4][0]
+    for x in outs[variant]:
+        d = np.abs(x - ref) / (np.abs(ref) + 0.05)
+        assert d.max() < 0.1, (variant, cap, float(d.max()), np.nonzero(d.max(0) > 0.1)[0][:8])
