@@ -6,6 +6,7 @@
 // overlapped ingest.  Without a GPU (CI container) the slots fall back to
 // pageable memory and h2d degenerates to memcpy.
 #include "kf_stream.h"
+#include "kf_tiff.h"
 
 #include <fcntl.h>
 #include <hip/hip_runtime_api.h>
@@ -107,6 +108,27 @@ class HostRing {
     cv_.notify_one();
   }
 
+  // Decode a window of one GeoTIFF band (kf_tiff.cpp, its own thread pool)
+  // into slot s at slot_off, in the background.
+  void read_tiff_async(int s, const std::string& path, int band, uint64_t r0, uint64_t r1, uint64_t c0, uint64_t c1,
+                       size_t elem_bytes, size_t slot_off, int nthreads) {
+    check_range(s, slot_off, (size_t)((r1 - r0) * (c1 - c0)) * elem_bytes);
+    pending_[s]++;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back([=] {
+        try {
+          kf::tiff::read_window(path, band, slots_[s] + slot_off, r0, r1, c0, c1, nthreads);
+        } catch (const std::exception& e) {
+          std::lock_guard<std::mutex> g2(err_mu_);
+          errors_[s] = std::string(e.what()) + ": " + path;
+        }
+        pending_[s]--;
+      });
+    }
+    cv_.notify_one();
+  }
+
   void wait_reads(int s) {
     while (pending_.at(s).load() > 0) std::this_thread::yield();
     std::lock_guard<std::mutex> g(err_mu_);
@@ -189,6 +211,7 @@ void bind_stream(py::module_& m) {
       .def_property_readonly("n_slots", &HostRing::n_slots)
       .def_property_readonly("pinned", &HostRing::pinned)
       .def("read_file_async", &HostRing::read_file_async)
+      .def("read_tiff_async", &HostRing::read_tiff_async)
       .def("wait_reads", &HostRing::wait_reads, py::call_guard<py::gil_scoped_release>())
       .def("h2d", &HostRing::h2d)
       .def("stream_wait", &HostRing::stream_wait)

@@ -24,6 +24,8 @@
 #include <unistd.h>
 #include <zlib.h>
 
+#include "kf_tiff.h"
+
 #include <algorithm>
 #include <atomic>
 #include <functional>

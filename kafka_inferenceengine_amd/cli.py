@@ -54,6 +54,8 @@ def _build(args, comm):
     elif args.sensor in ("s2", "multisensor"):
         if args.s2_folder:
             from .input_output.sentinel import Sentinel2Observations
+            if not args.emulator_folder:
+                raise SystemExit("--s2-folder needs --emulator-folder")
             obs = Sentinel2Observations(args.s2_folder, args.emulator_folder, mask)
         elif args.sensor == "s2":
             obs = k.SyntheticS2Observations(mask, n_bands=10, n_train=args.n_train or 250, **syn)
@@ -119,9 +121,15 @@ def cmd_run(args):
     if hasattr(out, "flush"):
         out.flush()
     if comm.rank == 0:
-        print(json.dumps({"timesteps": len(kf.history), "pixels": kf.n_total,
-                          "gn_iterations": [h.get("gn_iterations") for h in kf.history],
-                          "finite": bool(np.isfinite(state.x[:, :state.N].cpu().numpy()).all())}))
+        rec = {"timesteps": len(kf.history), "pixels": kf.n_total,
+               "gn_iterations": [h.get("gn_iterations") for h in kf.history],
+               "finite": bool(np.isfinite(state.x[:, :state.N].cpu().numpy()).all())}
+        if kf.timer.enabled:
+            rec["phases_ms"] = kf.timer.cumulative()
+            ing = getattr(kf.observations, "_ingest", None)
+            if ing is not None:
+                rec["ingest"] = {"bytes_read": ing.bytes_read, "bytes_h2d": ing.bytes_h2d, "pinned": ing.pinned}
+        print(json.dumps(rec))
     comm.destroy()
 
 
@@ -156,6 +164,21 @@ def cmd_farm(args):
     if res is not None:
         print(json.dumps({"chunks": len(res), "pixels": sum(v or 0 for v in res.values())}))
     comm.destroy()
+
+
+def cmd_synth_s2(args):
+    """Write a synthetic Sentinel-2 archive (tiled-DEFLATE GeoTIFF granules +
+    emulators) for file-driven runs: ``run --sensor s2 --s2-folder OUT/data
+    --emulator-folder OUT/emus``."""
+    import torch
+
+    from .input_output.synthetic import synthesize_s2_archive
+
+    h, w = args.size
+    dev = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    data, emus, dates = synthesize_s2_archive(args.out, np.ones((h, w), bool), args.dates, args.n_train, args.seed,
+                                              dev, args.cloud)
+    print(json.dumps({"data": data, "emulators": emus, "dates": [d.isoformat() for d in dates]}))
 
 
 def cmd_chunks(args):
@@ -206,6 +229,15 @@ def main(argv=None):
     f.add_argument("--out", default=None)
     f.add_argument("--device", default=None)
     f.set_defaults(fn=cmd_farm)
+    y = sub.add_parser("synth-s2", help="write a synthetic Sentinel-2 GeoTIFF archive")
+    y.add_argument("--out", required=True)
+    y.add_argument("--size", type=int, nargs=2, default=[512, 512], metavar=("H", "W"))
+    y.add_argument("--dates", type=int, default=4)
+    y.add_argument("--n-train", type=int, default=250)
+    y.add_argument("--seed", type=int, default=0)
+    y.add_argument("--cloud", type=float, default=0.2)
+    y.add_argument("--device", default=None)
+    y.set_defaults(fn=cmd_synth_s2)
     c = sub.add_parser("chunks", help="print get_chunks")
     c.add_argument("nx", type=int)
     c.add_argument("ny", type=int)

@@ -122,6 +122,10 @@ class LinearKalman:
         self.band_comm = band if (band is not None and band.world > 1) else None
         self._bp_buf = None
         self.history = []
+        if hasattr(observations, "bind_engine"):
+            # file readers learn the strip / device here and switch to the
+            # device ingest path (pinned native decode -> async H2D)
+            observations.bind_engine(self)
         LOG.info("Starting KaFKA run!!!")
 
     # ------------------------------------------------------------ model

@@ -30,7 +30,7 @@ import numpy as np
 import scipy.sparse as sp
 
 from ..models.gp import GaussianProcessEmulator
-from .tiff import read_tiff
+from .tiff import read_tiff, write_tiff
 
 S2MSIdata = namedtuple("S2MSIdata", "observations uncertainty mask metadata emulator")
 SARdata = namedtuple("SARdata", "observations uncertainty mask metadata emulator")
@@ -124,9 +124,24 @@ def _crop(a, roi):
 
 # ------------------------------------------------------------- Sentinel-2
 class Sentinel2Observations:
-    def __init__(self, parent_folder, emulator_folder, state_mask, chunk=None, roi=None, rel_unc=0.05):
+    """Sentinel-2 L2 surface-reflectance granules (``Sentinel2_Observations.py``).
+
+    Host protocol: ``get_band_data`` returns the reference's ``S2MSIdata``
+    record (reflectance, sparse inverse-variance diagonal, mask, angles,
+    emulator).  Device protocol (after ``bind_engine``): every band of a date
+    is decoded as raw uint16 DN by the native reader straight into a pinned
+    slot, copied on the ingest stream, gathered onto the strip's active pixels
+    and decoded inside the analysis kernel (``OBS_DN16``: reflectance = DN x
+    1e-4, valid = DN > 0, sigma = rel_unc x reflectance, weight = 1 / sigma^2 —
+    the reference's :163-179 without the N x N sparse weight matrix).
+    ``prefetch(date)`` starts the next date's decode under the current
+    kernels."""
+
+    def __init__(self, parent_folder, emulator_folder, state_mask, chunk=None, roi=None, rel_unc=0.05,
+                 device_ingest: bool = True):
         if not os.path.exists(parent_folder):
             raise IOError("S2 data folder doesn't exist")
+        self.device_ingest = device_ingest
         self.parent = parent_folder
         self.emulator_folder = emulator_folder
         self.state_mask = state_mask
@@ -136,7 +151,9 @@ class Sentinel2Observations:
         self.emulator_files = sorted(glob.glob(os.path.join(emulator_folder, "*.npz")))
         self._find_granules(parent_folder)
         self._emu_cache = {}
+        self._meta_cache = {}
         self.chunk = chunk
+        self._ingest = None
 
     def _find_granules(self, parent_folder):
         self.dates, self.date_data = [], {}
@@ -171,20 +188,98 @@ class Sentinel2Observations:
         dist = (szas - sza) ** 2 + (vzas - vza) ** 2 + (raas - raa) ** 2
         return self.emulator_files[int(np.argmin(dist))]
 
+    def _date_meta(self, timestep):
+        """(angles dict, emulator set) of a date, parsed once."""
+        if timestep not in self._meta_cache:
+            folder = self.date_data[timestep]
+            sza, saa, vza, vaa = parse_xml(os.path.join(folder, "metadata.xml"))
+            metadata = dict(zip(["sza", "saa", "vza", "vaa"], [sza, saa, vza, vaa]))
+            efile = self._find_emulator(sza, saa, vza, vaa)
+            if efile not in self._emu_cache:  # the reference re-unpickled per band and iteration
+                self._emu_cache[efile] = load_emulator_set(efile)
+            self._meta_cache[timestep] = (metadata, self._emu_cache[efile])
+        return self._meta_cache[timestep]
+
     def get_band_data(self, timestep, band):
         folder = self.date_data[timestep]
-        sza, saa, vza, vaa = parse_xml(os.path.join(folder, "metadata.xml"))
-        metadata = dict(zip(["sza", "saa", "vza", "vaa"], [sza, saa, vza, vaa]))
-        efile = self._find_emulator(sza, saa, vza, vaa)
-        if efile not in self._emu_cache:  # the reference re-unpickled per band and iteration
-            self._emu_cache[efile] = load_emulator_set(efile)
+        metadata, ems = self._date_meta(timestep)
         rho, _ = read_tiff(os.path.join(folder, f"B{self.band_map[band]}_sur.tif"))
         rho = _crop(rho.astype(np.float64), self.roi)
         mask = rho > 0
         rho = np.where(mask, rho / 10000., 0.0)
         unc = _weights(rho * self.rel_unc, mask)
         key = f"S2A_MSI_{S2_EMULATOR_BANDS[band]:02d}"
-        return S2MSIdata(rho, unc, mask, metadata, self._emu_cache[efile].get(key))
+        return S2MSIdata(rho, unc, mask, metadata, ems.get(key))
+
+    # ---------------------------------------------------------- device path
+    def bind_engine(self, engine):
+        """Device ingest for ``engine``'s strip (called by LinearKalman)."""
+        import torch
+
+        from ..ops import kernels as K
+        from .streaming import RasterIngest
+
+        if not self.device_ingest:
+            return
+        self.partition = part = engine.partition
+        self._device = engine.device
+        H, W = part.local_mask.shape
+        ulx, uly = (self.roi[0], self.roi[1]) if self.roi is not None else (0, 0)
+        self._window = (uly + part.r0, uly + part.r0 + H, ulx, ulx + W)
+        self._ingest = RasterIngest(len(self.band_map), (H, W), torch.int16, self._device)
+        self._identity = part.N == H * W
+        self._idx = None if self._identity else torch.from_numpy(part.local_idx).to(self._device)
+        self._K = K
+
+    def _files(self, timestep):
+        folder = self.date_data[timestep]
+        return [(os.path.join(folder, f"B{b}_sur.tif"), 0, self._window) for b in self.band_map]
+
+    def prefetch(self, timestep):
+        if self._ingest is not None and timestep in self.date_data:
+            self._ingest.prefetch(timestep, self._files(timestep))
+
+    def __getattr__(self, name):
+        # the engine probes hasattr(obs, "get_device_band_data"): only bound
+        # readers expose the device protocol
+        if name == "get_device_band_data" and self.__dict__.get("_ingest") is not None:
+            return self._get_device_band_data
+        raise AttributeError(name)
+
+    def _get_device_band_data(self, timestep, band):
+        from ..engine.bands import DeviceBand
+
+        metadata, ems = self._date_meta(timestep)
+        key = f"S2A_MSI_{S2_EMULATOR_BANDS[band]:02d}"
+        planes = self._ingest.acquire(timestep, self._files(timestep))
+        dn = planes[band].reshape(-1)
+        if not self._identity:
+            dn = self._K.gather(dn, self._idx)
+        return DeviceBand(self._K.OBS_DN16, dn=dn, scale=1e-4, rel_unc=self.rel_unc, unc_floor=0.0,
+                          metadata=metadata, emulator=ems.get(key))
+
+
+def write_s2_archive(root, dn_by_date: dict, emulators: dict, geotransform=None, projection=None,
+                     angles=(31.0, 0.0, 8.0, 118.0), emulator_angles=((8.0, 31.0, 118.0),)):
+    """Synthetic on-disk S2 archive in the reader's layout:
+    ``root/data/YYYY/MM/DD/<granule>/{B02..B12}_sur.tif`` (uint16 DN x 1e4,
+    tiled DEFLATE), ``aot.tif``, ``metadata.xml``; ``root/emus/*_{vza}_{sza}_{raa}.npz``.
+    ``dn_by_date``: {date: uint16 array [10, H, W]}; ``emulators``: {key: emulator}
+    with keys ``S2A_MSI_{band:02d}``.  Returns (data folder, emulator folder)."""
+    data = os.path.join(root, "data")
+    emus = os.path.join(root, "emus")
+    os.makedirs(emus, exist_ok=True)
+    for vza, sza, raa in emulator_angles:
+        save_emulator_set(os.path.join(emus, f"prosail_{vza:g}_{sza:g}_{raa:g}.npz"), emulators)
+    for date, dn in dn_by_date.items():
+        g = os.path.join(data, f"{date.year:04d}", f"{date.month:02d}", f"{date.day:02d}", "S2A_GRANULE")
+        os.makedirs(g, exist_ok=True)
+        for i, b in enumerate(S2_BAND_MAP):
+            write_tiff(os.path.join(g, f"B{b}_sur.tif"), np.asarray(dn[i], dtype=np.uint16), geotransform,
+                       projection)
+        write_tiff(os.path.join(g, "aot.tif"), np.zeros((8, 8), np.uint8))
+        write_s2_metadata(os.path.join(g, "metadata.xml"), *angles)
+    return data, emus
 
 
 # ------------------------------------------------------------- Sentinel-1

@@ -79,3 +79,81 @@ class DateStreamer:
             self.ring.stream_wait(k, int(torch.cuda.current_stream(self.device).cuda_stream))
         self._current = k
         return self.bufs[b]
+
+
+class RasterIngest:
+    """Granule ingest from GeoTIFF files: every band of a date is decoded by the
+    native reader (``csrc/kf_tiff.cpp``, thread pool, DEFLATE) straight into one
+    pinned ``HostRing`` slot in the background, shipped with hipMemcpyAsync on
+    a side stream into one of two device buffers, and the compute stream waits
+    on that copy's event only.  ``prefetch(key, files)`` for date t + 1 runs
+    under date t's Gauss-Newton kernels; replaces the per-band
+    GDAL reads of Sentinel2_Observations.py:148-185.
+
+    ``files``: list of ``(path, band_index_in_file, (r0, r1, c0, c1))``, all
+    windows of the same shape ``plane`` and element type ``dtype``."""
+
+    def __init__(self, n_planes: int, plane, dtype, device, n_slots: int = 2, io_threads: int | None = None):
+        import os
+
+        self.device = torch.device(device)
+        self.n_planes = int(n_planes)
+        self.plane = tuple(int(v) for v in plane)
+        self.dtype = dtype
+        self.esize = torch.empty((), dtype=dtype).element_size()
+        self.plane_bytes = self.plane[0] * self.plane[1] * self.esize
+        self.slot_bytes = self.plane_bytes * self.n_planes
+        self.ring = _ext.require_ext().HostRing(n_slots, self.slot_bytes, 2)
+        self.slot_key = [None] * n_slots
+        self.bufs = [torch.empty((self.n_planes,) + self.plane, dtype=dtype, device=self.device) for _ in range(2)]
+        self.buf_key = [None, None]
+        self.cuda = self.device.type == "cuda"
+        self.stream = torch.cuda.Stream(self.device) if self.cuda else None
+        self.io_threads = io_threads or max(1, min(16, (os.cpu_count() or 4)))
+        self._current = None
+        self.bytes_h2d = 0
+        self.bytes_read = 0
+
+    @property
+    def pinned(self) -> bool:
+        return bool(self.ring.pinned)
+
+    def prefetch(self, key, files) -> int:
+        """Start decoding ``files`` into a free pinned slot (no wait)."""
+        if key in self.slot_key:
+            return self.slot_key.index(key)
+        if len(files) != self.n_planes:
+            raise ValueError(f"{len(files)} files for {self.n_planes} planes")
+        cur = self.slot_key.index(self._current) if self._current in self.slot_key else -1
+        s = next((i for i in range(len(self.slot_key)) if i != cur and self.slot_key[i] is None),
+                 next(i for i in range(len(self.slot_key)) if i != cur))
+        self.ring.host_wait(s)          # the slot's previous H2D has finished reading it
+        for i, (path, band, (r0, r1, c0, c1)) in enumerate(files):
+            if (r1 - r0, c1 - c0) != self.plane:
+                raise ValueError(f"window {(r0, r1, c0, c1)} is not a {self.plane} plane")
+            self.ring.read_tiff_async(s, str(path), int(band), r0, r1, c0, c1, self.esize, i * self.plane_bytes,
+                                      self.io_threads)
+            self.bytes_read += self.plane_bytes
+        self.slot_key[s] = key
+        return s
+
+    def acquire(self, key, files) -> torch.Tensor:
+        """Device planes ``[n_planes, *plane]`` of ``key``; the current stream
+        waits for their copy."""
+        s = self.prefetch(key, files)
+        if key in self.buf_key:
+            b = self.buf_key.index(key)
+        else:
+            b = 1 if (self._current is not None and self.buf_key[0] == self._current) else 0
+            dst = self.bufs[b]
+            if self.cuda:
+                self.stream.wait_stream(torch.cuda.current_stream(self.device))
+                self.ring.h2d(s, dst.data_ptr(), self.slot_bytes, 0, int(self.stream.cuda_stream))
+            else:
+                self.ring.h2d(s, dst.data_ptr(), self.slot_bytes, 0, 0)
+            self.buf_key[b] = key
+            self.bytes_h2d += self.slot_bytes
+        if self.cuda:
+            self.ring.stream_wait(s, int(torch.cuda.current_stream(self.device).cuda_stream))
+        self._current = key
+        return self.bufs[b]

@@ -451,3 +451,31 @@ class MultiSensorObservations:
 
     def ingest_bytes(self) -> int:
         return sum(s.ingest_bytes() for s in self.sources)
+
+
+def synthesize_s2_archive(root, state_mask, n_dates: int = 4, n_train: int = 250, seed: int = 0, device=None,
+                          cloud_fraction: float = 0.2, geotransform=None, projection=None):
+    """Write a Sentinel-2 archive in the reader's on-disk layout
+    (``sentinel.write_s2_archive``: tiled-DEFLATE uint16 DN GeoTIFFs per band,
+    metadata.xml, angle-named emulator npz) whose reflectances are the
+    SyntheticS2Observations fields pushed through its PROSAIL-like emulators on
+    ``device`` — so a file-driven run converges like the synthetic one.
+    Returns (data folder, emulator folder, dates)."""
+    from .sentinel import S2_EMULATOR_BANDS, write_s2_archive
+
+    mask = np.asarray(state_mask).astype(bool)
+    dates = _date_list(dt.datetime(2017, 7, 3), n_dates, 2)
+    src = SyntheticS2Observations(mask, dates=dates, n_bands=10, n_train=n_train, seed=seed, device=device,
+                                  cloud_fraction=cloud_fraction, stream=False, n_pool=n_dates)
+    idx = src.partition.global_index()
+    H, W = mask.shape
+    dn_by_date = {}
+    for k, d in enumerate(dates):
+        e = src._synthesize(k).cpu().numpy().view(np.uint16)        # [10, N] active pixels
+        r = np.zeros((10, H * W), dtype=np.uint16)
+        r[:, idx] = e
+        dn_by_date[d] = r.reshape(10, H, W)
+        del e
+    ems = {f"S2A_MSI_{S2_EMULATOR_BANDS[b]:02d}": src.emulators[b] for b in range(10)}
+    data, emus = write_s2_archive(root, dn_by_date, ems, geotransform, projection)
+    return data, emus, dates

@@ -62,6 +62,7 @@ class PhaseTimer:
         self.enabled = bool(enabled or sync)
         self._pending = []
         self.totals = defaultdict(float)
+        self.run_totals = defaultdict(float)   # over the whole run (snapshots reset `totals`)
 
     def phase(self, name: str):
         if not self.enabled:
@@ -88,6 +89,12 @@ class PhaseTimer:
             finally:
                 self.totals[name] += 1e3 * (time.perf_counter() - t0)
 
+    def cumulative(self) -> dict:
+        """Per-phase ms over the whole run (pending events included)."""
+        cur = self.snapshot(reset=True)
+        del cur
+        return {k: round(v, 3) for k, v in self.run_totals.items()}
+
     def snapshot(self, reset: bool = True) -> dict:
         if self._pending:
             self._pending[-1][2].synchronize()
@@ -96,5 +103,7 @@ class PhaseTimer:
             self._pending = []
         out = {k: round(v, 3) for k, v in self.totals.items()}
         if reset:
+            for k, v in self.totals.items():
+                self.run_totals[k] += v
             self.totals = defaultdict(float)
         return out

@@ -40,8 +40,14 @@ def test_emulator_npz_roundtrip(tmp_path):
     assert np.allclose(em.predict(x)[0], em2.predict(x)[0])
 
 
-def _make_s2_archive(root, shape, dates, emulators):
+def _make_s2_archive(root, shape, dates, emulators, consistent=False):
+    """consistent=True: reflectance = emulator(truth near the SAIL prior mean),
+    so the Gauss-Newton loop converges (random reflectances never do)."""
     rng = np.random.default_rng(2)
+    truth = None
+    if consistent:
+        mu, _, _ = k.sail_prior()
+        truth = mu[None, :] + rng.normal(0, 0.03, (shape[0] * shape[1], mu.size))
     emu_dir = root / "emus"
     emu_dir.mkdir()
     S.save_emulator_set(emu_dir / "sail_10_30_120.npz",
@@ -54,7 +60,10 @@ def _make_s2_archive(root, shape, dates, emulators):
         k.write_tiff(g / "aot.tif", np.zeros(shape, np.float32))
         S.write_s2_metadata(g / "metadata.xml", 31.0, 0.0, 8.0, 118.0)
         for b, name in enumerate(S.S2_BAND_MAP):
-            rho = np.clip(rng.normal(0.15 + 0.02 * b, 0.02, shape), 0.01, 0.8)
+            if truth is not None:
+                rho = np.clip(emulators[b].predict(truth)[0].reshape(shape) + rng.normal(0, 0.002, shape), 0.01, 0.8)
+            else:
+                rho = np.clip(rng.normal(0.15 + 0.02 * b, 0.02, shape), 0.01, 0.8)
             dn = np.round(rho * 1e4).astype(np.uint16)
             dn[:2, :3] = 0  # no data
             k.write_tiff(g / f"B{name}_sur.tif", dn, compress="deflate")
@@ -65,7 +74,7 @@ def test_sentinel2_reader_feeds_engine(tmp_path):
     shape = (12, 10)
     dates = [dt.datetime(2017, 7, 3) + dt.timedelta(days=2 * i) for i in range(3)]
     ems = k.make_prosail_emulators(10, n_train=40)
-    data, emu = _make_s2_archive(tmp_path, shape, dates, ems)
+    data, emu = _make_s2_archive(tmp_path, shape, dates, ems, consistent=True)
     mask = np.ones(shape, bool)
     obs = S.Sentinel2Observations(str(data), str(emu), mask)
     assert obs.dates == dates and obs.bands_per_observation[dates[0]] == 10
@@ -73,12 +82,46 @@ def test_sentinel2_reader_feeds_engine(tmp_path):
     rec = obs.get_band_data(dates[0], 3)
     assert rec.mask.sum() == mask.sum() - 6 and rec.emulator is not None
     prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
-    kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
-                        state_propagation=None, prior=prior, device="cpu")
-    x0, Pinv = prior.process_prior(None)
     grid = [dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in dates]
-    st = kf.run(grid, x0, None, Pinv)
-    assert torch.isfinite(st.x).all()
+    states = []
+    for ingest in (False, True):   # reference records (host) vs native decode -> DN16 device ingest
+        obs = S.Sentinel2Observations(str(data), str(emu), mask, device_ingest=ingest)
+        kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
+                            state_propagation=None, prior=prior, device="cpu")
+        assert hasattr(obs, "get_device_band_data") == ingest
+        x0, Pinv = prior.process_prior(None)
+        st = kf.run(grid, x0, None, Pinv)
+        assert torch.isfinite(st.x).all()
+        assert all(h["gn_iterations"][0] < 25 for h in kf.history)
+        states.append(st.x.numpy().copy())
+    assert np.allclose(states[0], states[1], rtol=1e-4, atol=1e-5)
+    assert obs._ingest.bytes_read == 3 * 10 * shape[0] * shape[1] * 2
+
+
+def test_sentinel2_device_ingest_masked_strips(tmp_path):
+    """Masked state grid, two strips: the native window decode + gather onto
+    each strip's active pixels equals the host records."""
+    from kafka_inferenceengine_amd.parallel import StripPartition
+    shape = (14, 9)
+    dates = [dt.datetime(2017, 7, 3)]
+    ems = k.make_prosail_emulators(10, n_train=30)
+    data, emu = _make_s2_archive(tmp_path, shape, dates, ems)
+    mask = np.ones(shape, bool)
+    mask[3:6, 2:7] = False
+    for rank in range(2):
+        part = StripPartition(mask, rank, 2)
+
+        class _E:   # the two attributes bind_engine reads
+            partition, device = part, torch.device("cpu")
+        obs = S.Sentinel2Observations(str(data), str(emu), mask)
+        obs.bind_engine(_E)
+        for b in (0, 7):
+            db = obs.get_device_band_data(dates[0], b)
+            rec = obs.get_band_data(dates[0], b)
+            y, w = db.decode()
+            yr = rec.observations[part.r0:part.r1][part.local_mask]
+            assert np.allclose(y.numpy(), yr, atol=1e-7)
+            assert np.array_equal(w.numpy() > 0, rec.mask[part.r0:part.r1][part.local_mask])
 
 
 def test_sentinel1_reader(tmp_path):
