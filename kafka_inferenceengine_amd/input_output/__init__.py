@@ -8,5 +8,5 @@ from .output import DeviceOutput, KafkaOutput, KafkaOutputMemory  # noqa: F401
 from .synthetic import (MultiSensorObservations, SyntheticBHRObservations, SyntheticObservations,  # noqa: F401
                         SyntheticIdentityObservations, SyntheticOLCIObservations, SyntheticS1Observations,
                         SyntheticS2Observations)
-from .tiff import read_tiff, write_tiff  # noqa: F401
+from .tiff import read_tiff, read_tiff_window, tiff_info, write_tiff  # noqa: F401
 from .utils import find_overlap, get_chunks, raster_extent, reproject_image  # noqa: F401

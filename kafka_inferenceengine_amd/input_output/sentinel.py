@@ -29,7 +29,7 @@ from collections import namedtuple
 import numpy as np
 import scipy.sparse as sp
 
-from ..models.gp import GaussianProcessEmulator
+from ..models.gp import GaussianProcessEmulator, pack_emulator_set, unpack_emulator_set
 from .tiff import read_tiff, write_tiff
 
 S2MSIdata = namedtuple("S2MSIdata", "observations uncertainty mask metadata emulator")
@@ -196,9 +196,22 @@ class Sentinel2Observations:
             metadata = dict(zip(["sza", "saa", "vza", "vaa"], [sza, saa, vza, vaa]))
             efile = self._find_emulator(sza, saa, vza, vaa)
             if efile not in self._emu_cache:  # the reference re-unpickled per band and iteration
-                self._emu_cache[efile] = load_emulator_set(efile)
+                self._emu_cache[efile] = self._load_emulators(efile)
             self._meta_cache[timestep] = (metadata, self._emu_cache[efile])
         return self._meta_cache[timestep]
+
+    def _load_emulators(self, efile):
+        """Emulator set of a file.  Bound to a multi-rank engine, only rank 0
+        reads and parses it; the others receive it by C4 (one tensor broadcast,
+        ``Comm.broadcast_packed``).  Every rank asks for the same dates in the
+        same order, so the collective is matched."""
+        comm = getattr(self, "_comm", None)
+        if comm is None or not comm.distributed:
+            return load_emulator_set(efile)
+        header, buf = pack_emulator_set(load_emulator_set(efile)) if comm.rank == 0 else (None, None)
+        header, buf = comm.broadcast_packed(header, buf)
+        self.c4_broadcasts = getattr(self, "c4_broadcasts", 0) + 1
+        return unpack_emulator_set(header, buf)
 
     def get_band_data(self, timestep, band):
         folder = self.date_data[timestep]
@@ -219,6 +232,7 @@ class Sentinel2Observations:
         from ..ops import kernels as K
         from .streaming import RasterIngest
 
+        self._comm = getattr(engine, "comm", None)
         if not self.device_ingest:
             return
         self.partition = part = engine.partition

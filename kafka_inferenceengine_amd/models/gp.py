@@ -146,6 +146,35 @@ class GaussianProcessEmulator:
 
 
 # --------------------------------------------------------------------------
+# flat packing (C4 setup broadcast of emulator sets)
+
+def pack_emulator_set(ems: dict):
+    """{key: emulator} -> (header, float64 buffer): header = [(key, T, D, name)],
+    buffer = per emulator [signal, mean, inputs (T x D), alpha (T), lam (D)]."""
+    header, parts = [], []
+    for key, em in ems.items():
+        T, D = em.inputs.shape
+        header.append((str(key), int(T), int(D), str(em.name)))
+        parts += [np.array([em.signal, em.mean]), em.inputs.ravel(), em.alpha.ravel(), em.lam.ravel()]
+    return header, (np.concatenate(parts) if parts else np.zeros(0))
+
+
+def unpack_emulator_set(header, buf) -> dict:
+    out, o = {}, 0
+    for key, T, D, name in header:
+        sig, mu = buf[o], buf[o + 1]
+        o += 2
+        inputs = buf[o:o + T * D].reshape(T, D)
+        o += T * D
+        alpha = buf[o:o + T]
+        o += T
+        lam = buf[o:o + D]
+        o += D
+        out[key] = GaussianProcessEmulator(inputs.copy(), alpha.copy(), lam.copy(), float(sig), float(mu), name=name)
+    return out
+
+
+# --------------------------------------------------------------------------
 # split-f16 MFMA tables (csrc/kf_gp_mfma.h)
 
 GPM_MAX_D = 10

@@ -193,6 +193,22 @@ class Comm:
         dist.broadcast_object_list(lst, src=self.ranks[src], group=self.group)
         return lst[0]
 
+    def broadcast_packed(self, header, buf, src: int = 0):
+        """C4 for setup data: a small header (plain lists / strings / numbers made
+        by this process) as an object, the bulk as one float64 tensor broadcast
+        (RCCL on device, gloo on host).  Returns (header, numpy buffer) on every
+        rank; non-root ranks pass ``None, None``."""
+        if not self.distributed:
+            return header, buf
+        meta = self.broadcast_object((header, None if buf is None else int(buf.size)), src)
+        header, n = meta
+        use_dev = self.device.type == "cuda" and dist.get_backend(self.group) == "nccl"
+        dev = self.device if use_dev else torch.device("cpu")
+        t = (torch.from_numpy(buf.astype("float64")).to(dev) if self.rank == src
+             else torch.empty(n, dtype=torch.float64, device=dev))
+        dist.broadcast(t, src=self.ranks[src], group=self.group)
+        return header, t.cpu().numpy()
+
     def exchange_halo(self, send_up: torch.Tensor | None, send_down: torch.Tensor | None,
                       recv_up: torch.Tensor | None, recv_down: torch.Tensor | None):
         """C2 (blocking): send my first rows to rank-1 / last rows to rank+1 and

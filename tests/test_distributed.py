@@ -267,3 +267,105 @@ def test_band_parallel_checkpoint_single_writer(tmp_path):
     last = k.CheckpointManager.resolve(ck)
     x = np.fromfile(last / "state.rank0.x.f32", dtype="<f4").reshape(10, -1)
     assert np.array_equal(x, res[0][1][:, :x.shape[1]])
+
+
+def _gather_worker(rank, world, port, folder, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        k, mask, comm, part, obs = _problem(world, rank)
+        out = k.KafkaOutput(k.TIP_PARAMETERS, [500000., 10., 0., 4000000., 0., -10.], "EPSG:32630", folder,
+                            gather=True)
+        kf = k.LinearKalman(obs, out, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS,
+                            device="cpu", comm=comm, partition=part)
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        x0, Pinv = k.JRCPrior(k.TIP_PARAMETERS, mask).process_prior(None)
+        grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(3)]
+        kf.run(grid, x0, None, Pinv)
+        out.flush()
+        q.put((rank, sorted(os.path.basename(f) for f in out.written)))
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_output_gather_to_root_writes_one_raster(tmp_path):
+    """C3: with gather=True the strips are gathered to rank 0 (Comm.gather_to_root)
+    and written as one full-tile GeoTIFF equal to the single-rank output."""
+    import kafka_inferenceengine_amd as k
+    ctx = mp.get_context("spawn")
+    res = {}
+    for world in (1, 2):
+        q = ctx.Queue()
+        folder = str(tmp_path / f"w{world}")
+        port = _free_port()
+        procs = [ctx.Process(target=_gather_worker, args=(r, world, port, folder, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        got = dict(q.get(timeout=300) for _ in range(world))
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        assert got[0] and all(not v for r, v in got.items() if r)   # only rank 0 writes
+        res[world] = (folder, got[0])
+    assert res[1][1] == res[2][1]
+    for name in res[1][1]:
+        a, ia = k.read_tiff(os.path.join(res[1][0], name))
+        b, ib = k.read_tiff(os.path.join(res[2][0], name))
+        assert a.shape == b.shape == (30, 22)
+        assert np.allclose(a, b, rtol=1e-5, atol=1e-6), name
+        assert ia["geotransform"] == ib["geotransform"]
+
+
+def _s2_worker(rank, world, port, data, emus, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import kafka_inferenceengine_amd as k
+        from kafka_inferenceengine_amd.input_output import sentinel as S
+        from kafka_inferenceengine_amd.parallel import Comm, StripPartition
+        if rank > 0:   # C4: only rank 0 may read emulator files
+            def _no_read(path):
+                raise AssertionError(f"rank {rank} read {path}")
+            S.load_emulator_set = _no_read
+        mask = np.ones((16, 12), bool)
+        comm = Comm(rank, world, "cpu") if world > 1 else Comm.single("cpu")
+        part = StripPartition(mask, rank, world)
+        obs = S.Sentinel2Observations(data, emus, mask)
+        prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
+        kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
+                            state_propagation=None, prior=prior, device="cpu", comm=comm, partition=part)
+        x0, Pinv = prior.process_prior(None)
+        grid = [obs.dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in obs.dates]
+        st = kf.run(grid, x0, None, Pinv)
+        q.put((rank, st.x.numpy().copy(), getattr(obs, "c4_broadcasts", 0)))
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_s2_emulators_broadcast_from_rank0(tmp_path):
+    """C4: with two ranks only rank 0 reads the emulator files; rank 1 receives
+    the packed set by tensor broadcast, and the run equals one rank."""
+    import kafka_inferenceengine_amd as k
+    from kafka_inferenceengine_amd.input_output.synthetic import synthesize_s2_archive
+    data, emus, _ = synthesize_s2_archive(str(tmp_path), np.ones((16, 12), bool), n_dates=2, n_train=30,
+                                          device="cpu")
+    ctx = mp.get_context("spawn")
+    xs = {}
+    for world in (1, 2):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_s2_worker, args=(r, world, port, data, emus, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        got = sorted((q.get(timeout=300) for _ in range(world)), key=lambda t: t[0])
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        if world == 2:
+            assert all(c >= 1 for _, _, c in got)
+        xs[world] = np.concatenate([g[1] for g in got], 1)
+    assert np.allclose(xs[1], xs[2], rtol=1e-5, atol=1e-6)

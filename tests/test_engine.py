@@ -128,6 +128,10 @@ def test_kafka_output_tiff_roundtrip(tmp_path):
     unc, _ = k.read_tiff(tmp_path / f"TeLAI_{grid[-1].strftime('A%Y%j')}_unc.tif")
     assert np.allclose(unc[mask], kf.unc(st)[6].numpy(), rtol=1e-6)
     assert info["geotransform"][1] == 10.0 and info["projection"] == "EPSG:32630"
+    # native tiled DEFLATE with a ProjectedCSType GeoKey (GDAL / QGIS recognise the CRS)
+    hdr = k.tiff_info(tmp_path / f"TeLAI_{grid[-1].strftime('A%Y%j')}.tif")
+    assert hdr["tiled"] and hdr["compression"] == 8 and hdr["epsg"] == 32630
+    assert len(out.write_s) == len(grid) - 1 and len(out.written) == 14 * (len(grid) - 1)
 
 
 def test_memory_output_reference_signature():
