@@ -26,13 +26,41 @@ import numpy as np
 
 
 def _mask(args):
-    from .input_output.tiff import read_tiff
+    from .input_output.tiff import read_tiff, tiff_info
 
     if args.mask:
         m, info = read_tiff(args.mask)
         return m.astype(bool), info
+    ref = _file_reference_raster(args)
+    if ref is not None:                 # file-driven run: the grid of the data (ROI-cropped)
+        info = tiff_info(ref)
+        h, w = info["shape"]
+        roi = getattr(args, "roi", None)
+        if roi:
+            h, w = roi[3] - roi[1], roi[2] - roi[0]
+            gt = list(info.get("geotransform", [0, 1, 0, 0, 0, -1]))
+            gt[0] += roi[0] * gt[1]
+            gt[3] += roi[1] * gt[5]
+            info["geotransform"] = gt
+        return np.ones((h, w), dtype=bool), info
     h, w = args.size
     return np.ones((h, w), dtype=bool), {}
+
+
+def _file_reference_raster(args):
+    """First raster of a file-driven BHR / S1 run (defines the grid when no --mask)."""
+    import glob
+    import os
+
+    if getattr(args, "bhr_folder", None):
+        f = sorted(glob.glob(os.path.join(args.bhr_folder, "*_kernels_b0_k0.tif")))
+    elif getattr(args, "s1_folder", None):
+        f = sorted(glob.glob(os.path.join(args.s1_folder, "S1_*", "theta.tif")))
+    else:
+        return None
+    if not f:
+        raise SystemExit("no input rasters found in the data folder")
+    return f[0]
 
 
 def _build(args, comm):
@@ -45,7 +73,14 @@ def _build(args, comm):
     cfg = k.EngineConfig.from_args(args)
     syn = dict(partition=part, device=dev, stream=True, cloud_fraction=args.cloud, seed=args.seed)
     if args.sensor == "bhr":
-        obs = k.SyntheticBHRObservations(mask, n_train=args.n_train or 500, **syn)
+        if args.bhr_folder:      # MCD43 kernel-weight rasters (kafka_test.py:156-217)
+            from .input_output.sentinel import BHRObservations
+            emu = args.emulator or k.make_tip_emulators(n_train=args.n_train or 500)
+            roi = args.roi or [0, 0, None, None]
+            obs = BHRObservations(emu, args.bhr_folder, period=args.period, ulx=roi[0], uly=roi[1], lrx=roi[2],
+                                  lry=roi[3])
+        else:
+            obs = k.SyntheticBHRObservations(mask, n_train=args.n_train or 500, **syn)
         params, factory = k.TIP_PARAMETERS, k.create_nonlinear_observation_operator
         prior = k.JRCPrior(params, mask)
         prop = k.propagate_information_filter_LAI
@@ -68,7 +103,11 @@ def _build(args, comm):
         prior = k.SAILPrior(params, mask)
         prop, q, step = None, None, 2
     elif args.sensor == "s1":
-        obs = k.SyntheticS1Observations(mask, **syn)
+        if args.s1_folder:       # sigma0_VV / sigma0_VH / theta GeoTIFFs per acquisition
+            from .input_output.sentinel import S1Observations
+            obs = S1Observations(args.s1_folder, mask, roi=args.roi)
+        else:
+            obs = k.SyntheticS1Observations(mask, **syn)
         params, factory = ["lai", "sm"], k.create_sar_observation_operator
         prior = k.GaussianPrior(params, mask, [2.0, 0.25], np.diag([1.0, 0.01]))
         prop, q, step = None, None, 6
@@ -83,7 +122,8 @@ def _build(args, comm):
         raise SystemExit(f"unknown sensor {args.sensor}")
     if args.out:
         out = k.KafkaOutput(params, info.get("geotransform", [0, 1, 0, 0, 0, -1]), info.get("projection", ""),
-                            args.out, prefix=args.prefix)
+                            args.out, prefix=args.prefix, level=args.out_level, gather=args.out_gather,
+                            predictor=3 if args.out_fast else 1, strategy="rle" if args.out_fast else None)
     else:
         out = k.DeviceOutput(params)
     kf = k.LinearKalman(obs, out, mask, factory, params, state_propagation=prop,
@@ -129,6 +169,8 @@ def cmd_run(args):
             ing = getattr(kf.observations, "_ingest", None)
             if ing is not None:
                 rec["ingest"] = {"bytes_read": ing.bytes_read, "bytes_h2d": ing.bytes_h2d, "pinned": ing.pinned}
+        if getattr(out, "write_s", None):
+            rec["output"] = {"files": len(out.written), "write_ms": [round(1e3 * t, 1) for t in out.write_s]}
         print(json.dumps(rec))
     comm.destroy()
 
@@ -209,12 +251,21 @@ def main(argv=None):
     r.add_argument("--mask", default=None, help="state mask GeoTIFF (non-zero = active)")
     r.add_argument("--s2-folder", default=None)
     r.add_argument("--emulator-folder", default=None)
+    r.add_argument("--bhr-folder", default=None, help="MCD43 kernel rasters A%%Y%%j_kernels_b{0,1}_k{0,1,2}.tif + _qa")
+    r.add_argument("--s1-folder", default=None, help="S1_* acquisition folders with sigma0_VV/VH and theta")
+    r.add_argument("--emulator", default=None, help="emulator-set .npz for --bhr-folder (default: synthetic TIP)")
+    r.add_argument("--period", type=int, default=16, help="take every period-th BHR date")
+    r.add_argument("--roi", type=int, nargs=4, default=None, metavar=("ULX", "ULY", "LRX", "LRY"))
     r.add_argument("--steps", type=int, default=0, help="time steps (0: all dates)")
     r.add_argument("--n-train", type=int, default=None)
     r.add_argument("--cloud", type=float, default=0.2)
     r.add_argument("--seed", type=int, default=0)
     r.add_argument("--out", default=None, help="GeoTIFF output folder (default: device-resident output)")
     r.add_argument("--prefix", default=None)
+    r.add_argument("--out-level", type=int, default=6, help="DEFLATE level of the output GeoTIFFs (1: fastest)")
+    r.add_argument("--out-fast", action="store_true",
+                   help="floating-point predictor + run-length DEFLATE (about 3x faster encoding)")
+    r.add_argument("--out-gather", action="store_true", help="gather strips to rank 0 and write one raster")
     r.add_argument("--resume", default=None, help="checkpoint directory (latest) or checkpoint path")
     r.add_argument("--log-level", default="WARNING")
     EngineConfig.add_arguments(r)

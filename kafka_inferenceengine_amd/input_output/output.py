@@ -85,14 +85,16 @@ class KafkaOutput:
     go to pinned host memory by an async copy on a side stream, and a writer
     thread encodes tiled DEFLATE GeoTIFFs with the native parallel encoder
     (``csrc/kf_tiff.cpp``, EPSG GeoKeys from ``projection``) while the next
-    timesteps run.  ``level`` trades size for speed (1 ~ 3x faster than 6).
+    timesteps run.  ``level`` trades size for speed; ``predictor=3,
+    strategy="rle"`` (floating-point predictor, run-length zlib) encodes about
+    3x faster than level 6 at a similar ratio.
     With ``gather=True`` and several ranks, strips are gathered to rank 0
     (C3, ``Comm.gather_to_root``) and written as one raster; otherwise every
     rank writes its strip with a per-rank prefix and a shifted geotransform."""
 
     def __init__(self, parameter_list, geotransform, projection, folder, prefix=None, fmt="GTiff",
                  compress="deflate", asynchronous=True, level: int = 6, tile: int = 256, gather: bool = False,
-                 threads: int | None = None):
+                 threads: int | None = None, predictor: int = 1, strategy: str | None = None):
         self.geotransform = geotransform
         self.projection = projection
         self.folder = folder
@@ -104,6 +106,8 @@ class KafkaOutput:
         self.tile = int(tile)
         self.gather = bool(gather)
         self.threads = threads
+        self.predictor = int(predictor)
+        self.strategy = strategy
         os.makedirs(folder, exist_ok=True)
         self._w = _Writer() if asynchronous else None
         self._dev = None          # DeviceOutput: device planes the analysis kernel writes
@@ -133,7 +137,7 @@ class KafkaOutput:
             for ii, param in enumerate(self.parameter_list):
                 fn = _fname(self.folder, param, timestep, prefix, suffix)
                 write_tiff(fn, planes[ii], gt, self.projection, self.compress, level=self.level, tile=self.tile,
-                           threads=self.threads)
+                           threads=self.threads, predictor=self.predictor, strategy=self.strategy)
                 self.written.append(fn)
         self.write_s.append(time.perf_counter() - t0)
 

@@ -46,8 +46,19 @@ def _native():
     return ext if (ext is not None and hasattr(ext, "tiff_write")) else None
 
 
+_STRATEGY = {None: 0, "default": 0, "filtered": 1, "huffman": 2, "rle": 3}
+
+
 def _threads() -> int:
-    return max(1, min(int(os.environ.get("KAFKA_IO_THREADS", "0")) or (os.cpu_count() or 4), 64))
+    """KAFKA_IO_THREADS, else the OMP_NUM_THREADS share of a batch box (whose
+    affinity mask shows the whole machine), else the affinity mask."""
+    n = int(os.environ.get("KAFKA_IO_THREADS", "0") or 0) or int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if not n:
+        try:
+            n = len(os.sched_getaffinity(0))
+        except AttributeError:
+            n = os.cpu_count() or 4
+    return max(1, min(n, 64))
 
 
 def epsg_of(projection) -> int:
@@ -65,11 +76,13 @@ def epsg_of(projection) -> int:
 
 def write_tiff(path, array, geotransform=None, projection: str | None = None, compress: str | None = "deflate",
                rows_per_strip: int = 64, bigtiff: bool | None = None, nodata=None, tile: int | None = 256,
-               level: int = 6, threads: int | None = None):
+               level: int = 6, threads: int | None = None, predictor: int = 1, strategy: str | None = None):
     """Write a 2-D raster or a (bands, H, W) stack.  Native path: tiled
     (``tile`` px) DEFLATE, parallel compression, EPSG GeoKeys from
     ``projection``; ``tile=None`` (or no extension) writes the striped Python
-    layout."""
+    layout.  ``predictor`` 2 (integers) / 3 (floats) is the TIFF horizontal
+    predictor; ``strategy`` "rle" / "huffman" selects the zlib strategy (about
+    3x faster encoding of float rasters at a similar ratio)."""
     a = np.ascontiguousarray(np.asarray(array))
     if a.dtype == np.bool_:
         a = a.astype(np.uint8)
@@ -82,7 +95,8 @@ def write_tiff(path, array, geotransform=None, projection: str | None = None, co
         big = -1 if bigtiff is None else int(bool(bigtiff))
         E.tiff_write(str(path), planes.ctypes.data, nb, H, W, bits, fmt, int(tile),
                      level if compress == "deflate" else 0, threads or _threads(), gt, epsg_of(projection),
-                     "" if projection is None else str(projection), "" if nodata is None else str(nodata), big)
+                     "" if projection is None else str(projection), "" if nodata is None else str(nodata), big,
+                     int(predictor), _STRATEGY[strategy])
         return
     _write_tiff_py(path, a, geotransform, projection, compress, rows_per_strip, bigtiff, nodata)
 
@@ -241,7 +255,8 @@ def read_tiff(path):
 
 
 def _read_tiff_py(path):
-    """Pure-Python reader (strips, uncompressed / DEFLATE, either byte order)."""
+    """Pure-Python reader (strips or tiles, uncompressed / DEFLATE, predictor
+    1-3, either byte order) — the fallback and an independent decoder for tests."""
     with open(path, "rb") as f:
         b = f.read()
     bo = "<" if b[:2] == b"II" else ">"
@@ -279,23 +294,56 @@ def _read_tiff_py(path):
     dt = {(1, 8): "u1", (1, 16): "u2", (2, 16): "i2", (1, 32): "u4", (2, 32): "i4", (3, 32): "f4",
           (3, 64): "f8"}[(fmt, bits)]
     dtype = np.dtype(bo + dt)
-    out = bytearray()
-    for off, cnt in zip(tags[273], tags[279]):
-        chunk = b[off:off + cnt]
+    nb = tags.get(277, [1])[0]
+    planar = tags.get(284, [1])[0]
+    pred = tags.get(317, [1])[0]
+    spp = nb if planar == 1 else 1                 # samples per chunk pixel
+
+    def decode(chunk, w):
+        """-> rows of ``w * spp`` samples with the horizontal predictor undone."""
         if comp in (8, 32946):
             chunk = zlib.decompress(chunk)
         elif comp != 1:
             raise ValueError(f"unsupported TIFF compression {comp}")
-        out += chunk
-    nb = tags.get(277, [1])[0]
-    planar = tags.get(284, [1])[0]
-    arr = np.frombuffer(bytes(out[:nb * W * H * dtype.itemsize]), dtype=dtype)
+        if pred == 1:
+            return np.frombuffer(chunk, dtype=dtype)
+        isz = dtype.itemsize
+        rows = np.frombuffer(chunk, np.uint8)
+        rows = rows[:len(rows) // (w * spp * isz) * (w * spp * isz)].reshape(-1, w * spp * isz)
+        if pred == 2:
+            ui = np.dtype(bo + f"u{isz}")
+            v = rows.view(ui).reshape(rows.shape[0], w, spp)
+            return np.cumsum(v, axis=1, dtype=ui).astype(ui).view(dtype).ravel()
+        # 3: floating point — bytes differenced, MSB plane first (TIFF TN3)
+        u = np.cumsum(rows, axis=1, dtype=np.uint8).reshape(rows.shape[0], isz, w * spp)
+        u = u[:, ::-1, :] if bo == "<" else u
+        return np.ascontiguousarray(u.transpose(0, 2, 1)).view(dtype).ravel()
+
+    planes = nb if planar == 2 else 1
+    full = np.zeros((planes, H, W * spp), dtype=dtype)
+    if 322 in tags:                                 # tiled
+        tw, th = tags[322][0], tags[323][0]
+        across, down = -(-W // tw), -(-H // th)
+        for i, (off, cnt) in enumerate(zip(tags[324], tags[325])):
+            pl, t = divmod(i, across * down)
+            ty, tx = divmod(t, across)
+            tile = decode(b[off:off + cnt], tw).reshape(th, tw * spp)
+            r, c = min(th, H - ty * th), min(tw, W - tx * tw)
+            full[pl, ty * th:ty * th + r, tx * tw * spp:(tx * tw + c) * spp] = tile[:r, :c * spp]
+    else:
+        rps = tags.get(278, [H])[0]
+        per = -(-H // rps)
+        for i, (off, cnt) in enumerate(zip(tags[273], tags[279])):
+            pl, s_ = divmod(i, per)
+            rows = decode(b[off:off + cnt], W)
+            n_r = min(rps, H - s_ * rps)
+            full[pl, s_ * rps:s_ * rps + n_r] = rows[:n_r * W * spp].reshape(n_r, W * spp)
     if nb == 1:
-        arr = arr.reshape(H, W)
+        arr = full[0]
     elif planar == 2:
-        arr = arr.reshape(nb, H, W)
+        arr = full
     else:                    # chunky (pixel-interleaved) -> (bands, H, W)
-        arr = arr.reshape(H, W, nb).transpose(2, 0, 1).copy()
+        arr = full[0].reshape(H, W, nb).transpose(2, 0, 1).copy()
     info = {"shape": (H, W), "bands": nb}
     if 33550 in tags and 33922 in tags:
         sx, sy = tags[33550][0], tags[33550][1]

@@ -58,3 +58,40 @@ def test_farm_single_process_skips_empty_chunks():
     assert sorted(res) == [1, 2, 3, 4]
     assert [c[4] for c in seen] == [1]            # only chunk 1 overlaps the mask
     assert assign(10, 1, 4) == [1, 5, 9]
+
+
+def test_cli_run_bhr_and_s1_folders(tmp_path):
+    """File readers reachable from the CLI (kafka_test.py:156-217): MCD43
+    kernel rasters with an ROI, and Sentinel-1 sigma0 folders."""
+    import datetime as dt
+
+    import kafka_inferenceengine_amd as k
+
+    shape = (14, 12)
+    rng = np.random.default_rng(0)
+    bhr = tmp_path / "mcd43"
+    bhr.mkdir()
+    for i in range(4):
+        tag = (dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i)).strftime("A%Y%j")
+        for band in (0, 1):
+            for kk, v in enumerate((0.2, 0.05, 0.02) if band == 0 else (0.35, 0.1, 0.03)):
+                k.write_tiff(bhr / f"{tag}_kernels_b{band}_k{kk}.tif",
+                             (v * (1 + 0.05 * rng.standard_normal(shape))).astype(np.float32),
+                             [500000.0, 500.0, 0.0, 4400000.0, 0.0, -500.0], "EPSG:32630")
+        k.write_tiff(bhr / f"{tag}_qa.tif", rng.integers(0, 2, shape).astype(np.uint8))
+    out = _run("run", "--sensor", "bhr", "--bhr-folder", str(bhr), "--period", "1", "--roi", "2", "3", "10", "13",
+               "--n-train", "40", "--device", "cpu", "--out", str(tmp_path / "o"))
+    rec = json.loads(out.strip().splitlines()[-1])
+    assert rec["timesteps"] == 4 and rec["finite"] and rec["pixels"] == 80
+    m, info = k.read_tiff(sorted((tmp_path / "o").iterdir())[0])
+    assert m.shape == (10, 8) and info["geotransform"][0] == 501000.0 and info["epsg"] == 32630
+    s1 = tmp_path / "s1"
+    for day in ("20170405", "20170411"):
+        d = s1 / f"S1_A_IW_GRDH_1SDV_{day}T060000_x"
+        d.mkdir(parents=True)
+        for pol in ("VV", "VH"):
+            k.write_tiff(d / f"sigma0_{pol}.tif", rng.uniform(0.02, 0.2, shape).astype(np.float32))
+        k.write_tiff(d / "theta.tif", np.full(shape, 37.0, np.float32))
+    out = _run("run", "--sensor", "s1", "--s1-folder", str(s1), "--device", "cpu")
+    rec = json.loads(out.strip().splitlines()[-1])
+    assert rec["timesteps"] == 2 and rec["finite"] and rec["pixels"] == shape[0] * shape[1]

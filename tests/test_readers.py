@@ -276,3 +276,62 @@ def test_synergy_kernels_broadband(tmp_path):
         assert np.allclose(r.observations[r.mask], want[r.mask])
         w = r.uncertainty.diagonal().reshape(shape)
         assert w[0, 0] == 0 and np.allclose(w[1:, 1:], 1 / np.maximum(2.5e-3, 0.05 * np.abs(want[1:, 1:])) ** 2)
+
+
+def test_native_tiff_predictors_and_strategies(tmp_path):
+    """Native tiled writer with the horizontal / floating-point predictors and
+    the RLE / Huffman-only zlib strategies, decoded by the native reader and by
+    the independent pure-Python decoder."""
+    from kafka_inferenceengine_amd.input_output.tiff import _read_tiff_py, tiff_info
+    rng = np.random.default_rng(3)
+    f = (2.0 + np.cumsum(0.01 * rng.standard_normal((300, 517)), 1)).astype(np.float32)
+    u = rng.integers(0, 4000, (300, 517)).astype(np.uint16)
+    for a, pred, strat in ((f, 3, "rle"), (f, 3, "huffman"), (f, 1, "rle"), (f, 3, None), (u, 2, None),
+                           (u, 2, "rle"), (u, 1, None)):
+        p = tmp_path / f"p{pred}_{strat}_{a.dtype.name}.tif"
+        k.write_tiff(p, a, [0.0, 10.0, 0.0, 0.0, 0.0, -10.0], "EPSG:32630", level=1, tile=128,
+                     predictor=pred, strategy=strat)
+        assert tiff_info(p)["predictor"] == pred
+        b, _ = k.read_tiff(p)
+        c, _ = _read_tiff_py(p)
+        assert np.array_equal(a, b) and np.array_equal(a, c), (pred, strat, a.dtype)
+    # python decoder also covers striped planar stacks from the fallback writer
+    st = rng.random((3, 40, 33)).astype(np.float32)
+    p = tmp_path / "stack.tif"
+    k.write_tiff(p, st, tile=None, rows_per_strip=7)
+    assert np.array_equal(_read_tiff_py(p)[0], st)
+
+
+def test_reproject_utm_to_wgs84_golden(tmp_path):
+    """CRS-aware warp (reference utils.py:43-64): Barrax_pivots.tif (UTM 30N)
+    warped onto a WGS84 grid agrees with the pivot polygons rasterised straight
+    on that WGS84 grid (an independent path: point-in-polygon after the
+    polygon transform), and warping back onto the UTM grid restores the mask."""
+    if not (os.path.exists(REF_TIF) and os.path.exists(REF_JSON)):
+        return
+    from kafka_inferenceengine_amd.input_output.utils import reproject_image
+    m, info = k.read_tiff(REF_TIF)
+    x0, y0, x1, y1 = k.raster_extent_feature(REF_TIF).bounds()
+    res = 5e-5                                           # ~4.3 x 5.6 m at 39 N: finer than the 10 m source
+    W, H = int(np.ceil((x1 - x0) / res)), int(np.ceil((y1 - y0) / res))
+    gt = [x0, res, 0.0, y1, 0.0, -res]
+    warped = reproject_image(m, info["geotransform"], (H, W), gt, 0, src_crs=info["projection"], dst_crs=4326)
+    direct = k.rasterize_polygons(k.read_geojson_polygons(REF_JSON), gt, (H, W), "EPSG:4326")
+    w = warped > 0
+    assert w.sum() > 40000
+    # disagreement only along the polygon edges: < 2 % of the pivot area
+    assert (w ^ direct).sum() < 0.025 * direct.sum()
+    assert abs(int(w.sum()) - int(direct.sum())) < 0.002 * direct.sum()          # no systematic shrink/grow
+    cw, cd = np.argwhere(w).mean(0), np.argwhere(direct).mean(0)
+    assert np.abs(cw - cd).max() < 0.25                                         # no shift (target pixels)
+    back = reproject_image(warped, gt, m.shape, info["geotransform"], 0, src_crs=4326, dst_crs=info["projection"])
+    assert ((back > 0) ^ (m > 0)).sum() < 0.005 * (m > 0).sum()
+    # reference call form: file paths, target raster gives grid and CRS
+    tgt = tmp_path / "wgs84_grid.tif"
+    k.write_tiff(tgt, np.zeros((H, W), np.uint8), gt, "EPSG:4326")
+    assert np.array_equal(reproject_image(REF_TIF, str(tgt)), warped)
+    # same-CRS bilinear on a linear ramp is exact away from the edges
+    ramp = np.add.outer(np.arange(50.0), 2 * np.arange(60.0)).astype(np.float32)
+    out = reproject_image(ramp, [0, 1, 0, 0, 0, -1], (40, 40), [5.25, 1, 0, -5.5, 0, -1], resampling="bilinear")
+    rr, cc = np.meshgrid(np.arange(40) + 5.5 + 0.5 - 0.5, np.arange(40) + 5.25 + 0.5 - 0.5, indexing="ij")
+    assert np.allclose(out[:-2, :-2], (rr + 2 * cc)[:-2, :-2], atol=1e-4)
