@@ -70,6 +70,9 @@ def test_analysis_device_vs_host_and_oracle(cuda, dn16):
 
 
 def test_propagate_and_invert_device(cuda):
+    """Device propagate vs the host runner (the reference-API oracle of every
+    mode is tests/test_oracles.py::test_propagate_modes_vs_reference_api);
+    invert vs torch.linalg.inv."""
     rng = np.random.default_rng(1)
     N, n = 5000, 7
     A = C.spd_blocks(rng, N, n)
@@ -94,23 +97,13 @@ def test_propagate_and_invert_device(cuda):
 
 
 def test_gain_jacobi_hessian_unpack_device(cuda):
-    prob = C.tip_problem(N=4000, seed=12)
-    n, N = 7, 4000
-    res = []
-    for dev in (cuda, "cpu"):
-        tab = C.table(prob, dev)
-        Pcov = np.linalg.inv(prob["Pf"])
-        xo = torch.zeros((n, N), device=dev)
-        po = torch.zeros((28, N), device=dev)
-        K.gain(n, tab, C.soa(prob["x"], dev), C.soa(prob["xf"], dev), C.packed(Pcov, dev), xo, po)
-        a = C.packed(prob["Pf"], dev)
-        K.hessian(n, tab, C.soa(prob["x"], dev), a)
-        mean = torch.zeros((n, N), device=dev)
-        unc = torch.zeros((n, N), device=dev)
-        K.unpack(n, xo, C.packed(prob["Pf"], dev), mean, unc)
-        res.append([t.cpu() for t in (xo, po, a, mean, unc)])
-    for d, h in zip(*res):
-        assert close(d, h, 2e-3)
+    """Independent references: the GP Hessian against the NumPy emulator
+    Hessian, the Jacobi sweep against per-pixel NumPy solves, unpack / gather /
+    LUT against closed forms and torch (gain: tests/test_oracles.py)."""
+    from test_kernels import hessian_vs_numpy, jacobi_sweep_vs_numpy, unpack_gather_lut_vs_torch
+    hessian_vs_numpy(cuda)
+    jacobi_sweep_vs_numpy(cuda)
+    unpack_gather_lut_vs_torch(cuda)
 
 
 def test_operator_device_vs_numpy(cuda):
@@ -128,7 +121,11 @@ def test_operator_device_vs_numpy(cuda):
         assert np.allclose(h.cpu().numpy().T, full, atol=5e-5)
 
 
-def test_engine_gpu_matches_cpu(cuda):
+def test_engine_gpu_matches_cpu_and_oracle(cuda):
+    """The device engine against the float64 NumPy oracle of the reference run
+    loop (tests/oracle.py) and against the host runner."""
+    from oracle import oracle_run
+    from kafka_inferenceengine_amd.utils.blocks import interleaved_to_soa, pack_blocks, sparse_to_blocks
     mask = np.ones((48, 40), bool)
     mask[:5, :6] = False
     grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
@@ -145,6 +142,20 @@ def test_engine_gpu_matches_cpu(cuda):
     assert outs[0][2] == outs[1][2]
     assert close(outs[0][0], outs[1][0], 2e-3)
     assert close(outs[0][1], outs[1][1], 2e-3, floor=1.0)
+    obs = k.SyntheticBHRObservations(mask, n_train=100, device="cpu", stream=True, n_pool=3, field_cell=8)
+    x0, Pinv = k.JRCPrior(k.TIP_PARAMETERS, mask).process_prior(None)
+    Q = np.zeros_like(x0)
+    Q[6::7] = 0.04
+    xr, Pr, iters = oracle_run(obs, mask, k.create_nonlinear_observation_operator, 7, grid, x0, Pinv,
+                               propagator=k.propagate_information_filter_LAI, Q=Q)
+    N = int(mask.sum())
+    xs = outs[0][0][:, :N].numpy()
+    assert [g[0] for g in outs[0][2]] == iters
+    xo = interleaved_to_soa(xr, 7)
+    assert np.max(np.abs(xs - xo) / (np.abs(xo).max(axis=1, keepdims=True) + 1e-3)) < 2e-3
+    Po = pack_blocks(sparse_to_blocks(Pr, 7, check=False))
+    Ps = outs[0][1][:, :N].numpy()
+    assert np.max(np.abs(Ps - Po) / (np.abs(Po).max(axis=1, keepdims=True) + 1e-6)) < 2e-3
 
 
 def test_streamer_pinned_and_overlaps(cuda):

@@ -193,17 +193,21 @@ def test_operator_gp_sar_linear_vs_numpy():
 
 
 def test_hessian_vs_numpy():
+    hessian_vs_numpy("cpu")
+
+
+def hessian_vs_numpy(device):
     prob = C.tip_problem(N=300, seed=6)
-    tab = C.table(prob, "cpu")
-    a = torch.zeros((28, 300))
-    K.hessian(7, tab, C.soa(prob["x"], "cpu"), a)
+    tab = C.table(prob, device)
+    a = torch.zeros((28, 300), device=device)
+    K.hessian(7, tab, C.soa(prob["x"], device), a)
     ref = np.zeros((300, 7, 7))
     for b, (y, w) in enumerate(prob["bands"]):
         mp = k.TIP_BAND_MAPPER[b]
         f, _ = prob["ems"][b].predict(prob["x"][:, mp])
         Hs = prob["ems"][b].hessian(prob["x"][:, mp])
         ref[np.ix_(np.arange(300), mp, mp)] -= (w * (y - f))[:, None, None] * Hs
-    got = unpack_blocks(a.numpy(), 7)
+    got = unpack_blocks(a.cpu().numpy(), 7)
     assert np.max(np.abs(got - ref)) / (np.abs(ref).max() + 1e-9) < 2e-3
 
 
@@ -221,27 +225,36 @@ def test_gp_hessian_finite_difference():
 
 
 def test_unpack_and_gather_and_lut():
+    unpack_gather_lut_vs_torch("cpu")
+
+
+def unpack_gather_lut_vs_torch(device):
     rng = np.random.default_rng(7)
     N = 200
     x = rng.normal(size=(N, 7))
     A = C.spd_blocks(rng, N, 7)
-    idx = torch.tensor(np.sort(rng.choice(400, N, replace=False)), dtype=torch.int64)
-    mean = torch.zeros((7, 400))
-    unc = torch.zeros((7, 400))
-    K.unpack(7, C.soa(x, "cpu"), C.packed(A, "cpu"), mean, unc, idx=idx)
-    assert np.allclose(mean.numpy()[:, idx.numpy()], x.T.astype(np.float32))
-    assert np.allclose(unc.numpy()[:, idx.numpy()], 1 / np.sqrt(np.einsum("nii->ni", A)).T, rtol=1e-6)
-    src = torch.arange(1000, dtype=torch.float32)
+    idx = torch.tensor(np.sort(rng.choice(400, N, replace=False)), dtype=torch.int64, device=device)
+    mean = torch.zeros((7, 400), device=device)
+    unc = torch.zeros((7, 400), device=device)
+    K.unpack(7, C.soa(x, device), C.packed(A, device), mean, unc, idx=idx)
+    ii = idx.cpu().numpy()
+    assert np.allclose(mean.cpu().numpy()[:, ii], x.T.astype(np.float32))
+    assert np.allclose(unc.cpu().numpy()[:, ii], 1 / np.sqrt(np.einsum("nii->ni", A)).T, rtol=1e-6)
+    src = torch.arange(1000, dtype=torch.float32, device=device)
     g = K.gather(src, idx)
     assert torch.equal(g, src[idx])
-    lut = torch.tensor(rng.normal(size=(50, 3)), dtype=torch.float32)
-    pts = torch.tensor(rng.normal(size=(3, 300)), dtype=torch.float32)
+    lut = torch.tensor(rng.normal(size=(50, 3)), dtype=torch.float32, device=device)
+    pts = torch.tensor(rng.normal(size=(3, 300)), dtype=torch.float32, device=device)
     got = K.lut_nearest(lut, pts)
-    ref = torch.cdist(pts.T, lut).argmin(1)
-    assert torch.equal(got.long(), ref)
+    ref = torch.cdist(pts.T.cpu(), lut.cpu()).argmin(1)
+    assert torch.equal(got.long().cpu(), ref)
 
 
 def test_jacobi_sweep_vs_numpy():
+    jacobi_sweep_vs_numpy("cpu")
+
+
+def jacobi_sweep_vs_numpy(device):
     from kafka_inferenceengine_amd.parallel import StripPartition
     rng = np.random.default_rng(8)
     mask = rng.random((12, 9)) > 0.2
@@ -250,11 +263,12 @@ def test_jacobi_sweep_vs_numpy():
     A = C.spd_blocks(rng, N, n)
     b = rng.normal(size=(N, n))
     x = rng.normal(size=(N, n))
-    nbr = torch.from_numpy(part.neighbour_table())
-    out = torch.zeros((n, N))
+    nbr = torch.from_numpy(part.neighbour_table()).to(device)
+    out = torch.zeros((n, N), device=device)
     gamma, regmask = 3.0, 0b0101
-    K.jacobi(n, C.packed(A, "cpu"), C.soa(b, "cpu"), C.soa(x, "cpu"), nbr, C.soa(x, "cpu"), out, gamma, regmask, N)
-    nb = nbr.numpy()
+    K.jacobi(n, C.packed(A, device), C.soa(b, device), C.soa(x, device), nbr, C.soa(x, device), out, gamma, regmask,
+             N)
+    nb = nbr.cpu().numpy()
     ref = np.zeros((N, n))
     for p in range(N):
         Ap, bp = A[p].copy(), b[p].copy()
@@ -264,7 +278,7 @@ def test_jacobi_sweep_vs_numpy():
                 Ap[j, j] += gamma * len(qs)
                 bp[j] += gamma * sum(x[q, j] for q in qs)
         ref[p] = np.linalg.solve(Ap, bp)
-    assert np.allclose(out.numpy().T, ref, rtol=1e-4, atol=1e-5)
+    assert np.allclose(out.cpu().numpy().T, ref, rtol=1e-4, atol=1e-5)
 
 
 def test_neighbour_table_matches_raster():
