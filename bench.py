@@ -46,6 +46,14 @@ CONFIGS = {
                                        "bf16 observations, LAI propagator", baseline=BASELINE_7P),
     "prosail10": dict(size=10980, n_train=250, model="PROSAIL 10-param, 10-band S2 GP emulators, SAIL prior reset",
                       baseline=BASELINE_10P),
+    # harder 10p-10b problem: T=500, strongly non-linear
+    # emulators (Beer-law gap fraction, saturating leaf optics), wider truth,
+    # and the reference's measured 6 Gauss-Newton iterations per date
+    #  -- fixed (min = max = 6): at full-tile scale the reference
+    # criterion ||dx|| / len(x) < 1e-3 is met after 2 iterations by any problem
+    "prosail10_hard": dict(size=10980, n_train=500, hard=True, spread=1.0, rel_unc=0.04, gn=6,
+                           model="PROSAIL 10-param, 10-band S2 GP emulators (T=500, non-linear), SAIL prior reset, "
+                                 "6 GN iterations/date", baseline=BASELINE_10P),
     "spatial": dict(size=10980, n_train=500, gamma=5.0, sweeps=4,
                     model="JRC-TIP 7-param + GMRF spatial prior on TLAI (block-Jacobi, halo exchange)",
                     baseline=BASELINE_7P),
@@ -104,6 +112,10 @@ def build(cfg_name, a, mask, part, dev, comm):
         if cfg_name == "prosail10":
             obs = k.SyntheticS2Observations(mask, dates=dates, n_bands=10, n_train=T, partition=part, device=dev,
                                             n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=seed)
+        elif cfg_name == "prosail10_hard":
+            obs = k.SyntheticS2Observations(mask, dates=dates, n_bands=10, n_train=T, partition=part, device=dev,
+                                            n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=seed,
+                                            hard=True, spread_scale=c["spread"], rel_unc=c["rel_unc"])
         else:
             s2 = k.SyntheticS2Observations(mask, dates=dates, n_bands=13, n_train=T, partition=part, device=dev,
                                            n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=seed)
@@ -112,9 +124,10 @@ def build(cfg_name, a, mask, part, dev, comm):
                                                seed=seed + 21)
             obs = k.MultiSensorObservations([s2, olci])
         prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
+        gn = {"min_iterations": c["gn"], "max_iterations": c["gn"]} if "gn" in c else {}
         kf = k.LinearKalman(obs, k.DeviceOutput(k.SAIL_PARAMETERS), mask, k.create_prosail_observation_operator,
                             k.SAIL_PARAMETERS, state_propagation=None, prior=prior,
-                            config=mkcfg(), comm=comm, partition=part)
+                            config=mkcfg(**gn), comm=comm, partition=part)
         state = kf.state_from_prior(prior)
     return obs, kf, state, dates
 
@@ -241,6 +254,7 @@ def main():
         metric = HEADLINE_METRIC if a.config == "tip7" and H == 10980 else \
             f"pixel-state updates/sec (whole node), {H}x{W} tile, {a.config}"
         ingest = sum(s.ingest_bytes() for s in srcs) // max(1, a.warmup + a.steps)
+        n_gn = sum(sum(g) if isinstance(g, (list, tuple)) else (g or 0) for g in gn)
         rec = {"metric": metric, "value": round(value, 1), "unit": "pixel-state updates/s", "n_gpus": n_dev,
                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 3),
                "higher_is_better": True, "scaling": "strong",
@@ -251,7 +265,8 @@ def main():
                "config": {"name": a.config, "model": c["model"], "tile": f"{H}x{W}", "active_pixels": part.N_total,
                           "global_batch": part.N_total, "seq_len": 1,
                           "gp_train_points": a.n_train or c.get("n_train"), "parallelism": f"tile-dp{world}" + (f" x band-tp{B}" if B > 1 else ""),
-                          "gn_iterations": gn, "finite": ok, "fallback_frac": round(fallback, 6), "ingest_bytes_per_step": ingest,
+                          "gn_iterations": gn, "ms_per_gn_iteration": round(1e3 * elapsed / max(1, n_gn), 3),
+                          "finite": ok, "fallback_frac": round(fallback, 6), "ingest_bytes_per_step": ingest,
                           "baseline_updates_per_s": c["baseline"]}}
         if n_dev != n_ranks:
             rec["rehearsal"] = f"{n_ranks} ranks on {n_dev} device(s): logic rehearsal, not a scaling point"

@@ -315,6 +315,20 @@ static Tag mk_ascii(uint16_t tag, const std::string& s) {
   return t;
 }
 
+// Raw file of n bytes written by parallel pwrite of 64 MiB pieces (checkpoint
+// payloads: a 10980^2 PROSAIL state is ~31 GB); optional fsync before return.
+void write_raw(const std::string& path, const void* data, uint64_t n, int nthreads, bool sync) {
+  File f(path, O_WRONLY | O_CREAT | O_TRUNC);
+  if (n && ::ftruncate(f.fd, (off_t)n) != 0) throw std::runtime_error("ftruncate failed: " + path);
+  const uint64_t piece = 64ull << 20, np = (n + piece - 1) / piece;
+  const uint8_t* src = static_cast<const uint8_t*>(data);
+  parallel_for((int64_t)np, nthreads, [&](int64_t i) {
+    const uint64_t off = (uint64_t)i * piece;
+    f.write_at(src + off, std::min(piece, n - off), off);
+  });
+  if (sync && ::fsync(f.fd) != 0) throw std::runtime_error("fsync failed: " + path);
+}
+
 void write(const std::string& path, const void* data, int nb, uint64_t H, uint64_t W, int bits, int fmt,
            uint32_t tile, int level, int nthreads, const std::vector<double>& gt, int epsg,
            const std::string& citation, const std::string& nodata, int force_big, int predictor, int strategy) {
@@ -505,6 +519,10 @@ void bind_tiff(py::module_& m) {
                         uint64_t c1, int nthreads) {
     py::gil_scoped_release nogil;
     tiff::read_window(path, band, reinterpret_cast<void*>(dst), r0, r1, c0, c1, nthreads);
+  });
+  m.def("write_raw", [](const std::string& path, uintptr_t src, uint64_t n, int nthreads, bool sync) {
+    py::gil_scoped_release nogil;
+    tiff::write_raw(path, reinterpret_cast<const void*>(src), n, nthreads, sync);
   });
   m.def("tiff_write", [](const std::string& path, uintptr_t src, int nb, uint64_t H, uint64_t W, int bits, int fmt,
                          uint32_t tile, int level, int nthreads, const std::vector<double>& gt, int epsg,

@@ -169,6 +169,10 @@ def cmd_run(args):
             ing = getattr(kf.observations, "_ingest", None)
             if ing is not None:
                 rec["ingest"] = {"bytes_read": ing.bytes_read, "bytes_h2d": ing.bytes_h2d, "pinned": ing.pinned}
+        ck = getattr(kf, "checkpointer", None)
+        if ck is not None and ck.stats["bytes"]:
+            rec["checkpoint"] = {k_: [round(v, 3) for v in vals] for k_, vals in ck.stats.items() if k_ != "bytes"}
+            rec["checkpoint"]["GB"] = [round(b / 1e9, 2) for b in ck.stats["bytes"]]
         if getattr(out, "write_s", None):
             rec["output"] = {"files": len(out.written), "write_ms": [round(1e3 * t, 1) for t in out.write_s]}
         print(json.dumps(rec))

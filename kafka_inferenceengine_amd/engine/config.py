@@ -54,6 +54,7 @@ class EngineConfig:
     metrics_path: str | None = None           # JSONL metrics (per date / timestep)
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0                 # timesteps between checkpoints (0: off)
+    checkpoint_keep: int = 0                  # committed checkpoints kept (older ones pruned; 0: all)
     comm_timeout_s: float = 600.0
     phase_timing: bool = False                # per-phase hipEvent timers without metrics_path
     sync_timing: bool = False                 # device-synchronising per-phase timers

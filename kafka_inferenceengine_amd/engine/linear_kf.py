@@ -222,6 +222,7 @@ class LinearKalman:
         from ..input_output.checkpoint import CheckpointManager
 
         ckpt = CheckpointManager(self.config.checkpoint_dir, self) if self.config.checkpoint_dir else None
+        self.checkpointer = ckpt
         resume_t = None
         analysis = None
         if resume_from is not None:

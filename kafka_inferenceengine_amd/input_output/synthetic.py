@@ -334,16 +334,16 @@ class SyntheticS2Observations(SyntheticObservations):
     BAND_NAMES = ["02", "03", "04", "05", "06", "07", "08", "8A", "09", "12", "01", "10", "11"]
 
     def __init__(self, state_mask, dates=None, n_bands=10, emulators=None, n_train=250, n_params=10,
-                 state_maps=None, **kw):
+                 state_maps=None, spread_scale: float = 0.5, hard: bool = False, **kw):
         from ..models.gp import make_prosail_emulators
         from ..models.priors import sail_prior
 
-        ems = emulators or make_prosail_emulators(n_bands, n_train, kw.get("seed", 0), n_params)
+        ems = emulators or make_prosail_emulators(n_bands, n_train, kw.get("seed", 0), n_params, hard=hard)
         maps = state_maps or [list(range(ems[b].n_inputs)) for b in range(n_bands)]
         specs = [gp_spec(ems[b], maps[b]) for b in range(n_bands)]
         mean, cov, _ = sail_prior()
         mean, cov = mean[:n_params], cov[:n_params, :n_params]
-        spread = 0.5 * np.maximum(np.sqrt(np.diag(cov)), 0.02)
+        spread = float(spread_scale) * np.maximum(np.sqrt(np.diag(cov)), 0.02)
         lo, hi, c = _truth_box(ems, maps, n_params, mean, spread)
         dates = dates or _date_list(dt.datetime(2017, 7, 3), 10, 2)
         kw.setdefault("temporal_params", (6,))

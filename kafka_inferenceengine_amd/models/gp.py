@@ -323,11 +323,26 @@ def tip_bhr_target(band: int):
     return f
 
 
-def prosail_target(band: int, n_params: int = 10):
-    """Smooth reflectance-like function of the 10 transformed PROSAIL parameters."""
+def prosail_target(band: int, n_params: int = 10, hard: bool = False):
+    """Smooth reflectance-like function of the 10 transformed PROSAIL parameters.
+    ``hard``: a canopy/soil mixture with Beer-law gap fraction and leaf-optics
+    saturation — curved enough that Gauss-Newton takes several iterations per
+    date, as the reference's real PROSAIL emulators do (6)."""
     rng = np.random.default_rng(1000 + band)
     w = rng.normal(0, 0.08, n_params)
     b = rng.uniform(0.5, 2.0, n_params)
+    if hard:
+        from .priors import sail_prior
+        wh = rng.normal(0, 1.2, n_params)
+        ctr = sail_prior()[0][:n_params]
+
+        def fh(X):
+            lai_t = np.clip(X[:, 6], 0.0, 1.0)                      # exp(-LAI/2)
+            gap = lai_t ** (1.5 + 0.25 * (band % 4))               # view/sun path gap fraction
+            leaf = 0.05 + 0.45 / (1.0 + np.exp(-(X - ctr) @ wh))   # saturating leaf optics
+            soil = 0.08 + 0.25 * np.clip(X[:, min(8, X.shape[1] - 1)], 0.0, 1.5) ** 2
+            return leaf * (1.0 - gap) + soil * gap
+        return fh
 
     def f(X):
         lai_t = np.clip(X[:, 6], 0.0, 1.0)  # exp(-LAI/2)
@@ -353,13 +368,16 @@ def make_tip_emulators(n_train: int = 500, seed: int = 0):
     return ems
 
 
-def make_prosail_emulators(n_bands: int = 10, n_train: int = 250, seed: int = 0, n_params: int = 10):
-    """Per-band PROSAIL-like emulators over the 10 transformed parameters."""
+def make_prosail_emulators(n_bands: int = 10, n_train: int = 250, seed: int = 0, n_params: int = 10,
+                           hard: bool = False):
+    """Per-band PROSAIL-like emulators over the 10 transformed parameters
+    (``hard``: the strongly non-linear targets of :func:`prosail_target`)."""
     from .priors import sail_prior
 
     mean, covar, _ = sail_prior()
     sig = np.sqrt(np.diag(covar))
     lo = mean - 3 * np.maximum(sig, 0.05)
     hi = mean + 3 * np.maximum(sig, 0.05)
-    return [GaussianProcessEmulator.synthetic(prosail_target(b, n_params), lo[:n_params], hi[:n_params], n_train,
-                                              seed + b, name=f"prosail_b{b}") for b in range(n_bands)]
+    return [GaussianProcessEmulator.synthetic(prosail_target(b, n_params, hard), lo[:n_params], hi[:n_params],
+                                              n_train, seed + b, name=f"prosail_b{b}{'h' if hard else ''}")
+            for b in range(n_bands)]

@@ -6,7 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" && mkdir -p gpurun_out
 SZ=${SZ:-10980}; D=${D:-3}; OUT=${OUT:-/tmp/kafka_s2_archive}
 # RUNARGS: extra run flags, e.g. "--out /tmp/kafka_out --out-level 1" or
-# "--checkpoint-dir /tmp/kafka_ckpt --checkpoint-every 1"
+# "--checkpoint-dir /tmp/kafka_ckpt --checkpoint-every 1 --checkpoint-keep 1"
 RUNARGS=${RUNARGS:-}
 df -h /tmp | tail -1; free -g | head -2
 rm -rf "$OUT"

@@ -115,6 +115,17 @@ def test_checkpoint_resume_bit_identical(tmp_path):
     assert torch.equal(st.x, full.x) and torch.equal(st.P, full.P)
 
 
+def test_checkpoint_retention_keeps_newest(tmp_path):
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=4)
+    grid = _grid(5)
+    kf = _engine(mask, obs, Q, checkpoint_dir=str(tmp_path), checkpoint_every=1, checkpoint_keep=2)
+    kf.run(grid, x0, None, Pinv)
+    kept = sorted(p.name for p in tmp_path.iterdir())
+    assert kept == [g.strftime("A%Y%j") for g in grid[-2:]]
+    assert k.CheckpointManager.latest(tmp_path).name == grid[-1].strftime("A%Y%j")
+    assert kf.checkpointer.stats["bytes"] and len(kf.checkpointer.stats["write_s"]) == 4
+
+
 def test_kafka_output_tiff_roundtrip(tmp_path):
     mask, obs, prior, x0, Pinv, Q = _setup(seed=5)
     grid = _grid(3)
