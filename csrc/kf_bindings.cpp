@@ -131,6 +131,13 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .def_readwrite("ld", &GainArgs::ld)
       .def_readwrite("n_bands", &GainArgs::n_bands)
       .def_readwrite("joseph", &GainArgs::joseph)
+      .def_readwrite("fast_d", &GainArgs::fast_d)
+      .def_readwrite("fast_obs", &GainArgs::fast_obs)
+      .def_readwrite("out_plane", &GainArgs::out_plane)
+      .PTR_FIELD(GainArgs, prop, const PropArgs*)
+      .PTR_FIELD(GainArgs, out_mean, float*)
+      .PTR_FIELD(GainArgs, out_unc, float*)
+      .PTR_FIELD(GainArgs, out_idx, const int64_t*)
       .PTR_FIELD(GainArgs, bands, const BandDesc*)
       .PTR_FIELD(GainArgs, x_prev, const float*)
       .PTR_FIELD(GainArgs, x_f, const float*)

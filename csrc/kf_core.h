@@ -999,66 +999,149 @@ KF_HD bool pixel_invert(const float* src, float* dst, int64_t ld, int64_t p) {
 // K1g: covariance / gain form, bands processed as sequential scalar updates
 // (equal to the joint update for diagonal R):
 //   s = h^T P h + 1/w,  k = P h / s,  x += k (y' - h^T x),  P -= k (P h)^T
-// with y' = y - H0 + h . x0 (iterated EKF linearised about x0).
+// with y' = y - H0 + h . x0 (iterated EKF linearised about x0).  Same fast
+// paths as K1 (FD: all-GP bands with FD inputs, FOBS: one encoding), the
+// forecast fused from the previous analysis covariance (prop) and the output
+// rasters written by the last iteration (out_mean / out_unc).
 struct GainArgs {
   int64_t N, ld;
   int32_t n_bands, joseph;
+  int32_t fast_d, fast_obs;  // host hint, as AnalysisArgs
   const BandDesc* bands;
-  const float* x_prev;
+  const float* x_prev;   // linearisation point (null with prop: the forecast)
   const float* x_f;
   const float* p_f;      // forecast covariance (packed)
   float* x_out;
-  float* p_out;          // analysis covariance (packed)
+  float* p_out;          // analysis covariance (packed, may be null)
   uint8_t* status;
   double* partials;
+  const PropArgs* prop;  // fused forecast (device copy; p_a = analysis COVARIANCE); x_f / p_f unused
+  float* out_mean;       // fused output: x and 1/sqrt(diag P^-1) into [NP][out_plane] rasters
+  float* out_unc;
+  const int64_t* out_idx;
+  int64_t out_plane;
 };
 
+// The partial-prior-reset forecast (forecast_partial) of an analysis held as a
+// covariance, returned as a covariance: Pa^-1 = inv(P_a) supplies the
+// propagated diagonals, C = reset precision with those diagonals, P_f = C^-1.
+// PROP_PRIOR (mask 0) and PROP_INFO_APPROX (all propagated, C0 = 0) map onto
+// it as for K1 (ops/kernels.py:prop_args).
 template <int NP>
+KF_HD uint8_t forecast_partial_cov(const KF_CONST_AS PropArgs* a, int64_t p, float (&xf)[NP],
+                                   float (&P)[ntri(NP)]) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a->ld;
+  uint8_t st = 0;
+  float C[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) C[t] = a->reset_cinv[t];
+  if (a->prop_mask) {
+    float U[NT], Pi[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) U[t] = a->p_a[t * ld + p];
+    if (!chol_packed<NP>(U)) st |= ST_NONSPD;
+    chol_inverse<NP>(U, Pi);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      if ((a->prop_mask >> j) & 1u) {
+        const float q = a->q_pix ? a->q_pix[j * ld + p] : a->q[j];
+        C[tri(NP, j, j)] = kf_rcp(kf_rcp(Pi[tri(NP, j, j)]) + q);
+      }
+    }
+  }
+  forecast_partial_mean<NP>(a, p, xf);
+  if (!chol_packed<NP>(C)) st |= ST_NONSPD;
+  chol_inverse<NP>(C, P);
+  return st;
+}
+
+template <int NP, int FD = 0, int FOBS = 0>
 KF_HD float pixel_gain(const GainArgs& a, int64_t p) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a.ld;
   float x0[NP], x[NP], P[NT];
   uint8_t st = 0;
+  if (a.prop) {
+    st |= forecast_partial_cov<NP>(opaque(cptr(a.prop)), p, x, P);
+  } else {
 #pragma unroll
-  for (int j = 0; j < NP; ++j) { x0[j] = a.x_prev[j * ld + p]; x[j] = a.x_f[j * ld + p]; }
+    for (int j = 0; j < NP; ++j) x[j] = a.x_f[j * ld + p];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) P[t] = a.p_f[t * ld + p];
+    for (int t = 0; t < NT; ++t) P[t] = a.p_f[t * ld + p];
+  }
+  if (a.x_prev) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
+  } else {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) x0[j] = x[j];
+  }
+  int nobs = 0;
   for (int bi = 0; bi < a.n_bands; ++bi) {
     const BandDesc bd = cptr(a.bands)[bi];
     float y, w;
-    decode_obs(bd, p, y, w);
+    decode_obs<FOBS>(bd, p, y, w);
     if (!(w > 0.f)) { if (bd.h0_out) bd.h0_out[p] = 0.f; continue; }
     float H0, h[NP];
-    const bool ok = eval_operator<NP>(bd, p, ld, x0, H0, h);
-    if (bd.h0_out) bd.h0_out[p] = H0;
+    bool ok;
+    if constexpr (FD > 0) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      gp_eval<NP, FD, 4, false, true>(bd, x0, H0, h, a.bands + bi);
+#else
+      gp_eval<NP, FD>(bd, x0, H0, h);
+#endif
+      ok = finitef(H0);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);
+    } else {
+      ok = eval_operator<NP>(bd, p, ld, x0, H0, h);
+    }
+    float* h0o = bd.h0_out;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (FD > 0) h0o = opaque(cptr(a.bands + bi))->h0_out;
+#endif
+    if (h0o) h0o[p] = H0;
     if (!ok) { st |= ST_BAD_OP; continue; }
+    ++nobs;
     float ph[NP];
     symv<NP>(P, h, ph);
-    float s = 1.f / w, innov = y - H0;
+    const float r = kf_rcp(w);                  // observation variance
+    float s = r, innov = y - H0;
 #pragma unroll
     for (int j = 0; j < NP; ++j) { s = fmaf(h[j], ph[j], s); innov = fmaf(h[j], x0[j] - x[j], innov); }
-    const float is = 1.f / s;
+    const float is = kf_rcp(s);
+    float k[NP];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) x[j] = fmaf(ph[j] * is, innov, x[j]);
+    for (int j = 0; j < NP; ++j) { k[j] = ph[j] * is; x[j] = fmaf(k[j], innov, x[j]); }
     if (a.joseph) {
-      // P = (I - k h^T) P (I - k h^T)^T + k k^T / w
-      float k[NP];
-#pragma unroll
-      for (int j = 0; j < NP; ++j) k[j] = ph[j] * is;
-      float hp[NP];  // h^T P  == ph (P symmetric)
-#pragma unroll
-      for (int j = 0; j < NP; ++j) hp[j] = ph[j];
-      const float hph = s - 1.f / w;
+      // P = (I - k h^T) P (I - k h^T)^T + k k^T r = P - k ph^T - ph k^T + k k^T (h^T P h + r)
 #pragma unroll
       for (int i = 0; i < NP; ++i)
 #pragma unroll
         for (int j = i; j < NP; ++j)
-          P[tri(NP, i, j)] = P[tri(NP, i, j)] - k[i] * hp[j] - hp[i] * k[j] + k[i] * k[j] * (hph + 1.f / w);
+          P[tri(NP, i, j)] = P[tri(NP, i, j)] - k[i] * ph[j] - ph[i] * k[j] + k[i] * k[j] * s;
     } else {
 #pragma unroll
       for (int i = 0; i < NP; ++i)
 #pragma unroll
-        for (int j = i; j < NP; ++j) P[tri(NP, i, j)] = fmaf(-ph[i] * is, ph[j], P[tri(NP, i, j)]);
+        for (int j = i; j < NP; ++j) P[tri(NP, i, j)] = fmaf(-k[i], ph[j], P[tri(NP, i, j)]);
+    }
+  }
+  if (nobs == 0) st |= ST_NO_OBS;
+  bool fin = true;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) fin = fin && finitef(x[j]);
+  if (!fin) {
+    // health fallback: keep the forecast for this pixel
+    st |= ST_NONFINITE | ST_FALLBACK;
+    if (a.prop) {
+      forecast_partial_cov<NP>(opaque(cptr(a.prop)), p, x, P);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) x[j] = a.x_f[j * ld + p];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) P[t] = a.p_f[t * ld + p];
     }
   }
   float dn = 0.f;
@@ -1068,8 +1151,25 @@ KF_HD float pixel_gain(const GainArgs& a, int64_t p) {
     const float d = x[j] - x0[j];
     dn = fmaf(d, d, dn);
   }
+  if (a.p_out) {
 #pragma unroll
-  for (int t = 0; t < NT; ++t) a.p_out[t * ld + p] = P[t];
+    for (int t = 0; t < NT; ++t) a.p_out[t * ld + p] = P[t];
+  }
+  if (a.out_mean) {
+    // fused output: 1/sqrt(diag P^-1), the information form's uncertainty raster
+    float U[NT], Pi[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) U[t] = P[t];
+    if (!chol_packed<NP>(U)) st |= ST_NONSPD;
+    chol_inverse<NP>(U, Pi);
+    const int64_t r = a.out_idx ? a.out_idx[p] : p;
+    const int64_t pl = a.out_plane;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      a.out_mean[j * pl + r] = x[j];
+      a.out_unc[j * pl + r] = kf_rsqrt(Pi[tri(NP, j, j)]);
+    }
+  }
   if (a.status) a.status[p] = st;
   return dn;
 }

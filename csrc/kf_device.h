@@ -86,13 +86,36 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
 #endif
 }
 
-template <int NP>
+template <int NP, int FD = 0, int FOBS = 0>
 __global__ __launch_bounds__(BLOCK) void gain_kernel(GainArgs a) {
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
-    acc += (double)pixel_gain<NP>(a, p);
+    acc += (double)pixel_gain<NP, FD, FOBS>(a, p);
   if (a.partials) block_partial(acc, a.partials);
+}
+
+// K1g launch: the all-GP fast instantiations (as l_analysis) or the generic kernel.
+template <int NP>
+static void l_gain(const GainArgs& a, int grid, hipStream_t s) {
+#define KF_GAIN_FAST(D_)                                                                                 \
+  if (a.fast_d == D_) {                                                                                 \
+    if (a.fast_obs == OBS_DN16) {                                                                       \
+      hipLaunchKernelGGL((gain_kernel<NP, D_, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);            \
+      return;                                                                                           \
+    }                                                                                                   \
+    if (a.fast_obs == OBS_F32) {                                                                        \
+      hipLaunchKernelGGL((gain_kernel<NP, D_, OBS_F32>), dim3(grid), dim3(BLOCK), 0, s, a);             \
+      return;                                                                                           \
+    }                                                                                                   \
+  }
+  if constexpr (NP == 7) {
+    KF_GAIN_FAST(4)
+  } else if constexpr (NP == 10) {
+    KF_GAIN_FAST(10)
+  }
+#undef KF_GAIN_FAST
+  hipLaunchKernelGGL(gain_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
 }
 
 template <int NP>

@@ -44,10 +44,6 @@ __global__ __launch_bounds__(BLOCK) void lut_nearest_kernel(const float* lut, in
 }
 
 template <int NP>
-static void l_gain(const GainArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(gain_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
-}
-template <int NP>
 static void l_jacobi(const JacobiArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL(jacobi_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
 }

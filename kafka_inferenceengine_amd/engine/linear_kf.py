@@ -331,6 +331,8 @@ class LinearKalman:
                          reset_cinv=pack_matrix(np.asarray(prior_dev.cinv)))
                 if lazy and self._analysis_kind() == PRECISION:
                     return self._lazy(d, analysis, None)
+                if lazy and analysis.kind == COVARIANCE:
+                    return self._lazy_cov(d, analysis)
                 out = self._run_propagate(d, analysis, None, PRECISION)
                 return self._as_kind(out, self._analysis_kind())
             elif prop is None:
@@ -344,8 +346,12 @@ class LinearKalman:
                 d["reset_mean"] = np.asarray(spec.reset_mean)
                 d["reset_cinv"] = pack_matrix(np.asarray(spec.reset_cinv))
             in_kind = COVARIANCE if spec.mode == PROP_STANDARD else PRECISION
-            src = self._as_kind(analysis, in_kind)
             out_kind = COVARIANCE if spec.output == "covariance" else PRECISION
+            if (lazy and self.prior is None and in_kind == PRECISION and out_kind == PRECISION
+                    and analysis.kind == COVARIANCE and self._analysis_kind() == COVARIANCE):
+                # gain form: the K1g kernel evaluates this forecast from the analysis covariance
+                return self._lazy_cov(d, analysis)
+            src = self._as_kind(analysis, in_kind)
             blend_pix = (None, None)
             if self.prior is not None:
                 if out_kind == COVARIANCE:
@@ -372,6 +378,21 @@ class LinearKalman:
         if not K.prop_is_light(d["mode"], d.get("blend", False)):
             return materialize()
         return LazyForecast(src, d, blend_pix, self._q_pix, materialize)
+
+    def _lazy_cov(self, d, src: KFState):
+        """Gain-form twin of :meth:`_lazy`: a light propagation of an analysis
+        held as a covariance, evaluated per pixel by the K1g kernel
+        (kf_core.h:forecast_partial_cov) instead of invert + propagate + invert
+        passes; other consumers materialise it through those passes."""
+        timer = self.timer
+
+        def materialize():
+            with timer.phase("propagate"):
+                out = self._run_propagate(d, self._as_kind(src, PRECISION), None, PRECISION)
+            return self._as_kind(out, COVARIANCE)
+        if not K.prop_is_light(d["mode"], d.get("blend", False)):
+            return materialize()
+        return LazyForecast(src, d, None, self._q_pix, materialize, kind=COVARIANCE)
 
     def _analysis_kind(self):
         return COVARIANCE if self.config.analysis_form == "gain" else PRECISION
@@ -477,7 +498,7 @@ class LinearKalman:
         table = None
         specs = [sp for sp, _ in bands]
         cfg = self.config
-        if not (cfg.return_innovations or cfg.analysis_form == "gain" or cfg.spatial_gamma > 0 or
+        if not (cfg.return_innovations or cfg.spatial_gamma > 0 or
                 self.band_comm is not None or any(sp.kind == OP_PRECOMP for sp in specs)) and \
                 self._split_plan_kind(specs) is None:
             table = build_table(specs, [d for _, d in bands], self.n_params, self._cache, self.device, None)
@@ -687,7 +708,8 @@ class LinearKalman:
         elif table is None or h0_outs is not None:
             table = build_table(specs, dbs, n, self._cache, self.device, h0_outs)
         prop = None
-        if isinstance(forecast, LazyForecast) and not (gain or precomp or split or bp) and N:
+        if (isinstance(forecast, LazyForecast) and forecast.kind == (COVARIANCE if gain else PRECISION)
+                and not (precomp or split or bp) and N):
             # fused propagation: the kernel computes the forecast per pixel from
             # the previous analysis; the first iteration linearises at it
             prop = forecast.handle()
@@ -722,7 +744,7 @@ class LinearKalman:
         # kernel itself in every iteration that can end the loop (the last one wins)
         plain = not (gain or precomp or split or bp or cfg.spatial_gamma > 0 or cfg.hessian_correction)
         out_t = None
-        if plain and N and cfg.fuse_output and hasattr(self.output, "device_targets"):
+        if (plain or (gain and not precomp)) and N and cfg.fuse_output and hasattr(self.output, "device_targets"):
             out_t = self.output.device_targets(self, self.device)
         while True:
             # the analysis precision is only needed from the iteration that can
@@ -735,8 +757,8 @@ class LinearKalman:
             with self.timer.phase("analysis"):
                 if N:
                     if gain:
-                        K.gain(n, table, x_prev, fc.x, fc.P, x_new, P_out, status, self._partials, N=N,
-                               joseph=cfg.joseph)
+                        K.gain(n, table, x_prev, None if prop else fc.x, None if prop else fc.P, x_new, A_keep,
+                               status, self._partials, N=N, joseph=cfg.joseph, prop=prop, out=out_now)
                     elif cfg.spatial_gamma > 0:
                         self._regularised_iteration(table, x_prev, fc, x_new, P_out, status, prop)
                     elif bp:

@@ -107,9 +107,10 @@ class LazyForecast:
 
     kind = PRECISION
 
-    def __init__(self, src: KFState, spec: dict, blend_pix, q_pix, materialize):
+    def __init__(self, src: KFState, spec: dict, blend_pix, q_pix, materialize, kind=PRECISION):
         self.src, self.spec, self.blend_pix, self.q_pix = src, spec, blend_pix, q_pix
         self._materialize = materialize
+        self.kind = kind     # form of the forecast it stands for (COVARIANCE: gain-form K1g consumer)
 
     @property
     def N(self) -> int:

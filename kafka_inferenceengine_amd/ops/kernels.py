@@ -264,23 +264,57 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     return partials
 
 
-def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out, status=None, partials=None, N=None,
-         joseph=False):
-    """K1g covariance/gain-form analysis (sequential scalar band updates)."""
+def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status=None, partials=None, N=None,
+         joseph=False, prop=None, out=None, fast=True):
+    """K1g covariance/gain-form analysis (sequential scalar band updates).
+
+    ``prop`` (:func:`prop_args` with ``fused=True`` over the analysis
+    COVARIANCE) fuses the forecast as for :func:`analysis` (x_f / p_f None;
+    ``x_prev=None`` linearises at it); ``out = (mean, unc, idx)`` writes the
+    output rasters (x, 1/sqrt(diag P^-1)) from the kernel; ``p_out`` may be
+    None in iterations that cannot end the Gauss-Newton loop."""
     check_np(n_params)
-    N = int(x_prev.shape[1] if N is None else N)
-    dev = x_prev.device
+    ref = next(t for t in (x_prev, x_f, x_out) if t is not None)
+    N = int(ref.shape[1] if N is None else N)
+    dev = ref.device
     nt = ntri(n_params)
+    if prop is None and (x_prev is None or x_f is None or p_f is None):
+        raise ValueError("x_prev, x_f and p_f are required unless the propagation is fused")
+    if prop is not None and (x_f is not None or p_f is not None):
+        raise ValueError("fused propagation replaces x_f/p_f")
     for t, r, nm in ((x_prev, n_params, "x_prev"), (x_f, n_params, "x_f"), (p_f, nt, "p_f"),
                      (x_out, n_params, "x_out"), (p_out, nt, "p_out")):
         _check_soa(t, r, N, nm, device=dev)
+    ld = ref.shape[1]
+    for t in (x_prev, x_f, p_f, x_out, p_out):
+        if t is not None and t.shape[1] != ld:
+            raise ValueError("all SoA operands must share the leading dimension")
+    if prop is not None and (prop.args.ld != ld or prop.args.N < N or prop.device != dev or not prop.fused):
+        raise ValueError("fused propagation arguments do not match the gain layout/device")
     _check_vec(status, N, "status", torch.uint8, dev)
     a = ext().GainArgs()
-    a.N, a.ld, a.n_bands, a.joseph = N, x_prev.shape[1], bands.n, int(bool(joseph))
+    a.N, a.ld, a.n_bands, a.joseph = N, ld, bands.n, int(bool(joseph))
+    a.fast_d, a.fast_obs = (bands.fast_d, bands.fast_obs) if fast else (0, 0)
+    if a.fast_d < 0:     # precomputed / linear fast paths exist for K1 only
+        a.fast_d, a.fast_obs = 0, 0
     a.bands = bands.ptr
     a.x_prev, a.x_f, a.p_f, a.x_out, a.p_out = map(_ptr, (x_prev, x_f, p_f, x_out, p_out))
     a.status, a.partials = _ptr(status), _ptr(partials)
-    ext().gain(n_params, a, grid_for(N), _dev(x_prev), _stream(x_prev))
+    if prop is not None:
+        a.prop = _ptr(prop.device_copy())
+    if out is not None:
+        mean, unc, idx = out
+        plane = mean.shape[1]
+        for t, nm in ((mean, "out mean"), (unc, "out unc")):
+            _check_soa(t, n_params, 0, nm, device=dev)
+            if t.shape[1] != plane:
+                raise ValueError("out mean / unc planes differ")
+        if idx is not None:
+            _check_vec(idx, N, "out idx", torch.int64, dev)
+        elif plane < N:
+            raise ValueError("identity output needs plane >= N")
+        a.out_mean, a.out_unc, a.out_idx, a.out_plane = _ptr(mean), _ptr(unc), _ptr(idx), plane
+    ext().gain(n_params, a, grid_for(N), _dev(ref), _stream(ref))
     return partials
 
 

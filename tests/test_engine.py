@@ -91,6 +91,26 @@ def test_engine_host_propagator_and_precomputed_operator_paths():
     assert ((st.P - ref.P).abs() / rowmax).max() < 2e-3
 
 
+def test_gain_form_fused_forecast_and_output():
+    """Gain form with the forecast evaluated inside the K1g kernel and the
+    output rasters written by it, against the materialised forecast (invert +
+    propagate + invert passes) and the unpack pass."""
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=5)
+    grid = _grid(4)
+    res = []
+    for fuse in (False, True):
+        out = k.DeviceOutput(k.TIP_PARAMETERS)
+        kf = _engine(mask, obs, Q, out=out, analysis_form="gain", fuse_propagation=fuse, fuse_output=fuse)
+        st = kf.run(grid, x0, None, Pinv)
+        res.append((st.x.clone(), st.P.clone(), out.mean.clone(), out.unc.clone(),
+                    [h.get("gn_iterations") for h in kf.history]))
+    (x1, P1, m1, u1, g1), (x2, P2, m2, u2, g2) = res
+    assert g1 == g2
+    assert torch.allclose(x1, x2, atol=1e-5, rtol=1e-4)
+    assert ((P1 - P2).abs() / P1.abs().amax(dim=1, keepdim=True).clamp(min=1e-6)).max() < 1e-4
+    assert torch.allclose(m1, m2, atol=1e-5, rtol=1e-4) and torch.allclose(u1, u2, rtol=1e-4)
+
+
 def test_gain_form_equals_information_form():
     mask, obs, prior, x0, Pinv, Q = _setup(seed=3)
     grid = _grid(4)

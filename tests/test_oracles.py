@@ -276,3 +276,43 @@ def test_propagate_modes_vs_reference_api(dev):
         xr, Cr = T.blend_prior(np.tile(mu * 1.1, N), blocks_to_sparse(np.broadcast_to(Pi * 0.5, (N, n, n)).copy()),
                                (xa * m).ravel(), blocks_to_sparse(A), quirk=quirk, n_params=n)
         assert rel(xf, xr.reshape(N, n)) < 1e-4 and rel(Pf, sparse_to_blocks(Cr, n, check=False)) < 1e-5
+
+
+def test_gain_fused_forecast_and_output_vs_oracle(dev):
+    """K1g with the LAI forecast fused (from the analysis COVARIANCE, first
+    Gauss-Newton iteration: linearised at the forecast) and the output rasters
+    written by the kernel, against NumPy: forecast precision = prior with the
+    propagated diagonal 1/(1/(P_a^-1)_jj + q_j), gain_blocks, 1/sqrt(diag P^-1)."""
+    prob = C.tip_problem(N=3000, seed=27)
+    n, N = prob["n"], prob["N"]
+    rng = np.random.default_rng(27)
+    mu, _, Pi = k.tip_prior()
+    Pa = np.linalg.inv(C.spd_blocks(rng, N, n, 20.0))          # analysis covariance
+    xa = prob["x"]
+    q = np.full(n, 0.0)
+    q[6] = 0.04
+    spec = {"mode": 1, "m": np.ones(n), "q": q, "prop_mask": 1 << 6, "reset_mean": mu,
+            "reset_cinv": pack_matrix(Pi), "blend": False}
+    # NumPy forecast
+    Cf = np.broadcast_to(Pi, (N, n, n)).copy()
+    Cf[:, 6, 6] = 1.0 / (1.0 / np.linalg.inv(Pa)[:, 6, 6] + q[6])
+    Pf = np.linalg.inv(Cf)
+    xf = np.broadcast_to(mu, (N, n)).copy()
+    xf[:, 6] = xa[:, 6]
+    bands = C.oracle_bands(prob, xf)
+    xr, Pr = gain_blocks(xf, xf, Pf, bands)
+    unc_r = 1.0 / np.sqrt(np.einsum("nii->ni", np.linalg.inv(Pr)))
+    tab = C.table(prob, dev)
+    xo = torch.zeros((n, N), device=dev)
+    po = torch.zeros((ntri(n), N), device=dev)
+    mean = torch.zeros((n, N), device=dev)
+    unc = torch.zeros((n, N), device=dev)
+    h = K.prop_args(n, spec, C.soa(xa, dev), C.packed(Pa, dev), fused=True)
+    K.gain(n, tab, None, None, None, xo, po, prop=h, out=(mean, unc, None))
+    ex = x_err(xo.cpu().numpy().T, xr)
+    d = np.sqrt(np.einsum("nii->ni", Pr))
+    ep = float(np.max(np.abs(unpack_blocks(po.cpu().numpy(), n) - Pr) / (d[:, :, None] * d[:, None, :])))
+    eu = float(np.max(np.abs(unc.cpu().numpy().T - unc_r) / unc_r))
+    print(f"gain fused on {dev}: x {ex:.2e} P {ep:.2e} unc {eu:.2e}")
+    assert ex < 1e-4 and ep < 2e-4 and eu < 1e-4, (ex, ep, eu)
+    assert torch.equal(mean, xo)
