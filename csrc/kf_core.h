@@ -74,7 +74,7 @@ template <int NP> KF_HD constexpr int sym(int i, int j) { return i <= j ? tri(NP
 
 // ---------------------------------------------------------------------------
 // enums shared with Python (kafka_inferenceengine_amd/ops/_abi.py)
-enum ObsKind : int32_t { OBS_NONE = 0, OBS_F32 = 1, OBS_DN16 = 2, OBS_BF16 = 3 };
+enum ObsKind : int32_t { OBS_NONE = 0, OBS_F32 = 1, OBS_DN16 = 2, OBS_BF16 = 3, OBS_BF16Y = 4 };
 enum OpKind : int32_t { OP_PRECOMP = 0, OP_LINEAR = 1, OP_GP = 2, OP_SAR = 3 };
 enum PropMode : int32_t {
   PROP_PRIOR = 0,         // no_propagation: reset to prior (kf_tools.py:316-353)
@@ -354,6 +354,14 @@ KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y_out, float& w_out)
     const bool keep = (!bd.mask || bd.mask[p]) && (wv > 0.f) && finitef(wv) && finitef(yv);
     y = keep ? yv : 0.f;
     w = keep ? wv : 0.f;
+  } else if (FOBS == OBS_BF16Y || (FOBS == 0 && bd.obs == OBS_BF16Y)) {
+    // bf16 y only (half the ingest bytes of (y, w) pairs), NaN = no data; the
+    // weight follows the relative-uncertainty model of the DN16 path
+    const float yv = bf16_to_f32(reinterpret_cast<const uint16_t*>(bd.y)[p]);
+    const float sig = fmaxf(bd.rel_unc * fabsf(yv), bd.unc_floor);
+    const bool keep = (!bd.mask || bd.mask[p]) && finitef(yv) && sig > 0.f;
+    y = keep ? yv : 0.f;
+    w = keep ? kf_rcp(sig * sig) : 0.f;
   }
   y_out = y;
   w_out = w;

@@ -328,8 +328,12 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
     hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_F32>), dim3(grid), dim3(BLOCK), 0, s, a);
   } else if constexpr (FD <= 0) {
     // bf16 (y, w) observations: precomputed / linear operators only
-    if (a.fast_obs != OBS_BF16) return false;
-    hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_BF16>), dim3(grid), dim3(BLOCK), 0, s, a);
+    if (a.fast_obs == OBS_BF16)
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_BF16>), dim3(grid), dim3(BLOCK), 0, s, a);
+    else if (a.fast_obs == OBS_BF16Y)
+      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_BF16Y>), dim3(grid), dim3(BLOCK), 0, s, a);
+    else
+      return false;
   } else {
     return false;
   }

@@ -23,7 +23,7 @@ from ..ops import kernels as K
 @dataclass
 class DeviceBand:
     """One observation band on the active-pixel grid (device or CPU tensors)."""
-    kind: int                                   # K.OBS_DN16 | K.OBS_F32
+    kind: int                                   # K.OBS_DN16 | K.OBS_F32 | K.OBS_BF16 | K.OBS_BF16Y
     dn: torch.Tensor | None = None              # uint16 bit patterns, stored as int16 [N]
     y: torch.Tensor | None = None               # float32 [N]
     w: torch.Tensor | None = None               # float32 [N] inverse variance
@@ -49,6 +49,14 @@ class DeviceBand:
             valid = (dn > 0) & (sig > 0)
             w = torch.where(valid, 1.0 / torch.where(valid, sig * sig, torch.ones_like(sig)), torch.zeros_like(y))
             return torch.where(dn > 0, y, torch.zeros_like(y)), w
+        if self.kind == K.OBS_BF16Y:
+            yy = (self.y.to(torch.int32) << 16).view(torch.float32)
+            sig = torch.clamp(self.rel_unc * yy.abs(), min=self.unc_floor)
+            ok = torch.isfinite(yy) & (sig > 0)
+            if self.mask is not None:
+                ok = ok & self.mask.bool()
+            w = torch.where(ok, 1.0 / torch.where(ok, sig * sig, torch.ones_like(sig)), torch.zeros_like(yy))
+            return torch.where(ok, yy, torch.zeros_like(yy)), w
         if self.kind == K.OBS_BF16:
             yy = (self.y.to(torch.int32) << 16).view(torch.float32)
             w = (self.w.to(torch.int32) << 16).view(torch.float32)
@@ -154,8 +162,8 @@ def band_desc(spec: OperatorSpec, obs: DeviceBand | None, n_params: int, cache: 
         d.dn = obs.dn.data_ptr()
         keep.append(obs.dn)
     else:
-        d.y, d.w = obs.y.data_ptr(), obs.w.data_ptr()
-        keep += [obs.y, obs.w]
+        d.y, d.w = obs.y.data_ptr(), (obs.w.data_ptr() if obs.w is not None else 0)
+        keep += [t for t in (obs.y, obs.w) if t is not None]
         if obs.mask is not None:
             d.mask = obs.mask.data_ptr()
             keep.append(obs.mask)
@@ -167,6 +175,50 @@ def band_desc(spec: OperatorSpec, obs: DeviceBand | None, n_params: int, cache: 
         d.h0_out = h0_out.data_ptr()
         keep.append(h0_out)
     return d, keep
+
+
+def _ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+class TableCache:
+    """Band descriptor tables by content: a table holds only pointers and
+    scalars, so two dates whose bands sit in the same buffers (streamer slots,
+    resident pools) with the same operators share one device table.  The key
+    is every descriptor input (operator spec identity, observation encoding and
+    scalars, tensor addresses); cached tables do not keep observation tensors
+    alive (an address that is reused by a later band IS that band's buffer).
+    Specs are held so their ids stay unique while cached."""
+
+    def __init__(self, size: int = 16):
+        from collections import OrderedDict
+        self.size = size
+        self._d = OrderedDict()
+        self.hits = self.misses = 0
+
+    @staticmethod
+    def key(specs, obs_list, n_params, device):
+        return (n_params, str(device)) + tuple(
+            (id(sp), ob.kind, _ptr(ob.dn), _ptr(ob.y), _ptr(ob.w), _ptr(ob.mask), _ptr(ob.aux), float(ob.scale),
+             float(ob.rel_unc), float(ob.unc_floor)) for sp, ob in zip(specs, obs_list))
+
+    def get(self, specs, obs_list, n_params, cache, device) -> K.BandTable:
+        k = self.key(specs, obs_list, n_params, device)
+        hit = self._d.get(k)
+        if hit is not None:
+            self._d.move_to_end(k)
+            self.hits += 1
+            return hit[0]
+        self.misses += 1
+        tab = build_table(specs, obs_list, n_params, cache, device)
+        # keep the GP record / MFMA tables (cache-owned) and the specs, not the observations
+        obs_ids = {id(t) for ob in obs_list for t in (ob.dn, ob.y, ob.w, ob.mask, ob.aux) if t is not None}
+        tab = K.BandTable(tab.buf, tab.n, tuple(t for t in tab.keepalive if id(t) not in obs_ids), tab.fast_d,
+                          tab.fast_obs, tab.gpm_frags)
+        self._d[k] = (tab, tuple(specs))
+        while len(self._d) > self.size:
+            self._d.popitem(last=False)
+        return tab
 
 
 def build_table(specs, obs_list, n_params, cache, device, h0_outs=None, pre=None) -> K.BandTable:

@@ -16,6 +16,7 @@ the engine converts at the boundary and runs that piece on the host.
 """
 from __future__ import annotations
 
+import bisect
 import logging
 import time
 from collections import namedtuple
@@ -34,7 +35,7 @@ from ..parallel.comm import Comm
 from ..parallel.partition import StripPartition
 from ..utils.blocks import ntri, pack_matrix, soa_to_interleaved, tri_pos
 from ..utils.metrics import MetricsLogger, PhaseTimer
-from .bands import DeviceBand, RecordCache, build_table
+from .bands import DeviceBand, RecordCache, TableCache, build_table
 from .config import EngineConfig
 from .state import COVARIANCE, PRECISION, KFState, LazyForecast
 
@@ -97,6 +98,9 @@ class LinearKalman:
         self.current_timestep = None
         self.previous_state = None
         self._cache = RecordCache()
+        self._tables = TableCache()
+        self._prop_bufs = {}            # fused-propagation argument blocks on the device, by content
+        self._prop_dicts = {}           # propagation argument dicts by (propagator, prior, Q) identity
         self._partials = K.partials_buffer(max(self.N, 1), self.device)
         # one reduction slot per GN iteration: norms of iterations that cannot end
         # the loop (n_iter < min_iterations) are read after the loop, not waited on
@@ -250,6 +254,15 @@ class LinearKalman:
             self.metrics_summary()
         return analysis
 
+    def _upcoming(self, all_dates, first):
+        """Dates >= first (a slice when the list is sorted: O(log n) per step)."""
+        key = (id(all_dates), len(all_dates))
+        if getattr(self, "_dates_sorted", (None,))[0] != key:
+            self._dates_sorted = (key, all(a <= b for a, b in zip(all_dates, all_dates[1:])))
+        if self._dates_sorted[1]:
+            return all_dates[bisect.bisect_left(all_dates, first):]
+        return [d for d in all_dates if d >= first]
+
     def step(self, timestep, locate_times, state: KFState, advance: bool = True, all_dates=None,
              next_step=None) -> KFState:
         """One time-grid step: advance (unless ``advance`` is False, i.e. ``state``
@@ -267,7 +280,8 @@ class LinearKalman:
         forecast = state
         spec, self._spec = self._spec, None
         if advance:
-            LOG.info("Advancing state, %s" % timestep.strftime("%Y-%m-%d"))
+            if LOG.isEnabledFor(logging.INFO):
+                LOG.info("Advancing state, %s" % timestep.strftime("%Y-%m-%d"))
             if (spec is not None and spec.ts == timestep and len(locate_times) and spec.date == locate_times[0]
                     and spec.cand.x is state.x and spec.cand.P is state.P):
                 forecast = spec.forecast
@@ -283,7 +297,7 @@ class LinearKalman:
                 info = {"n_dates": 0}
             else:
                 all_dates = list(self.observations.dates) if all_dates is None else all_dates
-                upcoming = [d for d in all_dates if d >= locate_times[0]]
+                upcoming = self._upcoming(all_dates, locate_times[0])
                 analysis, info = self._assimilate_dates(locate_times, forecast, upcoming)
         finally:
             self._next_step = None
@@ -322,16 +336,31 @@ class LinearKalman:
             if (prop is not None and spec is None) or (self.prior is not None and prior_dev is None):
                 return self._advance_host(analysis, date)
             n = self.n_params
+            memo_key = (id(spec), id(prior_dev) if prior_dev is not None else None, id(self._m), id(self._q),
+                        bool(self.config.reference_quirks), self._analysis_kind(), analysis.kind)
+            memo = self._prop_dicts.get(memo_key)
+            if memo is not None and lazy:
+                # same propagator / prior / Q objects as an earlier step: reuse the
+                # (immutable) argument dict, so the fused argument block is reused too
+                kind, d = memo[0], memo[1]
+                if kind == "lazy":
+                    return self._lazy(d, self._as_kind(analysis, PRECISION), None)
+                if kind == "lazy_cov":
+                    return self._lazy_cov(d, analysis)
             d = {"m": self._m, "q": self._q}
+            d["_key"] = memo_key
+            keep = (spec, prior_dev, self._m, self._q)
             if prop is None and self.prior is None:
                 spec = PropagatorSpec(PROP_IDENTITY)
             elif prop is None and prior_dev.constant:
                 # prior only (kf_tools.py:165-166): reset to the prior, no blend needed
                 d.update(mode=PROP_PRIOR, prop_mask=0, reset_mean=np.asarray(prior_dev.mean),
                          reset_cinv=pack_matrix(np.asarray(prior_dev.cinv)))
-                if lazy and self._analysis_kind() == PRECISION:
+                if lazy and self._analysis_kind() == PRECISION and analysis.kind == PRECISION:
+                    self._remember_prop(memo_key, "lazy", d, keep)
                     return self._lazy(d, analysis, None)
                 if lazy and analysis.kind == COVARIANCE:
+                    self._remember_prop(memo_key, "lazy_cov", d, keep)
                     return self._lazy_cov(d, analysis)
                 out = self._run_propagate(d, analysis, None, PRECISION)
                 return self._as_kind(out, self._analysis_kind())
@@ -350,6 +379,7 @@ class LinearKalman:
             if (lazy and self.prior is None and in_kind == PRECISION and out_kind == PRECISION
                     and analysis.kind == COVARIANCE and self._analysis_kind() == COVARIANCE):
                 # gain form: the K1g kernel evaluates this forecast from the analysis covariance
+                self._remember_prop(memo_key, "lazy_cov", d, keep)
                 return self._lazy_cov(d, analysis)
             src = self._as_kind(analysis, in_kind)
             blend_pix = (None, None)
@@ -365,9 +395,16 @@ class LinearKalman:
                 self._fill_blend(d, prior_dev)
                 blend_pix = self._blend_pix(prior_dev)
             if lazy and out_kind == PRECISION and self._analysis_kind() == PRECISION:
+                if blend_pix == (None, None) and src.kind == PRECISION:
+                    self._remember_prop(memo_key, "lazy", d, keep)
                 return self._lazy(d, src, blend_pix)
             out = self._run_propagate(d, src, blend_pix, out_kind)
             return self._as_kind(out, self._analysis_kind())
+
+    def _remember_prop(self, key, kind, d, keep):
+        if len(self._prop_dicts) > 32:
+            self._prop_dicts.clear()
+        self._prop_dicts[key] = (kind, d, keep)
 
     def _lazy(self, d, src: KFState, blend_pix):
         timer = self.timer
@@ -377,7 +414,7 @@ class LinearKalman:
                 return self._run_propagate(d, src, blend_pix, PRECISION)
         if not K.prop_is_light(d["mode"], d.get("blend", False)):
             return materialize()
-        return LazyForecast(src, d, blend_pix, self._q_pix, materialize)
+        return LazyForecast(src, d, blend_pix, self._q_pix, materialize, cache=self._prop_bufs)
 
     def _lazy_cov(self, d, src: KFState):
         """Gain-form twin of :meth:`_lazy`: a light propagation of an analysis
@@ -392,7 +429,7 @@ class LinearKalman:
             return self._as_kind(out, COVARIANCE)
         if not K.prop_is_light(d["mode"], d.get("blend", False)):
             return materialize()
-        return LazyForecast(src, d, None, self._q_pix, materialize, kind=COVARIANCE)
+        return LazyForecast(src, d, None, self._q_pix, materialize, kind=COVARIANCE, cache=self._prop_bufs)
 
     def _analysis_kind(self):
         return COVARIANCE if self.config.analysis_form == "gain" else PRECISION
@@ -457,7 +494,8 @@ class LinearKalman:
     def _assimilate_dates(self, locate_times, forecast: KFState, upcoming):
         info = {"n_dates": len(locate_times), "gn_iterations": [], "norms": []}
         for i, step in enumerate(locate_times):
-            LOG.info("Assimilating %s..." % step.strftime("%Y-%m-%d"))
+            if LOG.isEnabledFor(logging.INFO):
+                LOG.info("Assimilating %s..." % step.strftime("%Y-%m-%d"))
             t0 = time.perf_counter()
             if self.config.band_sequential:
                 res = self._assimilate_sequential(step, self._materialize(forecast))
@@ -501,7 +539,7 @@ class LinearKalman:
         if not (cfg.return_innovations or cfg.spatial_gamma > 0 or
                 self.band_comm is not None or any(sp.kind == OP_PRECOMP for sp in specs)) and \
                 self._split_plan_kind(specs) is None:
-            table = build_table(specs, [d for _, d in bands], self.n_params, self._cache, self.device, None)
+            table = self._tables.get(specs, [d for _, d in bands], self.n_params, self._cache, self.device)
         self._prepared = (date, bands, table)
 
     def _speculate(self, cand: KFState, ts, date):
@@ -592,6 +630,9 @@ class LinearKalman:
             # band-parallel: this rank owns bands b = slot, slot + B, ...
             mine = range(self.band_comm.rank, nb, self.band_comm.world)
         with self.timer.phase("ingest"):
+            if hasattr(obs, "get_device_bands") and len(mine) == nb:
+                dbs = obs.get_device_bands(date)     # one acquire of the date's buffers
+                return [(self._operator_spec(db, b, date), db) for b, db in enumerate(dbs)]
             for b in mine:
                 if hasattr(obs, "get_device_band_data"):
                     db = obs.get_device_band_data(date, b)
@@ -705,8 +746,10 @@ class LinearKalman:
         split = None if (precomp or gain or bp or cfg.spatial_gamma > 0) else self._split_plan(specs, dbs, h0_outs)
         if precomp or split:
             table = None
-        elif table is None or h0_outs is not None:
+        elif h0_outs is not None:
             table = build_table(specs, dbs, n, self._cache, self.device, h0_outs)
+        elif table is None:
+            table = self._tables.get(specs, dbs, n, self._cache, self.device)
         prop = None
         if (isinstance(forecast, LazyForecast) and forecast.kind == (COVARIANCE if gain else PRECISION)
                 and not (precomp or split or bp) and N):

@@ -107,9 +107,10 @@ class LazyForecast:
 
     kind = PRECISION
 
-    def __init__(self, src: KFState, spec: dict, blend_pix, q_pix, materialize, kind=PRECISION):
+    def __init__(self, src: KFState, spec: dict, blend_pix, q_pix, materialize, kind=PRECISION, cache=None):
         self.src, self.spec, self.blend_pix, self.q_pix = src, spec, blend_pix, q_pix
         self._materialize = materialize
+        self._cache = cache  # engine dict: content key -> (PropArgs, device copy)
         self.kind = kind     # form of the forecast it stands for (COVARIANCE: gain-form K1g consumer)
 
     @property
@@ -124,11 +125,39 @@ class LazyForecast:
     def device(self):
         return self.src.device
 
+    def _key(self, bm, bc):
+        import numpy as np
+
+        def v(x):
+            return np.asarray(x).tobytes() if not isinstance(x, (int, float, bool, str)) else x
+        ptr = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
+        head = (ptr(self.src.x), ptr(self.src.P), self.N, self.src.x.shape[1], ptr(self.q_pix), ptr(bm), ptr(bc),
+                str(self.src.x.device))
+        if "_key" in self.spec:        # memoised argument dict (LinearKalman.advance_state)
+            return head + (self.spec["_key"],)
+        return head + tuple((k, v(x)) for k, x in sorted(self.spec.items()))
+
     def handle(self):
+        """Fused-propagation arguments; the packed device block is reused across
+        dates whose analysis buffers and propagation parameters coincide (the
+        block holds only addresses and parameters)."""
         from ..ops import kernels as K
         bm, bc = self.blend_pix if self.blend_pix else (None, None)
-        return K.prop_args(self.n_params, self.spec, self.src.x, self.src.P, N=self.N, q_pix=self.q_pix,
-                           blend_mean_pix=bm, blend_cinv_pix=bc, fused=True)
+        key = None
+        if self._cache is not None:
+            key = self._key(bm, bc)
+            hit = self._cache.get(key)
+            if hit is not None:
+                h = K.PropHandle(hit[0], self.src.x.device, (self.src.x, self.src.P), fused=True)
+                h._buf = hit[1]
+                return h
+        h = K.prop_args(self.n_params, self.spec, self.src.x, self.src.P, N=self.N, q_pix=self.q_pix,
+                        blend_mean_pix=bm, blend_cinv_pix=bc, fused=True)
+        if key is not None:
+            if len(self._cache) >= 16:
+                self._cache.pop(next(iter(self._cache)))
+            self._cache[key] = (h.args, h.device_copy())
+        return h
 
     def materialize(self) -> KFState:
         return self._materialize()

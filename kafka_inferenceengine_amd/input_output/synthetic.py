@@ -139,7 +139,10 @@ class SyntheticObservations:
         return self._gidx
 
     def pool_index(self, date) -> int:
-        return self.dates.index(date) % self.n_pool
+        pos = self.__dict__.get("_date_pos")
+        if pos is None or len(pos) != len(self.dates):
+            pos = self._date_pos = {d: i for i, d in enumerate(self.dates)}
+        return pos[date] % self.n_pool
 
     def truth(self, k: int) -> torch.Tensor:
         """True state [n_params, N] for pool entry k (smooth in space and time)."""
@@ -157,12 +160,15 @@ class SyntheticObservations:
     def _aux_local(self):
         if self.aux is None:
             return None
+        if getattr(self, "_aux_t", None) is not None:
+            return self._aux_t
         a = np.asarray(self.aux, dtype=np.float32)
         if a.ndim == 2:
             a = a.ravel()[self.partition.global_index()]
         else:
             a = np.broadcast_to(a, (self.N,))
-        return torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+        self._aux_t = torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+        return self._aux_t
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """Noise-free observations [n_bands, N] of state x through the band operators."""
@@ -183,7 +189,7 @@ class SyntheticObservations:
         cloud = SmoothField(self.state_mask.shape, max(2, self.field_cell // 2), self.seed * 7919 + k)
         thr = float(np.quantile(cloud.grid.numpy(), 1.0 - self.cloud_fraction)) if self.cloud_fraction > 0 else np.inf
         clear = cloud.at(g) <= thr
-        if self.encoding == "dn16":
+        if self.encoding in ("dn16", "bf16y"):
             out = torch.empty((self.n_bands, self.N), dtype=torch.int16, device=self.device)
         elif self.encoding == "bf16":
             out = torch.empty((2 * self.n_bands, self.N), dtype=torch.int16, device=self.device)
@@ -197,6 +203,10 @@ class SyntheticObservations:
                 dn = torch.clamp(torch.round(yb / self.scale), 1, 65535)
                 dn = torch.where(ok, dn, torch.zeros_like(dn)).to(torch.int32)
                 out[b] = torch.where(dn > 32767, dn - 65536, dn).to(torch.int16)  # uint16 bit pattern
+            elif self.encoding == "bf16y":
+                # y only; the kernel derives w from rel_unc / unc_floor; NaN = cloud
+                yv = torch.where(ok, yb, torch.full_like(yb, float("nan")))
+                out[b] = yv.to(torch.bfloat16).view(torch.int16)
             else:
                 sig = torch.clamp(self.rel_unc * yb.abs(), min=max(self.unc_floor, 1e-12))
                 yv = torch.where(ok, yb, torch.zeros_like(yb))
@@ -210,13 +220,13 @@ class SyntheticObservations:
         return out
 
     def _entry_shape(self):
-        return (self.n_bands, self.N) if self.encoding == "dn16" else (2 * self.n_bands, self.N)
+        return (self.n_bands, self.N) if self.encoding in ("dn16", "bf16y") else (2 * self.n_bands, self.N)
 
     def _ensure_pool(self):
         if self._streamer is not None or self._pool:
             return
         if self.stream_mode:
-            dtype = torch.int16 if self.encoding in ("dn16", "bf16") else torch.float32
+            dtype = torch.int16 if self.encoding in ("dn16", "bf16", "bf16y") else torch.float32
             self._streamer = DateStreamer(self.n_pool, self._entry_shape(), dtype, self.device)
             for k in range(self.n_pool):
                 data = self._synthesize(k)
@@ -243,21 +253,31 @@ class SyntheticObservations:
     def ingest_bytes(self) -> int:
         return 0 if self._streamer is None else self._streamer.bytes_h2d
 
+    def band_spec(self, date, band):
+        return self.band_specs[band]
+
     def get_device_band_data(self, date, band) -> DeviceBand:
-        e = self._entry(self.pool_index(date))
-        aux = self._aux_local()
+        return self._band(self._entry(self.pool_index(date)), band, self._aux_local())
+
+    def _band(self, e, band, aux) -> DeviceBand:
         meta = dict(self.metadata)
         spec = self.band_specs[band]
         if self.encoding == "dn16":
             return DeviceBand(K.OBS_DN16, dn=e[band],
                               scale=self.scale, rel_unc=self.rel_unc, unc_floor=self.unc_floor, metadata=meta,
                               emulator=spec.emulator, aux=aux)
+        if self.encoding == "bf16y":
+            return DeviceBand(K.OBS_BF16Y, y=e[band], rel_unc=self.rel_unc, unc_floor=self.unc_floor, metadata=meta,
+                              emulator=spec.emulator, aux=aux)
         kind = K.OBS_BF16 if self.encoding == "bf16" else K.OBS_F32
         return DeviceBand(kind, y=e[band], w=e[self.n_bands + band], metadata=meta, emulator=spec.emulator,
                           aux=aux)
 
     def get_device_bands(self, date):
-        return [self.get_device_band_data(date, b) for b in range(self.bands_per_observation[date])]
+        """Every band of ``date`` from one pool-entry acquire (one stream wait)."""
+        e = self._entry(self.pool_index(date))
+        aux = self._aux_local()
+        return [self._band(e, b, aux) for b in range(self.bands_per_observation[date])]
 
     def get_band_data(self, date, band):
         """Reference record on this rank's strip raster (numpy, float64)."""
@@ -389,7 +409,9 @@ class SyntheticS1Observations(SyntheticObservations):
 class SyntheticIdentityObservations(SyntheticObservations):
     """Direct (identity) observations of every state element — band k observes
     parameter k (BASELINE config 2; the reference's identity operator,
-    utils.py:119-126, fixed).  Default encoding: bf16 (y, w) pairs."""
+    utils.py:119-126, fixed).  Default encoding: bf16 y with the weight derived
+    in-kernel from the relative-uncertainty model (``bf16y``: 2 B per band and
+    pixel; ``encoding="bf16"`` streams explicit (y, w) pairs)."""
 
     sensor = "identity"
 
@@ -404,7 +426,7 @@ class SyntheticIdentityObservations(SyntheticObservations):
         sigma = np.asarray(sigma, dtype=np.float64)[:n_params]
         specs = [_linear_device_spec(n_params, None, None, b) for b in range(n_params)]
         dates = dates or _date_list(dt.datetime(2017, 1, 1), 30, 5)
-        kw.setdefault("encoding", "bf16")
+        kw.setdefault("encoding", "bf16y")
         kw.setdefault("rel_unc", 0.1)
         kw.setdefault("unc_floor", 0.01)
         super().__init__(state_mask, dates, specs, mean, 0.5 * sigma, mean - 2 * sigma, mean + 2 * sigma, **kw)

@@ -256,11 +256,21 @@ def create_linear_observation_operator(n_params, emulator, metadata, mask, state
     return _rows_to_csr(np.ascontiguousarray(rows), valid, n_params)
 
 
+_LINEAR_SPECS = {}
+
+
 def _linear_device_spec(n_params, emulator, metadata, band, band_mapper=None):
+    """Memoised (one OperatorSpec object per operator: band tables are cached by
+    spec identity, engine/bands.py:TableCache)."""
     op = emulator if isinstance(emulator, LinearOperator) else LinearOperator.select(n_params, band or 0)
     coef = np.zeros(n_params)
     coef[:len(op.coef)] = op.coef
-    return OperatorSpec(OP_LINEAR, list(range(n_params)), list(map(float, coef)), [], float(op.offset))
+    key = (n_params, tuple(map(float, coef)), float(op.offset))
+    spec = _LINEAR_SPECS.get(key)
+    if spec is None:
+        spec = _LINEAR_SPECS[key] = OperatorSpec(OP_LINEAR, list(range(n_params)), list(map(float, coef)), [],
+                                                 float(op.offset))
+    return spec
 
 
 create_linear_observation_operator.device_spec = _linear_device_spec

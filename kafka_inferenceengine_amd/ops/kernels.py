@@ -19,7 +19,7 @@ from ..models.gp import gpm_frags_per_chunk
 from ..utils.blocks import ntri
 from . import _ext
 
-OBS_NONE, OBS_F32, OBS_DN16, OBS_BF16 = 0, 1, 2, 3
+OBS_NONE, OBS_F32, OBS_DN16, OBS_BF16, OBS_BF16Y = 0, 1, 2, 3, 4
 ST_NONSPD, ST_NONFINITE, ST_BAD_OP, ST_NO_OBS, ST_FALLBACK = 1, 2, 4, 8, 16
 SUPPORTED_NP = (1, 2, 3, 4, 7, 10)
 
@@ -131,9 +131,9 @@ def make_band_table(descs: list, device, keepalive=()) -> BandTable:
         ds = {d.d for d in descs}
         if len(ds) == 1 and one_obs in (OBS_F32, OBS_DN16):
             fast_d, fast_obs = next(iter(ds)), one_obs
-    elif descs and one_obs in (OBS_F32, OBS_DN16, OBS_BF16) and all(d.op == OP_PRECOMP for d in descs):
+    elif descs and one_obs in (OBS_F32, OBS_DN16, OBS_BF16, OBS_BF16Y) and all(d.op == OP_PRECOMP for d in descs):
         fast_d, fast_obs = FD_PRECOMP, one_obs
-    elif descs and one_obs in (OBS_F32, OBS_DN16, OBS_BF16) and all(d.op == OP_LINEAR for d in descs):
+    elif descs and one_obs in (OBS_F32, OBS_DN16, OBS_BF16, OBS_BF16Y) and all(d.op == OP_LINEAR for d in descs):
         fast_d, fast_obs = FD_LINEAR, one_obs
     gpm_frags = 0
     if fast_d > 0 and all(d.gpm_nchunk > 0 for d in descs):

@@ -290,13 +290,16 @@ def test_structured_metrics_and_summary(tmp_path):
     assert len(summary["ranks"]) == 1 and summary["ranks"][0]["n_dates"] == len(dates)
 
 
-def test_identity_operator_engine_matches_oracle():
+@pytest.mark.parametrize("encoding", ["bf16y", "bf16"])
+def test_identity_operator_engine_matches_oracle(encoding):
     """BASELINE config 2 semantics: 7 direct (identity) observations of the TIP
-    state, bf16 (y, w) ingest, LAI propagator — engine (host runner) vs the
-    float64 oracle driving the reference-API linear operator factory."""
+    state, bf16 ingest (y only with the weight derived in-kernel, or (y, w)
+    pairs), LAI propagator — engine (host runner) vs the float64 oracle driving
+    the reference-API linear operator factory."""
     mask = np.ones((16, 12), bool)
     mask[:2, :3] = False
-    obs = k.SyntheticIdentityObservations(mask, device="cpu", stream=False, n_pool=4, field_cell=8)
+    obs = k.SyntheticIdentityObservations(mask, device="cpu", stream=False, n_pool=4, field_cell=8,
+                                          encoding=encoding)
     prior = k.JRCPrior(k.TIP_PARAMETERS, mask)
     x0, Pinv = prior.process_prior(None)
     Q = np.zeros_like(x0)
