@@ -55,6 +55,7 @@ class EngineConfig:
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0                 # timesteps between checkpoints (0: off)
     checkpoint_keep: int = 0                  # committed checkpoints kept (older ones pruned; 0: all)
+    gc_freeze: bool = True                    # run(): move setup objects to the permanent GC generation
     comm_timeout_s: float = 600.0
     phase_timing: bool = False                # per-phase hipEvent timers without metrics_path
     sync_timing: bool = False                 # device-synchronising per-phase timers

@@ -227,6 +227,11 @@ class LinearKalman:
 
         ckpt = CheckpointManager(self.config.checkpoint_dir, self) if self.config.checkpoint_dir else None
         self.checkpointer = ckpt
+        if self.config.gc_freeze:
+            # long-lived setup objects out of the collector's full passes (which
+            # otherwise stall sub-millisecond time steps by milliseconds)
+            import gc
+            gc.freeze()
         resume_t = None
         analysis = None
         if resume_from is not None:
@@ -401,6 +406,12 @@ class LinearKalman:
             out = self._run_propagate(d, src, blend_pix, out_kind)
             return self._as_kind(out, self._analysis_kind())
 
+    def cache_stats(self) -> dict:
+        """Host-side reuse counters (band tables, fused-argument blocks)."""
+        return {"table_hits": self._tables.hits, "table_misses": self._tables.misses,
+                "prop_hits": self._prop_bufs.get("_hits", 0), "prop_misses": self._prop_bufs.get("_misses", 0),
+                **{f"spec_{k}": v for k, v in self.spec_stats.items()}}
+
     def _remember_prop(self, key, kind, d, keep):
         if len(self._prop_dicts) > 32:
             self._prop_dicts.clear()
@@ -503,9 +514,15 @@ class LinearKalman:
                 prep = self._prepared
                 self._prepared = None
                 bands = prep[1] if (prep is not None and prep[0] == step) else self._device_bands(step)
-                nxt = [d for d in upcoming if d > step]
+                if getattr(self, "_dates_sorted", (None, False))[1]:
+                    nxt = upcoming[bisect.bisect_right(upcoming, step):]
+                else:
+                    nxt = [d for d in upcoming if d > step]
                 if nxt and self.config.prefetch and hasattr(self.observations, "prefetch"):
-                    self.observations.prefetch(nxt[0])
+                    # as many dates ahead as the source has buffers for (one copy
+                    # per step stays on the DMA engine back to back)
+                    for d_ahead in nxt[:max(1, int(getattr(self.observations, "max_prefetch", 1)))]:
+                        self.observations.prefetch(d_ahead)
                 if nxt and self.config.lookahead:
                     self._lookahead_fn = lambda d=nxt[0]: self._prepare_date(d)
                     ns = self._next_step
@@ -561,7 +578,7 @@ class LinearKalman:
         prop = fc.handle()
         x1 = torch.empty_like(cand.x)
         P1 = torch.empty_like(cand.P)
-        status = torch.zeros(max(self.N, 1), dtype=torch.uint8, device=self.device)
+        status = torch.empty(max(self.N, 1), dtype=torch.uint8, device=self.device)   # written per pixel
         red = self._red_hist[1:2]
         with self.timer.phase("analysis"):
             if self.N:
@@ -768,7 +785,8 @@ class LinearKalman:
             x_prev = fc.x.clone()
             x_new = torch.empty_like(fc.x)
             P_out = torch.empty_like(fc.P)
-        status = torch.zeros(max(N, 1), dtype=torch.uint8, device=self.device)
+        # every analysis / gain kernel writes the status of each of its N pixels
+        status = torch.empty(max(N, 1), dtype=torch.uint8, device=self.device)
         norms = []
         deferred = []
         n_iter = 1

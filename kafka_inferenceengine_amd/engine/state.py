@@ -148,14 +148,17 @@ class LazyForecast:
             key = self._key(bm, bc)
             hit = self._cache.get(key)
             if hit is not None:
+                self._cache["_hits"] = self._cache.get("_hits", 0) + 1
                 h = K.PropHandle(hit[0], self.src.x.device, (self.src.x, self.src.P), fused=True)
                 h._buf = hit[1]
                 return h
         h = K.prop_args(self.n_params, self.spec, self.src.x, self.src.P, N=self.N, q_pix=self.q_pix,
                         blend_mean_pix=bm, blend_cinv_pix=bc, fused=True)
         if key is not None:
-            if len(self._cache) >= 16:
-                self._cache.pop(next(iter(self._cache)))
+            self._cache["_misses"] = self._cache.get("_misses", 0) + 1
+            if len(self._cache) >= 256:
+                for k in [k for k in self._cache if not isinstance(k, str)][:64]:
+                    del self._cache[k]
             self._cache[key] = (h.args, h.device_copy())
         return h
 

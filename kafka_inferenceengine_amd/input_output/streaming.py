@@ -15,7 +15,11 @@ from ..ops import _ext
 
 
 class DateStreamer:
-    def __init__(self, n_pool: int, entry_shape, dtype, device, n_threads: int = 2):
+    """``n_bufs`` device buffers: 2 double-buffer (date t+1 in flight under date
+    t); 3 lets the caller prefetch two dates ahead, so a copy that takes longer
+    than one step's kernels still streams back to back."""
+
+    def __init__(self, n_pool: int, entry_shape, dtype, device, n_threads: int = 2, n_bufs: int = 2):
         self.device = torch.device(device)
         self.entry_shape = tuple(entry_shape)
         self.dtype = dtype
@@ -25,8 +29,11 @@ class DateStreamer:
         self.entry_bytes = numel * torch.empty((), dtype=dtype).element_size()
         self.ring = _ext.require_ext().HostRing(n_pool, self.entry_bytes, n_threads)
         self.n_pool = n_pool
-        self.bufs = [torch.empty(self.entry_shape, dtype=dtype, device=self.device) for _ in range(2)]
-        self.loaded = [None, None]          # pool index held by each device buffer
+        self.n_bufs = max(2, int(n_bufs))
+        self.bufs = [torch.empty(self.entry_shape, dtype=dtype, device=self.device) for _ in range(self.n_bufs)]
+        self.loaded = [None] * self.n_bufs  # pool index held by each device buffer
+        self._stamp = [0] * self.n_bufs     # last load / acquire (eviction: oldest not in use)
+        self._clock = 0
         self.cuda = self.device.type == "cuda"
         self.stream = torch.cuda.Stream(self.device) if self.cuda else None
         self.bytes_h2d = 0
@@ -47,19 +54,31 @@ class DateStreamer:
         """Background read of a raw file into slot k (native reader threads)."""
         self.ring.read_file_async(k, str(path), int(offset), self.entry_bytes, 0)
 
-    def _slot_for(self, k: int) -> int:
-        if self.loaded[0] == k:
-            return 0
-        if self.loaded[1] == k:
-            return 1
+    @property
+    def max_ahead(self) -> int:
+        """Dates that can be in flight beyond the one being consumed."""
+        return self.n_bufs - 1
+
+    def _slot_for(self, key) -> int:
+        for b, v in enumerate(self.loaded):
+            if v == key:
+                return b
         return -1
 
-    def prefetch(self, k: int) -> int:
-        b = self._slot_for(k)
+    def prefetch(self, k: int, key=None) -> int:
+        """H2D of host entry ``k`` into a free device buffer, tagged ``key``
+        (default k).  A key already resident is not copied again; callers that
+        recycle host entries for distinct dates pass the date as the key, so
+        every date is streamed."""
+        key = k if key is None else key
+        b = self._slot_for(key)
+        self._clock += 1
         if b >= 0:
             return b
-        # evict the buffer that does not hold the entry being consumed
-        b = 1 if (self._current is not None and self.loaded[0] == self._current) else 0
+        # evict the least recently loaded / acquired buffer that is not being consumed
+        cand = [i for i in range(self.n_bufs) if self.loaded[i] is None or self.loaded[i] != self._current]
+        b = min(cand, key=lambda i: (self.loaded[i] is not None, self._stamp[i]))
+        self._stamp[b] = self._clock
         dst = self.bufs[b]
         if self.cuda:
             # the buffer's previous consumer is everything queued so far on the compute stream
@@ -67,17 +86,19 @@ class DateStreamer:
             self.ring.h2d(k, dst.data_ptr(), self.entry_bytes, 0, int(self.stream.cuda_stream))
         else:
             self.ring.h2d(k, dst.data_ptr(), self.entry_bytes, 0, 0)
-        self.loaded[b] = k
+        self.loaded[b] = key
         self.bytes_h2d += self.entry_bytes
         return b
 
     _current = None
 
-    def acquire(self, k: int) -> torch.Tensor:
-        b = self.prefetch(k)
+    def acquire(self, k: int, key=None) -> torch.Tensor:
+        key = k if key is None else key
+        b = self.prefetch(k, key)
+        self._stamp[b] = self._clock
         if self.cuda:
             self.ring.stream_wait(k, int(torch.cuda.current_stream(self.device).cuda_stream))
-        self._current = k
+        self._current = key
         return self.bufs[b]
 
 

@@ -227,7 +227,8 @@ class SyntheticObservations:
             return
         if self.stream_mode:
             dtype = torch.int16 if self.encoding in ("dn16", "bf16", "bf16y") else torch.float32
-            self._streamer = DateStreamer(self.n_pool, self._entry_shape(), dtype, self.device)
+            self._streamer = DateStreamer(self.n_pool, self._entry_shape(), dtype, self.device,
+                                          n_bufs=3 if self.n_pool >= 3 else 2)
             for k in range(self.n_pool):
                 data = self._synthesize(k)
                 self._streamer.host_view(k).copy_(data.cpu())
@@ -236,10 +237,12 @@ class SyntheticObservations:
             for k in range(self.n_pool):
                 self._pool[k] = self._synthesize(k)
 
-    def _entry(self, k: int) -> torch.Tensor:
+    def _entry(self, k: int, key=None) -> torch.Tensor:
+        """Pool entry k on the device; streamed per date (``key``): a recycled
+        host entry is copied again for every date that uses it."""
         self._ensure_pool()
         if self._streamer is not None:
-            return self._streamer.acquire(k)
+            return self._streamer.acquire(k, key)
         return self._pool[k]
 
     # ------------------------------------------------------ protocol
@@ -248,7 +251,13 @@ class SyntheticObservations:
             return
         self._ensure_pool()
         if self._streamer is not None:
-            self._streamer.prefetch(self.pool_index(date))
+            self._streamer.prefetch(self.pool_index(date), date)
+
+    @property
+    def max_prefetch(self) -> int:
+        """Dates the engine may prefetch ahead of the one being assimilated."""
+        self._ensure_pool()
+        return self._streamer.max_ahead if self._streamer is not None else 1
 
     def ingest_bytes(self) -> int:
         return 0 if self._streamer is None else self._streamer.bytes_h2d
@@ -257,7 +266,7 @@ class SyntheticObservations:
         return self.band_specs[band]
 
     def get_device_band_data(self, date, band) -> DeviceBand:
-        return self._band(self._entry(self.pool_index(date)), band, self._aux_local())
+        return self._band(self._entry(self.pool_index(date), date), band, self._aux_local())
 
     def _band(self, e, band, aux) -> DeviceBand:
         meta = dict(self.metadata)
@@ -275,7 +284,7 @@ class SyntheticObservations:
 
     def get_device_bands(self, date):
         """Every band of ``date`` from one pool-entry acquire (one stream wait)."""
-        e = self._entry(self.pool_index(date))
+        e = self._entry(self.pool_index(date), date)
         aux = self._aux_local()
         return [self._band(e, b, aux) for b in range(self.bands_per_observation[date])]
 
@@ -470,6 +479,12 @@ class MultiSensorObservations:
         for s in self.sources:
             if date in s.bands_per_observation:
                 s.prefetch(date)
+
+    @property
+    def max_prefetch(self) -> int:
+        """Dates the engine may prefetch ahead of the one being assimilated."""
+        self._ensure_pool()
+        return self._streamer.max_ahead if self._streamer is not None else 1
 
     def ingest_bytes(self) -> int:
         return sum(s.ingest_bytes() for s in self.sources)

@@ -108,15 +108,55 @@ FD_LINEAR = -2    # kf_core.h: fast analysis kernel for all-linear (identity/sel
 DEFAULT_VARIANT = int(os.environ.get("KAFKA_ANALYSIS_VARIANT", "0"))
 
 
+class _PinnedRing:
+    """Pinned staging ring for small host->device copies (descriptor tables,
+    launch-argument blocks): allocated once per device, so no copy pays for a
+    pinned allocation (which can stall the host for milliseconds).  A slot is
+    reused only after the copy that last read it has run (its event)."""
+
+    SLOT = 16 << 10
+    SLOTS = 64
+
+    def __init__(self, device):
+        self.device = device
+        self.buf = torch.empty(self.SLOT * self.SLOTS, dtype=torch.uint8, pin_memory=True)
+        self.events = [None] * self.SLOTS
+        self.i = 0
+
+    def copy(self, cpu: torch.Tensor) -> torch.Tensor:
+        n = cpu.numel() * cpu.element_size()
+        j = self.i
+        self.i = (self.i + 1) % self.SLOTS
+        if self.events[j] is not None:
+            self.events[j].synchronize()         # 64 copies ago: normally long done
+        stage = self.buf[j * self.SLOT:j * self.SLOT + n]
+        stage.copy_(cpu.reshape(-1).view(torch.uint8))
+        out = torch.empty(n, dtype=torch.uint8, device=self.device)
+        out.copy_(stage, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.events[j] = ev
+        return out.view(cpu.dtype).view(cpu.shape)
+
+
+_RINGS = {}
+
+
 def small_h2d(cpu: torch.Tensor, device) -> torch.Tensor:
     """Copy a small host buffer (descriptor table, launch arguments) to the
-    device without blocking the host: staged in pinned memory (torch's caching
-    host allocator keeps the block until the copy has run) and queued on the
+    device without blocking the host: staged in a pinned ring and queued on the
     current stream.  A pageable ``.to(device)`` would wait for every kernel
     already queued, which stalls the host's preparation of the next launch."""
     device = torch.device(device)
     if device.type != "cuda":
         return cpu.clone()
+    cpu = cpu.contiguous()
+    if cpu.numel() * cpu.element_size() <= _PinnedRing.SLOT:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        ring = _RINGS.get(idx)
+        if ring is None:
+            ring = _RINGS[idx] = _PinnedRing(torch.device("cuda", idx))
+        return ring.copy(cpu)
     return cpu.pin_memory().to(device, non_blocking=True)
 
 

@@ -28,6 +28,30 @@ import torch
 import torch.distributed as dist
 
 
+class _PinnedMailbox:
+    """Pinned f64 slots for norm read-backs, allocated once: a per-iteration
+    pinned allocation can stall the host (and the stream) for milliseconds when
+    the host runs ahead of the device.  A slot is reused after its copy ran."""
+
+    SLOTS = 256
+
+    def __init__(self, width: int):
+        self.buf = torch.zeros((self.SLOTS, max(1, width)), dtype=torch.float64, pin_memory=True)
+        self.events = [None] * self.SLOTS
+        self.i = 0
+
+    def take(self, n: int):
+        j = self.i
+        self.i = (self.i + 1) % self.SLOTS
+        if self.events[j] is not None:
+            self.events[j].synchronize()
+            self.events[j] = None
+        return j, self.buf[j, :n]
+
+
+_MAILBOXES = {}
+
+
 class PendingSum:
     """Deferred C1 result (``Comm.sum_f64_async``)."""
 
@@ -35,13 +59,18 @@ class PendingSum:
         self.n = n
         self.event = None
         if vals.is_cuda:
-            # async copy into pinned memory + an event: result() waits for THIS
-            # value only, not for work queued on the stream after it (the next
-            # step's speculatively queued iteration)
-            self.vals = torch.empty(vals.shape, dtype=vals.dtype, pin_memory=True)
-            self.vals.copy_(vals, non_blocking=True)
+            # async copy into a pinned mailbox slot + an event: result() waits for
+            # THIS value only, not for work queued on the stream after it (the
+            # next step's speculatively queued iteration)
+            key = (vals.device.index, vals.numel())
+            box = _MAILBOXES.get(key)
+            if box is None:
+                box = _MAILBOXES[key] = _PinnedMailbox(vals.numel())
+            j, self.vals = box.take(vals.numel())
+            self.vals.copy_(vals.reshape(-1).to(torch.float64), non_blocking=True)
             self.event = torch.cuda.Event()
             self.event.record(torch.cuda.current_stream(vals.device))
+            box.events[j] = self.event
         else:
             self.vals = vals
 

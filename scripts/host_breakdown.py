@@ -1,0 +1,67 @@
+"""Per-step host-time breakdown of the identity7 engine loop (wall time of the
+main engine methods; --noop replaces the kernels by no-ops to isolate Python).
+
+    SIZE=1024 python scripts/host_breakdown.py [--noop]
+"""
+import os, sys, time, datetime as dt, collections, functools
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import numpy as np, torch
+from kafka_inferenceengine_amd.ops import kernels as K
+E = K.ext()
+NOOP = {"analysis", "reduce_partials", "gain", "propagate", "unpack", "gather"}
+class Fake:
+    def __getattr__(self, nm):
+        if nm in NOOP:
+            return lambda *a, **k: None
+        return getattr(E, nm)
+if "--noop" in sys.argv:      # host-only: kernels replaced by no-ops (CPU)
+    f = Fake(); K.ext = lambda: f
+import kafka_inferenceengine_amd as k
+import kafka_inferenceengine_amd.engine.linear_kf as L
+import kafka_inferenceengine_amd.engine.state as S
+acc = collections.Counter(); cnt = collections.Counter()
+def wrap(obj, name, label=None):
+    fn = getattr(obj, name); label = label or name
+    @functools.wraps(fn)
+    def w(*a, **kw):
+        t = time.perf_counter()
+        try: return fn(*a, **kw)
+        finally: acc[label] += time.perf_counter() - t; cnt[label] += 1
+    setattr(obj, name, w)
+for nm in ["advance_state", "_device_bands", "_prepare_date", "_speculate", "do_all_bands_state", "_dump", "_assimilate_dates"]:
+    wrap(L.LinearKalman, nm)
+wrap(K, "analysis", "K.analysis"); wrap(K, "reduce_partials", "K.reduce"); wrap(S.LazyForecast, "handle")
+import kafka_inferenceengine_amd.engine.linear_kf as LL
+LL.K = K
+from kafka_inferenceengine_amd.inference import iterate_time_grid
+SIZE = int(os.environ.get("SIZE", "1024" if torch.cuda.is_available() else "32"))
+DEV = "cuda" if torch.cuda.is_available() else "cpu"
+mask = np.ones((SIZE, SIZE), bool)
+dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(400)]
+obs = k.SyntheticIdentityObservations(mask, dates=dates, device=DEV, n_pool=3, stream=True, cloud_fraction=0.2)
+kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_linear_observation_operator,
+                    k.TIP_PARAMETERS, state_propagation=k.propagate_information_filter_LAI)
+wrap(kf.comm, "sum_f64_async", "comm.sum_f64_async")
+import kafka_inferenceengine_amd.parallel.comm as CM
+for cls in [c for c in vars(CM).values() if isinstance(c, type) and hasattr(c, "result")]:
+    wrap(cls, "result", f"{cls.__name__}.result (host wait)")
+kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+state = kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask))
+grid = [dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in dates]
+steps = list(iterate_time_grid(grid, dates))
+def run(lo, hi, st):
+    for i in range(lo, hi):
+        t, loc, first = steps[i]
+        nxt = steps[i + 1][:2] if i + 1 < hi else None
+        st = kf.step(t, loc, st, advance=i > 0, all_dates=dates, next_step=nxt)
+    return st
+state = run(0, 20, state); acc.clear(); cnt.clear()
+if DEV == "cuda":
+    torch.cuda.synchronize()
+t0 = time.perf_counter(); state = run(20, 380, state)
+if DEV == "cuda":
+    torch.cuda.synchronize()
+T = (time.perf_counter() - t0) / 360 * 1e6
+print(f"step {T:.0f} us")
+for k_, v in acc.most_common(): print(f"{k_:34s} {v/360*1e6:7.1f} us/step  ({cnt[k_]/360:.1f} calls)")
+print("caches", kf.cache_stats())

@@ -3,6 +3,10 @@ after edits: maps every cited line of a changed file from the committed
 version (git HEAD, or --rev) to the working tree with difflib and rewrites the
 citation.  Lines that were deleted are reported for a manual look.
 
+Idempotent: the citations are always mapped from PARITY.md as committed at
+--rev (its text must otherwise equal the working copy's, or the script stops),
+so running it twice between commits does not shift them twice.
+
     python scripts/remap_parity_lines.py [--rev HEAD] [--dry-run]
 """
 import argparse
@@ -41,7 +45,15 @@ def main():
     ap.add_argument("--dry-run", action="store_true")
     a = ap.parse_args()
     doc = ROOT / "docs" / "PARITY.md"
-    text = doc.read_text()
+    work = doc.read_text()
+    try:
+        text = subprocess.run(["git", "show", f"{a.rev}:docs/PARITY.md"], cwd=ROOT, capture_output=True, text=True,
+                              check=True).stdout
+    except subprocess.CalledProcessError:
+        text = work
+    if CITE.sub("`CITE", text) != CITE.sub("`CITE", work):
+        raise SystemExit("docs/PARITY.md has edits beyond citation numbers since " + a.rev +
+                         ": commit them first (the citations are mapped from the committed text)")
     maps, lost = {}, []
 
     def fix(mo):

@@ -376,3 +376,28 @@ def test_prior_blend_same_on_host_and_device_paths(quirks):
         st = kf.run(grid, x0, None, Pinv)
         out.append(st.x[:, :st.N].numpy().copy())
     assert np.allclose(out[0], out[1], rtol=1e-4, atol=1e-5)
+
+
+def test_streamer_copies_every_date_with_three_buffers():
+    """Host entries are recycled across dates (pool of 3), but every date is
+    streamed: device buffers are keyed by the date, so a resident copy of the
+    same host entry is never reused for another date; three buffers allow two
+    dates in flight beyond the one being consumed."""
+    from kafka_inferenceengine_amd.input_output.streaming import DateStreamer
+    s = DateStreamer(3, (2, 64), torch.int16, "cpu", n_bufs=3)
+    for kk in range(3):
+        s.host_view(kk).fill_(kk + 1)
+    assert s.max_ahead == 2
+    per = s.entry_bytes
+    for day in range(9):
+        b = s.acquire(day % 3, key=("d", day))
+        s.prefetch((day + 1) % 3, ("d", day + 1))
+        s.prefetch((day + 2) % 3, ("d", day + 2))
+        assert int(b[0, 0]) == day % 3 + 1
+    assert s.bytes_h2d == per * 11          # dates 0..10 each copied exactly once
+    # engine-level: a 3-entry pool over 6 dates streams 6 copies
+    mask = np.ones((8, 8), bool)
+    obs = k.SyntheticIdentityObservations(mask, device="cpu", stream=True, n_pool=3)
+    for d in obs.dates[:6]:
+        obs.get_device_bands(d)
+    assert obs.ingest_bytes() == 6 * obs._streamer.entry_bytes
