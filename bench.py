@@ -221,7 +221,7 @@ def main():
         nxt = steps[j][:2] if (j < a.warmup + a.steps and j != a.warmup) else None
         state = kf.step(t, loc, state, advance=not first, all_dates=dates, next_step=nxt)
         first = False
-        if dev.type == "cuda" and i < a.warmup:
+        if dev.type == "cuda" and i == a.warmup - 1:
             torch.cuda.synchronize()
         msgs.append(f"step {i}{' (warmup)' if i < a.warmup else ''} {(time.perf_counter() - t0) * 1e3:.1f} ms "
                     f"gn_iters={kf.history[-1].get('gn_iterations')}")
