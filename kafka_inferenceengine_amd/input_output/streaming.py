@@ -33,6 +33,7 @@ class DateStreamer:
         self.bufs = [torch.empty(self.entry_shape, dtype=dtype, device=self.device) for _ in range(self.n_bufs)]
         self.loaded = [None] * self.n_bufs  # pool index held by each device buffer
         self._stamp = [0] * self.n_bufs     # last load / acquire (eviction: oldest not in use)
+        self._inflight = []                 # host slots of copies issued and not yet waited for
         self._clock = 0
         self.cuda = self.device.type == "cuda"
         self.stream = torch.cuda.Stream(self.device) if self.cuda else None
@@ -61,10 +62,19 @@ class DateStreamer:
         measured), which belongs in setup, not in the first time steps."""
         if not self.cuda:
             return
-        for r in range(2 * max(4, self.n_bufs)):     # enough overlapping copies for every HW queue
+        # the steady-state pattern: compute work in flight, the copy stream waiting
+        # on the compute stream, copies back to back (prefetch)
+        scratch = torch.empty(16 << 20, dtype=torch.float32, device=self.device)
+        cur = torch.cuda.current_stream(self.device)
+        for r in range(2 * max(4, self.n_bufs)):
+            scratch.mul_(0.5)
+            self.stream.wait_stream(cur)
             b = r % self.n_bufs
             self.ring.h2d(r % self.n_pool, self.bufs[b].data_ptr(), self.entry_bytes, 0, int(self.stream.cuda_stream))
+            self.ring.stream_wait(r % self.n_pool, int(cur.cuda_stream))
         torch.cuda.synchronize(self.device)
+        del scratch
+        self._inflight = []
         self.loaded = [None] * self.n_bufs
 
     @property
@@ -94,9 +104,15 @@ class DateStreamer:
         self._stamp[b] = self._clock
         dst = self.bufs[b]
         if self.cuda:
+            # bound the host's run-ahead to n_bufs - 1 copies in flight: the host
+            # waits (microseconds, on the oldest copy) instead of letting the
+            # runtime's command backlog grow until it stalls for milliseconds
+            while len(self._inflight) >= self.n_bufs - 1:
+                self.ring.host_wait(self._inflight.pop(0))
             # the buffer's previous consumer is everything queued so far on the compute stream
             self.stream.wait_stream(torch.cuda.current_stream(self.device))
             self.ring.h2d(k, dst.data_ptr(), self.entry_bytes, 0, int(self.stream.cuda_stream))
+            self._inflight.append(k)
         else:
             self.ring.h2d(k, dst.data_ptr(), self.entry_bytes, 0, 0)
         self.loaded[b] = key
