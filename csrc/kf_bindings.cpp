@@ -102,6 +102,7 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .def_readwrite("fast_obs", &AnalysisArgs::fast_obs)
       .def_readwrite("variant", &AnalysisArgs::variant)
       .def_readwrite("gpm_frags", &AnalysisArgs::gpm_frags)
+      .def_readwrite("gpm_global", &AnalysisArgs::gpm_global)
       .PTR_FIELD(AnalysisArgs, bands, const BandDesc*)
       .PTR_FIELD(AnalysisArgs, x_prev, const float*)
       .PTR_FIELD(AnalysisArgs, x_f, const float*)
@@ -169,6 +170,10 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(JacobiArgs, u, const float*)
       .PTR_FIELD(JacobiArgs, v, float*)
       .PTR_FIELD(JacobiArgs, z_out, float*)
+      .PTR_FIELD(JacobiArgs, out_mean, float*)
+      .PTR_FIELD(JacobiArgs, out_unc, float*)
+      .PTR_FIELD(JacobiArgs, out_idx, const int64_t*)
+      .def_readwrite("out_plane", &JacobiArgs::out_plane)
       .GEO_FIELDS(JacobiArgs, geo);
 
   py::class_<PropArgs>(m, "PropArgs")

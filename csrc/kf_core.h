@@ -159,6 +159,7 @@ struct AnalysisArgs {
   int32_t fast_d, fast_obs;  // host hint: all bands GP with fast_d inputs, one encoding (0: generic)
   int32_t variant;           // kernel variant selector (tuning; 0 = default)
   int32_t gpm_frags;         // > 0: every band has an MFMA table; LDS fragments (16 B) of all bands + 1 zero
+  int32_t gpm_global;        // 1: every band has an MFMA table, read from global memory (too large for LDS)
   const BandDesc* bands;
   const float* x_prev;   // [NP][ld] linearisation point
   const float* x_f;      // [NP][ld] forecast mean
@@ -1209,6 +1210,12 @@ struct JacobiArgs {
   float* z_out;          // [k][ld_ext] regularised components (SWEEP writes the local part)
   StripGeo geo;          // dense strip: neighbours from the index (nbr unused)
   int64_t p0, pn;        // pixel range [p0, p0 + pn) of this launch (pn = 0: all N); C2 overlap
+  // FINISH only, optional: fused output dump (unpack_kernel's work) of x and
+  // 1/sqrt(diag A) with A = a_in (the analysis precision of this iteration)
+  float* out_mean;       // [NP][out_plane]
+  float* out_unc;        // [NP][out_plane]
+  const int64_t* out_idx;   // raster position of pixel p (nullptr: p)
+  int64_t out_plane;
 };
 
 template <typename JA>
@@ -1320,6 +1327,90 @@ KF_HD float pixel_reg_finish(const JacobiArgs& a, int64_t p) {
     a.x_out[j * ld + p] = x;
     const float d = x - a.x_ref[j * ld + p];
     dn = fmaf(d, d, dn);
+    if (a.out_mean) {
+      const int64_t r = a.out_idx ? a.out_idx[p] : p;
+      KF_DCHECK(r >= 0 && r < a.out_plane);
+      a.out_mean[j * a.out_plane + r] = x;
+      a.out_unc[j * a.out_plane + r] = kf_rsqrt(a.a_in[tri(NP, j, j) * ld + p]);
+    }
+  }
+  return dn;
+}
+
+// One regularised field (k = 1, the GMRF-on-LAI configuration): the sweep and
+// finish passes for U pixels per thread (i0, i0 + stride, ...), every load
+// issued before the first store.  These passes stream ~16 and ~120 B/px; one
+// pixel per thread and iteration left them latency-bound (one HBM round trip
+// per grid-stride step).  Neighbours are read branch-free (a missing one
+// reads the pixel itself and is weighted 0).
+constexpr int JACOBI_SWEEP1 = 4, JACOBI_FINISH1 = 5, JACOBI_U = 4;
+
+template <typename JA>
+KF_HD float reg_nsum1(const JA& a, int64_t p) {
+  float s = 0.f;
+#pragma unroll
+  for (int q4 = 0; q4 < 4; ++q4) {
+    const int32_t q = jacobi_neighbour(a, p, q4);
+    const float zq = a.x_ext[q >= 0 ? (int64_t)q : p];
+    s += q >= 0 ? zq : 0.f;
+  }
+  return s;
+}
+
+template <int NP, int U>
+KF_HD float reg_sweep1(const JacobiArgs& a, int64_t i0, int64_t stride, int64_t n) {
+  const int64_t ld = a.ld;
+  const int j0 = __builtin_ctz(a.reg_mask);
+  float z[U];
+  int64_t pp[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = i0 + u * stride;
+    pp[u] = a.p0 + (i < n ? i : i0);
+    const float s = reg_nsum1(a, pp[u]);
+    z[u] = fmaf(a.gamma, a.v[j0 * ld + pp[u]] * s, a.u[j0 * ld + pp[u]]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (i0 + u * stride < n) a.z_out[pp[u]] = z[u];
+  return 0.f;
+}
+
+template <int NP, int U>
+KF_HD float reg_finish1(const JacobiArgs& a, int64_t i0, int64_t stride, int64_t n) {
+  const int64_t ld = a.ld;
+  float x[U][NP];
+  int64_t pp[U];
+  float dn = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = i0 + u * stride;
+    pp[u] = a.p0 + (i < n ? i : i0);
+    const float s = reg_nsum1(a, pp[u]);
+    float du = 0.f;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      x[u][j] = fmaf(a.gamma, a.v[j * ld + pp[u]] * s, a.u[j * ld + pp[u]]);
+      const float d = x[u][j] - a.x_ref[j * ld + pp[u]];
+      du = fmaf(d, d, du);
+    }
+    dn += i < n ? du : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (i0 + u * stride >= n) continue;
+    const int64_t p = pp[u];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) a.x_out[j * ld + p] = x[u][j];
+    if (a.out_mean) {
+      const int64_t r = a.out_idx ? a.out_idx[p] : p;
+      KF_DCHECK(r >= 0 && r < a.out_plane);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        a.out_mean[j * a.out_plane + r] = x[u][j];
+        a.out_unc[j * a.out_plane + r] = kf_rsqrt(a.a_in[tri(NP, j, j) * ld + p]);
+      }
+    }
   }
   return dn;
 }

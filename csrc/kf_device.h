@@ -86,6 +86,26 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
 #endif
 }
 
+// K1 on the matrix cores with every band's table read from global memory
+// (gp_mfma_sums_g): many-band GP states (PROSAIL: ten bands, 358-716 KiB of
+// tables) whose tables exceed the LDS.  No LDS, so the waves per SIMD follow
+// the VGPR count alone.
+template <int NP, int D, int FOBS>
+__global__ __launch_bounds__(BLOCK) void analysis_mfma_g_kernel(AnalysisArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double acc = 0.0;
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t base = (int64_t)blockIdx.x * BLOCK + (threadIdx.x - lane); base < a.N; base += stride) {
+    const int64_t p = base + lane;
+    const bool act = p < a.N;
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, 2, 2, true>(a, act ? p : a.N - 1, act, nullptr);
+    acc += act ? (double)dn : 0.0;
+  }
+  if (a.partials) block_partial(acc, a.partials);
+#endif
+}
+
 template <int NP, int FD = 0, int FOBS = 0>
 __global__ __launch_bounds__(BLOCK) void gain_kernel(GainArgs a) {
   double acc = 0.0;
@@ -118,13 +138,26 @@ static void l_gain(const GainArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL(gain_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
 }
 
-template <int NP>
+// MODE < 0: runtime a.mode (prepare / classic: Cholesky-sized registers);
+// the streaming sweep and finish passes get instantiations of their own so
+// that their occupancy is not set by the prepare path's register count.
+template <int NP, int MODE = -1>
 __global__ __launch_bounds__(BLOCK) void jacobi_kernel(JacobiArgs a) {
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   const int64_t n = a.pn > 0 ? a.pn : a.N;
-  for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride)
-    acc += (double)pixel_jacobi<NP>(a, a.p0 + i);
+  if constexpr (MODE == JACOBI_SWEEP1 || MODE == JACOBI_FINISH1) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += JACOBI_U * stride) {
+      if constexpr (MODE == JACOBI_SWEEP1) reg_sweep1<NP, JACOBI_U>(a, i, stride, n);
+      else acc += (double)reg_finish1<NP, JACOBI_U>(a, i, stride, n);
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+      if constexpr (MODE == JACOBI_SWEEP) acc += (double)pixel_reg_sweep<NP>(a, a.p0 + i);
+      else if constexpr (MODE == JACOBI_FINISH) acc += (double)pixel_reg_finish<NP>(a, a.p0 + i);
+      else acc += (double)pixel_jacobi<NP>(a, a.p0 + i);
+    }
+  }
   if (a.partials) block_partial(acc, a.partials);
 }
 
@@ -311,6 +344,17 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
 #undef KF_MFMA_LAUNCH
 #undef KF_MFMA_GO
       return true;
+    }
+    if constexpr (FD == NP && NP >= 7) {
+      if (a.gpm_global && a.variant != 4) {
+        if (a.fast_obs == OBS_DN16)
+          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
+        else if (a.fast_obs == OBS_F32)
+          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_F32>), dim3(grid), dim3(BLOCK), 0, s, a);
+        else
+          return false;
+        return true;
+      }
     }
   }
   // variant (A/B tuning, scripts/bench_kernels.py): 0 unroll-4 pairs (default),

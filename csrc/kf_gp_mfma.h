@@ -221,6 +221,89 @@ __device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, cons
     }
   }
 }
+
+// The same sums with the band's table read from global memory (L2-resident:
+// used when the tables of all bands do not fit the 160 KiB of LDS, e.g. ten
+// PROSAIL bands).  The next chunk's fragments are loaded while the current one
+// runs (register double buffer), so the L2 latency sits under the exp/MFMA
+// work of the chunk.  tab + nchunk * FPC holds a zero fragment (models/gp.py).
+typedef const __attribute__((address_space(1))) kf_h8* kf_gtab;
+
+template <int D, int BPP = 2>
+__device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, const float (&xi)[D], float c,
+                                               float (&S)[D + 1]) {
+  static_assert(D >= 1 && D <= GPM_MAX_D, "GP input count for the matrix-core path");
+  static_assert(BPP == 2, "global-table path: both column blocks per pass");
+  constexpr int NK = gpm_k_steps(D), NLS = gpm_sum_lanes(D), FPC = gpm_frags_per_chunk(D);
+  const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+  const kf_gtab tab = (kf_gtab)tab_;
+  const bool ls = col <= D;
+  const kf_gtab sp = ls ? tab + 64 * NK + h * (D + 1) + col : tab + (int64_t)nchunk * FPC;
+  const int sstep = ls ? FPC : 0, soff = ls ? NLS : 0;
+  const kf_f16v zero = {};
+#pragma unroll
+  for (int f = 0; f <= D; ++f) S[f] = 0.f;
+  kf_h8 xb[2][NK];
+  kf_f16v acc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    gpm_operand<D>(xi, c, i, xb[i]);
+    acc[i] = zero;
+  }
+  kf_h8 ea[NK], sa[2][2];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) ea[kk] = tab[64 * kk + lane];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    sa[q][0] = sp[(2 * q) * soff];
+    sa[q][1] = sp[(2 * q + 1) * soff];
+  }
+  for (int ch = 0; ch < nchunk; ++ch) {
+    // prefetch chunk ch + 1 (the last chunk re-reads itself)
+    const int nx = ch + 1 < nchunk ? ch + 1 : ch;
+    const kf_gtab t = tab + (int64_t)nx * FPC;
+    const kf_gtab st = sp + (int64_t)nx * sstep;
+    kf_h8 ean[NK], san[2][2];
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) ean[kk] = t[64 * kk + lane];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      san[q][0] = st[(2 * q) * soff];
+      san[q][1] = st[(2 * q + 1) * soff];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      kf_f16v e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[0], xb[i][0], zero, 0, 0, 0);
+#pragma unroll
+      for (int kk = 1; kk < NK; ++kk) e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[kk], xb[i][kk], e, 0, 0, 0);
+      kf_h8 mh[2], ml[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        gpm_exp_split(e, 8 * q, mh[q], ml[q]);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][0], mh[q], acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][0], ml[q], acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][1], mh[q], acc[i], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) ea[kk] = ean[kk];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      sa[q][0] = san[q][0];
+      sa[q][1] = san[q][1];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int f = 0; f <= D; ++f) {
+      const float mine = acc[i][(f & 3) + 4 * (f >> 3)];
+      const float theirs = gpm_partner32(mine);
+      const float v = (((f >> 2) & 1) == h) ? mine : theirs;
+      S[f] = h == i ? v : S[f];
+    }
+  }
+}
 #endif
 
 }  // namespace kf
@@ -237,7 +320,7 @@ namespace kf {
 // pixels on some waves under full occupancy on MI355X while this order never
 // did (scripts/debug_mfma_tiles.py, r2 bisect); tests/test_gpu_mfma.py
 // ::test_gp_mfma_realistic_tile_matches_valu guards it.)
-template <int NP, int D, int FOBS, int BPP = 2, int NBM = 2>
+template <int NP, int D, int FOBS, int BPP = 2, int NBM = 2, bool GT = false>
 __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
                                                      const kf_h8* lds) {
   constexpr int NT = ntri(NP);
@@ -290,7 +373,8 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
       }
       c *= -0.5f * LOG2E;
       float S[D + 1];
-      gp_mfma_sums<D, BPP>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
+      if constexpr (GT) gp_mfma_sums_g<D, BPP>(bdp->gpm, nch, xi, c, S);
+      else gp_mfma_sums<D, BPP>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
       const KF_CONST_AS BandDesc* q = opaque(bdp);   // epilogue fields: not live across the chunk loop
       const float sc = q->gpm_scale;
       float Sd[D];

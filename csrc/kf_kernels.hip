@@ -45,7 +45,17 @@ __global__ __launch_bounds__(BLOCK) void lut_nearest_kernel(const float* lut, in
 
 template <int NP>
 static void l_jacobi(const JacobiArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(jacobi_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
+  const bool one = a.k == 1 && a.reg_mask != 0 && (a.reg_mask & (a.reg_mask - 1)) == 0;
+  if (a.mode == JACOBI_SWEEP && one)
+    hipLaunchKernelGGL((jacobi_kernel<NP, JACOBI_SWEEP1>), dim3(grid), dim3(BLOCK), 0, s, a);
+  else if (a.mode == JACOBI_FINISH && one)
+    hipLaunchKernelGGL((jacobi_kernel<NP, JACOBI_FINISH1>), dim3(grid), dim3(BLOCK), 0, s, a);
+  else if (a.mode == JACOBI_SWEEP)
+    hipLaunchKernelGGL((jacobi_kernel<NP, JACOBI_SWEEP>), dim3(grid), dim3(BLOCK), 0, s, a);
+  else if (a.mode == JACOBI_FINISH)
+    hipLaunchKernelGGL((jacobi_kernel<NP, JACOBI_FINISH>), dim3(grid), dim3(BLOCK), 0, s, a);
+  else
+    hipLaunchKernelGGL(jacobi_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
 }
 template <int NP>
 static void l_propagate(const PropArgs& a, int grid, hipStream_t s) {

@@ -96,7 +96,10 @@ class RecordCache:
                 hit = (None, spec.records)
             else:
                 tab, nch, scale = built
-                t = torch.from_numpy(np.ascontiguousarray(tab).view(np.int16)).to(device)
+                # + one zero fragment after the chunks (the global-table kernel's
+                # rows past D read it: kf_gp_mfma.h:gp_mfma_sums_g)
+                flat = np.concatenate([np.ascontiguousarray(tab).reshape(-1, 8), np.zeros((1, 8), np.float16)])
+                t = torch.from_numpy(flat.view(np.int16)).to(device)
                 hit = ((t, nch, scale), spec.records)
             self._m[key] = hit
         return hit[0]
@@ -214,7 +217,7 @@ class TableCache:
         # keep the GP record / MFMA tables (cache-owned) and the specs, not the observations
         obs_ids = {id(t) for ob in obs_list for t in (ob.dn, ob.y, ob.w, ob.mask, ob.aux) if t is not None}
         tab = K.BandTable(tab.buf, tab.n, tuple(t for t in tab.keepalive if id(t) not in obs_ids), tab.fast_d,
-                          tab.fast_obs, tab.gpm_frags)
+                          tab.fast_obs, tab.gpm_frags, tab.gpm_global)
         self._d[k] = (tab, tuple(specs))
         while len(self._d) > self.size:
             self._d.popitem(last=False)

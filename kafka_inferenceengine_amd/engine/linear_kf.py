@@ -804,8 +804,10 @@ class LinearKalman:
         # fused output: an output with device rasters is written by the analysis
         # kernel itself in every iteration that can end the loop (the last one wins)
         plain = not (gain or precomp or split or bp or cfg.spatial_gamma > 0 or cfg.hessian_correction)
+        spatial = cfg.spatial_gamma > 0 and not (gain or precomp or bp or cfg.hessian_correction)
         out_t = None
-        if (plain or (gain and not precomp)) and N and cfg.fuse_output and hasattr(self.output, "device_targets"):
+        if ((plain or spatial or (gain and not precomp)) and N and cfg.fuse_output
+                and hasattr(self.output, "device_targets")):
             out_t = self.output.device_targets(self, self.device)
         while True:
             # the analysis precision is only needed from the iteration that can
@@ -821,7 +823,7 @@ class LinearKalman:
                         K.gain(n, table, x_prev, None if prop else fc.x, None if prop else fc.P, x_new, A_keep,
                                status, self._partials, N=N, joseph=cfg.joseph, prop=prop, out=out_now)
                     elif cfg.spatial_gamma > 0:
-                        self._regularised_iteration(table, x_prev, fc, x_new, P_out, status, prop)
+                        self._regularised_iteration(table, x_prev, fc, x_new, A_keep, status, prop, out_now)
                     elif bp:
                         self._band_parallel_iteration(table, x_prev, fc, x_new, A_keep, status)
                     elif split is not None:
@@ -977,7 +979,7 @@ class LinearKalman:
                            a_in=a_in, b_in=b_in)
                 prev = (A_c, b_c)
 
-    def _regularised_iteration(self, table, x_prev, fc: KFState | None, x_out, A_out, status, prop=None):
+    def _regularised_iteration(self, table, x_prev, fc: KFState | None, x_out, A_out, status, prop=None, out=None):
         """GMRF spatial prior (K9 + C2), affine block-Jacobi form (kf_core.h):
         the analysis kernel assembles (A, b) and, instead of solving, factors
         A_reg = A + g deg E_R once and writes u = A_reg^-1 b and V = A_reg^-1 E_R;
@@ -1001,7 +1003,7 @@ class LinearKalman:
         rows = reg.reg_rows()
         fx, fP = (fc.x, fc.P) if fc is not None else (None, None)
         if not rows:   # nothing regularised: plain analysis
-            K.analysis(n, table, x_prev, fx, fP, x_out, A_out, None, status, self._partials, N=N, prop=prop)
+            K.analysis(n, table, x_prev, fx, fP, x_out, A_out, None, status, self._partials, N=N, prop=prop, out=out)
             return
         k = len(rows)
         ld = x_out.shape[1]
@@ -1037,7 +1039,8 @@ class LinearKalman:
             else:
                 K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo)
                 cur = reg.fill_halo(nxt)
-        K.reg_finish(n, u, v, cur, nbr, x_ref, x_out, gamma, reg.reg_mask, N, partials=self._partials, geo=geo)
+        K.reg_finish(n, u, v, cur, nbr, x_ref, x_out, gamma, reg.reg_mask, N, partials=self._partials, geo=geo,
+                     out=out, a_prec=A_out if out is not None else None)
 
     # ------------------------------------------------ band-parallel (TP-like)
     def _band_parallel_iteration(self, table, x_prev, fc: KFState, x_out, A_out, status):

@@ -88,6 +88,7 @@ class BandTable:
     fast_d: int = 0
     fast_obs: int = 0
     gpm_frags: int = 0      # > 0: GP on the matrix cores, LDS fragments of all bands (kf_gp_mfma.h)
+    gpm_global: bool = False  # GP on the matrix cores, tables read from global memory (too large for LDS)
 
     @property
     def ptr(self) -> int:
@@ -101,6 +102,8 @@ OP_GP = 2
 
 # LDS budget of the matrix-core GP analysis (every band's table staged per workgroup)
 GPM_MAX_LDS = 160 * 1024
+GPM_MAX_BANDS = 4          # kf_gp_mfma.h: bands of the LDS-staged matrix-core path
+GPM_GLOBAL_D = (7, 10)     # full-state GP input counts with a global-table instantiation
 
 FD_PRECOMP = -1   # kf_core.h: fast analysis kernel for all-precomputed operators
 FD_LINEAR = -2    # kf_core.h: fast analysis kernel for all-linear (identity/selection) operators
@@ -175,12 +178,14 @@ def make_band_table(descs: list, device, keepalive=()) -> BandTable:
         fast_d, fast_obs = FD_PRECOMP, one_obs
     elif descs and one_obs in (OBS_F32, OBS_DN16, OBS_BF16, OBS_BF16Y) and all(d.op == OP_LINEAR for d in descs):
         fast_d, fast_obs = FD_LINEAR, one_obs
-    gpm_frags = 0
+    gpm_frags, gpm_global = 0, False
     if fast_d > 0 and all(d.gpm_nchunk > 0 for d in descs):
         gpm_frags = sum(d.gpm_nchunk for d in descs) * gpm_frags_per_chunk(fast_d) + 1   # + zero fragment
-        if gpm_frags * 16 > GPM_MAX_LDS:
-            gpm_frags = 0
-    return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs, gpm_frags)
+        if gpm_frags * 16 > GPM_MAX_LDS or len(descs) > GPM_MAX_BANDS:
+            # too large for LDS: the global-table kernel (compiled for full-state
+            # GPs of 7 and 10 parameters, kf_device.h:analysis_mfma_g_kernel)
+            gpm_frags, gpm_global = 0, fast_d in GPM_GLOBAL_D
+    return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs, gpm_frags, gpm_global)
 
 
 # ------------------------------------------------------------------ ops
@@ -252,6 +257,7 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     a.fast_d, a.fast_obs = (bands.fast_d, bands.fast_obs) if fast else (0, 0)
     a.variant = DEFAULT_VARIANT if variant is None else int(variant)
     a.gpm_frags = bands.gpm_frags if fast else 0
+    a.gpm_global = int(bool(bands.gpm_global) and fast and bands.fast_d == n_params)
     a.bands = bands.ptr
     a.x_prev, a.x_f, a.pf_inv = _ptr(x_prev), _ptr(x_f), _ptr(pf_inv)
     a.x_out, a.a_out, a.b_out = _ptr(x_out), _ptr(a_out), _ptr(b_out)
@@ -462,9 +468,12 @@ def reg_sweep(n_params, u, v, z_ext, nbr, z_out, gamma, reg_mask, N, geo=None, r
     ext().jacobi(n_params, a, grid_for(n), _dev(u), _stream(u))
 
 
-def reg_finish(n_params, u, v, z_ext, nbr, x_ref, x_out, gamma, reg_mask, N, partials=None, geo=None):
+def reg_finish(n_params, u, v, z_ext, nbr, x_ref, x_out, gamma, reg_mask, N, partials=None, geo=None, out=None,
+               a_prec=None):
     """K9 affine form, last sweep: x = u + g V s(z_ext) for every parameter, with
-    the convergence partials of (x - x_ref)."""
+    the convergence partials of (x - x_ref).  ``out = (mean, unc, idx)`` also
+    writes x and 1/sqrt(diag a_prec) into the output rasters (the unpack pass
+    fused, as :func:`analysis` does for the unregularised path)."""
     check_np(n_params)
     dev = u.device
     k = bin(int(reg_mask)).count("1")
@@ -480,6 +489,22 @@ def reg_finish(n_params, u, v, z_ext, nbr, x_ref, x_out, gamma, reg_mask, N, par
     a = _reg_args(n_params, JACOBI_FINISH, N, ld, gamma, reg_mask, nbr, geo)
     a.ld_ext = z_ext.shape[1]
     a.u, a.v, a.x_ext, a.x_ref, a.x_out, a.partials = map(_ptr, (u, v, z_ext, x_ref, x_out, partials))
+    if out is not None:
+        mean, unc, idx = out
+        _check_soa(a_prec, ntri(n_params), N, "a_prec", device=dev)
+        if a_prec.shape[1] != ld:
+            raise ValueError("a_prec must share the leading dimension")
+        plane = mean.shape[1]
+        for t, nm in ((mean, "out mean"), (unc, "out unc")):
+            _check_soa(t, n_params, 0, nm, device=dev)
+            if t.shape[1] != plane:
+                raise ValueError("out mean / unc planes differ")
+        if idx is not None:
+            _check_vec(idx, N, "out idx", torch.int64, dev)
+        elif plane < N:
+            raise ValueError("identity output needs plane >= N")
+        a.a_in = _ptr(a_prec)
+        a.out_mean, a.out_unc, a.out_idx, a.out_plane = _ptr(mean), _ptr(unc), _ptr(idx), plane
     ext().jacobi(n_params, a, grid_for(N), _dev(u), _stream(u))
     return partials
 

@@ -257,15 +257,18 @@ def test_fused_propagation_engine_equals_materialized(with_prior):
     assert torch.allclose(a.P, b.P, rtol=1e-6, atol=1e-6)
 
 
-def test_fused_output_equals_unpack():
+@pytest.mark.parametrize("spatial", [False, True])
+def test_fused_output_equals_unpack(spatial):
     """EngineConfig.fuse_output: DeviceOutput rasters written by the final
-    analysis iteration equal the separate unpack pass."""
+    analysis iteration (spatial prior: by the regulariser's finish pass) equal
+    the separate unpack pass."""
     mask, obs, prior, x0, Pinv, Q = _setup(seed=6)
     grid = _grid(4)
+    reg = dict(spatial_gamma=50.0, spatial_params=[6], jacobi_sweeps=4) if spatial else {}
     res = []
     for fuse in (False, True):
         out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
-        kf = _engine(mask, obs, Q, out=out, fuse_output=fuse)
+        kf = _engine(mask, obs, Q, out=out, fuse_output=fuse, **reg)
         kf.run(grid, x0, None, Pinv)
         res.append(out)
     a, b = res

@@ -232,7 +232,11 @@ def test_gpu_runs_are_bit_reproducible(cuda):
 
 
 
-def test_fused_output_gpu(cuda):
+@pytest.mark.parametrize("spatial", [False, True])
+def test_fused_output_gpu(cuda, spatial):
+    """Fused output (analysis kernel, or the regulariser finish pass with a
+    spatial prior) equals the separate unpack kernel on the device."""
+    reg = dict(spatial_gamma=50.0, spatial_params=[6], jacobi_sweeps=4) if spatial else {}
     mask = np.ones((40, 36), bool)
     mask[3:9, 2:20] = False
     grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(4)]
@@ -241,7 +245,7 @@ def test_fused_output_gpu(cuda):
         obs = k.SyntheticBHRObservations(mask, n_train=80, device=cuda, stream=False, n_pool=2, field_cell=8)
         out = k.DeviceOutput(k.TIP_PARAMETERS)
         kf = k.LinearKalman(obs, out, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device=cuda,
-                            config=k.EngineConfig(fuse_output=fuse))
+                            config=k.EngineConfig(fuse_output=fuse, **reg))
         kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
         kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
         outs.append((out.mean.cpu(), out.unc.cpu()))

@@ -88,22 +88,28 @@ def dbands(prob, device, idx=None):
                        w=torch.from_numpy(prob["obs"][i][1]).to(device)) for i in idx]
 
 
-def run_fused(prob, device, specs=None, db=None):
+def run_fused(prob, device, specs=None, db=None, variant=None, expect_global=None):
     n, N = prob["n"], prob["N"]
     tab = build_table(specs or prob["specs"], db or dbands(prob, device), n, RecordCache(), device)
+    if expect_global is not None:
+        assert tab.gpm_global == expect_global and tab.gpm_frags == 0
     xo = torch.zeros((n, N), device=device)
     ao = torch.zeros((ntri(n), N), device=device)
     st = torch.zeros(N, dtype=torch.uint8, device=device)
     K.analysis(n, tab, C.soa(prob["x"], device), C.soa(prob["xf"], device), C.packed(prob["Pf"], device), xo, ao,
-               None, st, None)
+               None, st, None, variant=variant)
     return xo.cpu().numpy().T, ao.cpu().numpy(), st.cpu().numpy()
 
 
 # ------------------------------------------------------------------ tests
-def test_prosail_fused_vs_oracle(dev):
-    """analysis_kernel<10,10>: 10 PROSAIL GP bands fused in one pass."""
+@pytest.mark.parametrize("variant", [0, 4])
+def test_prosail_fused_vs_oracle(dev, variant):
+    """Ten PROSAIL GP bands (D = 10) fused in one pass: on the device variant 0
+    is the matrix-core kernel with the tables read from global memory
+    (analysis_mfma_g_kernel<10,10>: 10 bands x 8 chunks do not fit the LDS),
+    variant 4 the VALU record loop (analysis_kernel<10,10>)."""
     prob = prosail_problem()
-    x, a, st = run_fused(prob, dev)
+    x, a, st = run_fused(prob, dev, variant=variant, expect_global=True)
     xr, Ar = analysis_blocks(prob["x"], prob["xf"], prob["Pf"], oracle_bands(prob, prob["x"]))
     ex, ea = x_err(x, xr), a_err(a, Ar, 10)
     print(f"prosail fused on {dev}: x {ex:.2e} A {ea:.2e}")
