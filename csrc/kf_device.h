@@ -90,8 +90,8 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
 // (gp_mfma_sums_g): many-band GP states (PROSAIL: ten bands, 358-716 KiB of
 // tables) whose tables exceed the LDS.  No LDS, so the waves per SIMD follow
 // the VGPR count alone.
-template <int NP, int D, int FOBS>
-__global__ __launch_bounds__(BLOCK) void analysis_mfma_g_kernel(AnalysisArgs a) {
+template <int NP, int D, int FOBS, bool PF = false>
+__global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   double acc = 0.0;
   const int lane = threadIdx.x & 63;
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(BLOCK) void analysis_mfma_g_kernel(AnalysisArgs a) 
   for (int64_t base = (int64_t)blockIdx.x * BLOCK + (threadIdx.x - lane); base < a.N; base += stride) {
     const int64_t p = base + lane;
     const bool act = p < a.N;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, 2, 2, true>(a, act ? p : a.N - 1, act, nullptr);
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, 2, 2, true, PF>(a, act ? p : a.N - 1, act, nullptr);
     acc += act ? (double)dn : 0.0;
   }
   if (a.partials) block_partial(acc, a.partials);
@@ -347,7 +347,12 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
     }
     if constexpr (FD == NP && NP >= 7) {
       if (a.gpm_global && a.variant != 4) {
-        if (a.fast_obs == OBS_DN16)
+        // variant 7 (A/B): register double buffer (next chunk's fragments
+        // loaded under the current one): 191.7 vs 191.6 ms/step without, so
+        // the default leaves the latency to the other wave
+        if (a.fast_obs == OBS_DN16 && a.variant == 7)
+          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, true>), dim3(grid), dim3(BLOCK), 0, s, a);
+        else if (a.fast_obs == OBS_DN16)
           hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
         else if (a.fast_obs == OBS_F32)
           hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_F32>), dim3(grid), dim3(BLOCK), 0, s, a);

@@ -229,7 +229,7 @@ __device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, cons
 // work of the chunk.  tab + nchunk * FPC holds a zero fragment (models/gp.py).
 typedef const __attribute__((address_space(1))) kf_h8* kf_gtab;
 
-template <int D, int BPP = 2>
+template <int D, int BPP = 2, bool PF = true>
 __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, const float (&xi)[D], float c,
                                                float (&S)[D + 1]) {
   static_assert(D >= 1 && D <= GPM_MAX_D, "GP input count for the matrix-core path");
@@ -251,16 +251,19 @@ __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, con
     acc[i] = zero;
   }
   kf_h8 ea[NK], sa[2][2];
+  if constexpr (PF) {
 #pragma unroll
-  for (int kk = 0; kk < NK; ++kk) ea[kk] = tab[64 * kk + lane];
+    for (int kk = 0; kk < NK; ++kk) ea[kk] = tab[64 * kk + lane];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    sa[q][0] = sp[(2 * q) * soff];
-    sa[q][1] = sp[(2 * q + 1) * soff];
+    for (int q = 0; q < 2; ++q) {
+      sa[q][0] = sp[(2 * q) * soff];
+      sa[q][1] = sp[(2 * q + 1) * soff];
+    }
   }
   for (int ch = 0; ch < nchunk; ++ch) {
-    // prefetch chunk ch + 1 (the last chunk re-reads itself)
-    const int nx = ch + 1 < nchunk ? ch + 1 : ch;
+    // prefetch chunk ch + 1 (the last chunk re-reads itself); PF = false: load
+    // chunk ch here (no register double buffer, the waves hide the latency)
+    const int nx = PF ? (ch + 1 < nchunk ? ch + 1 : ch) : ch;
     const kf_gtab t = tab + (int64_t)nx * FPC;
     const kf_gtab st = sp + (int64_t)nx * sstep;
     kf_h8 ean[NK], san[2][2];
@@ -270,6 +273,15 @@ __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, con
     for (int q = 0; q < 2; ++q) {
       san[q][0] = st[(2 * q) * soff];
       san[q][1] = st[(2 * q + 1) * soff];
+    }
+    if constexpr (!PF) {
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) ea[kk] = ean[kk];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        sa[q][0] = san[q][0];
+        sa[q][1] = san[q][1];
+      }
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -320,7 +332,7 @@ namespace kf {
 // pixels on some waves under full occupancy on MI355X while this order never
 // did (scripts/debug_mfma_tiles.py, r2 bisect); tests/test_gpu_mfma.py
 // ::test_gp_mfma_realistic_tile_matches_valu guards it.)
-template <int NP, int D, int FOBS, int BPP = 2, int NBM = 2, bool GT = false>
+template <int NP, int D, int FOBS, int BPP = 2, int NBM = 2, bool GT = false, bool PF = true>
 __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
                                                      const kf_h8* lds) {
   constexpr int NT = ntri(NP);
@@ -373,7 +385,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
       }
       c *= -0.5f * LOG2E;
       float S[D + 1];
-      if constexpr (GT) gp_mfma_sums_g<D, BPP>(bdp->gpm, nch, xi, c, S);
+      if constexpr (GT) gp_mfma_sums_g<D, BPP, PF>(bdp->gpm, nch, xi, c, S);
       else gp_mfma_sums<D, BPP>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
       const KF_CONST_AS BandDesc* q = opaque(bdp);   // epilogue fields: not live across the chunk loop
       const float sc = q->gpm_scale;

@@ -36,6 +36,8 @@ class EngineConfig:
     # auto: split when a GP band has >= gp_split_min_d inputs or a date has >= gp_split_min_bands
     # GP bands.  Measured (profiles/r1_v8_split_vs_fused.log, compact records): PROSAIL 10 bands
     # x D=10 fused 300 ms vs split 306 ms/step; 34 bands split (one chunk) 133 vs fused 142 ms.
+    # On a GPU, full-state GP bands with matrix-core tables (D = n_params in 7, 10) stay fused
+    # under 'auto' at any band count (global-table kernel: 34 bands 631 vs 1064 ms/step split).
     gp_split_min_d: int = 99
     gp_split_min_bands: int = 13
     band_chunk: int = 0                       # bands per split chunk; 0 = as many as fit in half the free HBM

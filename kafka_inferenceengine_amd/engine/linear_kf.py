@@ -918,6 +918,12 @@ class LinearKalman:
             return None
         if cfg.gp_split == "auto" and d < cfg.gp_split_min_d and len(specs) < cfg.gp_split_min_bands:
             return None
+        if (cfg.gp_split == "auto" and on_dev and d == self.n_params and d in K.GPM_GLOBAL_D
+                and K.DEFAULT_VARIANT != 4 and all(self._cache.get_mfma(s, self.device) is not None for s in specs)):
+            # many full-state GP bands: the fused matrix-core kernel with the
+            # tables in global memory beats the split path (34 bands: 631 vs
+            # 1064 ms/step, profiles/r2_v10_prosail_mfma_g_ab.log)
+            return None
         return d
 
     def _split_plan(self, specs, dbs, h0_outs):
