@@ -321,6 +321,16 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
   // GP on the matrix cores when the host attached split-f16 tables to every band
   // (variant 4 forces the VALU record loop, for A/B)
   if constexpr (FD > 0 && FD <= GPM_MAX_D) {
+    if constexpr (NP == 7 && FD == 4) {
+      // variant 8 (A/B): the LDS-sized JRC-TIP tables read from global memory
+      // instead (no LDS: the waves per SIMD follow the VGPRs, not the table)
+      if (a.gpm_frags > 0 && a.variant == 8) {
+        if (a.fast_obs == OBS_DN16) {
+          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
+          return true;
+        }
+      }
+    }
     if (a.gpm_frags > 0 && a.variant != 4 && a.n_bands <= GPM_MAX_BANDS) {
       // variant 5 (A/B): one 32-pixel column block per pass
       const size_t lds = (size_t)a.gpm_frags * sizeof(kf_h8);
