@@ -110,7 +110,7 @@ struct BandDesc {
   int64_t pre_ld;              // leading dim of pre_h
   const void* gpm;             // GP split-f16 MFMA fragments (kf_gp_mfma.h, models/gp.py:mfma_tables)
   float gpm_scale;             // 2^sigma: undoes the f16-range shift folded into the table's L'
-  int32_t pad_;
+  int32_t map_identity;        // 1: map[d] == d for every input d (full-state GP: no gather / scatter)
 };
 
 struct PropArgs {

@@ -115,6 +115,37 @@ __device__ __forceinline__ void gpm_operand(const float (&xi)[D], float c, int b
   }
 }
 
+// Both column blocks' exponent B operands at once (BPP = 2): the lane splits
+// and packs its OWN pixel's values into both K halves (F0: slots 16kk..+7,
+// F1: 16kk+8..+15) and sends the half its partner l ^ 32 needs, so each value
+// is split once and one dword per fragment register crosses the wave halves,
+// instead of every raw input being swapped and split again per block.
+//   block 0 (pixels 0..31):  lanes h = 0 own F0, lanes h = 1 the partner's F1
+//   block 1 (pixels 32..63): lanes h = 0 the partner's F0, lanes h = 1 own F1
+template <int D>
+__device__ __forceinline__ void gpm_operands(const float (&xi)[D], float c, kf_h8 (&xb)[2][gpm_k_steps(D)]) {
+  const bool h1 = (threadIdx.x & 32) != 0;
+  _Float16 xh[D], xl[D], ch, cl;
+#pragma unroll
+  for (int d = 0; d < D; ++d) gpm_split16(fminf(fmaxf(xi[d], -6.0e4f), 6.0e4f), xh[d], xl[d]);
+  gpm_split16(fmaxf(c, -6.0e4f), ch, cl);
+#pragma unroll
+  for (int kk = 0; kk < gpm_k_steps(D); ++kk) {
+    const kf_u4 f0 = gpm_xfrag<D>(16 * kk, xh, xl, ch, cl), f1 = gpm_xfrag<D>(16 * kk + 8, xh, xl, ch, cl);
+    kf_u4 b0, b1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // h = 0 sends F1 (its partner's half), h = 1 sends F0
+      const uint32_t send = h1 ? f0[q] : f1[q];
+      const uint32_t recv = __builtin_bit_cast(uint32_t, gpm_partner32(__builtin_bit_cast(float, send)));
+      b0[q] = h1 ? recv : f0[q];
+      b1[q] = h1 ? f1[q] : recv;
+    }
+    xb[0][kk] = __builtin_bit_cast(kf_h8, b0);
+    xb[1][kk] = __builtin_bit_cast(kf_h8, b1);
+  }
+}
+
 // m = 2^e for 8 accumulator registers, split into f16 hi (round toward zero)
 // and lo = f16(m - hi).
 __device__ __forceinline__ void gpm_exp_split(const kf_f16v& e, int r0, kf_h8& mh, kf_h8& ml) {
@@ -172,11 +203,14 @@ __device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, cons
   for (int pass = 0; pass < 2 / BPP; ++pass) {
     kf_h8 xb[BPP][NK];
     kf_f16v acc[BPP];
+    if constexpr (BPP == 2) {
+      gpm_operands<D>(xi, c, xb);
+    } else {
 #pragma unroll
-    for (int i = 0; i < BPP; ++i) {
-      gpm_operand<D>(xi, c, pass * BPP + i, xb[i]);
-      acc[i] = zero;
+      for (int i = 0; i < BPP; ++i) gpm_operand<D>(xi, c, pass * BPP + i, xb[i]);
     }
+#pragma unroll
+    for (int i = 0; i < BPP; ++i) acc[i] = zero;
     // (a software-pipelined order -- next chunk's exponent MFMAs between the two
     // K halves -- removes the s_nop padding but measured 4-7 % slower: more
     // VGPRs, fewer waves; the other waves already fill the MFMA latency)
@@ -245,11 +279,9 @@ __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, con
   for (int f = 0; f <= D; ++f) S[f] = 0.f;
   kf_h8 xb[2][NK];
   kf_f16v acc[2];
+  gpm_operands<D>(xi, c, xb);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    gpm_operand<D>(xi, c, i, xb[i]);
-    acc[i] = zero;
-  }
+  for (int i = 0; i < 2; ++i) acc[i] = zero;
   kf_h8 ea[NK], sa[2][2];
   if constexpr (PF) {
 #pragma unroll
@@ -316,6 +348,7 @@ __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, con
     }
   }
 }
+
 #endif
 
 }  // namespace kf
@@ -332,6 +365,38 @@ namespace kf {
 // pixels on some waves under full occupancy on MI355X while this order never
 // did (scripts/debug_mfma_tiles.py, r2 bisect); tests/test_gpu_mfma.py
 // ::test_gp_mfma_realistic_tile_matches_valu guards it.)
+// Centred GP inputs and the exponent constant sum_d lambda_d xi_d^2 of a band.
+// A full-state GP (map[d] == d, wave-uniform flag) reads x0 directly; other
+// maps select through gather_state (NP - 1 v_cndmask per input).
+template <int NP, int D>
+__device__ __forceinline__ void gpm_inputs(const KF_CONST_AS BandDesc* bdp, const float (&x0)[NP], float (&xi)[D],
+                                           float& c) {
+  if (bdp->map_identity) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) xi[d] = x0[d < NP ? d : NP - 1] - bdp->center[d];
+  } else {
+#pragma unroll
+    for (int d = 0; d < D; ++d) xi[d] = gather_state<NP>(x0, bdp->map[d]) - bdp->center[d];
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) c = fmaf(bdp->coef[d] * xi[d], xi[d], c);
+}
+
+// gp_epilogue with the same identity-map shortcut (h[d] = g_d, no scatter).
+template <int NP, int D>
+__device__ __forceinline__ void gpm_epilogue(const KF_CONST_AS BandDesc* q, const float (&xi)[D], float S0,
+                                             const float (&S)[D], float& H0, float (&h)[NP]) {
+  if (q->map_identity) {
+    H0 = q->offset + S0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) h[j] = 0.f;
+#pragma unroll
+    for (int d = 0; d < D && d < NP; ++d) h[d] = fmaf(-q->coef[d] * xi[d], S0, LN2 * S[d]);
+  } else {
+    gp_epilogue<NP, D>(q->offset, q->coef, q->map, xi, S0, S, H0, h);
+  }
+}
+
 template <int NP, int D, int FOBS, int BPP = 2, int NBM = 2, bool GT = false, bool PF = true>
 __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
                                                      const kf_h8* lds) {
@@ -376,13 +441,10 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     for (int j = 0; j < NP; ++j) h[j] = 0.f;
     bool ok = false;
     const int nch = bdp->gpm_nchunk;
-    if (__any(use)) {
+    const bool any = __any(use);
+    if (any) {
       float xi[D], c = 0.f;
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        xi[d] = gather_state<NP>(x0, bdp->map[d]) - bdp->center[d];
-        c = fmaf(bdp->coef[d] * xi[d], xi[d], c);
-      }
+      gpm_inputs<NP, D>(bdp, x0, xi, c);
       c *= -0.5f * LOG2E;
       float S[D + 1];
       if constexpr (GT) gp_mfma_sums_g<D, BPP, PF>(bdp->gpm, nch, xi, c, S);
@@ -392,7 +454,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
       float Sd[D];
 #pragma unroll
       for (int d = 0; d < D; ++d) Sd[d] = S[1 + d] * sc;
-      gp_epilogue<NP, D>(q->offset, q->coef, q->map, xi, S[0] * sc, Sd, H0, h);
+      gpm_epilogue<NP, D>(q, xi, S[0] * sc, Sd, H0, h);
       ok = finitef(H0);
 #pragma unroll
       for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);

@@ -157,6 +157,7 @@ def band_desc(spec: OperatorSpec, obs: DeviceBand | None, n_params: int, cache: 
     if any(i < 0 or i >= n_params for i in smap):
         raise ValueError(f"state map {smap} out of range for n_params={n_params}")
     d.map = smap
+    d.map_identity = int(len(smap) >= int(d.d) > 0 and smap[:int(d.d)] == list(range(int(d.d))))
     d.coef = [float(c) for c in spec.coef]
     d.center = [float(c) for c in spec.center]
     if obs is None:

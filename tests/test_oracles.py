@@ -117,12 +117,13 @@ def test_prosail_fused_vs_oracle(dev, variant):
     assert not np.any(st & K.ST_FALLBACK)
 
 
-def test_multisensor_34_band_fused_vs_oracle(dev):
+@pytest.mark.parametrize("variant", [0, 4])
+def test_multisensor_34_band_fused_vs_oracle(dev, variant):
     """34 full-state GP bands (the S2 + OLCI-like multi-sensor date) in one
     fused pass: on the device the global-table matrix-core kernel, which the
     auto split policy now prefers to the split path for such dates."""
     prob = prosail_problem(N=2048, n_bands=34, seed=26)
-    x, a, st = run_fused(prob, dev, expect_global=True)
+    x, a, st = run_fused(prob, dev, variant=variant, expect_global=True)
     xr, Ar = analysis_blocks(prob["x"], prob["xf"], prob["Pf"], oracle_bands(prob, prob["x"]))
     ex, ea = x_err(x, xr), a_err(a, Ar, 10)
     print(f"34-band fused on {dev}: x {ex:.2e} A {ea:.2e}")
