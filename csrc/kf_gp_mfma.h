@@ -146,6 +146,23 @@ __device__ __forceinline__ void gpm_operands(const float (&xi)[D], float c, kf_h
   }
 }
 
+// The lane's own pixel (32 h + col) is column col of block h.  Field f of
+// that column sits in register (f&3) + 4(f>>3) of lane 32 ((f>>2)&1) + col,
+// the lane itself or its partner l ^ 32, so each lane sends the OTHER block's
+// value (the one its partner's pixel needs): one exchange per field.
+template <int D>
+__device__ __forceinline__ void gpm_extract2(const kf_f16v (&acc)[2], float (&S)[D + 1]) {
+  const bool h1 = (threadIdx.x & 32) != 0;
+#pragma unroll
+  for (int f = 0; f <= D; ++f) {
+    const int r = (f & 3) + 4 * (f >> 3);
+    const float own = h1 ? acc[1][r] : acc[0][r];
+    const float send = h1 ? acc[0][r] : acc[1][r];
+    const float recv = gpm_partner32(send);
+    S[f] = (((f >> 2) & 1) == (h1 ? 1 : 0)) ? own : recv;
+  }
+}
+
 // m = 2^e for 8 accumulator registers, split into f16 hi (round toward zero)
 // and lo = f16(m - hi).
 __device__ __forceinline__ void gpm_exp_split(const kf_f16v& e, int r0, kf_h8& mh, kf_h8& ml) {
@@ -242,15 +259,19 @@ __device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, cons
     }
     // field f of pixel 32 blk + col sits in register (f&3) + 4(f>>3) of lane
     // 32 ((f>>2)&1) + col: the lane itself or its partner l ^ 32
+    if constexpr (BPP == 2) {
+      gpm_extract2<D>(acc, S);
+    } else {
 #pragma unroll
-    for (int i = 0; i < BPP; ++i) {
-      const int blk = pass * BPP + i;
+      for (int i = 0; i < BPP; ++i) {
+        const int blk = pass * BPP + i;
 #pragma unroll
-      for (int f = 0; f <= D; ++f) {
-        const float mine = acc[i][(f & 3) + 4 * (f >> 3)];
-        const float theirs = gpm_partner32(mine);
-        const float v = (((f >> 2) & 1) == h) ? mine : theirs;
-        S[f] = h == blk ? v : S[f];
+        for (int f = 0; f <= D; ++f) {
+          const float mine = acc[i][(f & 3) + 4 * (f >> 3)];
+          const float theirs = gpm_partner32(mine);
+          const float v = (((f >> 2) & 1) == h) ? mine : theirs;
+          S[f] = h == blk ? v : S[f];
+        }
       }
     }
   }
@@ -337,16 +358,7 @@ __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, con
       sa[q][1] = san[q][1];
     }
   }
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-#pragma unroll
-    for (int f = 0; f <= D; ++f) {
-      const float mine = acc[i][(f & 3) + 4 * (f >> 3)];
-      const float theirs = gpm_partner32(mine);
-      const float v = (((f >> 2) & 1) == h) ? mine : theirs;
-      S[f] = h == i ? v : S[f];
-    }
-  }
+  gpm_extract2<D>(acc, S);
 }
 
 #endif
