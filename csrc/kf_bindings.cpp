@@ -136,6 +136,7 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .def_readwrite("fast_d", &GainArgs::fast_d)
       .def_readwrite("fast_obs", &GainArgs::fast_obs)
       .def_readwrite("out_plane", &GainArgs::out_plane)
+      .def_readwrite("gpm_frags", &GainArgs::gpm_frags)
       .PTR_FIELD(GainArgs, prop, const PropArgs*)
       .PTR_FIELD(GainArgs, out_mean, float*)
       .PTR_FIELD(GainArgs, out_unc, float*)

@@ -1029,6 +1029,8 @@ struct GainArgs {
   float* out_unc;
   const int64_t* out_idx;
   int64_t out_plane;
+  int32_t gpm_frags;     // > 0: GP on the matrix cores (LDS tables, as AnalysisArgs); gain_mfma_kernel
+  int32_t pad_;
 };
 
 // The partial-prior-reset forecast (forecast_partial) of an analysis held as a
@@ -1064,6 +1066,41 @@ KF_HD uint8_t forecast_partial_cov(const KF_CONST_AS PropArgs* a, int64_t p, flo
   chol_inverse<NP>(C, P);
   return st;
 }
+
+// One scalar-band Kalman update of (x, P) (covariance form, diagonal R):
+// S = h^T P h + r, K = P h / S, x += K (y - H0 - h^T (x - x0)), P -= K (P h)^T
+// (Joseph: P = (I - K h^T) P (I - K h^T)^T + K K^T r).
+template <int NP>
+KF_HD void gain_band_update(float (&P)[ntri(NP)], float (&x)[NP], const float (&x0)[NP], const float (&h)[NP],
+                            float H0, float y, float w, bool joseph) {
+  float ph[NP];
+  symv<NP>(P, h, ph);
+  const float r = kf_rcp(w);                  // observation variance
+  float s = r, innov = y - H0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) { s = fmaf(h[j], ph[j], s); innov = fmaf(h[j], x0[j] - x[j], innov); }
+  const float is = kf_rcp(s);
+  float k[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) { k[j] = ph[j] * is; x[j] = fmaf(k[j], innov, x[j]); }
+  if (joseph) {
+    // P = (I - k h^T) P (I - k h^T)^T + k k^T r = P - k ph^T - ph k^T + k k^T (h^T P h + r)
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+#pragma unroll
+      for (int j = i; j < NP; ++j)
+        P[tri(NP, i, j)] = P[tri(NP, i, j)] - k[i] * ph[j] - ph[i] * k[j] + k[i] * k[j] * s;
+  } else {
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+#pragma unroll
+      for (int j = i; j < NP; ++j) P[tri(NP, i, j)] = fmaf(-k[i], ph[j], P[tri(NP, i, j)]);
+  }
+}
+
+template <int NP, typename GA>
+KF_HD float gain_finish(const GA& a, int64_t p, float (&x)[NP], float (&P)[ntri(NP)], const float (&x0)[NP],
+                        uint8_t st, int nobs);
 
 template <int NP, int FD = 0, int FOBS = 0>
 KF_HD float pixel_gain(const GainArgs& a, int64_t p) {
@@ -1113,30 +1150,18 @@ KF_HD float pixel_gain(const GainArgs& a, int64_t p) {
     if (h0o) h0o[p] = H0;
     if (!ok) { st |= ST_BAD_OP; continue; }
     ++nobs;
-    float ph[NP];
-    symv<NP>(P, h, ph);
-    const float r = kf_rcp(w);                  // observation variance
-    float s = r, innov = y - H0;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) { s = fmaf(h[j], ph[j], s); innov = fmaf(h[j], x0[j] - x[j], innov); }
-    const float is = kf_rcp(s);
-    float k[NP];
-#pragma unroll
-    for (int j = 0; j < NP; ++j) { k[j] = ph[j] * is; x[j] = fmaf(k[j], innov, x[j]); }
-    if (a.joseph) {
-      // P = (I - k h^T) P (I - k h^T)^T + k k^T r = P - k ph^T - ph k^T + k k^T (h^T P h + r)
-#pragma unroll
-      for (int i = 0; i < NP; ++i)
-#pragma unroll
-        for (int j = i; j < NP; ++j)
-          P[tri(NP, i, j)] = P[tri(NP, i, j)] - k[i] * ph[j] - ph[i] * k[j] + k[i] * k[j] * s;
-    } else {
-#pragma unroll
-      for (int i = 0; i < NP; ++i)
-#pragma unroll
-        for (int j = i; j < NP; ++j) P[tri(NP, i, j)] = fmaf(-k[i], ph[j], P[tri(NP, i, j)]);
-    }
+    gain_band_update<NP>(P, x, x0, h, H0, y, w, a.joseph != 0);
   }
+  return gain_finish<NP>(a, p, x, P, x0, st, nobs);
+}
+
+// K1g tail (shared with the matrix-core gain kernel, kf_gp_mfma.h): health
+// fallback, state / covariance stores, fused output; returns |x - x0|^2.
+template <int NP, typename GA>
+KF_HD float gain_finish(const GA& a, int64_t p, float (&x)[NP], float (&P)[ntri(NP)], const float (&x0)[NP],
+                        uint8_t st, int nobs) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a.ld;
   if (nobs == 0) st |= ST_NO_OBS;
   bool fin = true;
 #pragma unroll

@@ -106,6 +106,46 @@ __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs 
 #endif
 }
 
+// dynamic LDS above the 64 KiB default (tables of several bands, up to the
+// 160 KiB of a gfx950 CU)
+template <typename K>
+static void gpm_lds_attr(K kernel, size_t bytes) {
+  if (bytes > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+}
+
+// K1g with the GP on the matrix cores (JRC-TIP: tables staged in LDS once per
+// workgroup, as analysis_mfma_kernel).
+template <int NP, int D, int FOBS>
+__global__ __launch_bounds__(BLOCK) void gain_mfma_kernel(GainArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  extern __shared__ kf_h8 gpm_lds[];
+  {
+    int off = 0;
+    for (int bi = 0; bi < a.n_bands; ++bi) {
+      const KF_CONST_AS BandDesc* bd = cptr(a.bands) + bi;
+      const int n = bd->gpm_nchunk * gpm_frags_per_chunk(D);
+      const kf_h8* src = (const kf_h8*)bd->gpm;
+      for (int i = threadIdx.x; i < n; i += BLOCK) gpm_lds[off + i] = src[i];
+      off += n;
+    }
+    if (threadIdx.x == 0) gpm_lds[a.gpm_frags - 1] = kf_h8{};   // shared zero fragment
+  }
+  __syncthreads();
+  double acc = 0.0;
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t base = (int64_t)blockIdx.x * BLOCK + (threadIdx.x - lane); base < a.N; base += stride) {
+    const int64_t p = base + lane;
+    const bool act = p < a.N;
+    const float dn = pixel_gain_mfma<NP, D, FOBS>(a, act ? p : a.N - 1, act, gpm_lds);
+    acc += act ? (double)dn : 0.0;
+  }
+  if (a.partials) block_partial(acc, a.partials);
+#endif
+}
+
 template <int NP, int FD = 0, int FOBS = 0>
 __global__ __launch_bounds__(BLOCK) void gain_kernel(GainArgs a) {
   double acc = 0.0;
@@ -130,6 +170,18 @@ static void l_gain(const GainArgs& a, int grid, hipStream_t s) {
     }                                                                                                   \
   }
   if constexpr (NP == 7) {
+    if (a.fast_d == 4 && a.gpm_frags > 0 && a.n_bands <= GPM_MAX_BANDS &&
+        (a.fast_obs == OBS_DN16 || a.fast_obs == OBS_F32)) {
+      const size_t lds = (size_t)a.gpm_frags * sizeof(kf_h8);
+      if (a.fast_obs == OBS_DN16) {
+        gpm_lds_attr(gain_mfma_kernel<NP, 4, OBS_DN16>, lds);
+        hipLaunchKernelGGL((gain_mfma_kernel<NP, 4, OBS_DN16>), dim3(grid), dim3(BLOCK), lds, s, a);
+      } else {
+        gpm_lds_attr(gain_mfma_kernel<NP, 4, OBS_F32>, lds);
+        hipLaunchKernelGGL((gain_mfma_kernel<NP, 4, OBS_F32>), dim3(grid), dim3(BLOCK), lds, s, a);
+      }
+      return;
+    }
     KF_GAIN_FAST(4)
   } else if constexpr (NP == 10) {
     KF_GAIN_FAST(10)
@@ -306,15 +358,6 @@ inline int grid_for(int64_t N, int max_blocks) {
     case 10: FN<10>(__VA_ARGS__); break;          \
     default: return hipErrorInvalidValue;         \
   }
-
-// dynamic LDS above the 64 KiB default (tables of several bands, up to the
-// 160 KiB of a gfx950 CU)
-template <typename K>
-static void gpm_lds_attr(K kernel, size_t bytes) {
-  if (bytes > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)bytes);
-}
 
 template <int NP, int FD>
 static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {

@@ -496,5 +496,70 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
       opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
   return analysis_epilogue<NP>(ka, p, A, b, x0, st);
 }
+
+// K1g (gain / covariance form) with the GP on the matrix cores: pixel_gain
+// (kf_core.h) with lane = pixel, the band's GP sums wave-cooperative as in
+// pixel_analysis_mfma, then the same scalar-band update and tail.
+template <int NP, int D, int FOBS>
+__device__ __forceinline__ float pixel_gain_mfma(const GainArgs& a, int64_t p, bool act, const kf_h8* lds) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a.ld;
+  float x0[NP], x[NP], P[NT];
+  uint8_t st = 0;
+  if (a.prop) {
+    st |= forecast_partial_cov<NP>(opaque(cptr(a.prop)), p, x, P);
+  } else {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) x[j] = a.x_f[j * ld + p];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) P[t] = a.p_f[t * ld + p];
+  }
+  if (a.x_prev) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
+  } else {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) x0[j] = x[j];
+  }
+  int nobs = 0;
+  int off = 0;
+  for (int bi = 0; bi < a.n_bands; ++bi) {
+    const KF_CONST_AS BandDesc* bdp = cptr(a.bands) + bi;
+    float y, w;
+    decode_obs<FOBS>(*bdp, p, y, w);
+    const bool use = act && (w > 0.f);
+    float H0 = 0.f, h[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) h[j] = 0.f;
+    bool ok = false;
+    const int nch = bdp->gpm_nchunk;
+    if (__any(use)) {
+      float xi[D], c = 0.f;
+      gpm_inputs<NP, D>(bdp, x0, xi, c);
+      c *= -0.5f * LOG2E;
+      float S[D + 1];
+      gp_mfma_sums<D, 2>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
+      const KF_CONST_AS BandDesc* q = opaque(bdp);
+      const float sc = q->gpm_scale;
+      float Sd[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) Sd[d] = S[1 + d] * sc;
+      gpm_epilogue<NP, D>(q, xi, S[0] * sc, Sd, H0, h);
+      ok = finitef(H0);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);
+    }
+    off += nch * gpm_frags_per_chunk(D);
+    float* h0o = opaque(bdp)->h0_out;
+    if (act && h0o) h0o[p] = use ? H0 : 0.f;
+    if (use && !ok) st |= ST_BAD_OP;
+    if (use && ok) {
+      ++nobs;
+      gain_band_update<NP>(P, x, x0, h, H0, y, w, a.joseph != 0);
+    }
+  }
+  if (!act) return 0.f;
+  return gain_finish<NP>(a, p, x, P, x0, st, nobs);
+}
 #endif
 }  // namespace kf

@@ -343,6 +343,8 @@ def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status
     a.fast_d, a.fast_obs = (bands.fast_d, bands.fast_obs) if fast else (0, 0)
     if a.fast_d < 0:     # precomputed / linear fast paths exist for K1 only
         a.fast_d, a.fast_obs = 0, 0
+    # GP on the matrix cores with LDS tables (kf_device.h:gain_mfma_kernel, JRC-TIP)
+    a.gpm_frags = bands.gpm_frags if (fast and DEFAULT_VARIANT != 4) else 0
     a.bands = bands.ptr
     a.x_prev, a.x_f, a.p_f, a.x_out, a.p_out = map(_ptr, (x_prev, x_f, p_f, x_out, p_out))
     a.status, a.partials = _ptr(status), _ptr(partials)
