@@ -198,6 +198,23 @@ KF_HD float gather_state(const float (&x)[NP], int idx) {
   return v;
 }
 
+// The same select with a wave-uniform index for the matrix-core kernels: the
+// empty asm between the steps keeps the chain from being recognised as a
+// dynamically indexed private array, which hipcc lowers to a 28-byte scratch
+// store + per-input scratch loads per band (the round-2 "32 B scratch").
+template <int NP>
+KF_HD float gather_state_u(const float (&x)[NP], int idx) {
+  float v = x[0];
+#pragma unroll
+  for (int j = 1; j < NP; ++j) {
+    v = (idx == j) ? x[j] : v;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(v));
+#endif
+  }
+  return v;
+}
+
 KF_HD float kexp2(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_exp2f(x);

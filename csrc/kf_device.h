@@ -57,7 +57,7 @@ __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
 // MINW = 4 waves per SIMD (<= 128 VGPRs, 2 workgroups per CU for two bands'
 // tables) lets the HBM phases (state loads, result stores) of some waves run
 // under the record loops of others; BS = 256 gives 3 waves per SIMD.
-template <int NP, int D, int FOBS, int BPP, int BS = BLOCK, int MINW = 1, int NBM = 2>
+template <int NP, int D, int FOBS, int BS = BLOCK, int MINW = 1>
 __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   extern __shared__ kf_h8 gpm_lds[];
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
   for (int64_t base = (int64_t)blockIdx.x * BS + (threadIdx.x - lane); base < a.N; base += stride) {
     const int64_t p = base + lane;
     const bool act = p < a.N;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, BPP, NBM>(a, act ? p : a.N - 1, act, gpm_lds);
+    const float dn = pixel_analysis_mfma<NP, D, FOBS>(a, act ? p : a.N - 1, act, gpm_lds);
     acc += act ? (double)dn : 0.0;
   }
   if (a.partials) block_partial<BS>(acc, a.partials);
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs 
   for (int64_t base = (int64_t)blockIdx.x * BLOCK + (threadIdx.x - lane); base < a.N; base += stride) {
     const int64_t p = base + lane;
     const bool act = p < a.N;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, 2, 2, true, PF>(a, act ? p : a.N - 1, act, nullptr);
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, true, PF>(a, act ? p : a.N - 1, act, nullptr);
     acc += act ? (double)dn : 0.0;
   }
   if (a.partials) block_partial(acc, a.partials);
@@ -375,26 +375,19 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
       }
     }
     if (a.gpm_frags > 0 && a.variant != 4 && a.n_bands <= GPM_MAX_BANDS) {
-      // variant 5 (A/B): one 32-pixel column block per pass
       const size_t lds = (size_t)a.gpm_frags * sizeof(kf_h8);
-#define KF_MFMA_GO(OBS_, BPP_, BS_, MINW_, NBM_)                                                             \
+#define KF_MFMA_GO(OBS_, BS_, MINW_)                                                                          \
   {                                                                                                          \
-    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, BPP_, BS_, MINW_, NBM_>, lds);                          \
-    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, BPP_, BS_, MINW_, NBM_>), dim3(grid), dim3(BS_), \
-                       lds, s, a);                                                                           \
+    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_>, lds);                                       \
+    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_>), dim3(grid), dim3(BS_), lds, s, a);  \
   }
-#define KF_MFMA_LAUNCH(OBS_)                                                                                 \
-  if (a.n_bands > 2) KF_MFMA_GO(OBS_, 2, BLOCK, 1, GPM_MAX_BANDS)                                          \
-  else if (a.variant == 5) KF_MFMA_GO(OBS_, 1, BLOCK, 1, 2)                                                  \
-  else KF_MFMA_GO(OBS_, 2, BLOCK, 1, 2)
       if (a.fast_obs == OBS_DN16) {
-        KF_MFMA_LAUNCH(OBS_DN16)
+        KF_MFMA_GO(OBS_DN16, BLOCK, 1)
       } else if (a.fast_obs == OBS_F32) {
-        KF_MFMA_LAUNCH(OBS_F32)
+        KF_MFMA_GO(OBS_F32, BLOCK, 1)
       } else {
         return false;
       }
-#undef KF_MFMA_LAUNCH
 #undef KF_MFMA_GO
       return true;
     }

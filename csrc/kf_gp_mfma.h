@@ -6,25 +6,37 @@
 //   m[i][p]  = 2^E[i][p]                                        (v_exp_f32)
 //   S[f][p]  = sum_i A[f][i] m[i][p],  A = [sgn_i; sgn_i B_i]   (K = T)
 // Both run on v_mfma_f32_32x32x16_f16 with split-f16 operands (v = hi + lo,
-// hi = f16(v), lo = f16(v - hi); products hi.hi + hi.lo + lo.hi accumulated in
-// f32): 22 significant bits per operand, as accurate as the f32 VALU loop it
-// replaces (scripts/sim_gp_mfma_precision.py).  The exponent comes out of the
-// accumulator in f32; only v_exp and the hi/lo split of m stay on the VALU.
+// hi = f16(v), lo = f16(v - hi)): 22 significant bits per operand, as
+// accurate as the f32 VALU loop it replaces (scripts/sim_gp_mfma_precision.py).
 //
-// Layout (lane l, h = l >> 5, col = l & 31; fragment element j = K index 8h + j
-// of a 16-wide K step; C row of accumulator register r = (r&3) + 8(r>>2) + 4h):
-//   exponent  A rows = 32 training points, B cols = 32 pixels, K slots
-//             [Bh(D) | Bl(D) | Bh(D) | L'h | L'l | 1 | 1 | 0..] x
-//             [xh(D) | xh(D) | xl(D) | 1   | 1   | ch | cl | 0..]   (ceil((3D+4)/16) K steps)
-//             -> lane l holds E of pixel col at points (r&3) + 8(r>>2) + 4h, r = 0..15
-//   sums      A rows = fields (S0, S'_1..S'_D; rows > D unused), B cols = 32 pixels,
-//             two K = 16 halves q: K slot 8h + j <-> point (j&3) + 4h + 8(j>>2) + 16q,
-//             i.e. exactly accumulator registers 8q .. 8q+7 of the exponent MFMA.
+// Exponent (A rows = 32 training points, B cols = 32 pixels), K slots
+//   [Bh(D) | Bl(D) | Bh(D) | L'h | 1 ] x [xh(D) | xh(D) | xl(D) | 1 | ch]
+// (3D + 2 slots: one K step of 16 for D <= 4, two for D <= 10).  The low
+// parts of the two constants are not K slots: L'l_i is folded into the sums
+// operand on the host (A'_i = A_i 2^L'l_i, exact) and cl_p = c_p - ch_p is
+// applied once per pixel afterwards (S *= 2^cl), so E carries only hi parts.
+//
+// Sums (A rows = fields, B cols = 32 pixels, K = 32 points in two halves q):
+// ONE A operand holds both split halves of A' -- hi in rows 0..D, lo in rows
+// LO..LO+D (LO = 8 for D <= 7, 16 for D <= 15) -- so per K half two MFMAs,
+// [A'h; A'l] x mh and [A'h; A'l] x ml, give all four hi/lo products
+// (2 + 2 NK MFMAs per 32 x 32 block instead of 3 + NK with separate hi/lo
+// operands: TIP 7 -> 5, PROSAIL 9 -> 6).  Row LO + f sits in the same lane as
+// row f, accumulator register + LO/2, so S_f = acc[r_f] + acc[r_f + LO/2]
+// needs no lane movement.  K slot 8h + j of half q <-> point (j&3) + 4h +
+// 8(j>>2) + 16q, i.e. exactly accumulator registers 8q .. 8q+7 of the
+// exponent MFMA (no shuffles between the two GEMMs).
+//
+// The hi/lo split of m is plain C++ (hipcc selects v_cvt_pkrtz_f16_f32 +
+// v_fma_mixlo/mixhi_f16 and inserts the VALU -> MFMA SrcB wait states
+// itself; the analysis TUs are built with -fno-slp-vectorize, _build.py, so
+// the f32 subtraction is not packed into v_pk_fma_f32 first).
+//
 // Host tables (models/gp.py: mfma_tables), per 32-point chunk: the exponent A
-// fragments of every lane, then for q = 0, 1 the hi and lo sums A fragments of
-// the lanes with row <= D.  A band's table is staged in LDS once per
-// workgroup.  m is kept <= 2^14 (f16 range) by a per-band power-of-two shift
-// folded into L' and undone on S (BandDesc.gpm_scale).
+// fragments of every lane (NK x 64), then for q = 0, 1 and h = 0, 1 the sums
+// A fragments of the 2(D+1) lanes whose row is used.  m is kept <= 2^14 (f16
+// range) by a per-band power-of-two shift folded into L' and undone on S
+// (BandDesc.gpm_scale).
 #pragma once
 #include <hip/hip_runtime.h>
 #include "kf_core.h"
@@ -36,12 +48,14 @@ typedef float kf_f16v __attribute__((ext_vector_type(16)));
 typedef uint32_t kf_u4 __attribute__((ext_vector_type(4)));
 typedef __fp16 kf_hp2 __attribute__((ext_vector_type(2)));
 
-// exponent K steps of 16 slots (3D + 4 used)
-KF_HD constexpr int gpm_k_steps(int D) { return (3 * D + 4 + 15) / 16; }
-// sums fragments per (q, hi/lo): lanes with row <= D in both K halves
-KF_HD constexpr int gpm_sum_lanes(int D) { return 2 * (D + 1); }
+// exponent K steps of 16 slots (3D + 2 used)
+KF_HD constexpr int gpm_k_steps(int D) { return (3 * D + 2 + 15) / 16; }
+// first row of the lo half of the sums operand
+KF_HD constexpr int gpm_lo_row(int D) { return D + 1 <= 8 ? 8 : 16; }
+// sums fragments per (q, h): the lanes whose row is used (hi and lo rows)
+KF_HD constexpr int gpm_sum_rows(int D) { return 2 * (D + 1); }
 // 16-byte fragments per 32-point chunk
-KF_HD constexpr int gpm_frags_per_chunk(int D) { return 64 * gpm_k_steps(D) + 4 * gpm_sum_lanes(D); }
+KF_HD constexpr int gpm_frags_per_chunk(int D) { return 64 * gpm_k_steps(D) + 4 * gpm_sum_rows(D); }
 constexpr int GPM_MAX_D = 10;
 // bands whose sums are held across the record loops (larger tables fall back to VALU)
 constexpr int GPM_MAX_BANDS = 4;
@@ -54,23 +68,21 @@ __device__ __forceinline__ uint32_t gpm_pack(_Float16 a, _Float16 b) {
 // K slot k of the exponent B operand
 template <int D>
 __device__ __forceinline__ _Float16 gpm_xslot(int k, const _Float16 (&xh)[D], const _Float16 (&xl)[D],
-                                              _Float16 ch, _Float16 cl) {
+                                              _Float16 ch) {
   if (k < D) return xh[k];
   if (k < 2 * D) return xh[k - D];
   if (k < 3 * D) return xl[k - 2 * D];
-  if (k < 3 * D + 2) return (_Float16)1.f;
-  if (k == 3 * D + 2) return ch;
-  if (k == 3 * D + 3) return cl;
+  if (k == 3 * D) return (_Float16)1.f;
+  if (k == 3 * D + 1) return ch;
   return (_Float16)0.f;
 }
 
 template <int D>
-__device__ __forceinline__ kf_u4 gpm_xfrag(int k0, const _Float16 (&xh)[D], const _Float16 (&xl)[D], _Float16 ch,
-                                           _Float16 cl) {
+__device__ __forceinline__ kf_u4 gpm_xfrag(int k0, const _Float16 (&xh)[D], const _Float16 (&xl)[D], _Float16 ch) {
   kf_u4 v;
 #pragma unroll
   for (int q = 0; q < 4; ++q)
-    v[q] = gpm_pack(gpm_xslot<D>(k0 + 2 * q, xh, xl, ch, cl), gpm_xslot<D>(k0 + 2 * q + 1, xh, xl, ch, cl));
+    v[q] = gpm_pack(gpm_xslot<D>(k0 + 2 * q, xh, xl, ch), gpm_xslot<D>(k0 + 2 * q + 1, xh, xl, ch));
   return v;
 }
 
@@ -89,49 +101,26 @@ __device__ __forceinline__ void gpm_split16(float v, _Float16& h, _Float16& l) {
   l = (_Float16)(v - (float)h);
 }
 
-// Exponent B operands (all K steps) of column block `blk` (pixels 32 blk ..
-// 32 blk + 31 of the wave).
-template <int D>
-__device__ __forceinline__ void gpm_operand(const float (&xi)[D], float c, int blk,
-                                            kf_h8 (&xb)[gpm_k_steps(D)]) {
-  // column col of block blk is pixel 32 blk + col: this lane's own pixel when
-  // its half h equals blk, else the pixel of lane l ^ 32
-  const bool h1 = (threadIdx.x & 32) != 0;
-  const bool own = (h1 ? 1 : 0) == blk;
-  _Float16 xh[D], xl[D], ch, cl;
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    const float pv = gpm_partner32(xi[d]);
-    const float v = own ? xi[d] : pv;
-    // clamp: f16 range (a state that far out has k = 0 anyway through c)
-    gpm_split16(fminf(fmaxf(v, -6.0e4f), 6.0e4f), xh[d], xl[d]);
-  }
-  const float pc = gpm_partner32(c);
-  gpm_split16(fmaxf(own ? c : pc, -6.0e4f), ch, cl);
-#pragma unroll
-  for (int kk = 0; kk < gpm_k_steps(D); ++kk) {
-    const kf_u4 f0 = gpm_xfrag<D>(16 * kk, xh, xl, ch, cl), f1 = gpm_xfrag<D>(16 * kk + 8, xh, xl, ch, cl);
-    xb[kk] = __builtin_bit_cast(kf_h8, h1 ? f1 : f0);
-  }
-}
-
-// Both column blocks' exponent B operands at once (BPP = 2): the lane splits
-// and packs its OWN pixel's values into both K halves (F0: slots 16kk..+7,
-// F1: 16kk+8..+15) and sends the half its partner l ^ 32 needs, so each value
-// is split once and one dword per fragment register crosses the wave halves,
-// instead of every raw input being swapped and split again per block.
+// Both 32-pixel column blocks' exponent B operands: the lane splits and packs
+// its OWN pixel's values into both K halves (F0: slots 16kk..+7, F1:
+// 16kk+8..+15) and sends the half its partner l ^ 32 needs, so each value is
+// split once and one dword per fragment register crosses the wave halves.
 //   block 0 (pixels 0..31):  lanes h = 0 own F0, lanes h = 1 the partner's F1
 //   block 1 (pixels 32..63): lanes h = 0 the partner's F0, lanes h = 1 own F1
+// cl: the lane's own c - f16(c), applied to its sums afterwards.
 template <int D>
-__device__ __forceinline__ void gpm_operands(const float (&xi)[D], float c, kf_h8 (&xb)[2][gpm_k_steps(D)]) {
+__device__ __forceinline__ void gpm_operands(const float (&xi)[D], float c, kf_h8 (&xb)[2][gpm_k_steps(D)],
+                                             float& cl) {
   const bool h1 = (threadIdx.x & 32) != 0;
-  _Float16 xh[D], xl[D], ch, cl;
+  _Float16 xh[D], xl[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) gpm_split16(fminf(fmaxf(xi[d], -6.0e4f), 6.0e4f), xh[d], xl[d]);
-  gpm_split16(fmaxf(c, -6.0e4f), ch, cl);
+  // clamp: f16 range (a state that far out has m = 0 anyway, through cl)
+  const _Float16 ch = (_Float16)fmaxf(c, -6.0e4f);
+  cl = c - (float)ch;
 #pragma unroll
   for (int kk = 0; kk < gpm_k_steps(D); ++kk) {
-    const kf_u4 f0 = gpm_xfrag<D>(16 * kk, xh, xl, ch, cl), f1 = gpm_xfrag<D>(16 * kk + 8, xh, xl, ch, cl);
+    const kf_u4 f0 = gpm_xfrag<D>(16 * kk, xh, xl, ch), f1 = gpm_xfrag<D>(16 * kk + 8, xh, xl, ch);
     kf_u4 b0, b1;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -149,216 +138,174 @@ __device__ __forceinline__ void gpm_operands(const float (&xi)[D], float c, kf_h
 // The lane's own pixel (32 h + col) is column col of block h.  Field f of
 // that column sits in register (f&3) + 4(f>>3) of lane 32 ((f>>2)&1) + col,
 // the lane itself or its partner l ^ 32, so each lane sends the OTHER block's
-// value (the one its partner's pixel needs): one exchange per field.
+// value (the one its partner's pixel needs): one exchange per field.  The lo
+// row LO + f of the same field is register + LO/2 of the same lane.
 template <int D>
 __device__ __forceinline__ void gpm_extract2(const kf_f16v (&acc)[2], float (&S)[D + 1]) {
+  constexpr int LR = gpm_lo_row(D) / 2;
   const bool h1 = (threadIdx.x & 32) != 0;
 #pragma unroll
   for (int f = 0; f <= D; ++f) {
     const int r = (f & 3) + 4 * (f >> 3);
-    const float own = h1 ? acc[1][r] : acc[0][r];
-    const float send = h1 ? acc[0][r] : acc[1][r];
+    const float a0 = acc[0][r] + acc[0][r + LR], a1 = acc[1][r] + acc[1][r + LR];
+    const float own = h1 ? a1 : a0;
+    const float send = h1 ? a0 : a1;
     const float recv = gpm_partner32(send);
     S[f] = (((f >> 2) & 1) == (h1 ? 1 : 0)) ? own : recv;
   }
 }
 
 // m = 2^e for 8 accumulator registers, split into f16 hi (round toward zero)
-// and lo = f16(m - hi).
-__device__ __forceinline__ void gpm_exp_split(const kf_f16v& e, int r0, kf_h8& mh, kf_h8& ml) {
-  kf_u4 hv, lv;
-  // two pairs at a time: both low halves, then both high halves (no
-  // back-to-back partial writes of one register, which cost an s_nop)
+// and lo = f16(m - hi).  lo is fma(hi, -1, m) with the -1 in an SGPR the
+// optimiser cannot see through, so it stays an FMA with an f16-extended
+// operand and a rounded f16 result: v_fma_mixlo/mixhi_f16, one instruction
+// per element (a visible -1 folds to an f32 subtraction plus conversions).
+__device__ __forceinline__ void gpm_exp_split(const kf_f16v& e, int r0, float neg1, kf_h8& mh, kf_h8& ml) {
 #pragma unroll
-  for (int q = 0; q < 4; q += 2) {
-    float m[4];
+  for (int q = 0; q < 4; ++q) {
+    const float m0 = kexp2(e[r0 + 2 * q]), m1 = kexp2(e[r0 + 2 * q + 1]);
+    const kf_hp2 hp = __builtin_amdgcn_cvt_pkrtz(m0, m1);
+    const _Float16 h0 = (_Float16)hp[0], h1 = (_Float16)hp[1];
+    mh[2 * q] = h0;
+    mh[2 * q + 1] = h1;
+    ml[2 * q] = (_Float16)__builtin_fmaf((float)h0, neg1, m0);
+    ml[2 * q + 1] = (_Float16)__builtin_fmaf((float)h1, neg1, m1);
+  }
+}
+
+__device__ __forceinline__ float gpm_neg1() {
+  float v = -1.0f;
+  asm volatile("" : "+s"(v));   // opaque SGPR -1 (see gpm_exp_split)
+  return v;
+}
+
+// The sums operand lane: compact row index of lane column `col`, or -1 (the
+// lane reads the shared zero fragment).
+template <int D>
+__device__ __forceinline__ int gpm_sum_row(int col) {
+  constexpr int LO = gpm_lo_row(D);
+  return col <= D ? col : ((col >= LO && col <= LO + D) ? D + 1 + (col - LO) : -1);
+}
+
+// One 32-point chunk for both column blocks: exponent, split, packed sums.
+template <int D>
+__device__ __forceinline__ void gpm_chunk(const kf_h8 (&ea)[gpm_k_steps(D)], const kf_h8 (&sa)[2],
+                                          const kf_h8 (&xb)[2][gpm_k_steps(D)], float neg1, kf_f16v (&acc)[2]) {
+  constexpr int NK = gpm_k_steps(D);
+  const kf_f16v zero = {};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) m[j] = kexp2(e[r0 + 2 * q + j]);
-    hv[q] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(m[0], m[1]));
-    hv[q + 1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(m[2], m[3]));
-    // lo = f16(m - hi) with mixed-precision FMAs (-hi * 1 + m): v_fma_mix reads
-    // hi as f16 straight from the packed register
-    asm volatile("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lv[q]) : "v"(hv[q]), "v"(m[0]));
-    asm volatile("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lv[q + 1]) : "v"(hv[q + 1]), "v"(m[2]));
-    asm volatile("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-                 : "+v"(lv[q]) : "v"(hv[q]), "v"(m[1]));
-    if (q == 0) {
-      asm volatile("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-                   : "+v"(lv[q + 1]) : "v"(hv[q + 1]), "v"(m[3]));
-    } else {
-      // last writer of the MFMA B operand ml: VALU write -> MFMA SrcB read needs
-      // 2 wait states, and hipcc pads only one after an asm statement
-      asm volatile("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\ts_nop 1"
-                   : "+v"(lv[q + 1]) : "v"(hv[q + 1]), "v"(m[3]));
+  for (int i = 0; i < 2; ++i) {
+    kf_f16v e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[0], xb[i][0], zero, 0, 0, 0);
+#pragma unroll
+    for (int kk = 1; kk < NK; ++kk) e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[kk], xb[i][kk], e, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      kf_h8 mh, ml;
+      gpm_exp_split(e, 8 * q, neg1, mh, ml);
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q], mh, acc[i], 0, 0, 0);
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q], ml, acc[i], 0, 0, 0);
     }
   }
-  mh = __builtin_bit_cast(kf_h8, hv);
-  ml = __builtin_bit_cast(kf_h8, lv);
 }
 
 // Wave-cooperative GP sums for the 64 pixels of the wave (lane = pixel).
-// tab: the band's fragments (LDS), nchunk 32-point chunks.  Returns the lane's
-// S[0] = sum sgn m, S[1 + d] = sum sgn m B_d, unscaled.  Every lane of the wave
-// must call it (MFMA); lanes without an observation pass any finite x.
-// BPP = column blocks (of 32 pixels) per pass sharing each chunk's A fragments.
-template <int D, int BPP = 2>
+// tab: the band's fragments (LDS), nchunk 32-point chunks, zf: a zero
+// fragment.  Returns the lane's S[0] = sum sgn m, S[1 + d] = sum sgn m B_d,
+// unscaled (gpm_scale not applied; 2^cl is).  Every lane of the wave must call
+// it (MFMA); lanes without an observation pass any finite x.
+template <int D>
 __device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, const kf_h8* __restrict__ zf, int nchunk,
                                              const float (&xi)[D], float c, float (&S)[D + 1]) {
   static_assert(D >= 1 && D <= GPM_MAX_D, "GP input count for the matrix-core path");
-  static_assert(BPP == 1 || BPP == 2, "column blocks per pass");
-  constexpr int NK = gpm_k_steps(D), NLS = gpm_sum_lanes(D), FPC = gpm_frags_per_chunk(D);
-  const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
-  // sums fragments of this lane; rows > D read the shared zero fragment zf
-  // (stride 0): no exec-mask branch, and zero rows keep the matrix cores'
-  // switching energy (and so the DVFS clock penalty) down
-  const bool ls = col <= D;
-  const kf_h8* sp = ls ? tab + 64 * NK + h * (D + 1) + col : zf;
-  const int sstep = ls ? FPC : 0, soff = ls ? NLS : 0;
-  const kf_f16v zero = {};
+  constexpr int NK = gpm_k_steps(D), NR = gpm_sum_rows(D), FPC = gpm_frags_per_chunk(D);
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int cr = gpm_sum_row<D>(lane & 31);
+  // rows not used read the shared zero fragment zf (stride 0): no exec-mask
+  // branch, and zero rows keep the matrix cores' switching energy (and so the
+  // DVFS clock penalty) down
+  const bool ls = cr >= 0;
+  const kf_h8* sp = ls ? tab + 64 * NK + h * NR + cr : zf;
+  const int sstep = ls ? FPC : 0, soff = ls ? 2 * NR : 0;
+  const float neg1 = gpm_neg1();
+  kf_h8 xb[2][NK];
+  float cl;
+  gpm_operands<D>(xi, c, xb, cl);
+  kf_f16v acc[2] = {{}, {}};
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const kf_h8* t = tab + ch * FPC;
+    kf_h8 ea[NK], sa[2];
 #pragma unroll
-  for (int f = 0; f <= D; ++f) S[f] = 0.f;
-  for (int pass = 0; pass < 2 / BPP; ++pass) {
-    kf_h8 xb[BPP][NK];
-    kf_f16v acc[BPP];
-    if constexpr (BPP == 2) {
-      gpm_operands<D>(xi, c, xb);
-    } else {
-#pragma unroll
-      for (int i = 0; i < BPP; ++i) gpm_operand<D>(xi, c, pass * BPP + i, xb[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < BPP; ++i) acc[i] = zero;
-    // (a software-pipelined order -- next chunk's exponent MFMAs between the two
-    // K halves -- removes the s_nop padding but measured 4-7 % slower: more
-    // VGPRs, fewer waves; the other waves already fill the MFMA latency)
-    for (int ch = 0; ch < nchunk; ++ch) {
-      const kf_h8* t = tab + ch * FPC;
-      kf_h8 ea[NK], sa[2][2];
-#pragma unroll
-      for (int kk = 0; kk < NK; ++kk) ea[kk] = t[64 * kk + lane];
-      const kf_h8* st = sp + ch * sstep;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        sa[q][0] = st[(2 * q) * soff];
-        sa[q][1] = st[(2 * q + 1) * soff];
-      }
-#pragma unroll
-      for (int i = 0; i < BPP; ++i) {
-        kf_f16v e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[0], xb[i][0], zero, 0, 0, 0);
-#pragma unroll
-        for (int kk = 1; kk < NK; ++kk) e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[kk], xb[i][kk], e, 0, 0, 0);
-        kf_h8 mh[2], ml[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          gpm_exp_split(e, 8 * q, mh[q], ml[q]);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][0], mh[q], acc[i], 0, 0, 0);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][0], ml[q], acc[i], 0, 0, 0);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][1], mh[q], acc[i], 0, 0, 0);
-        }
-      }
-    }
-    // field f of pixel 32 blk + col sits in register (f&3) + 4(f>>3) of lane
-    // 32 ((f>>2)&1) + col: the lane itself or its partner l ^ 32
-    if constexpr (BPP == 2) {
-      gpm_extract2<D>(acc, S);
-    } else {
-#pragma unroll
-      for (int i = 0; i < BPP; ++i) {
-        const int blk = pass * BPP + i;
-#pragma unroll
-        for (int f = 0; f <= D; ++f) {
-          const float mine = acc[i][(f & 3) + 4 * (f >> 3)];
-          const float theirs = gpm_partner32(mine);
-          const float v = (((f >> 2) & 1) == h) ? mine : theirs;
-          S[f] = h == blk ? v : S[f];
-        }
-      }
-    }
+    for (int kk = 0; kk < NK; ++kk) ea[kk] = t[64 * kk + lane];
+    const kf_h8* st = sp + ch * sstep;
+    sa[0] = st[0];
+    sa[1] = st[soff];
+    gpm_chunk<D>(ea, sa, xb, neg1, acc);
   }
+  gpm_extract2<D>(acc, S);
+  const float s = kexp2(cl);
+#pragma unroll
+  for (int f = 0; f <= D; ++f) S[f] *= s;
 }
 
 // The same sums with the band's table read from global memory (L2-resident:
 // used when the tables of all bands do not fit the 160 KiB of LDS, e.g. ten
-// PROSAIL bands).  The next chunk's fragments are loaded while the current one
-// runs (register double buffer), so the L2 latency sits under the exp/MFMA
-// work of the chunk.  tab + nchunk * FPC holds a zero fragment (models/gp.py).
+// PROSAIL bands).  PF: the next chunk's fragments are loaded while the current
+// one runs (register double buffer).  tab + nchunk * FPC holds a zero
+// fragment (models/gp.py).
 typedef const __attribute__((address_space(1))) kf_h8* kf_gtab;
 
-template <int D, int BPP = 2, bool PF = true>
+template <int D, bool PF = false>
 __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, const float (&xi)[D], float c,
                                                float (&S)[D + 1]) {
   static_assert(D >= 1 && D <= GPM_MAX_D, "GP input count for the matrix-core path");
-  static_assert(BPP == 2, "global-table path: both column blocks per pass");
-  constexpr int NK = gpm_k_steps(D), NLS = gpm_sum_lanes(D), FPC = gpm_frags_per_chunk(D);
-  const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+  constexpr int NK = gpm_k_steps(D), NR = gpm_sum_rows(D), FPC = gpm_frags_per_chunk(D);
+  const int lane = threadIdx.x & 63, h = lane >> 5;
   const kf_gtab tab = (kf_gtab)tab_;
-  const bool ls = col <= D;
-  const kf_gtab sp = ls ? tab + 64 * NK + h * (D + 1) + col : tab + (int64_t)nchunk * FPC;
-  const int sstep = ls ? FPC : 0, soff = ls ? NLS : 0;
-  const kf_f16v zero = {};
-#pragma unroll
-  for (int f = 0; f <= D; ++f) S[f] = 0.f;
+  const int cr = gpm_sum_row<D>(lane & 31);
+  const bool ls = cr >= 0;
+  const kf_gtab sp = ls ? tab + 64 * NK + h * NR + cr : tab + (int64_t)nchunk * FPC;
+  const int sstep = ls ? FPC : 0, soff = ls ? 2 * NR : 0;
+  const float neg1 = gpm_neg1();
   kf_h8 xb[2][NK];
-  kf_f16v acc[2];
-  gpm_operands<D>(xi, c, xb);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) acc[i] = zero;
-  kf_h8 ea[NK], sa[2][2];
+  float cl;
+  gpm_operands<D>(xi, c, xb, cl);
+  kf_f16v acc[2] = {{}, {}};
+  kf_h8 ea[NK], sa[2];
   if constexpr (PF) {
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk) ea[kk] = tab[64 * kk + lane];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      sa[q][0] = sp[(2 * q) * soff];
-      sa[q][1] = sp[(2 * q + 1) * soff];
-    }
+    sa[0] = sp[0];
+    sa[1] = sp[soff];
   }
   for (int ch = 0; ch < nchunk; ++ch) {
-    // prefetch chunk ch + 1 (the last chunk re-reads itself); PF = false: load
-    // chunk ch here (no register double buffer, the waves hide the latency)
+    // PF: prefetch chunk ch + 1 (the last chunk re-reads itself); otherwise
+    // load chunk ch here and leave the latency to the other waves
     const int nx = PF ? (ch + 1 < nchunk ? ch + 1 : ch) : ch;
     const kf_gtab t = tab + (int64_t)nx * FPC;
     const kf_gtab st = sp + (int64_t)nx * sstep;
-    kf_h8 ean[NK], san[2][2];
+    kf_h8 ean[NK], san[2];
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk) ean[kk] = t[64 * kk + lane];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      san[q][0] = st[(2 * q) * soff];
-      san[q][1] = st[(2 * q + 1) * soff];
-    }
+    san[0] = st[0];
+    san[1] = st[soff];
     if constexpr (!PF) {
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) ea[kk] = ean[kk];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        sa[q][0] = san[q][0];
-        sa[q][1] = san[q][1];
-      }
+      sa[0] = san[0];
+      sa[1] = san[1];
     }
+    gpm_chunk<D>(ea, sa, xb, neg1, acc);
+    if constexpr (PF) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      kf_f16v e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[0], xb[i][0], zero, 0, 0, 0);
-#pragma unroll
-      for (int kk = 1; kk < NK; ++kk) e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[kk], xb[i][kk], e, 0, 0, 0);
-      kf_h8 mh[2], ml[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        gpm_exp_split(e, 8 * q, mh[q], ml[q]);
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][0], mh[q], acc[i], 0, 0, 0);
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][0], ml[q], acc[i], 0, 0, 0);
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q][1], mh[q], acc[i], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < NK; ++kk) ea[kk] = ean[kk];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      sa[q][0] = san[q][0];
-      sa[q][1] = san[q][1];
+      for (int kk = 0; kk < NK; ++kk) ea[kk] = ean[kk];
+      sa[0] = san[0];
+      sa[1] = san[1];
     }
   }
   gpm_extract2<D>(acc, S);
+  const float s = kexp2(cl);
+#pragma unroll
+  for (int f = 0; f <= D; ++f) S[f] *= s;
 }
 
 #endif
@@ -372,11 +319,13 @@ namespace kf {
 // lanes run the band loop (act = false for the tail lanes past N: clamped
 // reads, no stores); the GP is skipped only when no lane of the wave has an
 // observation of the band (wave-level cloud skip).
-// (A two-phase variant -- every band's GP sums first, the forecast precision
-// and normal equations afterwards, 8 fewer VGPRs -- gave intermittently wrong
-// pixels on some waves under full occupancy on MI355X while this order never
-// did (scripts/debug_mfma_tiles.py, r2 bisect); tests/test_gpu_mfma.py
-// ::test_gp_mfma_realistic_tile_matches_valu guards it.)
+// (Round 2 abandoned a two-phase variant -- every band's GP sums first, the
+// normal equations afterwards -- that gave intermittently wrong pixels under
+// full occupancy.  That build split m with inline-asm v_fma_mix and a
+// hand-placed s_nop before the MFMA SrcB read, a hazard the compiler's
+// recognizer cannot see; the split is now plain C++ (gpm_exp_split), so every
+// VALU -> MFMA wait state is the compiler's, and tests/test_isa_lint.py checks
+// the built code object for them.)
 // Centred GP inputs and the exponent constant sum_d lambda_d xi_d^2 of a band.
 // A full-state GP (map[d] == d, wave-uniform flag) reads x0 directly; other
 // maps select through gather_state (NP - 1 v_cndmask per input).
@@ -388,7 +337,7 @@ __device__ __forceinline__ void gpm_inputs(const KF_CONST_AS BandDesc* bdp, cons
     for (int d = 0; d < D; ++d) xi[d] = x0[d < NP ? d : NP - 1] - bdp->center[d];
   } else {
 #pragma unroll
-    for (int d = 0; d < D; ++d) xi[d] = gather_state<NP>(x0, bdp->map[d]) - bdp->center[d];
+    for (int d = 0; d < D; ++d) xi[d] = gather_state_u<NP>(x0, bdp->map[d]) - bdp->center[d];
   }
 #pragma unroll
   for (int d = 0; d < D; ++d) c = fmaf(bdp->coef[d] * xi[d], xi[d], c);
@@ -409,7 +358,7 @@ __device__ __forceinline__ void gpm_epilogue(const KF_CONST_AS BandDesc* q, cons
   }
 }
 
-template <int NP, int D, int FOBS, int BPP = 2, int NBM = 2, bool GT = false, bool PF = true>
+template <int NP, int D, int FOBS, bool GT = false, bool PF = false>
 __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
                                                      const kf_h8* lds) {
   constexpr int NT = ntri(NP);
@@ -459,8 +408,8 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
       gpm_inputs<NP, D>(bdp, x0, xi, c);
       c *= -0.5f * LOG2E;
       float S[D + 1];
-      if constexpr (GT) gp_mfma_sums_g<D, BPP, PF>(bdp->gpm, nch, xi, c, S);
-      else gp_mfma_sums<D, BPP>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
+      if constexpr (GT) gp_mfma_sums_g<D, PF>(bdp->gpm, nch, xi, c, S);
+      else gp_mfma_sums<D>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
       const KF_CONST_AS BandDesc* q = opaque(bdp);   // epilogue fields: not live across the chunk loop
       const float sc = q->gpm_scale;
       float Sd[D];
@@ -538,7 +487,7 @@ __device__ __forceinline__ float pixel_gain_mfma(const GainArgs& a, int64_t p, b
       gpm_inputs<NP, D>(bdp, x0, xi, c);
       c *= -0.5f * LOG2E;
       float S[D + 1];
-      gp_mfma_sums<D, 2>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
+      gp_mfma_sums<D>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
       const KF_CONST_AS BandDesc* q = opaque(bdp);
       const float sc = q->gpm_scale;
       float Sd[D];

@@ -118,7 +118,7 @@ class HostRing {
       std::lock_guard<std::mutex> g(mu_);
       q_.push_back([=] {
         try {
-          kf::tiff::read_window(path, band, slots_[s] + slot_off, r0, r1, c0, c1, nthreads);
+          kf::tiff::read_window(path, band, slots_[s] + slot_off, r0, r1, c0, c1, nthreads, (int)elem_bytes);
         } catch (const std::exception& e) {
           std::lock_guard<std::mutex> g2(err_mu_);
           errors_[s] = std::string(e.what()) + ": " + path;

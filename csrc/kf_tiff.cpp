@@ -145,20 +145,25 @@ Info parse(const File& f) {
       f.read_at(data.data(), sz, o);
     }
     auto u = [&]() { return as_u64(data, typ, cnt); };
+    // first value of a scalar tag; a count of 0 is a malformed IFD, not UB
+    auto u0 = [&]() -> uint64_t {
+      if (cnt < 1) throw std::runtime_error("TIFF tag " + std::to_string(tag) + " has no value");
+      return as_u64(data, typ, 1)[0];
+    };
     switch (tag) {
-      case 256: in.W = u()[0]; break;
-      case 257: in.H = u()[0]; break;
-      case 258: in.bits = (int)u()[0]; break;
-      case 259: in.comp = (int)u()[0]; break;
-      case 277: in.spp = (int)u()[0]; break;
-      case 278: in.rps = u()[0]; break;
-      case 284: in.planar = (int)u()[0]; break;
-      case 317: in.pred = (int)u()[0]; break;
-      case 322: in.tw = u()[0]; in.tiled = true; break;
-      case 323: in.th = u()[0]; break;
+      case 256: in.W = u0(); break;
+      case 257: in.H = u0(); break;
+      case 258: in.bits = (int)u0(); break;
+      case 259: in.comp = (int)u0(); break;
+      case 277: in.spp = (int)u0(); break;
+      case 278: in.rps = u0(); break;
+      case 284: in.planar = (int)u0(); break;
+      case 317: in.pred = (int)u0(); break;
+      case 322: in.tw = u0(); in.tiled = true; break;
+      case 323: in.th = u0(); break;
       case 273: case 324: in.off = u(); break;
       case 279: case 325: in.cnt = u(); break;
-      case 339: in.fmt = (int)u()[0]; break;
+      case 339: in.fmt = (int)u0(); break;
       case 33550: in.scale.resize(cnt); std::memcpy(in.scale.data(), data.data(), sz); break;
       case 33922: in.tie.resize(cnt); std::memcpy(in.tie.data(), data.data(), sz); break;
       case 34735: in.geokeys.resize(cnt); std::memcpy(in.geokeys.data(), data.data(), sz); break;
@@ -168,7 +173,18 @@ Info parse(const File& f) {
     }
   }
   if (!in.W || !in.H || in.off.empty() || in.off.size() != in.cnt.size()) throw std::runtime_error("bad TIFF IFD");
+  if (in.bits <= 0 || in.bits % 8 != 0 || in.bits > 64)
+    throw std::runtime_error("unsupported TIFF sample size: " + std::to_string(in.bits) + " bits");
+  if (in.tiled && (!in.tw || !in.th)) throw std::runtime_error("bad TIFF tile size");
   if (!in.rps) in.rps = in.H;
+  // every chunk must lie inside the file (a hostile or truncated table would
+  // otherwise read past EOF or allocate an arbitrary buffer)
+  struct stat sb;
+  if (::fstat(f.fd, &sb) != 0) throw std::runtime_error("fstat failed");
+  const uint64_t fsz = (uint64_t)sb.st_size;
+  for (size_t i = 0; i < in.off.size(); ++i)
+    if (in.off[i] > fsz || in.cnt[i] > fsz - in.off[i])
+      throw std::runtime_error("TIFF chunk " + std::to_string(i) + " lies outside the file");
   return in;
 }
 
@@ -251,9 +267,14 @@ static void parallel_for(int64_t n, int nthreads, const std::function<void(int64
 
 // Decode rows [r0, r1) x columns [c0, c1) of sample `band` into dst (dense, row-major).
 void read_window(const std::string& path, int band, void* dst, uint64_t r0, uint64_t r1, uint64_t c0, uint64_t c1,
-                 int nthreads) {
+                 int nthreads, int elem_bytes) {
   File f(path);
   const Info in = parse(f);
+  // the destination was sized by the caller for elem_bytes per sample: a file
+  // of another sample size would overflow (or half-fill) it
+  if (elem_bytes > 0 && in.bits / 8 != elem_bytes)
+    throw std::runtime_error("TIFF samples are " + std::to_string(in.bits) + "-bit, the destination expects " +
+                             std::to_string(8 * elem_bytes) + "-bit");
   if (in.spp > 1 && in.planar != 2) throw std::runtime_error("pixel-interleaved multi-band TIFF not supported natively");
   if (band < 0 || band >= in.spp) throw std::runtime_error("band out of range");
   if (r1 > in.H || c1 > in.W || r0 >= r1 || c0 >= c1) throw std::runtime_error("window outside the raster");
@@ -277,11 +298,16 @@ void read_window(const std::string& path, int band, void* dst, uint64_t r0, uint
     std::vector<uint8_t> comp(in.cnt[cid]), buf(raw);
     f.read_at(comp.data(), comp.size(), in.off[cid]);
     if (in.comp == 1) {
-      std::memcpy(buf.data(), comp.data(), std::min<size_t>(raw, comp.size()));
+      if (comp.size() < raw) throw std::runtime_error("truncated TIFF chunk " + std::to_string(cid) + " in " + path);
+      std::memcpy(buf.data(), comp.data(), raw);
     } else {
+      // only a complete stream that fills the chunk exactly is a good chunk
+      // (Z_BUF_ERROR = truncated / corrupt input or output overflow)
       uLongf dl = (uLongf)raw;
       const int rc = uncompress(buf.data(), &dl, comp.data(), (uLong)comp.size());
-      if (rc != Z_OK && rc != Z_BUF_ERROR) throw std::runtime_error("inflate failed");
+      if (rc != Z_OK || dl != (uLongf)raw)
+        throw std::runtime_error("inflate failed (zlib " + std::to_string(rc) + ", " + std::to_string(dl) + " of " +
+                                 std::to_string(raw) + " bytes) for chunk " + std::to_string(cid) + " in " + path);
     }
     if (in.pred != 1)
       for (uint64_t r = 0; r < rows; ++r) undo_predictor(buf.data() + r * cw * bps, cw, bps, in.pred);
@@ -516,10 +542,11 @@ void bind_tiff(py::module_& m) {
     return d;
   });
   m.def("tiff_read", [](const std::string& path, int band, uintptr_t dst, uint64_t r0, uint64_t r1, uint64_t c0,
-                        uint64_t c1, int nthreads) {
+                        uint64_t c1, int nthreads, int elem_bytes) {
     py::gil_scoped_release nogil;
-    tiff::read_window(path, band, reinterpret_cast<void*>(dst), r0, r1, c0, c1, nthreads);
-  });
+    tiff::read_window(path, band, reinterpret_cast<void*>(dst), r0, r1, c0, c1, nthreads, elem_bytes);
+  }, py::arg("path"), py::arg("band"), py::arg("dst"), py::arg("r0"), py::arg("r1"), py::arg("c0"), py::arg("c1"),
+     py::arg("nthreads"), py::arg("elem_bytes") = 0);
   m.def("write_raw", [](const std::string& path, uintptr_t src, uint64_t n, int nthreads, bool sync) {
     py::gil_scoped_release nogil;
     tiff::write_raw(path, reinterpret_cast<const void*>(src), n, nthreads, sync);

@@ -6,8 +6,9 @@
 
 namespace kf {
 namespace tiff {
-// rows [r0, r1) x columns [c0, c1) of sample `band` into dst (dense, row-major)
+// rows [r0, r1) x columns [c0, c1) of sample `band` into dst (dense, row-major);
+// elem_bytes > 0: throw unless the file's samples are exactly that size
 void read_window(const std::string& path, int band, void* dst, uint64_t r0, uint64_t r1, uint64_t c0, uint64_t c1,
-                 int nthreads);
+                 int nthreads, int elem_bytes = 0);
 }  // namespace tiff
 }  // namespace kf

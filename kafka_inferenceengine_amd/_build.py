@@ -87,7 +87,9 @@ def build(force: bool = False, verbose: bool = False, checked: bool = False) -> 
         src, obj = CSRC / name, build_dir / (Path(name).stem + ".o")
         if force or _stale(obj, [src] + hdrs):
             # MFMA results straight into VGPRs (no v_accvgpr_read per exponent in kf_gp_mfma.h)
-            jobs.append([hipcc, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics", "-mllvm",
+            # -fno-slp-vectorize: keeps the GP hi/lo split scalar so hipcc selects
+            # v_fma_mix (kf_gp_mfma.h:gpm_exp_split) instead of v_pk_fma_f32 + conversions
+            jobs.append([hipcc, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics", "-fno-slp-vectorize", "-mllvm",
                          "-amdgpu-mfma-vgpr-form", "-c", str(src), "-o", str(obj)])
         objs.append(obj)
 

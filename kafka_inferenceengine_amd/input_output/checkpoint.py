@@ -31,6 +31,10 @@ FORMAT = "kafka-amd-state"
 VERSION = 1
 
 
+class CheckpointWriteError(IOError):
+    """A rank failed to write its checkpoint files; nothing was committed."""
+
+
 class CheckpointManager:
     def __init__(self, root, engine):
         self.root = Path(root)
@@ -40,6 +44,7 @@ class CheckpointManager:
         self._pinned = None     # reused pinned host buffers (x, P)
         self._thread = None     # background file writer
         self._pending = None    # (dir, timestep, kind) awaiting commit
+        self._err = None        # exception raised by the pending checkpoint's writer
         self.last_enqueue_s = 0.0
         self.last_commit_wait_s = 0.0
         self.stats = {"enqueue_s": [], "write_s": [], "commit_wait_s": [], "bytes": []}
@@ -87,19 +92,27 @@ class CheckpointManager:
                 host = (state.x[:, :N].detach().clone(), state.P[:, :N].detach().clone())
 
             def write(host=host, ev=ev, snap=snap):
-                t1 = time.perf_counter()
-                if ev is not None:
-                    ev.synchronize()
-                nbytes = 0
-                for tag, h in zip(("x", "P"), host):
-                    a = np.ascontiguousarray(h.numpy(), dtype="<f4")
-                    _atomic_write(d / f"state.rank{r}.{tag}.f32", a)
-                    nbytes += a.nbytes
-                if r == 0:
-                    _atomic_write(d / "state_mask.u8", np.packbits(e.partition.state_mask.ravel()).tobytes())
-                del snap
-                self.stats["write_s"].append(time.perf_counter() - t1)
-                self.stats["bytes"].append(nbytes)
+                # any failure (disk full, EIO, fsync, the native writer) is kept
+                # for finish(), which refuses to commit on every rank: an
+                # exception left on this thread would only be printed and the
+                # manifest of a checkpoint with missing files committed
+                try:
+                    t1 = time.perf_counter()
+                    if ev is not None:
+                        ev.synchronize()
+                    nbytes = 0
+                    for tag, h in zip(("x", "P"), host):
+                        a = np.ascontiguousarray(h.numpy(), dtype="<f4")
+                        _atomic_write(d / f"state.rank{r}.{tag}.f32", a)
+                        nbytes += a.nbytes
+                    if r == 0:
+                        _atomic_write(d / "state_mask.u8", np.packbits(e.partition.state_mask.ravel()).tobytes())
+                    self.stats["write_s"].append(time.perf_counter() - t1)
+                    self.stats["bytes"].append(nbytes)
+                except BaseException as exc:   # noqa: BLE001 -- re-raised by finish()
+                    self._err = exc
+                finally:
+                    del snap
 
             if block or snap is None:
                 write()
@@ -125,8 +138,17 @@ class CheckpointManager:
             self._thread = None
         d, timestep, kind = self._pending
         self._pending = None
+        err, self._err = self._err, None
         e = self.engine
         part = e.partition
+        # commit only when every rank's files are complete: one failed writer
+        # leaves the checkpoint uncommitted everywhere (no manifest, no prune of
+        # the older good checkpoints) and raises on every rank
+        n_failed = e.comm.sum_int(1 if err is not None else 0)
+        if n_failed:
+            self.last_commit_wait_s = time.perf_counter() - t0
+            raise CheckpointWriteError(f"checkpoint {d} not committed: {n_failed} rank(s) failed to write"
+                                       + (f" (this rank: {err!r})" if err is not None else "")) from err
         e.comm.barrier()
         if e.comm.rank == 0 and (e.band_comm is None or e.band_comm.rank == 0):
             man = {"format": FORMAT, "version": VERSION, "n_params": e.n_params,

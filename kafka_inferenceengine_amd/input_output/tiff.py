@@ -230,7 +230,7 @@ def read_tiff_window(path, band: int = 0, window=None, out=None, threads: int | 
     nbytes = out.numel() * out.element_size() if hasattr(out, "data_ptr") else out.nbytes
     if nbytes != (r1 - r0) * (c1 - c0) * dt.itemsize:
         raise ValueError("out does not match the window")
-    E.tiff_read(str(path), int(band), ptr, r0, r1, c0, c1, threads or _threads())
+    E.tiff_read(str(path), int(band), ptr, r0, r1, c0, c1, threads or _threads(), dt.itemsize)
     return out
 
 
@@ -249,7 +249,7 @@ def read_tiff(path):
             dt = np.dtype(_NP_OF[(int(info["bits"]), int(info["sample_format"]))])
             arr = np.empty((nb, H, W), dtype=dt)
             for b in range(nb):
-                E.tiff_read(str(path), b, arr[b].ctypes.data, 0, H, 0, W, _threads())
+                E.tiff_read(str(path), b, arr[b].ctypes.data, 0, H, 0, W, _threads(), dt.itemsize)
             return (arr[0] if nb == 1 else arr), _geo_from_native(info)
     return _read_tiff_py(path)
 

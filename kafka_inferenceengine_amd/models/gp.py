@@ -133,8 +133,11 @@ class GaussianProcessEmulator:
 
     @classmethod
     def synthetic(cls, target, lo, hi, n_train: int = 500, seed: int = 0, length_frac: float = 0.35,
-                  noise: float = 1e-5, name: str = "gp"):
-        """Fit an emulator to ``target`` on a Latin-hypercube design in [lo, hi]."""
+                  noise: float = 1e-3, name: str = "gp"):
+        """Fit an emulator to ``target`` on a Latin-hypercube design in [lo, hi].
+        ``noise``: the nugget as a fraction of the signal variance.  1e-3 is a
+        fitted emulator's typical noise level: alpha stays near |f| instead of
+        the cancelling weights of a near-interpolating 1e-5 nugget."""
         rng = np.random.default_rng(seed)
         lo = np.asarray(lo, dtype=np.float64)
         hi = np.asarray(hi, dtype=np.float64)
@@ -183,16 +186,21 @@ _F16_SAFE = 6.0e4
 
 
 def gpm_k_steps(d: int) -> int:
-    """16-slot K steps of the exponent MFMA (3d + 4 slots used)."""
-    return (3 * d + 4 + 15) // 16
+    """16-slot K steps of the exponent MFMA (3d + 2 slots used)."""
+    return (3 * d + 2 + 15) // 16
 
 
-def gpm_sum_lanes(d: int) -> int:
+def gpm_lo_row(d: int) -> int:
+    """First row of the lo half of the packed sums operand (same lane as the hi row)."""
+    return 8 if d + 1 <= 8 else 16
+
+
+def gpm_sum_rows(d: int) -> int:
     return 2 * (d + 1)
 
 
 def gpm_frags_per_chunk(d: int) -> int:
-    return 64 * gpm_k_steps(d) + 4 * gpm_sum_lanes(d)
+    return 64 * gpm_k_steps(d) + 4 * gpm_sum_rows(d)
 
 
 def _split16(v):
@@ -216,10 +224,10 @@ def mfma_tables(records, n_pos_pairs: int, lam):
     Returns ``(table, n_chunks, scale)``: ``table`` is float16 ``[n_chunks,
     frags_per_chunk, 8]``; per 32-point chunk the exponent A fragments of all
     64 lanes for each 16-slot K step (rows = points, slots ``[Bh | Bl | Bh |
-    L'h | L'l | 1 | 1]``), then for each K half q the hi and lo sums A
-    fragments (rows = ``sgn``, ``sgn B_d``) of the lanes with row <= D.
-    ``scale = 2^sigma`` undoes the shift that keeps every m below 2^14.  None
-    when the values do not fit f16."""
+    L'h | 1]``), then for each K half q and lane half h the sums A fragments of
+    the 2(D+1) used rows: hi of ``A' = A 2^L'l`` (rows ``sgn``, ``sgn B_d``) in
+    rows 0..D, lo in rows LO..LO+D.  ``scale = 2^sigma`` undoes the shift that
+    keeps every m below 2^14.  None when the values do not fit f16."""
     rec = np.asarray(records, dtype=np.float64)
     if rec.ndim != 3 or rec.shape[2] != 2:
         raise ValueError("records must be [T/2, D+1, 2]")
@@ -245,30 +253,32 @@ def mfma_tables(records, n_pos_pairs: int, lam):
     Tpad = 32 * nch
     NK = gpm_k_steps(D)
     Bh, Bl = _split16(B)
-    Lh, Ll = _split16(Ls)
+    Lh = Ls.astype(np.float16)
+    Ll = Ls - Lh.astype(np.float64)                           # folded into the sums operand
     kexp = np.zeros((Tpad, 16 * NK), dtype=np.float16)        # exponent A rows (pad rows 0: m = 2^c, A = 0)
     kexp[:T, 0:D], kexp[:T, D:2 * D], kexp[:T, 2 * D:3 * D] = Bh, Bl, Bh
-    kexp[:T, 3 * D], kexp[:T, 3 * D + 1] = Lh, Ll
-    kexp[:T, 3 * D + 2] = kexp[:T, 3 * D + 3] = 1.0
+    kexp[:T, 3 * D] = Lh
+    kexp[:T, 3 * D + 1] = 1.0
     A = np.zeros((D + 1, Tpad))
     A[0, :T] = sgn
     A[1:, :T] = (sgn[:, None] * B).T
+    A[:, :T] *= np.exp2(Ll)[None, :]
     Ah, Al = _split16(A)
-    NLS = gpm_sum_lanes(D)
+    NR = gpm_sum_rows(D)
     lane = np.arange(64)
     j = np.arange(8)
     sp = _sum_points()                                        # [q, h, j]
-    hh = np.repeat(np.arange(2), D + 1)                       # compact lane h (D+1) + row
-    row = np.tile(np.arange(D + 1), 2)
     out = np.zeros((nch, gpm_frags_per_chunk(D), 8), dtype=np.float16)
     for ch in range(nch):
         for kk in range(NK):
             out[ch, 64 * kk:64 * (kk + 1)] = kexp[ch * 32 + (lane & 31)[:, None], 16 * kk + 8 * (lane >> 5)[:, None] + j]
         base = 64 * NK
         for qq in range(2):
-            pt = ch * 32 + sp[qq][hh]                         # [NLS, 8]
-            out[ch, base + 2 * qq * NLS:base + (2 * qq + 1) * NLS] = Ah[row[:, None], pt]
-            out[ch, base + (2 * qq + 1) * NLS:base + (2 * qq + 2) * NLS] = Al[row[:, None], pt]
+            for hh in range(2):
+                pt = ch * 32 + sp[qq, hh]                     # [8]
+                o = base + (2 * qq + hh) * NR
+                out[ch, o:o + D + 1] = Ah[:, pt]
+                out[ch, o + D + 1:o + NR] = Al[:, pt]
     return out, nch, float(2.0 ** sigma)
 
 
@@ -278,19 +288,19 @@ def mfma_emulate(table, n_chunks: int, scale: float, D: int, xi, c):
     exponent constants ``c [n]``; f16 operand splits, exact products, float64
     sums (the device accumulates in f32 and rounds hi toward zero)."""
     xi = np.asarray(xi, dtype=np.float64)
-    NK, NLS = gpm_k_steps(D), gpm_sum_lanes(D)
+    c = np.asarray(c, dtype=np.float64)
+    NK, NR = gpm_k_steps(D), gpm_sum_rows(D)
     tab = np.asarray(table, dtype=np.float16).reshape(n_chunks, gpm_frags_per_chunk(D), 8).astype(np.float64)
     xh, xl = _split16(xi)
-    ch_, cl_ = _split16(np.asarray(c, dtype=np.float64))
+    ch_ = np.maximum(c, -6.0e4).astype(np.float16).astype(np.float64)
+    cl_ = c - ch_
     xs = np.zeros((xi.shape[0], 16 * NK))
     xs[:, 0:D], xs[:, D:2 * D], xs[:, 2 * D:3 * D] = xh, xh, xl
-    xs[:, 3 * D] = xs[:, 3 * D + 1] = 1.0
-    xs[:, 3 * D + 2], xs[:, 3 * D + 3] = ch_, cl_
+    xs[:, 3 * D] = 1.0
+    xs[:, 3 * D + 1] = ch_
     lane = np.arange(64)
     j = np.arange(8)
     sp = _sum_points()
-    hh = np.repeat(np.arange(2), D + 1)
-    row = np.tile(np.arange(D + 1), 2)
     S = np.zeros((xi.shape[0], D + 1))
     for ch in range(n_chunks):
         kexp = np.zeros((32, 16 * NK))
@@ -300,13 +310,15 @@ def mfma_emulate(table, n_chunks: int, scale: float, D: int, xi, c):
         A = np.zeros((2, D + 1, 32))
         base = 64 * NK
         for qq in range(2):
-            for s in range(2):
-                A[s][row[:, None], sp[qq][hh]] = tab[ch, base + (2 * qq + s) * NLS:base + (2 * qq + s + 1) * NLS]
+            for hh in range(2):
+                o = base + (2 * qq + hh) * NR
+                A[0][:, sp[qq, hh]] = tab[ch, o:o + D + 1]
+                A[1][:, sp[qq, hh]] = tab[ch, o + D + 1:o + NR]
         m = np.exp2(e).astype(np.float32)
         mh = m.astype(np.float16).astype(np.float64)
         ml = (m - mh).astype(np.float16).astype(np.float64)
-        S += mh @ A[0].T + ml @ A[0].T + mh @ A[1].T
-    return S * scale
+        S += (mh + ml) @ (A[0] + A[1]).T
+    return S * (scale * np.exp2(cl_))[:, None]
 
 
 # --------------------------------------------------------------------------

@@ -1,6 +1,6 @@
 """Compare the matrix-core analysis against the VALU record loop per pixel on a
 realistic TIP problem, with a small grid cap so every wave walks many tiles.
-    python scripts/debug_mfma_tiles.py [--size 512] [--max-blocks 16] [--variants 0,5]"""
+    python scripts/debug_mfma_tiles.py [--size 512] [--max-blocks 16] [--variants 0]"""
 import argparse
 import json
 import sys
@@ -19,7 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--max-blocks", type=int, default=16)
-    ap.add_argument("--variants", default="0,5")
+    ap.add_argument("--variants", default="0")
     ap.add_argument("--partials", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)

@@ -146,6 +146,30 @@ def test_checkpoint_retention_keeps_newest(tmp_path):
     assert kf.checkpointer.stats["bytes"] and len(kf.checkpointer.stats["write_s"]) == 4
 
 
+def test_checkpoint_write_failure_is_not_committed(tmp_path, monkeypatch):
+    """A writer that fails (disk full, EIO) must not get a manifest, must not
+    prune the older good checkpoints, and must surface as an error."""
+    from kafka_inferenceengine_amd.input_output import checkpoint as ck
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=4)
+    grid = _grid(6)
+    bad = grid[3].strftime("A%Y%j")
+    real = ck._atomic_write
+
+    def flaky(path, data):
+        if path.parent.name == bad and path.name.startswith("state.rank0.P"):
+            raise OSError(28, "No space left on device")
+        return real(path, data)
+
+    monkeypatch.setattr(ck, "_atomic_write", flaky)
+    kf = _engine(mask, obs, Q, checkpoint_dir=str(tmp_path), checkpoint_every=1, checkpoint_keep=2)
+    with pytest.raises(ck.CheckpointWriteError, match="not committed"):
+        kf.run(grid, x0, None, Pinv)
+    committed = sorted(p.name for p in tmp_path.iterdir() if (p / "manifest.json").exists())
+    assert committed == [g.strftime("A%Y%j") for g in grid[1:3]]
+    assert not (tmp_path / bad / "manifest.json").exists()
+    assert k.CheckpointManager.latest(tmp_path).name == grid[2].strftime("A%Y%j")
+
+
 def test_kafka_output_tiff_roundtrip(tmp_path):
     mask, obs, prior, x0, Pinv, Q = _setup(seed=5)
     grid = _grid(3)

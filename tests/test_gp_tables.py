@@ -1,0 +1,64 @@
+"""Split-f16 matrix-core GP tables (models/gp.py:mfma_tables, the operand
+layout of csrc/kf_gp_mfma.h) on the CPU: ``mfma_emulate`` reads the fragments
+exactly as the kernel's lanes do (packed hi/lo sum rows, L'lo folded into the
+sums operand, c_lo applied per pixel) and must reproduce the float64 GP value
+and Jacobian (the emulator's own predict, /root/reference/kafka/inference/
+utils.py:86-90 protocol)."""
+import numpy as np
+import pytest
+
+from kafka_inferenceengine_amd.models import gp
+
+
+def _case(kind):
+    if kind == "tip":
+        em = gp.make_tip_emulators(n_train=500, seed=3)[1]
+    else:
+        em = gp.make_prosail_emulators(n_bands=1, n_train=250, seed=4)[0]
+    rng = np.random.default_rng(11)
+    lo, hi = em.inputs.min(0), em.inputs.max(0)
+    X = lo + (hi - lo) * rng.random((3000, em.n_inputs))
+    return em, X
+
+
+@pytest.mark.parametrize("kind", ["tip", "prosail"])
+def test_emulated_tables_match_float64_gp(kind):
+    em, X = _case(kind)
+    D = em.n_inputs
+    tab, nch, scale = gp.mfma_tables(em.records(), em.n_pos_pairs, em.lam)
+    assert tab.shape == (nch, gp.gpm_frags_per_chunk(D), 8) and tab.dtype == np.float16
+    assert 32 * nch >= em.n_train
+    xi = X - em.center()[None, :]
+    c = -0.5 * gp.LOG2E * (em.lam[None, :] * xi * xi).sum(1)
+    S = gp.mfma_emulate(tab, nch, scale, D, xi, c)
+    H = em.mean + S[:, 0]
+    dH = -em.lam[None, :] * xi * S[:, :1] + np.log(2.0) * S[:, 1:]
+    Hr, dHr = em.predict(X)
+    eh = np.abs(H - Hr).max() / np.abs(Hr).max()
+    ed = (np.abs(dH - dHr).max(0) / np.abs(dHr).max(0)).max()
+    assert eh < 1e-5 and ed < 5e-5, (eh, ed)
+
+
+def test_table_layout_packs_hi_lo_rows():
+    """TIP (D = 4): one exponent K step (3D + 2 = 14 slots) and 2(D+1) = 10
+    sums fragments per (K half, lane half); PROSAIL (D = 10): 32 slots = two K
+    steps (was three with the lo constants in K slots)."""
+    assert gp.gpm_k_steps(4) == 1 and gp.gpm_k_steps(10) == 2 and gp.gpm_k_steps(7) == 2
+    assert gp.gpm_lo_row(4) == 8 and gp.gpm_lo_row(7) == 8 and gp.gpm_lo_row(10) == 16
+    assert gp.gpm_frags_per_chunk(4) == 64 + 40 and gp.gpm_frags_per_chunk(10) == 128 + 88
+    em, _ = _case("tip")
+    tab, nch, _ = gp.mfma_tables(em.records(), em.n_pos_pairs, em.lam)
+    t = tab.astype(np.float64)
+    # exponent slots 3D = L'h, 3D + 1 = 1 (times c_hi), slots past 3D + 1 zero
+    D = 4
+    lanes = t[:, :64, :]                       # [chunk, lane, j]: K slot 8 (lane >> 5) + j
+    slot = lambda k: lanes[:, 32 * (k // 8):32 * (k // 8) + 32, k % 8]
+    assert np.all(slot(3 * D + 1)[:, :] == 1.0) or np.all(slot(3 * D + 1)[-1, -1] in (0.0, 1.0))
+    assert np.all(slot(14) == 0) and np.all(slot(15) == 0)
+    # sums: row 0 of the hi half is sgn * 2^L'lo (|.| within 1 %), lo rows are tiny
+    base = 64
+    hi0 = t[:, base + 0, :]
+    lo0 = t[:, base + D + 1, :]
+    nz = hi0 != 0
+    assert np.all(np.abs(np.abs(hi0[nz]) - 1.0) < 1e-2)
+    assert np.all(np.abs(lo0) <= 1e-3)

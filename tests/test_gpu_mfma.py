@@ -83,8 +83,8 @@ def test_gp_mfma_operator_value_vs_float64(cuda, case):
         sel = w > 0
         err = np.abs(hd[sel] - H[sel]).max() / np.abs(H).max()
         err_valu = np.abs(hv[sel] - H[sel]).max() / np.abs(H).max()
-        # the TIP emulators cancel (|alpha| >> |f|): f32 itself is ~1e-4 there
-        assert err < max(2e-4, 2.0 * err_valu), (case, em.name, err, err_valu)
+        # emulators fitted with a realistic nugget (models/gp.py): |alpha| ~ |f|
+        assert err < 2e-5, (case, em.name, err, err_valu)
         assert np.all(hd[~sel] == 0)
 
 
@@ -97,9 +97,9 @@ def test_gp_mfma_analysis_vs_oracle_and_valu(cuda, case):
     scale = np.abs(xr) + 0.05
     err_m = np.max(np.abs(xm - xr) / scale)
     err_v = np.max(np.abs(xv - xr) / scale)
-    # split-f16 MFMA is at least as accurate as the f32 VALU loop (both limited
-    # by f32 cancellation in the TIP sums; r2 measured 1.2e-3 vs 2.1e-3 here)
-    assert err_m < 2e-3 and err_v < 4e-3 and err_m < 1.5 * err_v + 1e-4, (err_m, err_v)
+    # SURVEY.md §7.3 acceptance: 1e-4 relative on x against float64
+    print(f"x err mfma {err_m:.2e} valu {err_v:.2e}")
+    assert err_m < 1e-4 and err_m < 1.5 * err_v + 2e-5, (err_m, err_v)
     assert np.array_equal(sm, sv)
     from kafka_inferenceengine_amd.utils.blocks import unpack_blocks
     n = prob["n"]
@@ -107,9 +107,8 @@ def test_gp_mfma_analysis_vs_oracle_and_valu(cuda, case):
     norm = d[:, :, None] * d[:, None, :]              # |A_ij| <= sqrt(A_ii A_jj)
     rel_m = np.max(np.abs(unpack_blocks(am, n) - Ar) / norm)
     rel_v = np.max(np.abs(unpack_blocks(av, n) - Ar) / norm)
-    # f32 Jacobians of the cancelling TIP sums: both device paths sit at ~7e-3 here
-    print(f"x err mfma {err_m:.2e} valu {err_v:.2e}; A err mfma {rel_m:.2e} valu {rel_v:.2e}")
-    assert rel_m < 2e-2 and rel_m < 1.5 * rel_v + 1e-5, (rel_m, rel_v)
+    print(f"A err mfma {rel_m:.2e} valu {rel_v:.2e}")
+    assert rel_m < 1e-3 and rel_m < 1.5 * rel_v + 1e-5, (rel_m, rel_v)
     assert abs(rm - rv) / rv < 1e-2
 
 
@@ -123,17 +122,18 @@ def test_gp_mfma_tail_and_cloud_waves(cuda):
     _, xv, _, sv, _, _ = run(prob, cuda, variant=4)
     assert np.array_equal(sm, sv)
     assert np.all(sm[64 * 3:64 * 5] & K.ST_NO_OBS)
-    assert np.max(np.abs(xm - xv) / (np.abs(xv) + 0.05)) < 2e-3
+    assert np.max(np.abs(xm - xv) / (np.abs(xv) + 0.05)) < 2e-4
     assert np.all(h0[0][64 * 3:64 * 5] == 0)
 
 
 @pytest.mark.parametrize("cap", [0, 16])
-@pytest.mark.parametrize("variant", [0, 5])
-def test_gp_mfma_realistic_tile_matches_valu(cuda, variant, cap):
+def test_gp_mfma_realistic_tile_matches_valu(cuda, cap):
     """A 512^2 synthetic TIP tile with per-pixel states (one and many 64-pixel
-    tiles per wave): every pixel of both matrix-core variants agrees with the
-    VALU loop.  Guards the VALU -> MFMA operand wait states of the inline-asm
-    hi/lo split (a missing pad corrupted a quarter of some waves only)."""
+    tiles per wave): every pixel of the matrix-core kernel agrees with the VALU
+    loop to 5e-3.  Round 2's inline-asm hi/lo split once lost a wait state
+    and corrupted a quarter of some waves; the split is compiler-visible now
+    (tests/test_isa_lint.py checks the pads) and this stays as the runtime guard."""
+    variant = 0
     from kafka_inferenceengine_amd.utils.blocks import pack_matrix
     mask = np.ones((512, 512), bool)
     obs = k.SyntheticBHRObservations(mask, n_train=500, device=cuda, stream=False, n_pool=1)
@@ -160,4 +160,4 @@ def test_gp_mfma_realistic_tile_matches_valu(cuda, variant, cap):
     ref = outs[4][0]
     for x in outs[variant]:
         d = np.abs(x - ref) / (np.abs(ref) + 0.05)
-        assert d.max() < 0.1, (variant, cap, float(d.max()), np.nonzero(d.max(0) > 0.1)[0][:8])
+        assert d.max() < 5e-3, (variant, cap, float(d.max()), np.nonzero(d.max(0) > 5e-3)[0][:8])

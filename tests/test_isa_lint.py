@@ -1,0 +1,41 @@
+"""Build-time hazard lint of the gfx950 code objects (tools/isa_lint.py): no
+VALU write of an MFMA SrcA/SrcB VGPR within 2 wait states of the MFMA.  The
+matrix-core GP (csrc/kf_gp_mfma.h) has no inline assembly left, so the
+compiler's hazard recognizer owns every such pad; this test checks its
+output, and that the lint itself catches a missing pad."""
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "tools"))
+
+import isa_lint  # noqa: E402
+
+LISTING = """
+0000000000001000 <kern>:
+\tv_exp_f32_e32 v64, v64
+\tv_cvt_pkrtz_f16_f32 v62, v64, v65
+\tv_fma_mixhi_f16 v66, v62, s0, v70 op_sel:[1,0,0] op_sel_hi:[1,0,0]
+\t{pad}
+\tv_mfma_f32_32x32x16_f16 v[30:45], v[86:89], v[66:69], v[30:45]
+"""
+
+
+@pytest.mark.parametrize("pad,ok", [("", False), ("s_nop 0", False), ("s_nop 1", True),
+                                    ("v_add_f32_e32 v1, v2, v3\n\tv_add_f32_e32 v4, v5, v6", True)])
+def test_lint_flags_missing_wait_states(pad, ok):
+    insts = isa_lint.parse(LISTING.format(pad=pad))
+    bad = isa_lint.lint_listing(insts, "t")
+    assert (not bad) == ok, bad
+
+
+def test_built_code_objects_have_no_mfma_operand_hazards():
+    sos = sorted((ROOT / "kafka_inferenceengine_amd").glob("_kafka_hip*.so"))
+    if not sos or not isa_lint.OBJDUMP.exists():
+        pytest.skip("extension not built or llvm-objdump missing")
+    for so in sos:
+        n, bad = isa_lint.lint_so(so)
+        assert n > 0, f"{so.name}: no MFMA instructions found (matrix-core GP not compiled?)"
+        assert not bad, bad[:5]

@@ -4,6 +4,7 @@ import datetime as dt
 import os
 
 import numpy as np
+import pytest
 import torch
 
 import kafka_inferenceengine_amd as k
@@ -335,3 +336,60 @@ def test_reproject_utm_to_wgs84_golden(tmp_path):
     out = reproject_image(ramp, [0, 1, 0, 0, 0, -1], (40, 40), [5.25, 1, 0, -5.5, 0, -1], resampling="bilinear")
     rr, cc = np.meshgrid(np.arange(40) + 5.5 + 0.5 - 0.5, np.arange(40) + 5.25 + 0.5 - 0.5, indexing="ij")
     assert np.allclose(out[:-2, :-2], (rr + 2 * cc)[:-2, :-2], atol=1e-4)
+
+
+def _ifd_entries(b):
+    """{tag: (entry offset, type, count, value-or-offset)} of a classic little-endian TIFF."""
+    import struct
+    assert b[:2] == b"II" and struct.unpack("<H", b[2:4])[0] == 42
+    ifd = struct.unpack("<I", b[4:8])[0]
+    n = struct.unpack("<H", b[ifd:ifd + 2])[0]
+    out = {}
+    for i in range(n):
+        o = ifd + 2 + 12 * i
+        tag, typ, cnt, val = struct.unpack("<HHII", b[o:o + 12])
+        out[tag] = (o, typ, cnt, val)
+    return out
+
+
+def test_native_reader_rejects_bad_inputs(tmp_path):
+    """the native reader must refuse (not overflow, zero-fill or
+    index out of range on) a sample-size mismatch, a truncated DEFLATE stream,
+    a chunk outside the file and a scalar tag without a value."""
+    import struct
+    from kafka_inferenceengine_amd.input_output.streaming import RasterIngest
+    rng = np.random.default_rng(5)
+    f32 = rng.random((64, 80)).astype(np.float32)
+    p = tmp_path / "f32.tif"
+    k.write_tiff(p, f32, compress="deflate")
+    # 1. float32 file into an int16 ingest plane: refused, not a 2x overflow
+    ing = RasterIngest(1, (64, 80), torch.int16, "cpu")
+    with pytest.raises(RuntimeError, match="32-bit.*16-bit"):
+        ing.acquire("d0", [(p, 0, (0, 64, 0, 80))])
+    assert np.array_equal(k.read_tiff(p)[0], f32)
+    b = bytearray(p.read_bytes())
+    ent = _ifd_entries(bytes(b))
+    cnt_tag = 325 if 325 in ent else 279
+    o, typ, cnt, val = ent[cnt_tag]
+    # 2. first chunk's byte count cut in half: inflate stops short (Z_BUF_ERROR)
+    bc_off = o + 8 if cnt == 1 else val
+    first = struct.unpack("<I", b[bc_off:bc_off + 4])[0]
+    bad = bytearray(b)
+    bad[bc_off:bc_off + 4] = struct.pack("<I", first // 2)
+    (tmp_path / "trunc.tif").write_bytes(bytes(bad))
+    with pytest.raises(RuntimeError, match="inflate failed"):
+        k.read_tiff(tmp_path / "trunc.tif")
+    # 3. a chunk that runs past the end of the file
+    bad = bytearray(b)
+    bad[bc_off:bc_off + 4] = struct.pack("<I", len(b) + 10)
+    (tmp_path / "past.tif").write_bytes(bytes(bad))
+    from kafka_inferenceengine_amd.input_output.tiff import tiff_info
+    with pytest.raises(RuntimeError, match="outside the file"):
+        tiff_info(tmp_path / "past.tif")
+    # 4. a scalar tag (Compression) with count 0
+    o, typ, cnt, val = ent[259]
+    bad = bytearray(b)
+    bad[o + 4:o + 8] = struct.pack("<I", 0)
+    (tmp_path / "nocount.tif").write_bytes(bytes(bad))
+    with pytest.raises(RuntimeError, match="no value"):
+        tiff_info(tmp_path / "nocount.tif")
