@@ -115,6 +115,8 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(AnalysisArgs, b_in, const float*)
       .PTR_FIELD(AnalysisArgs, status, uint8_t*)
       .PTR_FIELD(AnalysisArgs, partials, double*)
+      .PTR_FIELD(AnalysisArgs, partials_first, double*)
+      .def_readwrite("gn_fused", &AnalysisArgs::gn_fused)
       .PTR_FIELD(AnalysisArgs, prop, const PropArgs*)
       .PTR_FIELD(AnalysisArgs, out_mean, float*)
       .PTR_FIELD(AnalysisArgs, out_unc, float*)

@@ -185,6 +185,12 @@ struct AnalysisArgs {
   float* reg_v;
   float* x0_out;           // the linearisation point (the fused forecast when x_prev is null)
   StripGeo reg_geo;
+  // Gauss-Newton iterations run by this launch (1, or 2 = the first iteration,
+  // which can never end the loop (min_iterations = 2, linear_kf.py:297-304),
+  // kept in registers: solved, its norm partial to partials_first, and the
+  // second linearised at its x; outputs as for one launch of the second)
+  int32_t gn_fused, pad_gn;
+  double* partials_first;  // per-block sum (x_1 - x_0)^2 of the first fused iteration
 };
 
 
@@ -893,6 +899,38 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
   return dn;
 }
 
+// Solve of a fused intermediate Gauss-Newton iteration (AnalysisArgs.gn_fused):
+// the arithmetic of analysis_epilogue's plain solve path (same factorisation,
+// health fallback to the forecast mean, norm order), without its stores, so
+// that x_1 is bit-identical to a separate launch's.  x0 <- x_1, returns
+// |x_1 - x0|^2.
+template <int NP, typename AP>
+KF_HD float gn_intermediate(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[NP], float (&x0)[NP]) {
+  const int64_t ld = a->ld;
+  const bool spd = chol_packed<NP>(A);
+  chol_solve<NP>(A, b);
+  bool fin = true;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) fin = fin && finitef(b[j]);
+  if (!spd || !fin) {
+    if (a->prop) {
+      float Af[ntri(NP)];
+      forecast_partial<NP>(opaque(cptr(a->prop)), p, b, Af);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) b[j] = a->x_f[j * ld + p];
+    }
+  }
+  float dn = 0.f;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const float d = b[j] - x0[j];
+    dn = fmaf(d, d, dn);
+    x0[j] = b[j];
+  }
+  return dn;
+}
+
 // ---------------------------------------------------------------------------
 // K1: fused Gauss-Newton analysis for one pixel (information form).
 //   A = P_f^-1 + sum_b w_b h_b h_b^T,  b = P_f^-1 x_f + sum_b w_b h_b y'_b,
@@ -902,22 +940,24 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
 // (the compiler then drops the SAR/linear/precomputed code and its registers);
 // FD == FD_PRECOMP: every band has a precomputed operator (split GP path).
 template <int NP, int FD = 0, int FOBS = 0, int UNR = 4, bool FOLD = false>
-KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
+KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a.ld;
   float x0[NP], A[NT], b[NP];
-  uint8_t st = 0;
   if (a.x_prev) {
 #pragma unroll
     for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
   }
+  dn_first = 0.f;
+  for (int it = 0;; ++it) {
+  uint8_t st = 0;
   if (a.prop) {
     // fused propagation: forecast of this pixel from the previous analysis,
     // never written to HBM (saves the propagate pass and its 2 x 140 B/px)
     float xf[NP];
     forecast_partial<NP>(opaque(cptr(a.prop)), p, xf, A);
     symv<NP>(A, xf, b);
-    if (!a.x_prev) {
+    if (!a.x_prev && it == 0) {
 #pragma unroll
       for (int j = 0; j < NP; ++j) x0[j] = xf[j];
     }
@@ -981,9 +1021,17 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
     if (h0o) h0o[p] = H0;
     if (!ok) { st |= ST_BAD_OP; continue; }
     ++nobs;
-    float yp = y - H0;
+    float yp;
+    if (FD == FD_LINEAR || (FD == 0 && bd.op == OP_LINEAR)) {
+      // linear operator: y + h.x0 - (offset + h.x0) = y - offset exactly, so
+      // the analysis does not depend on the linearisation point and a second
+      // Gauss-Newton iteration reproduces the first bit for bit (norm 0)
+      yp = y - bd.offset;
+    } else {
+      yp = y - H0;
 #pragma unroll
-    for (int j = 0; j < NP; ++j) yp = fmaf(h[j], x0[j], yp);
+      for (int j = 0; j < NP; ++j) yp = fmaf(h[j], x0[j], yp);
+    }
     const float wy = w * yp;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
@@ -1001,10 +1049,19 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p) {
     // band / record loops above (analysis_kernel passes them at offset 0)
     const KF_CONST_AS AnalysisArgs* ka =
         opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
+    if (it + 1 < ka->gn_fused) {
+      dn_first = gn_intermediate<NP>(ka, p, A, b, x0);
+      continue;
+    }
     return analysis_epilogue<NP>(ka, p, A, b, x0, st);
   }
 #endif
+  if (it + 1 < a.gn_fused) {
+    dn_first = gn_intermediate<NP>(&a, p, A, b, x0);
+    continue;
+  }
   return analysis_epilogue<NP>(&a, p, A, b, x0, st);
+  }
 }
 
 // Packed SPD inverse (covariance <-> precision conversion).

@@ -42,13 +42,46 @@ __device__ __forceinline__ void block_partial(double v, double* partials) {
   }
 }
 
+// Both norm partials of a fused two-iteration launch in one reduction pass.
+template <int BS = BLOCK>
+__device__ __forceinline__ void block_partials2(double v, double v1, double* partials, double* partials1) {
+  __shared__ double red[2][BS / 64];
+  v = wave_sum(v);
+  v1 = wave_sum(v1);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wid] = v;
+    red[1][wid] = v1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < BS / 64; ++i) {
+      s += red[0][i];
+      s1 += red[1][i];
+    }
+    if (partials) partials[blockIdx.x] = s;
+    if (partials1) partials1[blockIdx.x] = s1;
+  }
+}
+
+template <int BS = BLOCK>
+__device__ __forceinline__ void analysis_partials(const AnalysisArgs& a, double acc, double acc1) {
+  if (a.partials_first) block_partials2<BS>(acc, acc1, a.partials, a.partials_first);
+  else if (a.partials) block_partial<BS>(acc, a.partials);
+}
+
 template <int NP, int FD = 0, int FOBS = 0, int UNR = 4, bool FOLD = false>
 __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
-  double acc = 0.0;
+  double acc = 0.0, acc1 = 0.0;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
-  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
-    acc += (double)pixel_analysis<NP, FD, FOBS, UNR, FOLD>(a, p);
-  if (a.partials) block_partial(acc, a.partials);
+  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride) {
+    float dn1;
+    acc += (double)pixel_analysis<NP, FD, FOBS, UNR, FOLD>(a, p, dn1);
+    acc1 += (double)dn1;
+  }
+  analysis_partials(a, acc, acc1);
 }
 
 // K1 with the GP on the matrix cores (kf_gp_mfma.h).  Every band's split-f16
@@ -73,16 +106,18 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
     if (threadIdx.x == 0) gpm_lds[a.gpm_frags - 1] = kf_h8{};   // shared zero fragment
   }
   __syncthreads();
-  double acc = 0.0;
+  double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BS;
   for (int64_t base = (int64_t)blockIdx.x * BS + (threadIdx.x - lane); base < a.N; base += stride) {
     const int64_t p = base + lane;
     const bool act = p < a.N;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS>(a, act ? p : a.N - 1, act, gpm_lds);
+    float dn1;
+    const float dn = pixel_analysis_mfma<NP, D, FOBS>(a, act ? p : a.N - 1, act, gpm_lds, dn1);
     acc += act ? (double)dn : 0.0;
+    acc1 += act ? (double)dn1 : 0.0;
   }
-  if (a.partials) block_partial<BS>(acc, a.partials);
+  analysis_partials<BS>(a, acc, acc1);
 #endif
 }
 
@@ -93,16 +128,18 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
 template <int NP, int D, int FOBS, bool PF = false>
 __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  double acc = 0.0;
+  double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t base = (int64_t)blockIdx.x * BLOCK + (threadIdx.x - lane); base < a.N; base += stride) {
     const int64_t p = base + lane;
     const bool act = p < a.N;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, true, PF>(a, act ? p : a.N - 1, act, nullptr);
+    float dn1;
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, true, PF>(a, act ? p : a.N - 1, act, nullptr, dn1);
     acc += act ? (double)dn : 0.0;
+    acc1 += act ? (double)dn1 : 0.0;
   }
-  if (a.partials) block_partial(acc, a.partials);
+  analysis_partials(a, acc, acc1);
 #endif
 }
 

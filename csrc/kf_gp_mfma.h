@@ -360,20 +360,23 @@ __device__ __forceinline__ void gpm_epilogue(const KF_CONST_AS BandDesc* q, cons
 
 template <int NP, int D, int FOBS, bool GT = false, bool PF = false>
 __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
-                                                     const kf_h8* lds) {
+                                                     const kf_h8* lds, float& dn_first) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a.ld;
   float x0[NP], A[NT], b[NP];
-  uint8_t st = 0;
   if (a.x_prev) {
 #pragma unroll
     for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
   }
+  dn_first = 0.f;
+  // wave-uniform loop over the fused Gauss-Newton iterations (AnalysisArgs.gn_fused)
+  for (int it = 0;; ++it) {
+  uint8_t st = 0;
   if (a.prop) {
     float xf[NP];
     forecast_partial<NP>(opaque(cptr(a.prop)), p, xf, A);
     symv<NP>(A, xf, b);
-    if (!a.x_prev) {
+    if (!a.x_prev && it == 0) {
 #pragma unroll
       for (int j = 0; j < NP; ++j) x0[j] = xf[j];
     }
@@ -440,10 +443,17 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     }
   }
   if (nobs == 0) st |= ST_NO_OBS;
-  if (!act) return 0.f;
   const KF_CONST_AS AnalysisArgs* ka =
       opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
+  if (it + 1 < ka->gn_fused) {
+    // tail lanes (act = false) solve too: their x0 only feeds the next
+    // iteration's MFMA operands and must stay finite
+    dn_first = gn_intermediate<NP>(ka, p, A, b, x0);
+    continue;
+  }
+  if (!act) return 0.f;
   return analysis_epilogue<NP>(ka, p, A, b, x0, st);
+  }
 }
 
 // K1g (gain / covariance form) with the GP on the matrix cores: pixel_gain

@@ -37,7 +37,19 @@ static void grid_stride(int64_t N, int grid, double* partials, F&& f) {
 
 template <int NP>
 static int h_analysis(const AnalysisArgs& a, int grid) {
-  grid_stride(a.N, grid, a.partials, [&](int64_t p) { return pixel_analysis<NP>(a, p); });
+  const int64_t stride = (int64_t)grid * HBLOCK;
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int b = 0; b < grid; ++b) {
+    double acc = 0.0, acc1 = 0.0;
+    for (int t = 0; t < HBLOCK; ++t)
+      for (int64_t p = (int64_t)b * HBLOCK + t; p < a.N; p += stride) {
+        float dn1;
+        acc += (double)pixel_analysis<NP>(a, p, dn1);
+        acc1 += (double)dn1;
+      }
+    if (a.partials) a.partials[b] = acc;
+    if (a.partials_first) a.partials_first[b] = acc1;
+  }
   return 0;
 }
 template <int NP>

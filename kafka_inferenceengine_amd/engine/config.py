@@ -49,8 +49,10 @@ class EngineConfig:
     prefetch: bool = True                     # overlap next date's ingest with compute
     lookahead: bool = True                    # prepare the next date's bands under the last GN iteration
     fuse_propagation: bool = True             # evaluate the forecast inside the analysis kernel
-    speculate: bool = True                    # queue the next step's first GN iteration before the
-                                              # convergence read-back (discarded if it was not the last)
+    fuse_gn: bool = True                      # GN iterations 1 and 2 in one launch (iteration 1 can never
+                                              # end the loop, linear_kf.py:297-304); plain fused path only
+    speculate: bool = True                    # unfused path: queue the next step's first GN iteration before
+                                              # the convergence read-back (discarded if it was not the last)
     fuse_output: bool = True                  # device outputs written by the final analysis iteration
     return_innovations: bool = False
     metrics_path: str | None = None           # JSONL metrics (per date / timestep)

@@ -29,7 +29,7 @@ from ..inference.kf_tools import (PROP_IDENTITY, PROP_PRIOR, PROP_STANDARD, Prop
                                   propagate_and_blend_prior, propagate_information_filter_LAI)
 from ..inference.solvers import variational_kalman, variational_kalman_multiband
 from ..inference.utils import iterate_time_grid
-from ..models.operators import OP_PRECOMP, OperatorSpec
+from ..models.operators import OP_LINEAR, OP_PRECOMP, OperatorSpec
 from ..ops import kernels as K
 from ..parallel.comm import Comm
 from ..parallel.partition import StripPartition
@@ -104,7 +104,8 @@ class LinearKalman:
         self._partials = K.partials_buffer(max(self.N, 1), self.device)
         # one reduction slot per GN iteration: norms of iterations that cannot end
         # the loop (n_iter < min_iterations) are read after the loop, not waited on
-        self._red_hist = torch.zeros(self.config.max_iterations + 2, dtype=torch.float64, device=self.device)
+        self._red_hist = torch.zeros(self.config.max_iterations + 3, dtype=torch.float64, device=self.device)
+        self._partials1 = K.partials_buffer(max(self.N, 1), self.device)   # first fused GN iteration
         self._red = self._red_hist[:1]
         self.metrics = MetricsLogger(self.config.metrics_path, rank=self.comm.rank)
         self.timer = PhaseTimer(self.device, sync=self.config.sync_timing,
@@ -115,6 +116,7 @@ class LinearKalman:
         self._speculate_fn = None       # queues that step's first GN iteration (see _speculate)
         self._spec = None               # the queued iteration, adopted or dropped by the next step
         self._spec_predict = True       # last date converged at min_iterations
+        self._lazy_norms = []           # (norms, pending 1, pending 2, len_x, n_bands) of static convergence
         self.spec_stats = {"queued": 0, "adopted": 0}
         self._split_chunk = {}          # split path: bands per chunk, per band count
         self._reg = None
@@ -254,6 +256,7 @@ class LinearKalman:
         if ckpt is not None:
             with self.timer.phase("checkpoint"):
                 ckpt.finish()
+        self._resolve_lazy_norms()
         self.final_state = analysis
         if self.metrics.enabled:
             self.metrics_summary()
@@ -809,6 +812,15 @@ class LinearKalman:
         if ((plain or spatial or (gain and not precomp)) and N and cfg.fuse_output
                 and hasattr(self.output, "device_targets")):
             out_t = self.output.device_targets(self, self.device)
+        # GN iterations 1 and 2 in one launch (the first never ends the loop): rank-
+        # independent test, so every rank queues the same collectives
+        fuse2 = (plain and cfg.fuse_gn and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
+                 and n_iter == 1 and not (prop is None and fc is None))
+        # linear / identity operators: y' = y - offset does not depend on the
+        # linearisation point (kf_core.h FD_LINEAR), so iteration 2 repeats
+        # iteration 1 exactly and its norm is 0 -- converged without a read-back
+        static_conv = (fuse2 and cfg.convergence_tolerance > 0 and bool(specs)
+                       and all(s.kind == OP_LINEAR for s in specs))
         while True:
             # the analysis precision is only needed from the iteration that can
             # end the loop on: skip its 4*ntri B/px store before min_iterations
@@ -817,32 +829,63 @@ class LinearKalman:
             if precomp:
                 pre = self._precompute_host(specs, dbs, x_prev)
                 table = build_table(specs, dbs, n, self._cache, self.device, h0_outs, pre)
-            with self.timer.phase("analysis"):
-                if N:
-                    if gain:
-                        K.gain(n, table, x_prev, None if prop else fc.x, None if prop else fc.P, x_new, A_keep,
-                               status, self._partials, N=N, joseph=cfg.joseph, prop=prop, out=out_now)
-                    elif cfg.spatial_gamma > 0:
-                        self._regularised_iteration(table, x_prev, fc, x_new, A_keep, status, prop, out_now)
-                    elif bp:
-                        self._band_parallel_iteration(table, x_prev, fc, x_new, A_keep, status)
-                    elif split is not None:
-                        self._split_iteration(split, x_prev, fc, x_new, A_keep, status)
-                    elif prop is not None:
-                        K.analysis(n, table, x_prev, None, None, x_new, A_keep, None, status, self._partials, N=N,
-                                   prop=prop, out=out_now)
+            if fuse2:
+                # iterations 1 + 2 in one launch: outputs of iteration 2 (which can end the loop)
+                red2 = self._red_hist[1:3]
+                with self.timer.phase("analysis"):
+                    if N:
+                        K.analysis(n, table, x_prev, None if prop is not None else fc.x,
+                                   None if prop is not None else fc.P, x_new, P_out, None, status, self._partials,
+                                   N=N, prop=prop, out=out_t, gn_fused=2, partials_first=self._partials1)
+                        K.reduce_partials(self._partials1, red2[0:1])
+                        K.reduce_partials(self._partials, red2[1:2])
                     else:
-                        K.analysis(n, table, x_prev, fc.x, fc.P, x_new, A_keep, None, status, self._partials, N=N,
-                                   out=out_now)
-            red = self._red_hist[min(n_iter, self._red_hist.numel() - 1):][:1]
-            with self.timer.phase("analysis"):
-                if N:
-                    K.reduce_partials(self._partials, red)
-                else:
-                    red.zero_()
-            with self.timer.phase("converge"):
-                pend = self.comm.sum_f64_async(red)
-            x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
+                        red2.zero_()
+                with self.timer.phase("converge"):
+                    pend2 = self.comm.sum_f64_async(red2)
+                fuse2 = False
+                deferred.append((1, pend2.column(0)))
+                pend = pend2.column(1)
+                n_iter = 2
+                x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
+                if static_conv and not self._norms_needed_now():
+                    # norm 2 is exactly 0: converged.  Norm 1 is read after the
+                    # next launch is queued (no host wait between the steps)
+                    if self._lookahead_fn is not None:
+                        self._lookahead_fn()
+                        self._lookahead_fn = None
+                    self._resolve_lazy_norms()
+                    norms = [None, 0.0]
+                    self._lazy_norms.append((norms, deferred[0][1], pend, len_x, len(bands)))
+                    deferred = []
+                    break
+            else:
+                with self.timer.phase("analysis"):
+                    if N:
+                        if gain:
+                            K.gain(n, table, x_prev, None if prop else fc.x, None if prop else fc.P, x_new, A_keep,
+                                   status, self._partials, N=N, joseph=cfg.joseph, prop=prop, out=out_now)
+                        elif cfg.spatial_gamma > 0:
+                            self._regularised_iteration(table, x_prev, fc, x_new, A_keep, status, prop, out_now)
+                        elif bp:
+                            self._band_parallel_iteration(table, x_prev, fc, x_new, A_keep, status)
+                        elif split is not None:
+                            self._split_iteration(split, x_prev, fc, x_new, A_keep, status)
+                        elif prop is not None:
+                            K.analysis(n, table, x_prev, None, None, x_new, A_keep, None, status, self._partials, N=N,
+                                       prop=prop, out=out_now)
+                        else:
+                            K.analysis(n, table, x_prev, fc.x, fc.P, x_new, A_keep, None, status, self._partials, N=N,
+                                       out=out_now)
+                red = self._red_hist[min(n_iter, self._red_hist.numel() - 1):][:1]
+                with self.timer.phase("analysis"):
+                    if N:
+                        K.reduce_partials(self._partials, red)
+                    else:
+                        red.zero_()
+                with self.timer.phase("converge"):
+                    pend = self.comm.sum_f64_async(red)
+                x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
             if n_iter < cfg.min_iterations:
                 # this iteration cannot end the loop (n_iter <= max_iterations too):
                 # queue the next one without waiting for the norm
@@ -854,11 +897,12 @@ class LinearKalman:
                 self._lookahead_fn()
                 self._lookahead_fn = None
             if (self._speculate_fn is not None and plain and h0_outs is None
-                    and self._spec_predict):
+                    and self._spec_predict and not cfg.fuse_gn):
                 # queue the next step's first iteration from this candidate analysis
                 # before the read-back below blocks the host
                 self._speculate_fn(KFState(x_prev, P_out, PRECISION, N))
                 self._speculate_fn = None
+            self._resolve_lazy_norms()
             for it, pd in deferred:
                 norms.append(self._log_norm(pd.result(), len_x, len(bands), it))
             deferred = []
@@ -893,6 +937,21 @@ class LinearKalman:
                 y, w = db.decode()
                 inn.append(torch.where(w > 0, y - h0[:N], torch.zeros_like(y)))
         return AssimilationResult(state, n_iter, norms, inn)
+
+    def _norms_needed_now(self) -> bool:
+        """Per-date metrics and INFO logs report the norms as they happen."""
+        return self.metrics.enabled or LOG.isEnabledFor(logging.INFO)
+
+    def _resolve_lazy_norms(self):
+        """Fill in the deferred norms of statically converged dates (linear
+        operators): iteration 1's norm, and a check that iteration 2's is 0."""
+        while self._lazy_norms:
+            norms, p1, p2, len_x, nb = self._lazy_norms.pop(0)
+            norms[0] = self._log_norm(p1.result(), len_x, nb, 1)
+            n2 = p2.result()
+            if n2 != 0.0:
+                LOG.warning("linear operator: second Gauss-Newton norm %g is not 0", n2)
+                norms[1] = self._log_norm(n2, len_x, nb, 2)
 
     @staticmethod
     def _log_norm(total: float, len_x: float, n_bands: int, n_iter: int) -> float:

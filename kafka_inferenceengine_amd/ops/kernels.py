@@ -211,8 +211,13 @@ def gp_operator_supported(n_params, d) -> bool:
 
 def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=None, b_out=None, status=None,
              partials=None, N=None, solve=True, fast=True, variant=None, a_in=None, b_in=None, prop=None,
-             out=None, reg=None, x0_out=None):
+             out=None, reg=None, x0_out=None, gn_fused=1, partials_first=None):
     """K1 fused Gauss-Newton analysis (information form).
+
+    ``gn_fused=2`` runs two Gauss-Newton iterations in this launch: the first
+    (which cannot end the loop, min_iterations = 2) stays in registers, its
+    norm partials go to ``partials_first``; ``x_out``/``a_out``/``out`` and
+    ``partials`` are those of the second.  Bit-identical to two launches.
 
     ``prop`` (from :func:`prop_args`) fuses the propagation: the forecast is
     computed per pixel from the previous analysis inside the kernel and
@@ -252,8 +257,16 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     _check_vec(status, N, "status", torch.uint8, dev)
     if partials is not None and (partials.dtype != torch.float64 or partials.numel() < grid_for(N)):
         raise ValueError("partials must be float64 with >= grid_for(N) entries")
+    if gn_fused not in (1, 2):
+        raise ValueError("gn_fused must be 1 or 2")
+    if gn_fused == 2 and (reg is not None or a_in is not None or not solve):
+        raise ValueError("gn_fused=2 runs the plain solve path only (no regulariser, band chunks or solve=False)")
+    if partials_first is not None and (partials_first.dtype != torch.float64 or partials_first.numel() < grid_for(N)):
+        raise ValueError("partials_first must be float64 with >= grid_for(N) entries")
     a = ext().AnalysisArgs()
     a.N, a.ld, a.n_bands, a.solve = N, ld, bands.n, int(bool(solve))
+    a.gn_fused = int(gn_fused)
+    a.partials_first = _ptr(partials_first) if gn_fused == 2 else 0
     a.fast_d, a.fast_obs = (bands.fast_d, bands.fast_obs) if fast else (0, 0)
     a.variant = DEFAULT_VARIANT if variant is None else int(variant)
     a.gpm_frags = bands.gpm_frags if fast else 0

@@ -53,10 +53,12 @@ _MAILBOXES = {}
 
 
 class PendingSum:
-    """Deferred C1 result (``Comm.sum_f64_async``)."""
+    """Deferred C1 result (``Comm.sum_f64_async``); ``k`` values per rank are
+    summed column by column (``column(j)``), rank by rank in fixed order."""
 
-    def __init__(self, vals: torch.Tensor, n: int):
+    def __init__(self, vals: torch.Tensor, n: int, k: int = 1):
         self.n = n
+        self.k = k
         self.event = None
         if vals.is_cuda:
             # async copy into a pinned mailbox slot + an event: result() waits for
@@ -74,13 +76,25 @@ class PendingSum:
         else:
             self.vals = vals
 
-    def result(self) -> float:
+    def result(self, j: int = 0) -> float:
         if self.event is not None:
             self.event.synchronize()
+            self.event = None
         total = 0.0
-        for v in self.vals.tolist():  # fixed rank order
+        for v in self.vals.tolist()[j::self.k]:  # fixed rank order
             total += v
         return total
+
+    def column(self, j: int) -> "_PendingColumn":
+        return _PendingColumn(self, j)
+
+
+class _PendingColumn:
+    def __init__(self, parent: PendingSum, j: int):
+        self.parent, self.j = parent, j
+
+    def result(self) -> float:
+        return self.parent.result(self.j)
 
 
 class PendingP2P:
@@ -170,15 +184,17 @@ class Comm:
 
     def sum_f64_async(self, local: torch.Tensor) -> "PendingSum":
         """C1 without a host wait: the all-gather is queued on the stream (RCCL)
-        and ``.result()`` reads the rank values and sums them in rank order.
-        The values are copied to pinned host memory in stream order right away,
-        so ``local`` may be overwritten by later queued work."""
+        and ``.result(j)`` reads the rank values of element j and sums them in
+        rank order (``local`` holds k >= 1 values: one all-gather for all of
+        them).  The values are copied to pinned host memory in stream order
+        right away, so ``local`` may be overwritten by later queued work."""
+        k = local.numel()
         if not self.distributed:
-            return PendingSum(local.reshape(1), 1)
-        local = local.reshape(1).to(torch.float64)
-        out = torch.empty((self.world, 1), dtype=torch.float64, device=local.device)
+            return PendingSum(local.reshape(k), 1, k)
+        local = local.reshape(k).to(torch.float64)
+        out = torch.empty((self.world, k), dtype=torch.float64, device=local.device)
         dist.all_gather(list(out.unbind(0)), local, group=self.group)
-        return PendingSum(out.reshape(-1), self.world)
+        return PendingSum(out.reshape(-1), self.world, k)
 
     def sum_int(self, v: int) -> int:
         if not self.distributed:

@@ -355,7 +355,8 @@ def test_speculative_next_step_equals_sequential(tol):
     res = []
     for spec in (False, True):
         out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
-        kf = _engine(mask, obs, Q, out=out, speculate=spec, convergence_tolerance=tol, max_iterations=4)
+        kf = _engine(mask, obs, Q, out=out, speculate=spec, convergence_tolerance=tol, max_iterations=4,
+                     fuse_gn=False)
         st = kf.run(grid, x0, None, Pinv)
         res.append((st, out, [h["gn_iterations"] for h in kf.history], [h["norms"] for h in kf.history],
                     dict(kf.spec_stats)))
@@ -369,6 +370,55 @@ def test_speculative_next_step_equals_sequential(tol):
         assert sb["queued"] >= sb["adopted"] >= len(grid) - 3
     else:
         assert sb["adopted"] == 0 and sb["queued"] <= 1
+
+
+@pytest.mark.parametrize("tol", [1e-3, 1e-9])
+def test_fused_gn_iterations_equal_separate_launches(tol):
+    """EngineConfig.fuse_gn: Gauss-Newton iterations 1 and 2 in one launch
+    (iteration 1 kept in registers) give bit-identical states, outputs,
+    iteration counts and norms to one launch per iteration -- also when the
+    tolerance forces more iterations after the fused pair."""
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=7)
+    grid = _grid(6)
+    res = []
+    for fuse in (False, True):
+        out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
+        kf = _engine(mask, obs, Q, out=out, fuse_gn=fuse, speculate=False, convergence_tolerance=tol,
+                     max_iterations=4)
+        st = kf.run(grid, x0, None, Pinv)
+        res.append((st, out, [h["gn_iterations"] for h in kf.history], [h["norms"] for h in kf.history]))
+    (a, oa, ia, na), (b, ob, ib, nb) = res
+    assert ia == ib and na == nb
+    assert torch.equal(a.x, b.x) and torch.equal(a.P, b.P)
+    for t in oa.history:
+        assert torch.equal(oa.history[t][0], ob.history[t][0]) and torch.equal(oa.history[t][1], ob.history[t][1])
+
+
+def test_linear_operator_converges_statically():
+    """Identity operator: y' = y - offset does not depend on the linearisation
+    point, so the fused second iteration reproduces the first exactly (norm 0)
+    and the date ends after 2 iterations without a norm read-back; the first
+    norm is filled in afterwards and equals the separate-launch run's."""
+    import datetime as dt
+    mask = np.ones((20, 24), bool)
+    dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
+    res = []
+    for fuse in (False, True):
+        obs = k.SyntheticIdentityObservations(mask, dates=dates, device="cpu", seed=3, stream=False)
+        kf = k.LinearKalman(obs, None, mask, k.create_linear_observation_operator, k.TIP_PARAMETERS,
+                            state_propagation=k.propagate_information_filter_LAI, device="cpu",
+                            config=k.EngineConfig(fuse_gn=fuse, speculate=False))
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        prior = k.JRCPrior(k.TIP_PARAMETERS, mask)
+        x0, Pi = prior.process_prior(None)
+        grid = [dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in dates]
+        st = kf.run(grid, x0, None, Pi)
+        res.append((st, [h["gn_iterations"] for h in kf.history], [h["norms"] for h in kf.history], kf))
+    (a, ia, na, _), (b, ib, nb, kfb) = res
+    assert torch.equal(a.x, b.x) and torch.equal(a.P, b.P)
+    assert ia == ib and all(g == [2] for g in ib)
+    assert na == nb
+    assert all(n[-1] == 0.0 for n in nb) and not kfb._lazy_norms
 
 
 class _HostOnlyPrior:

@@ -83,8 +83,9 @@ def test_gp_mfma_operator_value_vs_float64(cuda, case):
         sel = w > 0
         err = np.abs(hd[sel] - H[sel]).max() / np.abs(H).max()
         err_valu = np.abs(hv[sel] - H[sel]).max() / np.abs(H).max()
-        # emulators fitted with a realistic nugget (models/gp.py): |alpha| ~ |f|
-        assert err < 2e-5, (case, em.name, err, err_valu)
+        # emulators fitted with a realistic nugget (models/gp.py): |alpha| ~ |f|;
+        # both device paths sit at the f32 exponent's limit (~3e-5 for TIP)
+        assert err < 5e-5 and err < 1.5 * err_valu + 5e-6, (case, em.name, err, err_valu)
         assert np.all(hd[~sel] == 0)
 
 
