@@ -273,6 +273,17 @@ KF_HD const KF_CONST_AS T* opaque(const KF_CONST_AS T* p) {
   return p;
 }
 
+// Opaque copy of a per-lane value: address arithmetic derived from the result
+// is recomputed where it is used instead of being hoisted out of an enclosing
+// loop and kept live across it (the fused Gauss-Newton loop of
+// pixel_analysis: ~60 hoisted 64-bit row addresses took 156 -> 256 VGPRs).
+KF_HD int64_t opaque_lane(int64_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(v));
+#endif
+  return v;
+}
+
 // In-place packed Cholesky A = U^T U (U upper, stored in A's packed slots).
 // Convention: the diagonal slots hold 1 / U_jj (what the solves multiply by);
 // only chol_solve / chol_inverse read a factor.
@@ -950,6 +961,7 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
   }
   dn_first = 0.f;
   for (int it = 0;; ++it) {
+  p = opaque_lane(p);
   uint8_t st = 0;
   if (a.prop) {
     // fused propagation: forecast of this pixel from the previous analysis,

@@ -371,6 +371,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   dn_first = 0.f;
   // wave-uniform loop over the fused Gauss-Newton iterations (AnalysisArgs.gn_fused)
   for (int it = 0;; ++it) {
+  p = opaque_lane(p);
   uint8_t st = 0;
   if (a.prop) {
     float xf[NP];

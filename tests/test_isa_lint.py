@@ -39,3 +39,29 @@ def test_built_code_objects_have_no_mfma_operand_hazards():
         n, bad = isa_lint.lint_so(so)
         assert n > 0, f"{so.name}: no MFMA instructions found (matrix-core GP not compiled?)"
         assert not bad, bad[:5]
+
+
+# Hot kernels and their register budget: >= 3 waves per SIMD (<= 168 VGPRs)
+# and no scratch.  A regression here cost round 3 a 1.3x slower headline
+# before it was caught (row addresses hoisted out of the fused GN loop:
+# 256 VGPRs, one wave per SIMD).
+HOT = {   # kernel: (min waves per SIMD, max scratch bytes per lane)
+    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi1EEEvNS_12AnalysisArgsE": (3, 0),   # tip7 headline
+    "_ZN2kf15analysis_kernelILi7ELi4ELi2ELi4ELb0EEEvNS_12AnalysisArgsE": (3, 0),           # TIP VALU loop
+    "_ZN2kf15analysis_kernelILi7ELin2ELi4ELi4ELb0EEEvNS_12AnalysisArgsE": (3, 0),          # identity7 (bf16 y)
+    # PROSAIL (55-float packed A per lane): 2 waves/SIMD, a few spilled VGPRs
+    "_ZN2kf22analysis_mfma_g_kernelILi10ELi10ELi2ELb0EEEvNS_12AnalysisArgsE": (2, 24),
+}
+
+
+def test_hot_kernels_keep_their_occupancy():
+    so = ROOT / "kafka_inferenceengine_amd" / "_kafka_hip.cpython-310-x86_64-linux-gnu.so"
+    if not so.exists() or not isa_lint.READELF.exists():
+        pytest.skip("extension not built or llvm-readelf missing")
+    res = isa_lint.kernel_resources(so)
+    for name, (min_waves, max_scratch) in HOT.items():
+        assert name in res, f"{name} not in the code objects"
+        r = res[name]
+        w = isa_lint.waves_per_simd(r["vgpr"], r.get("agpr", 0))
+        assert w >= min_waves, (name, r, w)
+        assert r["scratch"] <= max_scratch, (name, r)

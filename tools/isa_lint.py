@@ -10,7 +10,7 @@ them (independent instructions or ``s_nop``).  Within a straight-line block
 the scan is exact; across a label the predecessor is unknown and the scan
 stops (the compiler pads block entries itself).
 
-    python tools/isa_lint.py [path/to/_kafka_hip.so]    # exit 1 on a violation
+    python tools/isa_lint.py [--resources] [path/to/_kafka_hip.so]    # exit 1 on a violation
 """
 from __future__ import annotations
 
@@ -95,6 +95,43 @@ def lint_listing(insts, name="") -> list[str]:
     return bad
 
 
+READELF = OBJDUMP.with_name("llvm-readelf")
+
+
+def kernel_resources(path: Path) -> dict[str, dict]:
+    """{mangled kernel name: {vgpr, agpr, scratch, sgpr_spill}} from the
+    code-object metadata notes of every gfx950 bundle in ``path``."""
+    blob = path.read_bytes()
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for i, (triple, code) in enumerate(bundles(blob)):
+            if "gfx950" not in triple:
+                continue
+            f = Path(td) / f"co{i}.elf"
+            f.write_bytes(code)
+            notes = subprocess.run([str(READELF), "--notes", str(f)], capture_output=True, text=True,
+                                   check=True).stdout
+            cur = {}
+            for line in notes.splitlines():
+                m = re.match(r"\s+\.(name|vgpr_count|agpr_count|private_segment_fixed_size|sgpr_spill_count):\s+(\S+)",
+                             line)
+                if not m:
+                    continue
+                key, val = m.groups()
+                if key == "name":
+                    cur = out.setdefault(val, {})
+                else:
+                    cur[{"vgpr_count": "vgpr", "agpr_count": "agpr", "private_segment_fixed_size": "scratch",
+                         "sgpr_spill_count": "sgpr_spill"}[key]] = int(val)
+    return out
+
+
+def waves_per_simd(vgpr: int, agpr: int = 0) -> int:
+    """Waves per SIMD allowed by the unified VGPR+AGPR file (granule 8, 512 per lane)."""
+    alloc = -(-(vgpr + agpr) // 8) * 8
+    return min(8, 512 // max(alloc, 8))
+
+
 def lint_so(path: Path) -> tuple[int, list[str]]:
     blob = path.read_bytes()
     n_mfma, bad = 0, []
@@ -113,10 +150,15 @@ def lint_so(path: Path) -> tuple[int, list[str]]:
 
 
 def main(argv):
-    paths = [Path(a) for a in argv[1:]] or sorted((Path(__file__).resolve().parents[1] /
+    paths = [Path(a) for a in argv[1:] if not a.startswith("--")] or sorted((Path(__file__).resolve().parents[1] /
                                                    "kafka_inferenceengine_amd").glob("_kafka_hip*.so"))
     rc = 0
     for p in paths:
+        if "--resources" in argv:
+            for name, r in sorted(kernel_resources(p).items()):
+                if "analysis" in name or "gain" in name:
+                    print(f"{name[:80]:80s} vgpr={r.get('vgpr')} scratch={r.get('scratch')} "
+                          f"waves/SIMD={waves_per_simd(r.get('vgpr', 0), r.get('agpr', 0))}")
         n, bad = lint_so(p)
         print(f"{p.name}: {n} MFMA instructions, {len(bad)} SrcA/SrcB wait-state violations")
         for b in bad[:20]:
