@@ -780,10 +780,23 @@ KF_HD void pixel_propagate(const PropArgs& a, int64_t p) {
   if (a.status) a.status[p] |= st;
 }
 
+// Full-form right-hand side b = r + A x0 from the correction form r (DELTA).
+template <int NP>
+KF_HD void delta_to_full(const float (&A)[ntri(NP)], const float (&x0)[NP], float (&b)[NP]) {
+  float t[NP];
+  symv<NP>(A, x0, t);
+#pragma unroll
+  for (int j = 0; j < NP; ++j) b[j] += t[j];
+}
+
 // K1 epilogue: store (A, b) if requested, factor and solve, health fallback
 // to the forecast, store x and status; returns |x - x0|^2.  AP is a host or
 // constant-address-space pointer to the launch arguments.
-template <int NP, typename AP>
+// DELTA: b holds the correction form r = P_f^-1 (x_f - x0) + sum w h (y - H0)
+// and x = x0 + A^-1 r (the same analysis as x = A^-1 b with b = r + A x0, but
+// the f32 solve error scales with |x - x0| instead of |x|); b_out and the
+// regulariser get the full form.
+template <int NP, bool DELTA = false, typename AP>
 KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[NP], const float (&x0)[NP],
                               uint8_t st) {
   constexpr int NT = ntri(NP);
@@ -792,6 +805,7 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
 #pragma unroll
     for (int j = 0; j < NP; ++j) a->x0_out[j * ld + p] = x0[j];
   }
+  if (DELTA && (a->reg_v || a->b_out)) delta_to_full<NP>(A, x0, b);
   if (a->reg_v) {
     int deg = 0;
     if (a->reg_geo.w > 0) {
@@ -868,6 +882,10 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
     for (int j = 0; j < NP; ++j) dA[j] = A[tri(NP, j, j)];
     const bool spd = chol_packed<NP>(A);
     chol_solve<NP>(A, b);
+    if (DELTA && !a->b_out) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) b[j] += x0[j];
+    }
     bool fin = true;
 #pragma unroll
     for (int j = 0; j < NP; ++j) fin = fin && finitef(b[j]);
@@ -915,11 +933,15 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
 // health fallback to the forecast mean, norm order), without its stores, so
 // that x_1 is bit-identical to a separate launch's.  x0 <- x_1, returns
 // |x_1 - x0|^2.
-template <int NP, typename AP>
+template <int NP, bool DELTA = false, typename AP>
 KF_HD float gn_intermediate(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[NP], float (&x0)[NP]) {
   const int64_t ld = a->ld;
   const bool spd = chol_packed<NP>(A);
   chol_solve<NP>(A, b);
+  if (DELTA) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) b[j] += x0[j];
+  }
   bool fin = true;
 #pragma unroll
   for (int j = 0; j < NP; ++j) fin = fin && finitef(b[j]);
@@ -950,8 +972,26 @@ KF_HD float gn_intermediate(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[NP
 // FD > 0: fast path where every band is a GP with FD inputs and FOBS encoding
 // (the compiler then drops the SAR/linear/precomputed code and its registers);
 // FD == FD_PRECOMP: every band has a precomputed operator (split GP path).
+// Prior part of the right-hand side: P_f^-1 x_f (full form) or P_f^-1 (x_f - x0)
+// (correction form, DELTA; 0 when linearising at the forecast).
+template <int NP, bool DELTA>
+KF_HD void prior_rhs(const float (&A)[ntri(NP)], const float (&xf)[NP], const float (&x0)[NP], float (&b)[NP]) {
+  if (DELTA) {
+    float d[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) d[j] = xf[j] - x0[j];
+    symv<NP>(A, d, b);
+  } else {
+    symv<NP>(A, xf, b);
+  }
+}
+
+// DELTA (correction form, analysis_epilogue) for the GP and precomputed
+// operators; the linear operators keep the full form, whose y' = y - offset
+// makes a repeated iteration exact (static convergence, linear_kf.py).
 template <int NP, int FD = 0, int FOBS = 0, int UNR = 4, bool FOLD = false>
 KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
+  constexpr bool DELTA = FD > 0 || FD == FD_PRECOMP;
   constexpr int NT = ntri(NP);
   const int64_t ld = a.ld;
   float x0[NP], A[NT], b[NP];
@@ -968,24 +1008,30 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
     // never written to HBM (saves the propagate pass and its 2 x 140 B/px)
     float xf[NP];
     forecast_partial<NP>(opaque(cptr(a.prop)), p, xf, A);
-    symv<NP>(A, xf, b);
     if (!a.x_prev && it == 0) {
 #pragma unroll
       for (int j = 0; j < NP; ++j) x0[j] = xf[j];
     }
+    prior_rhs<NP, DELTA>(A, xf, x0, b);
   } else if (a.a_in) {
     // band-chunked accumulation: continue from a previous chunk's (A, b)
 #pragma unroll
     for (int t = 0; t < NT; ++t) A[t] = a.a_in[t * ld + p];
 #pragma unroll
     for (int j = 0; j < NP; ++j) b[j] = a.b_in[j * ld + p];
+    if (DELTA) {
+      float t[NP];
+      symv<NP>(A, x0, t);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) b[j] -= t[j];
+    }
   } else {
     float xf[NP];
 #pragma unroll
     for (int j = 0; j < NP; ++j) xf[j] = a.x_f[j * ld + p];
 #pragma unroll
     for (int t = 0; t < NT; ++t) A[t] = a.pf_inv[t * ld + p];
-    symv<NP>(A, xf, b);
+    prior_rhs<NP, DELTA>(A, xf, x0, b);
   }
   int nobs = 0;
   for (int bi = 0; bi < a.n_bands; ++bi) {
@@ -1034,7 +1080,9 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
     if (!ok) { st |= ST_BAD_OP; continue; }
     ++nobs;
     float yp;
-    if (FD == FD_LINEAR || (FD == 0 && bd.op == OP_LINEAR)) {
+    if (DELTA) {
+      yp = y - H0;   // correction form: the residual at x0
+    } else if (FD == FD_LINEAR || (FD == 0 && bd.op == OP_LINEAR)) {
       // linear operator: y + h.x0 - (offset + h.x0) = y - offset exactly, so
       // the analysis does not depend on the linearisation point and a second
       // Gauss-Newton iteration reproduces the first bit for bit (norm 0)
@@ -1062,17 +1110,17 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
     const KF_CONST_AS AnalysisArgs* ka =
         opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
     if (it + 1 < ka->gn_fused) {
-      dn_first = gn_intermediate<NP>(ka, p, A, b, x0);
+      dn_first = gn_intermediate<NP, DELTA>(ka, p, A, b, x0);
       continue;
     }
-    return analysis_epilogue<NP>(ka, p, A, b, x0, st);
+    return analysis_epilogue<NP, DELTA>(ka, p, A, b, x0, st);
   }
 #endif
   if (it + 1 < a.gn_fused) {
-    dn_first = gn_intermediate<NP>(&a, p, A, b, x0);
+    dn_first = gn_intermediate<NP, DELTA>(&a, p, A, b, x0);
     continue;
   }
-  return analysis_epilogue<NP>(&a, p, A, b, x0, st);
+  return analysis_epilogue<NP, DELTA>(&a, p, A, b, x0, st);
   }
 }
 

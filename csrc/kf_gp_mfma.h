@@ -373,26 +373,31 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   for (int it = 0;; ++it) {
   p = opaque_lane(p);
   uint8_t st = 0;
+  // correction form throughout (kf_core.h analysis_epilogue, DELTA)
   if (a.prop) {
     float xf[NP];
     forecast_partial<NP>(opaque(cptr(a.prop)), p, xf, A);
-    symv<NP>(A, xf, b);
     if (!a.x_prev && it == 0) {
 #pragma unroll
       for (int j = 0; j < NP; ++j) x0[j] = xf[j];
     }
+    prior_rhs<NP, true>(A, xf, x0, b);
   } else if (a.a_in) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) A[t] = a.a_in[t * ld + p];
 #pragma unroll
     for (int j = 0; j < NP; ++j) b[j] = a.b_in[j * ld + p];
+    float t[NP];
+    symv<NP>(A, x0, t);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) b[j] -= t[j];
   } else {
     float xf[NP];
 #pragma unroll
     for (int j = 0; j < NP; ++j) xf[j] = a.x_f[j * ld + p];
 #pragma unroll
     for (int t = 0; t < NT; ++t) A[t] = a.pf_inv[t * ld + p];
-    symv<NP>(A, xf, b);
+    prior_rhs<NP, true>(A, xf, x0, b);
   }
   int nobs = 0;
   int off = 0;
@@ -430,10 +435,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     if (use && !ok) st |= ST_BAD_OP;
     if (use && ok) {
       ++nobs;
-      float yp = y - H0;
-#pragma unroll
-      for (int j = 0; j < NP; ++j) yp = fmaf(h[j], x0[j], yp);
-      const float wy = w * yp;
+      const float wy = w * (y - H0);   // correction form: the residual at x0
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         const float wh = w * h[i];
@@ -449,11 +451,11 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   if (it + 1 < ka->gn_fused) {
     // tail lanes (act = false) solve too: their x0 only feeds the next
     // iteration's MFMA operands and must stay finite
-    dn_first = gn_intermediate<NP>(ka, p, A, b, x0);
+    dn_first = gn_intermediate<NP, true>(ka, p, A, b, x0);
     continue;
   }
   if (!act) return 0.f;
-  return analysis_epilogue<NP>(ka, p, A, b, x0, st);
+  return analysis_epilogue<NP, true>(ka, p, A, b, x0, st);
   }
 }
 
