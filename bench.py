@@ -84,7 +84,10 @@ def build(cfg_name, a, mask, part, dev, comm):
             else val.lower() in ("1", "true", "yes")
 
     def mkcfg(**kw):
-        return k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel, **{**kw, **over})
+        # phase_timing: hipEvent pairs around each phase on the compute stream
+        # (device time, resolved after the timed region) for the per-rank record
+        return k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel,
+                              phase_timing=not a.no_telemetry, **{**kw, **over})
     if cfg_name in ("tip7", "spatial"):
         dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(n_dates)]
         obs = k.SyntheticBHRObservations(mask, dates=dates, n_train=a.n_train or c["n_train"], partition=part,
@@ -151,6 +154,8 @@ def main():
                     help="override an EngineConfig field (A/B runs), e.g. --set gp_split=never")
     ap.add_argument("--band-parallel", type=int, default=1,
                     help="ranks per band group (strips x band groups; multi-band configs)")
+    ap.add_argument("--no-telemetry", action="store_true",
+                    help="no per-phase hipEvent timers (the per_rank record then has no phase times)")
     a = ap.parse_args()
     if a.watchdog > 0:
         import faulthandler
@@ -209,6 +214,8 @@ def main():
             comm.barrier()
             if dev.type == "cuda":
                 torch.cuda.synchronize()
+            ph0 = kf.timer.cumulative()   # phase totals of the warm-up steps (subtracted below)
+            h2d0 = sum(s.ingest_bytes() for s in srcs)
             t_start = time.perf_counter()
             if a.profile and g_rank == 0:
                 prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
@@ -232,9 +239,27 @@ def main():
     comm.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
-    elapsed = comm.max_float(time.perf_counter() - t_start)
+    t_local = time.perf_counter() - t_start
+    elapsed = comm.max_float(t_local)
     for m in msgs:
         log(m)
+    # per-rank telemetry of the timed steps (device time per phase from the
+    # engine's hipEvent pairs): where a multi-GPU run loses efficiency --
+    # analysis kernels (load), C1 norm all-gather (waits for the slowest rank),
+    # C2 halos, ingest -- gathered to rank 0 after the timed region
+    ph1 = kf.timer.cumulative()
+    phases = {kk: round(v - ph0.get(kk, 0.0), 3) for kk, v in ph1.items()}
+    mine = {"rank": g_rank, "strip_rank": rank, "N": int(part.N), "wall_ms": round(1e3 * t_local, 3),
+            "analysis_ms": phases.get("analysis", 0.0), "c1_ms": phases.get("converge", 0.0),
+            "halo_ms": round(phases.get("halo", 0.0) + phases.get("band_allreduce", 0.0), 3),
+            "ingest_ms": phases.get("ingest", 0.0), "phases_ms": phases,
+            "h2d_bytes": int(sum(s.ingest_bytes() for s in srcs) - h2d0),
+            "gn_iterations": [h.get("gn_iterations") for h in kf.history[a.warmup:]]}
+    per_rank = [mine]
+    if n_ranks > 1:
+        import torch.distributed as dist
+        per_rank = [None] * dist.get_world_size()
+        dist.all_gather_object(per_rank, mine)   # every rank of the job (strips x band groups)
     if hasattr(kf, "cache_stats"):
         log(f"host caches: {kf.cache_stats()}")
     if prof is not None:
@@ -275,6 +300,7 @@ def main():
                           "gn_iterations": gn, "ms_per_gn_iteration": round(1e3 * elapsed / max(1, n_gn), 3),
                           "finite": ok, "fallback_frac": round(fallback, 6), "ingest_bytes_per_step": ingest,
                           "baseline_updates_per_s": c["baseline"]}}
+        rec["per_rank"] = sorted(per_rank, key=lambda r: r["rank"])
         if n_dev != n_ranks:
             rec["rehearsal"] = f"{n_ranks} ranks on {n_dev} device(s): logic rehearsal, not a scaling point"
         print(json.dumps(rec), flush=True)

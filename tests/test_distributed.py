@@ -23,11 +23,11 @@ def _free_port():
     return p
 
 
-def _problem(world, rank, dense=False):
+def _problem(world, rank, dense=False, rows=30):
     import kafka_inferenceengine_amd as k
     from kafka_inferenceengine_amd.parallel import Comm, StripPartition
 
-    mask = np.ones((30, 22), bool)
+    mask = np.ones((rows, 22), bool)
     if not dense:   # dense strips take the index geometry and the overlapped C2 path
         mask[4:9, 3:12] = False
     comm = Comm(rank, world, "cpu") if world > 1 else Comm.single("cpu")
@@ -40,7 +40,10 @@ def _problem(world, rank, dense=False):
 def _run(world, rank, cfg, out_q):
     cfg = dict(cfg)
     dense = cfg.pop("_dense", False)
-    k, mask, comm, part, obs = _problem(world, rank, dense)
+    rows = cfg.pop("_rows", 30)
+    if world > 1:
+        torch.set_num_threads(1)   # 8 ranks on the 8 CPUs
+    k, mask, comm, part, obs = _problem(world, rank, dense, rows)
     kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device="cpu",
                         comm=comm, partition=part, config=k.EngineConfig(**cfg))
     kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
@@ -116,6 +119,24 @@ def test_four_ranks_regularised_halo_equal_one_rank(dense):
     assert [len(a) for a in n1[0]] == [len(a) for a in n4[0]]
 
 
+@pytest.mark.parametrize("cfg", [{"_rows": 48}, {"_rows": 48, "_dense": True, "spatial_gamma": 30.0,
+                                                 "spatial_params": [6], "jacobi_sweeps": 5}],
+                         ids=["tip7-independent", "spatial-dense-halo"])
+def test_eight_ranks_equal_one_rank(cfg):
+    """SURVEY.md §4 tier 3 at the node's full width: 8 strips (6 rows each; the
+    6 interior strips exchange halos with two neighbours) give the 1-rank
+    result and the same global convergence decisions on every rank."""
+    x1, P1, n1 = _gather(1, cfg)
+    x8, P8, n8 = _gather(8, cfg)
+    assert x1.shape == x8.shape
+    assert np.allclose(x1, x8, rtol=1e-5, atol=1e-6)
+    assert np.allclose(P1, P8, rtol=1e-5, atol=1e-3)
+    assert all(n == n8[0] for n in n8[1:])
+    assert [len(a) for a in n1[0]] == [len(a) for a in n8[0]]
+    if cfg.get("_dense"):
+        assert all(c > 0 for c in _gather.overlapped), _gather.overlapped
+
+
 def test_strip_partition_balances_active_pixels():
     from kafka_inferenceengine_amd.parallel import StripPartition
     rng = np.random.default_rng(0)
@@ -145,6 +166,13 @@ def test_bench_torchrun_gloo_two_ranks(extra):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["config"]["finite"]
     assert rec["config"]["fallback_frac"] < 0.01
+    # per-rank telemetry of the timed steps, gathered from every rank of the job
+    pr = rec["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1]
+    for r in pr:
+        assert r["N"] > 0 and r["analysis_ms"] > 0 and r["c1_ms"] >= 0 and r["h2d_bytes"] > 0
+        assert set(r) >= {"analysis_ms", "c1_ms", "halo_ms", "h2d_bytes", "N", "gn_iterations"}
+        assert len(r["gn_iterations"]) == 2
 
 
 def _bp_worker(rank, world, port, B, q):
@@ -178,7 +206,8 @@ def _bp_run(k, comm, StripPartition):
             kf.last_status.numpy().copy())
 
 
-@pytest.mark.parametrize("world,B", [(2, 2), (4, 2)], ids=["1strip-x-2bands", "2strips-x-2bands"])
+@pytest.mark.parametrize("world,B", [(2, 2), (4, 2), (8, 2)],
+                         ids=["1strip-x-2bands", "2strips-x-2bands", "4strips-x-2bands"])
 def test_band_parallel_equals_single_rank(world, B):
     """Band-parallel (TP-like) decomposition: bands split over the ranks of a
     strip, normal equations all-reduced (C5) — same result as one rank."""
