@@ -796,12 +796,17 @@ KF_HD void delta_to_full(const float (&A)[ntri(NP)], const float (&x0)[NP], floa
 // and x = x0 + A^-1 r (the same analysis as x = A^-1 b with b = r + A x0, but
 // the f32 solve error scales with |x - x0| instead of |x|); b_out and the
 // regulariser get the full form.
+// store = false: a fused intermediate Gauss-Newton iteration (AnalysisArgs.
+// gn_fused) -- the same solve and health fallback, x left in b, nothing stored.
+// The fused kernels reach this function from ONE call site for both kinds of
+// iteration, so the intermediate x is bit-identical to a separate launch's
+// (two inlined copies of the solve may be scheduled / contracted differently).
 template <int NP, bool DELTA = false, typename AP>
 KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[NP], const float (&x0)[NP],
-                              uint8_t st) {
+                              uint8_t st, bool store = true) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a->ld;
-  if (a->x0_out) {
+  if (store && a->x0_out) {
 #pragma unroll
     for (int j = 0; j < NP; ++j) a->x0_out[j * ld + p] = x0[j];
   }
@@ -867,11 +872,11 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
     if (a->status) a->status[p] = st;
     return 0.f;
   }
-  if (a->a_out) {
+  if (store && a->a_out) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = A[t];
   }
-  if (a->b_out) {
+  if (store && a->b_out) {
 #pragma unroll
     for (int j = 0; j < NP; ++j) a->b_out[j * ld + p] = b[j];
   }
@@ -902,18 +907,18 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
       }
 #pragma unroll
       for (int j = 0; j < NP; ++j) dA[j] = A[tri(NP, j, j)];
-      if (a->a_out) {
+      if (store && a->a_out) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = A[t];
       }
     }
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      a->x_out[j * ld + p] = b[j];
+      if (store) a->x_out[j * ld + p] = b[j];
       const float d = b[j] - x0[j];
       dn = fmaf(d, d, dn);
     }
-    if (a->out_mean) {
+    if (store && a->out_mean) {
       // fused output dump: the unpack pass's work without re-reading x and A
       const int64_t r = a->out_idx ? a->out_idx[p] : p;
       const int64_t pl = a->out_plane;
@@ -924,43 +929,7 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
       }
     }
   }
-  if (a->status) a->status[p] = st;
-  return dn;
-}
-
-// Solve of a fused intermediate Gauss-Newton iteration (AnalysisArgs.gn_fused):
-// the arithmetic of analysis_epilogue's plain solve path (same factorisation,
-// health fallback to the forecast mean, norm order), without its stores, so
-// that x_1 is bit-identical to a separate launch's.  x0 <- x_1, returns
-// |x_1 - x0|^2.
-template <int NP, bool DELTA = false, typename AP>
-KF_HD float gn_intermediate(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[NP], float (&x0)[NP]) {
-  const int64_t ld = a->ld;
-  const bool spd = chol_packed<NP>(A);
-  chol_solve<NP>(A, b);
-  if (DELTA) {
-#pragma unroll
-    for (int j = 0; j < NP; ++j) b[j] += x0[j];
-  }
-  bool fin = true;
-#pragma unroll
-  for (int j = 0; j < NP; ++j) fin = fin && finitef(b[j]);
-  if (!spd || !fin) {
-    if (a->prop) {
-      float Af[ntri(NP)];
-      forecast_partial<NP>(opaque(cptr(a->prop)), p, b, Af);
-    } else {
-#pragma unroll
-      for (int j = 0; j < NP; ++j) b[j] = a->x_f[j * ld + p];
-    }
-  }
-  float dn = 0.f;
-#pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    const float d = b[j] - x0[j];
-    dn = fmaf(d, d, dn);
-    x0[j] = b[j];
-  }
+  if (store && a->status) a->status[p] = st;
   return dn;
 }
 
@@ -1102,6 +1071,7 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
     }
   }
   if (nobs == 0) st |= ST_NO_OBS;
+  float dn;
 #if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (FD != 0) {
     // fast kernels: re-read the launch arguments from the kernarg segment
@@ -1109,18 +1079,20 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
     // band / record loops above (analysis_kernel passes them at offset 0)
     const KF_CONST_AS AnalysisArgs* ka =
         opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
-    if (it + 1 < ka->gn_fused) {
-      dn_first = gn_intermediate<NP, DELTA>(ka, p, A, b, x0);
-      continue;
-    }
-    return analysis_epilogue<NP, DELTA>(ka, p, A, b, x0, st);
-  }
+    const bool last = it + 1 >= ka->gn_fused;
+    dn = analysis_epilogue<NP, DELTA>(ka, p, A, b, x0, st, last);
+    if (last) return dn;
+  } else
 #endif
-  if (it + 1 < a.gn_fused) {
-    dn_first = gn_intermediate<NP, DELTA>(&a, p, A, b, x0);
-    continue;
+  {
+    const bool last = it + 1 >= a.gn_fused;
+    dn = analysis_epilogue<NP, DELTA>(&a, p, A, b, x0, st, last);
+    if (last) return dn;
   }
-  return analysis_epilogue<NP, DELTA>(&a, p, A, b, x0, st);
+  // fused intermediate iteration: x_1 (left in b) becomes the linearisation point
+  dn_first = dn;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) x0[j] = b[j];
   }
 }
 

@@ -448,14 +448,16 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   if (nobs == 0) st |= ST_NO_OBS;
   const KF_CONST_AS AnalysisArgs* ka =
       opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
-  if (it + 1 < ka->gn_fused) {
-    // tail lanes (act = false) solve too: their x0 only feeds the next
-    // iteration's MFMA operands and must stay finite
-    dn_first = gn_intermediate<NP, true>(ka, p, A, b, x0);
-    continue;
-  }
-  if (!act) return 0.f;
-  return analysis_epilogue<NP, true>(ka, p, A, b, x0, st);
+  // one epilogue call site for the fused intermediate and the final iteration
+  // (bit-identical intermediate x, kf_core.h); tail lanes (act = false) solve
+  // too but store nothing: their x0 only feeds the next iteration's MFMA
+  // operands and must stay finite
+  const bool last = it + 1 >= ka->gn_fused;
+  const float dn = analysis_epilogue<NP, true>(ka, p, A, b, x0, st, last && act);
+  if (last) return act ? dn : 0.f;
+  dn_first = dn;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) x0[j] = b[j];
   }
 }
 
