@@ -57,6 +57,33 @@ def _resolve_device(device):
     return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
 
+def _jacobian_blocks(Hm, N: int, n: int) -> np.ndarray:
+    """SoA Jacobian rows h [n, N] of a reference-protocol operator matrix
+    (``utils.py:197-215``: row i holds pixel i's gradient in columns n*i ..
+    n*i + n - 1), read straight from the sparse triplets -- one vectorised
+    pass instead of per-parameter CSR fancy indexing (which is O(N) Python-
+    level work per parameter and unusable at granule scale).  An entry outside
+    its row's block would couple pixels, which the reference never does
+    (SURVEY.md §0): refused."""
+    if sp.issparse(Hm):
+        coo = Hm.tocoo()
+        r, c, v = coo.row, coo.col, coo.data
+    else:
+        Hd = np.asarray(Hm)
+        r, c = np.nonzero(Hd)
+        v = Hd[r, c]
+    if Hm.shape[0] != N or Hm.shape[1] != N * n:
+        raise ValueError(f"operator matrix {Hm.shape} is not [N, n*N] = [{N}, {N * n}]")
+    pix, par = np.divmod(c.astype(np.int64), n)
+    off = pix != r
+    if off.any() and np.any(v[off] != 0):
+        raise ValueError("operator matrix couples pixels (entries outside the per-pixel blocks)")
+    h = np.zeros((n, N), dtype=np.float64)
+    keep = ~off
+    np.add.at(h, (par[keep], r[keep]), v[keep])   # duplicates (unsummed COO) add up
+    return h
+
+
 class LinearKalman:
     """Iterated (Gauss-Newton) information-form Kalman filter over rasters."""
 
@@ -719,9 +746,7 @@ class LinearKalman:
             else:
                 Hm = H
                 H0 = np.asarray(Hm.dot(x_flat)).ravel()
-            Hm = sp.csr_matrix(Hm)
-            rows = np.arange(self.N)
-            h = np.stack([np.asarray(Hm[rows, rows * self.n_params + j]).ravel() for j in range(self.n_params)])
+            h = _jacobian_blocks(Hm, self.N, self.n_params)
             dev = self.device
             pre.append((torch.from_numpy(np.ascontiguousarray(H0, dtype=np.float32)).to(dev),
                         torch.from_numpy(np.ascontiguousarray(h, dtype=np.float32)).to(dev)))
