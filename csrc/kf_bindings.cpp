@@ -174,6 +174,8 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(JacobiArgs, u, const float*)
       .PTR_FIELD(JacobiArgs, v, float*)
       .PTR_FIELD(JacobiArgs, z_out, float*)
+      .PTR_FIELD(JacobiArgs, z_prev, const float*)
+      .def_readwrite("omega", &JacobiArgs::omega)
       .PTR_FIELD(JacobiArgs, out_mean, float*)
       .PTR_FIELD(JacobiArgs, out_unc, float*)
       .PTR_FIELD(JacobiArgs, out_idx, const int64_t*)

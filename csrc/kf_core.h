@@ -1341,6 +1341,12 @@ struct JacobiArgs {
   float* z_out;          // [k][ld_ext] regularised components (SWEEP writes the local part)
   StripGeo geo;          // dense strip: neighbours from the index (nbr unused)
   int64_t p0, pn;        // pixel range [p0, p0 + pn) of this launch (pn = 0: all N); C2 overlap
+  // Chebyshev acceleration of the sweeps (SWEEP only): z_new = z_prev +
+  // omega (jacobi(z) - z_prev) with the semi-iterative weights of a Jacobi
+  // matrix whose spectrum lies in [-rho, rho] (linear_kf.py); z_prev = null:
+  // the plain Jacobi sweep
+  const float* z_prev;   // [k][ld_ext] the iterate before z (local part)
+  float omega;
   // FINISH only, optional: fused output dump (unpack_kernel's work) of x and
   // 1/sqrt(diag A) with A = a_in (the analysis precision of this iteration)
   float* out_mean;       // [NP][out_plane]
@@ -1434,7 +1440,12 @@ KF_HD float pixel_reg_sweep(const JacobiArgs& a, int64_t p) {
 #pragma unroll
       for (int c = 0; c < NP; ++c)
         if (c < a.k) z = fmaf(a.v[((int64_t)c * NP + j) * ld + p], s[c], z);
-      a.z_out[r * a.ld_ext + p] = fmaf(a.gamma, z, a.u[j * ld + p]);
+      float zn = fmaf(a.gamma, z, a.u[j * ld + p]);
+      if (a.z_prev) {
+        const float zp = a.z_prev[r * a.ld_ext + p];
+        zn = fmaf(a.omega, zn - zp, zp);
+      }
+      a.z_out[r * a.ld_ext + p] = zn;
       ++r;
     }
   }
@@ -1500,6 +1511,10 @@ KF_HD float reg_sweep1(const JacobiArgs& a, int64_t i0, int64_t stride, int64_t 
     pp[u] = a.p0 + (i < n ? i : i0);
     const float s = reg_nsum1(a, pp[u]);
     z[u] = fmaf(a.gamma, a.v[j0 * ld + pp[u]] * s, a.u[j0 * ld + pp[u]]);
+    if (a.z_prev) {
+      const float zp = a.z_prev[pp[u]];
+      z[u] = fmaf(a.omega, z[u] - zp, zp);
+    }
   }
 #pragma unroll
   for (int u = 0; u < U; ++u)

@@ -29,6 +29,13 @@ class EngineConfig:
     # spatial regulariser (new capability, off by default => reference results)
     spatial_gamma: float = 0.0
     spatial_params: list | None = None        # parameter indices smoothed (None: all)
+    # coupled GMRF solve per Gauss-Newton iteration: "chebyshev" (Chebyshev-
+    # accelerated block Jacobi, sweeps chosen from a Gershgorin bound of the
+    # Jacobi spectral radius to cut the error by spatial_tol) or "jacobi"
+    # (exactly jacobi_sweeps plain sweeps, the round-2 smoother)
+    spatial_solver: str = "chebyshev"
+    spatial_tol: float = 1e-3
+    spatial_max_sweeps: int = 64
     jacobi_sweeps: int = 4
     # GP operator placement: fused into the analysis kernel, or "split" (high-
     # occupancy operator kernel -> HBM -> analysis over band chunks)
@@ -70,6 +77,10 @@ class EngineConfig:
             raise ValueError("analysis_form must be 'information' or 'gain'")
         if self.spatial_gamma < 0:
             raise ValueError("spatial_gamma must be >= 0")
+        if self.spatial_solver not in ("chebyshev", "jacobi"):
+            raise ValueError("spatial_solver must be 'chebyshev' or 'jacobi'")
+        if not 0 < self.spatial_tol < 1 or self.spatial_max_sweeps < 1:
+            raise ValueError("spatial_tol must be in (0, 1) and spatial_max_sweeps >= 1")
         if self.spatial_gamma > 0 and self.analysis_form != "information":
             raise ValueError("the spatial regulariser runs in information form")
         if self.band_parallel < 1:

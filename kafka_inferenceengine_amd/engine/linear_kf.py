@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import bisect
 import logging
+import math
 import time
 from collections import namedtuple
 
@@ -144,6 +145,7 @@ class LinearKalman:
         self._spec = None               # the queued iteration, adopted or dropped by the next step
         self._spec_predict = True       # last date converged at min_iterations
         self._lazy_norms = []           # (norms, pending 1, pending 2, len_x, n_bands) of static convergence
+        self._reg_log = []              # per GN iteration of the spatial prior: rho, sweeps, residual
         self.spec_stats = {"queued": 0, "adopted": 0}
         self._split_chunk = {}          # split path: bands per chunk, per band count
         self._reg = None
@@ -569,6 +571,8 @@ class LinearKalman:
             info["norms"].append(res.norms[-1] if res.norms else None)
             rec = {"event": "date", "date": step.isoformat(), "n_iter": res.n_iter, "norms": res.norms,
                    "wall_s": time.perf_counter() - t0, "phases_ms": self.timer.snapshot()}
+            if self._reg_log:
+                rec["spatial"] = self._spatial_record()
             if self.metrics.enabled:
                 rec.update(self._health_metrics(rec["wall_s"]))
             self.metrics.log(rec)
@@ -963,6 +967,20 @@ class LinearKalman:
                 inn.append(torch.where(w > 0, y - h0[:N], torch.zeros_like(y)))
         return AssimilationResult(state, n_iter, norms, inn)
 
+    def _spatial_record(self) -> list:
+        """Per GN iteration of the date: solver, Jacobi bound rho, sweeps and --
+        with metrics on (one read-back + C1 sum) -- the RMS residual of the
+        coupled GMRF system after the sweeps."""
+        out = []
+        for r in self._reg_log:
+            e = {"solver": r["solver"], "rho": round(r["rho"], 6), "sweeps": r["sweeps"]}
+            if self.metrics.enabled:
+                tot = self.comm.sum_f64(r["r2"].reshape(1))
+                e["residual_rms"] = math.sqrt(max(tot, 0.0) / max(1, r["count"]))
+            out.append(e)
+        self._reg_log = []
+        return out
+
     def _norms_needed_now(self) -> bool:
         """Per-date metrics and INFO logs report the norms as they happen."""
         return self.metrics.enabled or LOG.isEnabledFor(logging.INFO)
@@ -1106,31 +1124,75 @@ class LinearKalman:
                    reg=dict(gamma=gamma, mask=reg.reg_mask, v_out=v, nbr=None if geo else reg.nbr, geo=geo),
                    x0_out=None if x_prev is not None else x0_buf)
         nbr = None if geo else reg.nbr
+        rho, sweeps = self._reg_schedule(reg, v, rows, k, gamma, sweeps)
         z = reg.z_buffers(k)
         z[0][:, :N].copy_(x_ref[rows, :N])
         cur = reg.fill_halo(z[0])
-        # C2 overlap on dense strips: the rows the neighbours need first, their
-        # exchange posted, then the interior while the rows are on the wire
-        w = geo["w"] if geo else 0
-        overlap = self.comm.distributed and w > 0 and N > 2 * w
-        for _ in range(sweeps - 1):
-            nxt = z[1] if cur is z[0] else z[0]
+        prev = None
+        omega = 1.0
+        # C2 overlap (dense or masked strips): the rows the neighbours need first,
+        # their exchange posted, then the interior while the rows are on the wire
+        overlap = self.comm.distributed and reg.split is not None
+        sa, sb = reg.split if overlap else (0, 0)
+        for it in range(sweeps - 1):
+            nxt = next(b for b in z if b is not cur and b is not prev)
+            # Chebyshev semi-iterative weights (omega_1 = 1: the first step is Jacobi)
+            if rho > 0 and it > 0:
+                omega = 1.0 / (1.0 - 0.5 * rho * rho) if it == 1 else 1.0 / (1.0 - 0.25 * rho * rho * omega)
+            zp = prev if (rho > 0 and it > 0) else None
             if overlap:
                 with self.timer.phase("reg_boundary"):
-                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(0, w))
-                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(N - w, w))
+                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(0, sa), z_prev=zp,
+                                omega=omega)
+                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(N - sb, sb),
+                                z_prev=zp, omega=omega)
                 with self.timer.phase("halo"):
                     pend = reg.start_fill(nxt)
                 with self.timer.phase("reg_interior"):
-                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(w, N - 2 * w))
+                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(sa, N - sa - sb),
+                                z_prev=zp, omega=omega)
                 with self.timer.phase("halo"):
-                    cur = reg.finish_fill(pend, nxt)
+                    nxt = reg.finish_fill(pend, nxt)
                 self.reg_overlapped_sweeps += 1
             else:
-                K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo)
-                cur = reg.fill_halo(nxt)
+                K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, z_prev=zp, omega=omega)
+                nxt = reg.fill_halo(nxt)
+            prev, cur = cur, nxt
         K.reg_finish(n, u, v, cur, nbr, x_ref, x_out, gamma, reg.reg_mask, N, partials=self._partials, geo=geo,
                      out=out, a_prec=A_out if out is not None else None)
+        # residual of the coupled solve: the finish applied one more Jacobi
+        # update to the last iterate, x_R - z = J z + f - z (device, read lazily)
+        r2 = (x_out[rows, :N] - cur[:, :N]).double().pow(2).sum() if N else torch.zeros((), dtype=torch.float64,
+                                                                                          device=self.device)
+        self._reg_log.append({"solver": self.config.spatial_solver, "rho": rho, "sweeps": sweeps, "r2": r2,
+                              "count": k * self.n_total})
+
+    def _reg_schedule(self, reg, v, rows, k, gamma, sweeps):
+        """(rho, sweeps) of this GN iteration's coupled solve.  Chebyshev: rho =
+        max over pixels of g deg ||V_RR||_inf, a Gershgorin bound of the Jacobi
+        matrix's spectral radius (its spectrum is real: J is similar to a
+        symmetric matrix), max-reduced over the ranks; the sweeps cut the error
+        by ``spatial_tol`` at the Chebyshev rate sigma = rho / (1 + sqrt(1 -
+        rho^2)) (plain Jacobi: rho).  One host read-back per GN iteration."""
+        cfg = self.config
+        if cfg.spatial_solver != "chebyshev":
+            return 0.0, sweeps
+        n, N = self.n_params, self.N
+        if N:
+            # V row (c * n + r_j): component r_j of column c (kf_core.h JacobiArgs)
+            blk = torch.stack([v[[c * n + r for c in range(k)], :N].abs().sum(0) for r in rows])   # [k, N]
+            rho_t = (gamma * blk.amax(0) * reg.degrees).amax().reshape(1).double()
+        else:
+            rho_t = torch.zeros(1, dtype=torch.float64, device=self.device)
+        rho = float(self.comm.all_reduce_(rho_t, op="max").item())
+        if not rho < 1.0:
+            LOG.warning("spatial prior: Jacobi bound rho=%.4f >= 1, plain Jacobi sweeps", rho)
+            return 0.0, max(1, int(cfg.spatial_max_sweeps))
+        if rho <= 0.0:
+            return 0.0, 1
+        sigma = rho / (1.0 + math.sqrt(max(0.0, 1.0 - rho * rho)))
+        need = math.log(2.0 / cfg.spatial_tol) / math.log(1.0 / sigma)
+        return rho, int(min(max(1, math.ceil(need)), int(cfg.spatial_max_sweeps)))
 
     # ------------------------------------------------ band-parallel (TP-like)
     def _band_parallel_iteration(self, table, x_prev, fc: KFState, x_out, A_out, status):

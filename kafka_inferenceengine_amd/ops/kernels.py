@@ -456,10 +456,12 @@ def reg_prepare(n_params, a_in, b_in, nbr, u_out, v_out, gamma, reg_mask, N, a_o
     ext().jacobi(n_params, a, grid_for(N), _dev(a_in), _stream(a_in))
 
 
-def reg_sweep(n_params, u, v, z_ext, nbr, z_out, gamma, reg_mask, N, geo=None, rows=None):
+def reg_sweep(n_params, u, v, z_ext, nbr, z_out, gamma, reg_mask, N, geo=None, rows=None, z_prev=None,
+              omega=1.0):
     """K9 affine sweep of the k regularised fields: z_out[:, :N] = u_R + g V_RR s(z_ext).
     ``rows = (p0, n)`` restricts it to local pixels [p0, p0 + n) (C2 overlap: the
-    boundary rows first, then the interior while the halo is in flight)."""
+    boundary rows first, then the interior while the halo is in flight).
+    ``z_prev``/``omega``: Chebyshev step z_out = z_prev + omega (jacobi - z_prev)."""
     check_np(n_params)
     dev = u.device
     k = bin(int(reg_mask)).count("1")
@@ -472,6 +474,11 @@ def reg_sweep(n_params, u, v, z_ext, nbr, z_out, gamma, reg_mask, N, geo=None, r
     a = _reg_args(n_params, JACOBI_SWEEP, N, u.shape[1], gamma, reg_mask, nbr, geo)
     a.ld_ext = z_ext.shape[1]
     a.u, a.v, a.x_ext, a.z_out = map(_ptr, (u, v, z_ext, z_out))
+    if z_prev is not None:
+        _check_soa(z_prev, k, N, "z_prev", device=dev)
+        if z_prev.shape[1] != z_ext.shape[1] or z_prev.data_ptr() in (z_out.data_ptr(),):
+            raise ValueError("z_prev must share z_ext's leading dimension and differ from z_out")
+        a.z_prev, a.omega = _ptr(z_prev), float(omega)
     n = N
     if rows is not None:
         p0, n = int(rows[0]), int(rows[1])

@@ -15,6 +15,7 @@ then finishes the exchange (``LinearKalman._regularised_iteration``).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from ..ops import kernels as K
@@ -30,6 +31,15 @@ class HaloExchanger:
         self.n_up, self.n_down = lay["n_up"], lay["n_down"]
         self.send_up_idx = torch.from_numpy(lay["send_up"]).to(device)
         self.send_down_idx = torch.from_numpy(lay["send_down"]).to(device)
+        # C2 overlap split, dense or masked: local pixels are in row-major order,
+        # so the rows the neighbours need are the index ranges [0, a) and
+        # [N - b, N); everything between is interior (reads no halo of the next
+        # iterate).  None when the boundary rows are not such ranges.
+        a, b = int(lay["send_up"].size), int(lay["send_down"].size)
+        N = self.N
+        ok = (np.array_equal(lay["send_up"], np.arange(a)) and np.array_equal(lay["send_down"], np.arange(N - b, N))
+              and a + b < N)
+        self.split = (a, b) if ok else None
         self._nbr = None
         self._device = torch.device(device)
         self._z = None
@@ -48,11 +58,20 @@ class HaloExchanger:
             self._nbr = torch.from_numpy(self.partition.neighbour_table()).to(self._device)
         return self._nbr
 
+    @property
+    def degrees(self) -> torch.Tensor:
+        """float32 [N]: active 4-neighbours of each local pixel (halo rows included)."""
+        if getattr(self, "_deg", None) is None:
+            nt = self.partition.neighbour_table()
+            self._deg = torch.from_numpy((nt >= 0).sum(0).astype("float32")).to(self._device)
+        return self._deg
+
     def z_buffers(self, k: int):
-        """Two extended [k, N + n_up + n_down] buffers for the regularised fields."""
+        """Three extended [k, N + n_up + n_down] buffers for the regularised fields
+        (Chebyshev keeps the previous iterate besides the current and next)."""
         if self._z is None or self._z[0].shape[0] != k:
             cols = self.N + self.n_up + self.n_down
-            self._z = [torch.zeros((k, cols), dtype=torch.float32, device=self._device) for _ in range(2)]
+            self._z = [torch.zeros((k, cols), dtype=torch.float32, device=self._device) for _ in range(3)]
             self._z_recv = (torch.zeros((k, self.n_up), dtype=torch.float32, device=self._device),
                             torch.zeros((k, self.n_down), dtype=torch.float32, device=self._device))
         return self._z
