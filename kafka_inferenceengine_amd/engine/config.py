@@ -35,6 +35,10 @@ class EngineConfig:
     # (exactly jacobi_sweeps plain sweeps, the round-2 smoother)
     spatial_solver: str = "chebyshev"
     spatial_tol: float = 1e-3
+    # inexact Newton: a Gauss-Newton iteration that cannot end the loop
+    # (n_iter < min_iterations) only needs a linearisation point, so its coupled
+    # solve stops at this looser tolerance (the final iteration uses spatial_tol)
+    spatial_tol_first: float = 1e-1
     spatial_max_sweeps: int = 64
     jacobi_sweeps: int = 4
     # GP operator placement: fused into the analysis kernel, or "split" (high-
@@ -79,7 +83,7 @@ class EngineConfig:
             raise ValueError("spatial_gamma must be >= 0")
         if self.spatial_solver not in ("chebyshev", "jacobi"):
             raise ValueError("spatial_solver must be 'chebyshev' or 'jacobi'")
-        if not 0 < self.spatial_tol < 1 or self.spatial_max_sweeps < 1:
+        if not 0 < self.spatial_tol < 1 or not 0 < self.spatial_tol_first < 1 or self.spatial_max_sweeps < 1:
             raise ValueError("spatial_tol must be in (0, 1) and spatial_max_sweeps >= 1")
         if self.spatial_gamma > 0 and self.analysis_form != "information":
             raise ValueError("the spatial regulariser runs in information form")

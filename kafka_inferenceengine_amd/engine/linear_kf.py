@@ -895,7 +895,8 @@ class LinearKalman:
                             K.gain(n, table, x_prev, None if prop else fc.x, None if prop else fc.P, x_new, A_keep,
                                    status, self._partials, N=N, joseph=cfg.joseph, prop=prop, out=out_now)
                         elif cfg.spatial_gamma > 0:
-                            self._regularised_iteration(table, x_prev, fc, x_new, A_keep, status, prop, out_now)
+                            self._regularised_iteration(table, x_prev, fc, x_new, A_keep, status, prop, out_now,
+                                                        final=n_iter >= cfg.min_iterations)
                         elif bp:
                             self._band_parallel_iteration(table, x_prev, fc, x_new, A_keep, status)
                         elif split is not None:
@@ -1087,7 +1088,8 @@ class LinearKalman:
                            a_in=a_in, b_in=b_in)
                 prev = (A_c, b_c)
 
-    def _regularised_iteration(self, table, x_prev, fc: KFState | None, x_out, A_out, status, prop=None, out=None):
+    def _regularised_iteration(self, table, x_prev, fc: KFState | None, x_out, A_out, status, prop=None, out=None,
+                               final=True):
         """GMRF spatial prior (K9 + C2), affine block-Jacobi form (kf_core.h):
         the analysis kernel assembles (A, b) and, instead of solving, factors
         A_reg = A + g deg E_R once and writes u = A_reg^-1 b and V = A_reg^-1 E_R;
@@ -1124,7 +1126,8 @@ class LinearKalman:
                    reg=dict(gamma=gamma, mask=reg.reg_mask, v_out=v, nbr=None if geo else reg.nbr, geo=geo),
                    x0_out=None if x_prev is not None else x0_buf)
         nbr = None if geo else reg.nbr
-        rho, sweeps = self._reg_schedule(reg, v, rows, k, gamma, sweeps)
+        rho, sweeps = self._reg_schedule(reg, v, rows, k, gamma, sweeps,
+                                         self.config.spatial_tol if final else self.config.spatial_tol_first)
         z = reg.z_buffers(k)
         z[0][:, :N].copy_(x_ref[rows, :N])
         cur = reg.fill_halo(z[0])
@@ -1167,13 +1170,15 @@ class LinearKalman:
         self._reg_log.append({"solver": self.config.spatial_solver, "rho": rho, "sweeps": sweeps, "r2": r2,
                               "count": k * self.n_total})
 
-    def _reg_schedule(self, reg, v, rows, k, gamma, sweeps):
+    def _reg_schedule(self, reg, v, rows, k, gamma, sweeps, tol):
         """(rho, sweeps) of this GN iteration's coupled solve.  Chebyshev: rho =
         max over pixels of g deg ||V_RR||_inf, a Gershgorin bound of the Jacobi
         matrix's spectral radius (its spectrum is real: J is similar to a
         symmetric matrix), max-reduced over the ranks; the sweeps cut the error
         by ``spatial_tol`` at the Chebyshev rate sigma = rho / (1 + sqrt(1 -
-        rho^2)) (plain Jacobi: rho).  One host read-back per GN iteration."""
+        rho^2)) (plain Jacobi: rho).  ``tol``: spatial_tol for an iteration that
+        can end the GN loop, spatial_tol_first before.  One host read-back per
+        GN iteration."""
         cfg = self.config
         if cfg.spatial_solver != "chebyshev":
             return 0.0, sweeps
@@ -1191,7 +1196,7 @@ class LinearKalman:
         if rho <= 0.0:
             return 0.0, 1
         sigma = rho / (1.0 + math.sqrt(max(0.0, 1.0 - rho * rho)))
-        need = math.log(2.0 / cfg.spatial_tol) / math.log(1.0 / sigma)
+        need = math.log(2.0 / tol) / math.log(1.0 / sigma)
         return rho, int(min(max(1, math.ceil(need)), int(cfg.spatial_max_sweeps)))
 
     # ------------------------------------------------ band-parallel (TP-like)
