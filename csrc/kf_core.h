@@ -1561,6 +1561,65 @@ KF_HD float reg_finish1(const JacobiArgs& a, int64_t i0, int64_t stride, int64_t
   return dn;
 }
 
+// Dense strips (StripGeo) with one regularised field: the row-loop forms of
+// reg_sweep1 / reg_finish1.  A block walks whole rows, its threads the
+// columns, so (row, column) are loop indices -- no per-neighbour integer
+// division of the pixel index (geo_neighbour) -- and the neighbour sum adds
+// up / down / left / right in reg_nsum1's order (bit-identical results).
+constexpr int JACOBI_SWEEP1D = 6, JACOBI_FINISH1D = 7;
+
+template <typename JA>
+KF_HD float reg_nsum_dense(const JA& a, uint32_t r, uint32_t c, int64_t p) {
+  const uint32_t w = (uint32_t)a.geo.w;
+  float s = 0.f;
+  if (r > 0) s += a.x_ext[p - w];
+  else if (a.geo.halo & 1) s += a.x_ext[a.N + c];
+  if (r + 1 < (uint32_t)a.geo.h) s += a.x_ext[p + w];
+  else if (a.geo.halo & 2) s += a.x_ext[a.N + a.geo.n_up + c];
+  if (c > 0) s += a.x_ext[p - 1];
+  if (c + 1 < w) s += a.x_ext[p + 1];
+  return s;
+}
+
+template <int NP>
+KF_HD void reg_sweep1d_px(const JacobiArgs& a, uint32_t r, uint32_t c, int j0) {
+  const int64_t p = (int64_t)r * a.geo.w + c;
+  const int64_t ld = a.ld;
+  float z = fmaf(a.gamma, a.v[j0 * ld + p] * reg_nsum_dense(a, r, c, p), a.u[j0 * ld + p]);
+  if (a.z_prev) {
+    const float zp = a.z_prev[p];
+    z = fmaf(a.omega, z - zp, zp);
+  }
+  a.z_out[p] = z;
+}
+
+template <int NP>
+KF_HD float reg_finish1d_px(const JacobiArgs& a, uint32_t r, uint32_t c) {
+  const int64_t p = (int64_t)r * a.geo.w + c;
+  const int64_t ld = a.ld;
+  const float s = reg_nsum_dense(a, r, c, p);
+  float dn = 0.f;
+  float x[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    x[j] = fmaf(a.gamma, a.v[j * ld + p] * s, a.u[j * ld + p]);
+    const float d = x[j] - a.x_ref[j * ld + p];
+    dn = fmaf(d, d, dn);
+  }
+#pragma unroll
+  for (int j = 0; j < NP; ++j) a.x_out[j * ld + p] = x[j];
+  if (a.out_mean) {
+    const int64_t ro = a.out_idx ? a.out_idx[p] : p;
+    KF_DCHECK(ro >= 0 && ro < a.out_plane);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      a.out_mean[j * a.out_plane + ro] = x[j];
+      a.out_unc[j * a.out_plane + ro] = kf_rsqrt(a.a_in[tri(NP, j, j) * ld + p]);
+    }
+  }
+  return dn;
+}
+
 template <int NP>
 KF_HD float pixel_jacobi_classic(const JacobiArgs& a, int64_t p);
 

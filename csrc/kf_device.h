@@ -235,7 +235,24 @@ __global__ __launch_bounds__(BLOCK) void jacobi_kernel(JacobiArgs a) {
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   const int64_t n = a.pn > 0 ? a.pn : a.N;
-  if constexpr (MODE == JACOBI_SWEEP1 || MODE == JACOBI_FINISH1) {
+  if constexpr (MODE == JACOBI_SWEEP1D || MODE == JACOBI_FINISH1D) {
+    // whole rows [p0 / w, (p0 + n) / w) of a dense strip (checked by the launcher)
+    const uint32_t w = (uint32_t)a.geo.w;
+    const uint32_t r0 = (uint32_t)(a.p0 / w), nr = (uint32_t)(n / w);
+    const int j0 = __builtin_ctz(a.reg_mask);
+    for (uint32_t rr = blockIdx.x; rr < nr; rr += gridDim.x) {
+      const uint32_t r = r0 + rr;
+      for (uint32_t c0 = threadIdx.x; c0 < w; c0 += JACOBI_U * BLOCK) {
+#pragma unroll
+        for (int u = 0; u < JACOBI_U; ++u) {
+          const uint32_t c = c0 + u * BLOCK;
+          if (c >= w) break;
+          if constexpr (MODE == JACOBI_SWEEP1D) reg_sweep1d_px<NP>(a, r, c, j0);
+          else acc += (double)reg_finish1d_px<NP>(a, r, c);
+        }
+      }
+    }
+  } else if constexpr (MODE == JACOBI_SWEEP1 || MODE == JACOBI_FINISH1) {
     for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += JACOBI_U * stride) {
       if constexpr (MODE == JACOBI_SWEEP1) reg_sweep1<NP, JACOBI_U>(a, i, stride, n);
       else acc += (double)reg_finish1<NP, JACOBI_U>(a, i, stride, n);

@@ -46,6 +46,18 @@ __global__ __launch_bounds__(BLOCK) void lut_nearest_kernel(const float* lut, in
 template <int NP>
 static void l_jacobi(const JacobiArgs& a, int grid, hipStream_t s) {
   const bool one = a.k == 1 && a.reg_mask != 0 && (a.reg_mask & (a.reg_mask - 1)) == 0;
+  // dense strip, whole rows: the row-loop kernels (no per-pixel index division)
+  const int64_t n = a.pn > 0 ? a.pn : a.N;
+  const bool rows = one && a.geo.w > 0 && a.p0 % a.geo.w == 0 && n % a.geo.w == 0 && n > 0;
+  if (rows && (a.mode == JACOBI_SWEEP || a.mode == JACOBI_FINISH)) {
+    const int64_t nr = n / a.geo.w;
+    const int g = (int)(nr < grid ? nr : grid);   // partials hold >= grid entries
+    if (a.mode == JACOBI_SWEEP)
+      hipLaunchKernelGGL((jacobi_kernel<NP, JACOBI_SWEEP1D>), dim3(g), dim3(BLOCK), 0, s, a);
+    else
+      hipLaunchKernelGGL((jacobi_kernel<NP, JACOBI_FINISH1D>), dim3(g), dim3(BLOCK), 0, s, a);
+    return;
+  }
   if (a.mode == JACOBI_SWEEP && one)
     hipLaunchKernelGGL((jacobi_kernel<NP, JACOBI_SWEEP1>), dim3(grid), dim3(BLOCK), 0, s, a);
   else if (a.mode == JACOBI_FINISH && one)

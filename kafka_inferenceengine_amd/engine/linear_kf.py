@@ -975,7 +975,7 @@ class LinearKalman:
         out = []
         for r in self._reg_log:
             e = {"solver": r["solver"], "rho": round(r["rho"], 6), "sweeps": r["sweeps"]}
-            if self.metrics.enabled:
+            if self.metrics.enabled and r["r2"] is not None:
                 tot = self.comm.sum_f64(r["r2"].reshape(1))
                 e["residual_rms"] = math.sqrt(max(tot, 0.0) / max(1, r["count"]))
             out.append(e)
@@ -1129,7 +1129,8 @@ class LinearKalman:
         rho, sweeps = self._reg_schedule(reg, v, rows, k, gamma, sweeps,
                                          self.config.spatial_tol if final else self.config.spatial_tol_first)
         z = reg.z_buffers(k)
-        z[0][:, :N].copy_(x_ref[rows, :N])
+        for i, r in enumerate(rows):
+            z[0][i, :N].copy_(x_ref[r, :N])
         cur = reg.fill_halo(z[0])
         prev = None
         omega = 1.0
@@ -1163,10 +1164,12 @@ class LinearKalman:
             prev, cur = cur, nxt
         K.reg_finish(n, u, v, cur, nbr, x_ref, x_out, gamma, reg.reg_mask, N, partials=self._partials, geo=geo,
                      out=out, a_prec=A_out if out is not None else None)
-        # residual of the coupled solve: the finish applied one more Jacobi
-        # update to the last iterate, x_R - z = J z + f - z (device, read lazily)
-        r2 = (x_out[rows, :N] - cur[:, :N]).double().pow(2).sum() if N else torch.zeros((), dtype=torch.float64,
-                                                                                          device=self.device)
+        # residual of the coupled solve (metrics only): the finish applied one more
+        # Jacobi update to the last iterate, x_R - z = J z + f - z (device, read lazily)
+        r2 = None
+        if self.metrics.enabled:
+            r2 = sum(((x_out[r, :N] - cur[i, :N]).double().pow(2).sum() for i, r in enumerate(rows)),
+                     torch.zeros((), dtype=torch.float64, device=self.device))
         self._reg_log.append({"solver": self.config.spatial_solver, "rho": rho, "sweeps": sweeps, "r2": r2,
                               "count": k * self.n_total})
 
@@ -1183,8 +1186,11 @@ class LinearKalman:
         if cfg.spatial_solver != "chebyshev":
             return 0.0, sweeps
         n, N = self.n_params, self.N
-        if N:
-            # V row (c * n + r_j): component r_j of column c (kf_core.h JacobiArgs)
+        if N and k == 1:
+            # V row (c * n + r_j): component r_j of column c (kf_core.h JacobiArgs); one
+            # field: V_RR >= 0 is the row itself (a view), one fused multiply + max
+            rho_t = (torch.amax(v[rows[0], :N] * reg.degrees) * gamma).reshape(1).double()
+        elif N:
             blk = torch.stack([v[[c * n + r for c in range(k)], :N].abs().sum(0) for r in rows])   # [k, N]
             rho_t = (gamma * blk.amax(0) * reg.degrees).amax().reshape(1).double()
         else:
