@@ -1581,40 +1581,68 @@ KF_HD float reg_nsum_dense(const JA& a, uint32_t r, uint32_t c, int64_t p) {
   return s;
 }
 
-template <int NP>
-KF_HD void reg_sweep1d_px(const JacobiArgs& a, uint32_t r, uint32_t c, int j0) {
-  const int64_t p = (int64_t)r * a.geo.w + c;
+// U pixels of row r at columns c0 + u * BLOCK (u < U): every load of the U
+// pixels is issued before the first store (the stores may alias the inputs
+// as far as the compiler knows, which would serialise a per-pixel order).
+template <int NP, int U, int BS>
+KF_HD void reg_sweep1d(const JacobiArgs& a, uint32_t r, uint32_t c0, int j0) {
+  const uint32_t w = (uint32_t)a.geo.w;
   const int64_t ld = a.ld;
-  float z = fmaf(a.gamma, a.v[j0 * ld + p] * reg_nsum_dense(a, r, c, p), a.u[j0 * ld + p]);
-  if (a.z_prev) {
-    const float zp = a.z_prev[p];
-    z = fmaf(a.omega, z - zp, zp);
+  float z[U];
+  int64_t pp[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t c = c0 + u * BS < w ? c0 + u * BS : c0;
+    const int64_t p = (int64_t)r * w + c;
+    pp[u] = p;
+    z[u] = fmaf(a.gamma, a.v[j0 * ld + p] * reg_nsum_dense(a, r, c, p), a.u[j0 * ld + p]);
+    if (a.z_prev) {
+      const float zp = a.z_prev[p];
+      z[u] = fmaf(a.omega, z[u] - zp, zp);
+    }
   }
-  a.z_out[p] = z;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (c0 + u * BS < w) a.z_out[pp[u]] = z[u];
 }
 
-template <int NP>
-KF_HD float reg_finish1d_px(const JacobiArgs& a, uint32_t r, uint32_t c) {
-  const int64_t p = (int64_t)r * a.geo.w + c;
+template <int NP, int U, int BS>
+KF_HD float reg_finish1d(const JacobiArgs& a, uint32_t r, uint32_t c0) {
+  const uint32_t w = (uint32_t)a.geo.w;
   const int64_t ld = a.ld;
-  const float s = reg_nsum_dense(a, r, c, p);
+  float x[U][NP];
+  int64_t pp[U];
   float dn = 0.f;
-  float x[NP];
 #pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    x[j] = fmaf(a.gamma, a.v[j * ld + p] * s, a.u[j * ld + p]);
-    const float d = x[j] - a.x_ref[j * ld + p];
-    dn = fmaf(d, d, dn);
-  }
-#pragma unroll
-  for (int j = 0; j < NP; ++j) a.x_out[j * ld + p] = x[j];
-  if (a.out_mean) {
-    const int64_t ro = a.out_idx ? a.out_idx[p] : p;
-    KF_DCHECK(ro >= 0 && ro < a.out_plane);
+  for (int u = 0; u < U; ++u) {
+    const bool in = c0 + u * BS < w;
+    const uint32_t c = in ? c0 + u * BS : c0;
+    const int64_t p = (int64_t)r * w + c;
+    pp[u] = p;
+    const float s = reg_nsum_dense(a, r, c, p);
+    float du = 0.f;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      a.out_mean[j * a.out_plane + ro] = x[j];
-      a.out_unc[j * a.out_plane + ro] = kf_rsqrt(a.a_in[tri(NP, j, j) * ld + p]);
+      x[u][j] = fmaf(a.gamma, a.v[j * ld + p] * s, a.u[j * ld + p]);
+      const float d = x[u][j] - a.x_ref[j * ld + p];
+      du = fmaf(d, d, du);
+    }
+    dn += in ? du : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (c0 + u * BS >= w) continue;
+    const int64_t p = pp[u];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) a.x_out[j * ld + p] = x[u][j];
+    if (a.out_mean) {
+      const int64_t ro = a.out_idx ? a.out_idx[p] : p;
+      KF_DCHECK(ro >= 0 && ro < a.out_plane);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        a.out_mean[j * a.out_plane + ro] = x[u][j];
+        a.out_unc[j * a.out_plane + ro] = kf_rsqrt(a.a_in[tri(NP, j, j) * ld + p]);
+      }
     }
   }
   return dn;

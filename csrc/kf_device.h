@@ -242,14 +242,12 @@ __global__ __launch_bounds__(BLOCK) void jacobi_kernel(JacobiArgs a) {
     const int j0 = __builtin_ctz(a.reg_mask);
     for (uint32_t rr = blockIdx.x; rr < nr; rr += gridDim.x) {
       const uint32_t r = r0 + rr;
-      for (uint32_t c0 = threadIdx.x; c0 < w; c0 += JACOBI_U * BLOCK) {
-#pragma unroll
-        for (int u = 0; u < JACOBI_U; ++u) {
-          const uint32_t c = c0 + u * BLOCK;
-          if (c >= w) break;
-          if constexpr (MODE == JACOBI_SWEEP1D) reg_sweep1d_px<NP>(a, r, c, j0);
-          else acc += (double)reg_finish1d_px<NP>(a, r, c);
-        }
+      // the finish carries NP values per pixel: 2 pixels per thread keep it at
+      // 4 waves per SIMD (<= 128 VGPRs; 4 pixels: 147, 3 waves)
+      constexpr int UU = MODE == JACOBI_SWEEP1D ? JACOBI_U : 2;
+      for (uint32_t c0 = threadIdx.x; c0 < w; c0 += UU * BLOCK) {
+        if constexpr (MODE == JACOBI_SWEEP1D) reg_sweep1d<NP, UU, BLOCK>(a, r, c0, j0);
+        else acc += (double)reg_finish1d<NP, UU, BLOCK>(a, r, c0);
       }
     }
   } else if constexpr (MODE == JACOBI_SWEEP1 || MODE == JACOBI_FINISH1) {
