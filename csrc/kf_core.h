@@ -111,7 +111,13 @@ struct BandDesc {
   const void* gpm;             // GP split-f16 MFMA fragments (kf_gp_mfma.h, models/gp.py:mfma_tables)
   float gpm_scale;             // 2^sigma: undoes the f16-range shift folded into the table's L'
   int32_t map_identity;        // 1: map[d] == d for every input d (full-state GP: no gather / scatter)
+  int32_t map_kind;            // GPM_MAP_*: a map known at compile time (JRC-TIP bands), 0: runtime map
 };
+
+// JRC-TIP band mappers (kafka/inference/kf_tools.py:19-23, band_selecta): the
+// matrix-core kernel gathers the GP inputs and updates only the 4 x 4 touched
+// entries of A with these compiled in instead of the runtime map's selects.
+constexpr int GPM_MAP_RUNTIME = 0, GPM_MAP_TIP_VIS = 2, GPM_MAP_TIP_NIR = 3;
 
 struct PropArgs {
   int64_t N, ld;

@@ -343,6 +343,49 @@ __device__ __forceinline__ void gpm_inputs(const KF_CONST_AS BandDesc* bdp, cons
   for (int d = 0; d < D; ++d) c = fmaf(bdp->coef[d] * xi[d], xi[d], c);
 }
 
+// Compile-time maps (BandDesc.map_kind, JRC-TIP): the gather of gpm_inputs and
+// the normal-equation update of the dense path restricted to the touched
+// entries, in the same operand order (bit-identical: the dense update adds
+// exact zeros elsewhere).
+struct GpmMap {
+  int m[4];
+  int inv[16];   // input index of state j, -1 if none
+};
+__device__ constexpr GpmMap gpm_const_map(int kind) {
+  GpmMap r{{0, 1, 6, 2}, {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1}};
+  if (kind == GPM_MAP_TIP_NIR) {
+    r.m[0] = 3; r.m[1] = 4; r.m[2] = 6; r.m[3] = 5;
+  }
+  for (int d = 0; d < 4; ++d) r.inv[r.m[d]] = d;
+  return r;
+}
+
+template <int NP, int D, int K>
+__device__ __forceinline__ void gpm_inputs_const(const KF_CONST_AS BandDesc* bdp, const float (&x0)[NP],
+                                                 float (&xi)[D], float& c) {
+  constexpr GpmMap M = gpm_const_map(K);
+#pragma unroll
+  for (int d = 0; d < D; ++d) xi[d] = x0[M.m[d]] - bdp->center[d];
+#pragma unroll
+  for (int d = 0; d < D; ++d) c = fmaf(bdp->coef[d] * xi[d], xi[d], c);
+}
+
+template <int NP, int D, int K>
+__device__ __forceinline__ void gpm_update_const(float (&A)[ntri(NP)], float (&b)[NP], const float (&g)[D],
+                                                 float w, float wy) {
+  constexpr GpmMap M = gpm_const_map(K);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    if (M.inv[i] < 0) continue;
+    const float hi = g[M.inv[i]];
+    const float wh = w * hi;
+    b[i] = fmaf(hi, wy, b[i]);
+#pragma unroll
+    for (int j = i; j < NP; ++j)
+      if (M.inv[j] >= 0) A[tri(NP, i, j)] = fmaf(wh, g[M.inv[j]], A[tri(NP, i, j)]);
+  }
+}
+
 // gp_epilogue with the same identity-map shortcut (h[d] = g_d, no scatter).
 template <int NP, int D>
 __device__ __forceinline__ void gpm_epilogue(const KF_CONST_AS BandDesc* q, const float (&xi)[D], float S0,
@@ -406,28 +449,34 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     float y, w;
     decode_obs<FOBS>(*bdp, p, y, w);
     const bool use = act && (w > 0.f);
-    float H0 = 0.f, h[NP];
+    float H0 = 0.f, g[D];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) h[j] = 0.f;
+    for (int d = 0; d < D; ++d) g[d] = 0.f;
     bool ok = false;
     const int nch = bdp->gpm_nchunk;
+    // wave-uniform: a compiled-in JRC-TIP map, or the runtime / identity map
+    constexpr bool TIPK = NP == 7 && D == 4;
+    const int mk = TIPK ? bdp->map_kind : GPM_MAP_RUNTIME;
     const bool any = __any(use);
     if (any) {
       float xi[D], c = 0.f;
-      gpm_inputs<NP, D>(bdp, x0, xi, c);
+      if (TIPK && mk == GPM_MAP_TIP_VIS) gpm_inputs_const<NP, D, GPM_MAP_TIP_VIS>(bdp, x0, xi, c);
+      else if (TIPK && mk == GPM_MAP_TIP_NIR) gpm_inputs_const<NP, D, GPM_MAP_TIP_NIR>(bdp, x0, xi, c);
+      else gpm_inputs<NP, D>(bdp, x0, xi, c);
       c *= -0.5f * LOG2E;
       float S[D + 1];
       if constexpr (GT) gp_mfma_sums_g<D, PF>(bdp->gpm, nch, xi, c, S);
       else gp_mfma_sums<D>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
       const KF_CONST_AS BandDesc* q = opaque(bdp);   // epilogue fields: not live across the chunk loop
       const float sc = q->gpm_scale;
-      float Sd[D];
+      const float S0 = S[0] * sc;
+      // f = offset + S0, df/dx_d = -lambda_d x_d S0 + ln2 S'_d (gp_epilogue)
+      H0 = q->offset + S0;
 #pragma unroll
-      for (int d = 0; d < D; ++d) Sd[d] = S[1 + d] * sc;
-      gpm_epilogue<NP, D>(q, xi, S[0] * sc, Sd, H0, h);
+      for (int d = 0; d < D; ++d) g[d] = fmaf(-q->coef[d] * xi[d], S0, LN2 * (S[1 + d] * sc));
       ok = finitef(H0);
 #pragma unroll
-      for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);
+      for (int d = 0; d < D; ++d) ok = ok && finitef(g[d]);
     }
     off += nch * gpm_frags_per_chunk(D);
     float* h0o = opaque(bdp)->h0_out;
@@ -436,12 +485,33 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     if (use && ok) {
       ++nobs;
       const float wy = w * (y - H0);   // correction form: the residual at x0
+      if (TIPK && mk == GPM_MAP_TIP_VIS) {
+        gpm_update_const<NP, D, GPM_MAP_TIP_VIS>(A, b, g, w, wy);
+      } else if (TIPK && mk == GPM_MAP_TIP_NIR) {
+        gpm_update_const<NP, D, GPM_MAP_TIP_NIR>(A, b, g, w, wy);
+      } else {
+        // scatter to the state (identity map: h[d] = g_d)
+        float h[NP];
+        const KF_CONST_AS BandDesc* q = opaque(bdp);
 #pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const float wh = w * h[i];
-        b[i] = fmaf(h[i], wy, b[i]);
+        for (int j = 0; j < NP; ++j) h[j] = 0.f;
+        if (q->map_identity) {
 #pragma unroll
-        for (int j = i; j < NP; ++j) A[tri(NP, i, j)] = fmaf(wh, h[j], A[tri(NP, i, j)]);
+          for (int d = 0; d < D && d < NP; ++d) h[d] = g[d];
+        } else {
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+#pragma unroll
+            for (int j = 0; j < NP; ++j) h[j] += (q->map[d] == j) ? g[d] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const float wh = w * h[i];
+          b[i] = fmaf(h[i], wy, b[i]);
+#pragma unroll
+          for (int j = i; j < NP; ++j) A[tri(NP, i, j)] = fmaf(wh, h[j], A[tri(NP, i, j)]);
+        }
       }
     }
   }

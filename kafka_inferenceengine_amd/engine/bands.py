@@ -158,6 +158,10 @@ def band_desc(spec: OperatorSpec, obs: DeviceBand | None, n_params: int, cache: 
         raise ValueError(f"state map {smap} out of range for n_params={n_params}")
     d.map = smap
     d.map_identity = int(len(smap) >= int(d.d) > 0 and smap[:int(d.d)] == list(range(int(d.d))))
+    # compile-time JRC-TIP maps (kf_core.h GPM_MAP_*): only for 7-parameter states
+    d.map_kind = 0
+    if spec.kind == OP_GP and n_params == 7 and int(d.d) == 4:
+        d.map_kind = {(0, 1, 6, 2): 2, (3, 4, 6, 5): 3}.get(tuple(smap[:4]), 0)
     d.coef = [float(c) for c in spec.coef]
     d.center = [float(c) for c in spec.center]
     if obs is None:
