@@ -77,6 +77,7 @@ def build(cfg_name, a, mask, part, dev, comm):
 
     c = CONFIGS[cfg_name]
     n_dates = a.warmup + a.steps + 1
+    stream = not a.resident
     seed = 0
     over = {}
     for kv in getattr(a, "set", None) or []:        # --set field=value (EngineConfig A/B knobs)
@@ -92,7 +93,7 @@ def build(cfg_name, a, mask, part, dev, comm):
     if cfg_name in ("tip7", "spatial"):
         dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(n_dates)]
         obs = k.SyntheticBHRObservations(mask, dates=dates, n_train=a.n_train or c["n_train"], partition=part,
-                                         device=dev, n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=seed)
+                                         device=dev, n_pool=a.pool, stream=stream, cloud_fraction=a.cloud, seed=seed)
         cfg = mkcfg()
         if cfg_name == "spatial":
             cfg = mkcfg(spatial_gamma=c["gamma"], spatial_params=[6], spatial_tol=c["tol"])
@@ -104,7 +105,7 @@ def build(cfg_name, a, mask, part, dev, comm):
     elif cfg_name == "identity7":
         dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(n_dates)]
         obs = k.SyntheticIdentityObservations(mask, dates=dates, partition=part, device=dev, n_pool=a.pool,
-                                              stream=True, cloud_fraction=a.cloud, seed=seed)
+                                              stream=stream, cloud_fraction=a.cloud, seed=seed)
         kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_linear_observation_operator,
                             k.TIP_PARAMETERS, state_propagation=k.propagate_information_filter_LAI,
                             config=mkcfg(), comm=comm, partition=part)
@@ -115,16 +116,16 @@ def build(cfg_name, a, mask, part, dev, comm):
         T = a.n_train or c["n_train"]
         if cfg_name == "prosail10":
             obs = k.SyntheticS2Observations(mask, dates=dates, n_bands=10, n_train=T, partition=part, device=dev,
-                                            n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=seed)
+                                            n_pool=a.pool, stream=stream, cloud_fraction=a.cloud, seed=seed)
         elif cfg_name == "prosail10_hard":
             obs = k.SyntheticS2Observations(mask, dates=dates, n_bands=10, n_train=T, partition=part, device=dev,
-                                            n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=seed,
+                                            n_pool=a.pool, stream=stream, cloud_fraction=a.cloud, seed=seed,
                                             hard=True, spread_scale=c["spread"], rel_unc=c["rel_unc"])
         else:
             s2 = k.SyntheticS2Observations(mask, dates=dates, n_bands=13, n_train=T, partition=part, device=dev,
-                                           n_pool=a.pool, stream=True, cloud_fraction=a.cloud, seed=seed)
+                                           n_pool=a.pool, stream=stream, cloud_fraction=a.cloud, seed=seed)
             olci = k.SyntheticOLCIObservations(mask, dates=dates, n_bands=21, n_train=T, partition=part,
-                                               device=dev, n_pool=a.pool, stream=True, cloud_fraction=a.cloud,
+                                               device=dev, n_pool=a.pool, stream=stream, cloud_fraction=a.cloud,
                                                seed=seed + 21)
             obs = k.MultiSensorObservations([s2, olci])
         prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
@@ -155,6 +156,9 @@ def main():
                     help="override an EngineConfig field (A/B runs), e.g. --set gp_split=never")
     ap.add_argument("--band-parallel", type=int, default=1,
                     help="ranks per band group (strips x band groups; multi-band configs)")
+    ap.add_argument("--resident", action="store_true",
+                    help="keep the synthetic observation pool in HBM (compute-only: no per-step H2D; "
+                         "the default re-uploads every date from pinned host memory)")
     ap.add_argument("--no-telemetry", action="store_true",
                     help="no per-phase hipEvent timers (the per_rank record then has no phase times)")
     a = ap.parse_args()
@@ -294,7 +298,9 @@ def main():
                "vs_baseline": round(value / c["baseline"], 2), "dtype": "fp32" if a.config != "identity7"
                else "fp32 state / bf16 observations",
                "data": f"synthetic (smooth random truth -> observation operators -> noise, {a.cloud:.0%} clouds), "
-                       "random-init GP emulators",
+                       "random-init GP emulators" + ("; observations device-resident (compute-only, no per-step H2D)"
+                                                     if a.resident else "; observations re-uploaded from pinned host "
+                                                     "memory every step"),
                "config": {"name": a.config, "model": c["model"], "tile": f"{H}x{W}", "active_pixels": part.N_total,
                           "global_batch": part.N_total, "seq_len": 1,
                           "gp_train_points": a.n_train or c.get("n_train"), "parallelism": f"tile-dp{world}" + (f" x band-tp{B}" if B > 1 else ""),
