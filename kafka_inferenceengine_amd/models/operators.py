@@ -20,6 +20,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 import scipy.sparse as sp
+import torch
 
 from .gp import GaussianProcessEmulator
 from .sar import POLARISATIONS, WaterCloudModel, sar_observation_operator
@@ -112,6 +113,8 @@ def run_emulator(gp, x, tol=None, lut_threshold: float = 1e6, lut_size: int = 50
 
     Above ``lut_threshold`` unique rows, the reference draws a 5000-sample
     MVN look-up table and assigns nearest neighbours (utils.py:75-84)."""
+    if torch.is_tensor(x):
+        return _run_emulator_device(gp, x, lut_threshold, lut_size, seed)
     x = np.asarray(x, dtype=np.float64)
     if x.shape[0] == 0:
         return np.zeros(0), np.zeros_like(x)
@@ -125,6 +128,33 @@ def run_emulator(gp, x, tol=None, lut_threshold: float = 1e6, lut_size: int = 50
     out = gp.predict(uniq, do_unc=False)
     H_, dH_ = (out[0], out[-1])
     return np.asarray(H_)[inv], np.asarray(dH_)[inv]
+
+
+def _run_emulator_device(gp, x, lut_threshold, lut_size, seed):
+    """run_emulator for a resident (N, D) tensor: the unique-row pass and the
+    LUT assignment stay on x's device (torch.unique, K7 ``lut_nearest``); only
+    the emulator itself runs on the host, over at most ``lut_size`` rows or the
+    unique rows.  Returns (H (N,), dH (N, D)) float32 tensors on x's device."""
+    from ..ops import kernels as K
+    dev = x.device
+    if x.shape[0] == 0:
+        return (torch.zeros(0, device=dev), torch.zeros_like(x, dtype=torch.float32))
+    x32 = x.to(torch.float32)
+    uniq, inv = torch.unique(x32, dim=0, return_inverse=True)
+    if uniq.shape[0] > lut_threshold:
+        LOG.info("Clustering parameter space")
+        xd = x32.double()
+        mean = xd.mean(0)
+        xc = xd - mean
+        cov = (xc.T @ xc) / max(x.shape[0] - 1, 1)
+        rng = np.random.default_rng(seed)
+        lut = rng.multivariate_normal(mean.cpu().numpy(), cov.cpu().numpy(), lut_size)
+        uniq = torch.as_tensor(lut, dtype=torch.float32, device=dev)
+        inv = K.lut_nearest(uniq, x32.T.contiguous()).long()
+    out = gp.predict(uniq.double().cpu().numpy(), do_unc=False)
+    H_ = torch.as_tensor(np.asarray(out[0]), dtype=torch.float32, device=dev)
+    dH_ = torch.as_tensor(np.asarray(out[-1]), dtype=torch.float32, device=dev)
+    return H_[inv], dH_[inv]
 
 
 def locate_in_lut(lut, im, chunk: int = 8192):
