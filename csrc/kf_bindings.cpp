@@ -278,6 +278,29 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
     else host_lut_nearest(P<const float>(lut), M, D, P<const float>(x), N, ld, P<int32_t>(out));
   });
 
+  m.def("reg_tiled", [](int64_t ld, int w, int h, int j0, uint32_t prev_mask, float gamma,
+                        const std::vector<float>& omega, uintptr_t u, uintptr_t v, uintptr_t z, uintptr_t zp,
+                        uintptr_t z_out, uintptr_t zp_out, bool device, uintptr_t stream) {
+    RegTileArgs a{};
+    a.ld = ld;
+    a.w = w;
+    a.h = h;
+    a.j0 = j0;
+    a.nsweep = (int32_t)omega.size();
+    if (a.nsweep < 1 || a.nsweep > REG_TILE_MAX_SWEEPS) throw std::runtime_error("reg_tiled: 1..8 sweeps");
+    a.prev_mask = prev_mask;
+    a.gamma = gamma;
+    set_arr(a.omega, omega, "omega");
+    a.u = P<const float>(u);
+    a.v = P<const float>(v);
+    a.z = P<const float>(z);
+    a.zp = P<const float>(zp);
+    a.z_out = P<float>(z_out);
+    a.zp_out = P<float>(zp_out);
+    if (device) check_hip(dev_reg_tiled(a, (hipStream_t)stream), "reg_tiled");
+    else if (host_reg_tiled(a) != 0) throw std::runtime_error("reg_tiled: bad arguments");
+  });
+
   bind_stream(m);
   bind_tiff(m);
 }

@@ -1654,6 +1654,47 @@ KF_HD float reg_finish1d(const JacobiArgs& a, uint32_t r, uint32_t c0) {
   return dn;
 }
 
+// Several sweeps of one regularised field in one pass over a dense strip with
+// no halo rows (world = 1, or a strip with no neighbours): temporal blocking.
+// A workgroup loads a tile plus a ring `nsweep` pixels wide into LDS, runs
+// every sweep there (the ring's values go stale one pixel per sweep, the
+// interior never reads a stale one) and writes the interior's last two
+// iterates.  Sweep s is reg_sweep1d's update with omega[s], Chebyshev against
+// the previous iterate when bit s of prev_mask is set (plain Jacobi
+// otherwise); the same operations in the same order, so the result is
+// bit-identical to nsweep launches of JACOBI_SWEEP1D.
+constexpr int REG_TILE_MAX_SWEEPS = 8;
+struct RegTileArgs {
+  int64_t ld;                // u / v leading dimension
+  int32_t w, h;              // strip geometry (w * h local pixels)
+  int32_t j0, nsweep;        // regularised row of u / v; sweeps in this pass
+  uint32_t prev_mask;        // bit s: sweep s is a Chebyshev step against the iterate before
+  float gamma;
+  float omega[REG_TILE_MAX_SWEEPS];
+  const float* u;            // [NP][ld]  (row j0 used)
+  const float* v;            // [k*NP][ld] (row j0 used)
+  const float* z;            // [w*h] current iterate
+  const float* zp;           // [w*h] the iterate before (read when bit 0 of prev_mask is set)
+  float* z_out;              // iterate after nsweep sweeps
+  float* zp_out;             // the iterate before that
+};
+
+// neighbour sum in reg_nsum_dense's order (up, down, left, right; missing ones skipped)
+KF_HD float reg_tile_nsum(const float* z, int64_t p, int64_t w, bool up, bool dn, bool lf, bool rt) {
+  float s = 0.f;
+  if (up) s += z[p - w];
+  if (dn) s += z[p + w];
+  if (lf) s += z[p - 1];
+  if (rt) s += z[p + 1];
+  return s;
+}
+
+KF_HD float reg_tile_step(const RegTileArgs& a, int s, float s_nb, float u, float v, float zp) {
+  float z = fmaf(a.gamma, v * s_nb, u);
+  if ((a.prev_mask >> s) & 1u) z = fmaf(a.omega[s], z - zp, zp);
+  return z;
+}
+
 template <int NP>
 KF_HD float pixel_jacobi_classic(const JacobiArgs& a, int64_t p);
 

@@ -4,6 +4,8 @@
 #include <omp.h>
 #include <string.h>
 #include "kf_launch.h"
+#include <algorithm>
+#include <vector>
 
 namespace kf {
 
@@ -187,6 +189,30 @@ int host_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, 
     }
     out[p] = bi;
   }
+  return 0;
+}
+
+// RegTileArgs on the host: the same sweeps over the whole strip, one at a time
+// (two scratch planes), so a host run equals the device's tiled pass.
+int host_reg_tiled(const RegTileArgs& a) {
+  const int64_t w = a.w, n = (int64_t)a.w * a.h;
+  if (a.nsweep < 1 || a.nsweep > REG_TILE_MAX_SWEEPS || n <= 0) return 1;
+  std::vector<float> cur(a.z, a.z + n), prev(n), nxt(n);
+  if (a.prev_mask & 1u) std::copy(a.zp, a.zp + n, prev.begin());
+  const float* u = a.u + a.j0 * a.ld;
+  const float* v = a.v + a.j0 * a.ld;
+  for (int s = 0; s < a.nsweep; ++s) {
+#pragma omp parallel for schedule(static)
+    for (int64_t p = 0; p < n; ++p) {
+      const int64_t r = p / w, c = p - r * w;
+      const float sn = reg_tile_nsum(cur.data(), p, w, r > 0, r + 1 < a.h, c > 0, c + 1 < w);
+      nxt[p] = reg_tile_step(a, s, sn, u[p], v[p], prev[p]);
+    }
+    std::swap(prev, cur);
+    std::swap(cur, nxt);
+  }
+  std::copy(cur.begin(), cur.end(), a.z_out);
+  std::copy(prev.begin(), prev.end(), a.zp_out);
   return 0;
 }
 

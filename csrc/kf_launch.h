@@ -41,6 +41,7 @@ hipError_t dev_gather(int elem_bytes, const void* src, const int64_t* idx, void*
                       int64_t src_ld, int64_t dst_ld, hipStream_t s);
 hipError_t dev_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out,
                            hipStream_t s);
+hipError_t dev_reg_tiled(const RegTileArgs& a, hipStream_t s);
 
 // Host runner: the same per-pixel code over OpenMP; the block partition
 // mirrors the device grid-stride mapping so partials have the same meaning.
@@ -58,5 +59,6 @@ int host_gp_operator(int np, const BandDesc* b, int nb, const float* x, int64_t 
 int host_unpack(int np, const float* x, const float* a, int64_t N, int64_t ld, const int64_t* idx, float* mean,
                 float* unc, int64_t plane);
 int host_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out);
+int host_reg_tiled(const RegTileArgs& a);
 
 }  // namespace kf

@@ -36,7 +36,7 @@ CHECKED_EXT_PATH = PKG_DIR / f"_kafka_hip_checked{EXT_SUFFIX}"
 HEADERS = ["kf_core.h", "kf_launch.h", "kf_stream.h", "kf_device.h", "kf_gp_mfma.h", "kf_tiff.h"]
 # device translation units (compiled concurrently: the NP = 7 / 10 analysis
 # instantiations dominate the build)
-HIP_SOURCES = ["kf_kernels.hip", "kf_analysis7.hip", "kf_analysis10.hip"]
+HIP_SOURCES = ["kf_kernels.hip", "kf_analysis7.hip", "kf_analysis10.hip", "kf_reg_tiled.hip"]
 
 
 def _pybind_includes() -> list[str]:

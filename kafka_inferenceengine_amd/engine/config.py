@@ -40,6 +40,10 @@ class EngineConfig:
     # solve stops at this looser tolerance (the final iteration uses spatial_tol)
     spatial_tol_first: float = 1e-1
     spatial_max_sweeps: int = 64
+    # one field on a dense strip without halo rows (one rank, or no strip
+    # neighbours): up to 8 sweeps per launch out of LDS (kf_reg_tiled.hip),
+    # bit-identical to one launch per sweep
+    spatial_tiled: bool = True
     jacobi_sweeps: int = 4
     # GP operator placement: fused into the analysis kernel, or "split" (high-
     # occupancy operator kernel -> HBM -> analysis over band chunks)

@@ -151,6 +151,8 @@ class LinearKalman:
         self._reg = None
         self._reg_uv = None             # affine regulariser: u = A_reg^-1 b, V = A_reg^-1 E_R, x0
         self._reg_geo = None
+        self._reg_z4 = None               # 4th regularised-field buffer of the tiled sweeps
+        self.reg_tiled_launches = 0       # K9 temporal-blocking launches (kf_reg_tiled.hip)
         self.reg_overlapped_sweeps = 0    # C2 sweeps whose halo exchange ran under the interior rows
         self._output_written = None
         band = getattr(self.comm, "band", None)
@@ -1133,17 +1135,35 @@ class LinearKalman:
             z[0][i, :N].copy_(x_ref[r, :N])
         cur = reg.fill_halo(z[0])
         prev = None
-        omega = 1.0
+        # Chebyshev semi-iterative weights (omega_1 = 1: the first step is Jacobi)
+        sched, omega = [], 1.0
+        for it in range(sweeps - 1):
+            if rho > 0 and it > 0:
+                omega = 1.0 / (1.0 - 0.5 * rho * rho) if it == 1 else 1.0 / (1.0 - 0.25 * rho * rho * omega)
+            sched.append((omega, rho > 0 and it > 0))
         # C2 overlap (dense or masked strips): the rows the neighbours need first,
         # their exchange posted, then the interior while the rows are on the wire
         overlap = self.comm.distributed and reg.split is not None
         sa, sb = reg.split if overlap else (0, 0)
-        for it in range(sweeps - 1):
+        tiled = (self.config.spatial_tiled and not overlap and k == 1 and geo is not None
+                 and int(geo["halo"]) == 0 and N > 0)
+        if tiled and sched:
+            if self._reg_z4 is None or self._reg_z4.shape != z[0].shape:
+                self._reg_z4 = torch.zeros_like(z[0])
+            spare = [b for b in (*z, self._reg_z4) if b is not cur]
+            prev = spare.pop()
+            for c0 in range(0, len(sched), K.REG_TILE_MAX_SWEEPS):
+                part = sched[c0:c0 + K.REG_TILE_MAX_SWEEPS]
+                o_cur, o_prev = spare[0], spare[1]
+                K.reg_sweeps_tiled(n, u, v, cur, prev, o_cur, o_prev, gamma, reg.reg_mask, N, geo,
+                                   [o for o, _ in part], [c for _, c in part])
+                spare = [cur, prev]
+                cur, prev = o_cur, o_prev
+            self.reg_tiled_launches += -(-len(sched) // K.REG_TILE_MAX_SWEEPS)
+            sched = []
+        for omega, use_prev in sched:
             nxt = next(b for b in z if b is not cur and b is not prev)
-            # Chebyshev semi-iterative weights (omega_1 = 1: the first step is Jacobi)
-            if rho > 0 and it > 0:
-                omega = 1.0 / (1.0 - 0.5 * rho * rho) if it == 1 else 1.0 / (1.0 - 0.25 * rho * rho * omega)
-            zp = prev if (rho > 0 and it > 0) else None
+            zp = prev if use_prev else None
             if overlap:
                 with self.timer.phase("reg_boundary"):
                     K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(0, sa), z_prev=zp,

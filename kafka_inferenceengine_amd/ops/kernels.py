@@ -490,6 +490,45 @@ def reg_sweep(n_params, u, v, z_ext, nbr, z_out, gamma, reg_mask, N, geo=None, r
     ext().jacobi(n_params, a, grid_for(n), _dev(u), _stream(u))
 
 
+REG_TILE_MAX_SWEEPS = 8
+
+
+def reg_sweeps_tiled(n_params, u, v, z, z_prev, z_out, zp_out, gamma, reg_mask, N, geo, omegas, chebyshev):
+    """K9 temporal blocking (csrc/kf_reg_tiled.hip): ``len(omegas)`` (<= 8) sweeps
+    of the one regularised field of a dense strip without halo rows in one
+    launch.  Sweep s is ``reg_sweep(..., z_prev=previous iterate,
+    omega=omegas[s])`` when ``chebyshev[s]``, the plain Jacobi sweep otherwise;
+    bit-identical to those launches.  Writes the last iterate to ``z_out`` and
+    the one before to ``zp_out`` (local parts, [1, >= N])."""
+    check_np(n_params)
+    dev = u.device
+    if bin(int(reg_mask)).count("1") != 1:
+        raise ValueError("reg_sweeps_tiled: one regularised field")
+    if geo is None or int(geo["halo"]) != 0:
+        raise ValueError("reg_sweeps_tiled: dense strip geometry without halo rows")
+    ns = len(omegas)
+    if not 1 <= ns <= REG_TILE_MAX_SWEEPS or len(chebyshev) != ns:
+        raise ValueError(f"reg_sweeps_tiled: 1..{REG_TILE_MAX_SWEEPS} sweeps, one flag per sweep")
+    _check_soa(u, n_params, N, "u", device=dev)
+    _check_soa(v, n_params, N, "v", device=dev)
+    if v.shape[1] != u.shape[1]:
+        raise ValueError("v must share u's leading dimension")
+    for t, nm in ((z, "z"), (z_out, "z_out"), (zp_out, "zp_out")):
+        _check_soa(t, 1, N, nm, device=dev)
+    mask = sum(1 << s for s, c in enumerate(chebyshev) if c)
+    if mask & 1:
+        if z_prev is None:
+            raise ValueError("reg_sweeps_tiled: the first sweep is a Chebyshev step but z_prev is None")
+        _check_soa(z_prev, 1, N, "z_prev", device=dev)
+    ptrs = {t.data_ptr() for t in (z, z_out, zp_out)}
+    if len(ptrs) != 3 or (z_prev is not None and z_prev.data_ptr() in (z_out.data_ptr(), zp_out.data_ptr())):
+        raise ValueError("reg_sweeps_tiled: outputs must not alias the inputs")
+    _set_geo(ext().JacobiArgs(), geo, N)   # validates w * h == N
+    j0 = (int(reg_mask) & -int(reg_mask)).bit_length() - 1
+    ext().reg_tiled(u.shape[1], int(geo["w"]), int(geo["h"]), j0, mask, float(gamma), [float(o) for o in omegas],
+                    _ptr(u), _ptr(v), _ptr(z), _ptr(z_prev), _ptr(z_out), _ptr(zp_out), _dev(u), _stream(u))
+
+
 def reg_finish(n_params, u, v, z_ext, nbr, x_ref, x_out, gamma, reg_mask, N, partials=None, geo=None, out=None,
                a_prec=None):
     """K9 affine form, last sweep: x = u + g V s(z_ext) for every parameter, with

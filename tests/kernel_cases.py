@@ -121,3 +121,27 @@ def fused_vs_materialized(device, mode, blend=False, quirk=False, prop_mask=0, N
 
 FUSED_CASES = [(1, False, False, 1 << 6), (1, False, False, 0b1010011), (0, False, False, 0),
                (2, False, False, 0)]
+
+
+def tiled_vs_sequential(device, h=150, w=300, omegas=(1.0, 1.3, 1.2, 1.25, 1.22), cheb=None, n=7, j0=2, seed=5):
+    """K9 temporal blocking (reg_sweeps_tiled) against one reg_sweep launch per
+    sweep on a dense strip without halo rows.  Returns ((z, zp) tiled, (z, zp)
+    sequential) as CPU tensors."""
+    rng = np.random.default_rng(seed)
+    N = h * w
+    ld = N + 64
+    geo = {"w": w, "h": h, "halo": 0, "n_up": 0}
+    cheb = [s > 0 for s in range(len(omegas))] if cheb is None else list(cheb)
+    u = torch.tensor(rng.normal(size=(n, ld)), dtype=torch.float32, device=device)
+    v = torch.tensor(rng.uniform(0.0, 0.2, size=(n, ld)), dtype=torch.float32, device=device)
+    z0 = torch.tensor(rng.normal(size=(1, ld)), dtype=torch.float32, device=device)
+    zm1 = torch.tensor(rng.normal(size=(1, ld)), dtype=torch.float32, device=device)
+    gamma, mask = 0.9, 1 << j0
+    zo, zpo = (torch.zeros(1, ld, device=device) for _ in range(2))
+    K.reg_sweeps_tiled(n, u, v, z0, zm1, zo, zpo, gamma, mask, N, geo, list(omegas), cheb)
+    cur, prev = z0.clone(), zm1.clone()
+    for om, c in zip(omegas, cheb):
+        nxt = torch.zeros(1, ld, device=device)
+        K.reg_sweep(n, u, v, cur, None, nxt, gamma, mask, N, geo=geo, z_prev=prev if c else None, omega=om)
+        prev, cur = cur, nxt
+    return (zo[:, :N].cpu(), zpo[:, :N].cpu()), (cur[:, :N].cpu(), prev[:, :N].cpu())

@@ -539,3 +539,24 @@ def test_reference_protocol_factory_at_1024_squared_is_fast():
     gref = ((1.0 - np.tanh(X) ** 2) * w[None, :]).T
     assert np.allclose(h[:, valid], gref[:, valid], rtol=1e-5, atol=1e-6)
     assert np.all(h[:, ~valid] == 0)
+
+
+def _spatial_dense_run(device, tiled, size=(40, 36)):
+    mask = np.ones(size, bool)
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(3)]
+    obs = k.SyntheticBHRObservations(mask, n_train=40, device=device, stream=False, n_pool=2, field_cell=8)
+    kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device=device,
+                        config=k.EngineConfig(spatial_gamma=20.0, spatial_params=[6], spatial_tiled=tiled,
+                                              spatial_tol=1e-6))
+    kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+    st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
+    return st.x.cpu(), kf.reg_tiled_launches
+
+
+def test_spatial_tiled_sweeps_equal_per_sweep_launches():
+    """K9 temporal blocking (several sweeps per launch) changes nothing: the
+    same states bit for bit as one launch per sweep (dense tile, one rank)."""
+    a, na = _spatial_dense_run("cpu", True)
+    b, nb = _spatial_dense_run("cpu", False)
+    assert na > 0 and nb == 0
+    assert torch.equal(a, b)

@@ -326,3 +326,23 @@ def test_checked_build_smoke_on_device(cuda):
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     assert "smoke ok" in r.stdout and "_kafka_hip_checked" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.parametrize("case", [dict(h=300, w=1000, omegas=(1.0, 1.3, 1.2, 1.25, 1.22, 1.21, 1.2, 1.2)),
+                                  dict(h=130, w=257, omegas=(1.1, 1.2, 1.3), cheb=(True, True, False)),
+                                  dict(h=7, w=5, omegas=(1.0,) * 8), dict(h=64, w=128, omegas=(1.0,), cheb=(False,))])
+def test_reg_sweeps_tiled_equals_sequential_on_device(cuda, case):
+    """The LDS-tiled multi-sweep kernel is bit-identical to one row-loop sweep
+    launch per sweep (partial tiles, domain edges, Jacobi and Chebyshev steps)."""
+    (zt, zpt), (zs, zps) = C.tiled_vs_sequential(cuda, **case)
+    assert torch.equal(zt, zs) and torch.equal(zpt, zps)
+    (ht, hpt), _ = C.tiled_vs_sequential("cpu", **case)
+    assert torch.equal(zt, ht) and torch.equal(zpt, hpt)
+
+
+def test_spatial_tiled_sweeps_equal_per_sweep_launches_on_device(cuda):
+    from test_engine import _spatial_dense_run
+    a, na = _spatial_dense_run(cuda, True, size=(200, 300))
+    b, nb = _spatial_dense_run(cuda, False, size=(200, 300))
+    assert na > 0 and nb == 0
+    assert torch.equal(a, b)

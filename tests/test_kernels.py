@@ -392,3 +392,27 @@ def test_dense_geometry_equals_neighbour_table():
     holes = mask.copy()
     holes[7, 3] = False
     assert StripPartition(holes, 1, 3).dense_geometry() is None
+
+
+@pytest.mark.parametrize("case", [dict(), dict(omegas=(1.1, 1.2, 1.3), cheb=(True, True, False)),
+                                  dict(h=7, w=5, omegas=(1.0,) * 8), dict(omegas=(1.0,), cheb=(False,))])
+def test_reg_sweeps_tiled_equals_sequential(case):
+    (zt, zpt), (zs, zps) = C.tiled_vs_sequential("cpu", **case)
+    assert torch.equal(zt, zs) and torch.equal(zpt, zps)
+
+
+def test_reg_sweeps_tiled_rejects_bad_args():
+    u = torch.zeros(7, 100)
+    z = torch.zeros(1, 100)
+    geo = {"w": 10, "h": 10, "halo": 0, "n_up": 0}
+    with pytest.raises(ValueError):
+        K.reg_sweeps_tiled(7, u, u, z, None, torch.zeros(1, 100), torch.zeros(1, 100), 1.0, 4, 100,
+                           dict(geo, halo=1), [1.0], [False])
+    with pytest.raises(ValueError):
+        K.reg_sweeps_tiled(7, u, u, z, None, torch.zeros(1, 100), torch.zeros(1, 100), 1.0, 4, 100, geo,
+                           [1.0] * 9, [False] * 9)
+    with pytest.raises(ValueError):
+        K.reg_sweeps_tiled(7, u, u, z, None, torch.zeros(1, 100), torch.zeros(1, 100), 1.0, 4, 100, geo,
+                           [1.0], [True])
+    with pytest.raises(ValueError):
+        K.reg_sweeps_tiled(7, u, u, z, None, z, torch.zeros(1, 100), 1.0, 4, 100, geo, [1.0], [False])
