@@ -250,6 +250,10 @@ __global__ __launch_bounds__(BLOCK) void jacobi_kernel(JacobiArgs a) {
         else acc += (double)reg_finish1d<NP, UU, BLOCK>(a, r, c0);
       }
     }
+  } else if constexpr (MODE == JACOBI_FINISH4) {
+    // 4-pixel groups of whole rows (w % 4 == 0 and 16-byte alignment: launcher)
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n / 4; i += stride)
+      acc += (double)reg_finish4<NP>(a, a.p0 + 4 * i);
   } else if constexpr (MODE == JACOBI_SWEEP1 || MODE == JACOBI_FINISH1) {
     for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += JACOBI_U * stride) {
       if constexpr (MODE == JACOBI_SWEEP1) reg_sweep1<NP, JACOBI_U>(a, i, stride, n);

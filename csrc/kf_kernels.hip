@@ -49,6 +49,16 @@ static void l_jacobi(const JacobiArgs& a, int grid, hipStream_t s) {
   // dense strip, whole rows: the row-loop kernels (no per-pixel index division)
   const int64_t n = a.pn > 0 ? a.pn : a.N;
   const bool rows = one && a.geo.w > 0 && a.p0 % a.geo.w == 0 && n % a.geo.w == 0 && n > 0;
+  const auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  const bool four = rows && a.mode == JACOBI_FINISH && a.geo.w % 4 == 0 && a.ld % 4 == 0 && a.ld_ext % 4 == 0 &&
+                    a.p0 % 4 == 0 && a.N % 4 == 0 && al16(a.u) && al16(a.v) && al16(a.x_ext) && al16(a.x_ref) &&
+                    al16(a.x_out) &&
+                    (!a.out_mean || (!a.out_idx && a.out_plane % 4 == 0 && al16(a.out_mean) && al16(a.out_unc) &&
+                                     al16(a.a_in)));
+  if (four) {
+    hipLaunchKernelGGL((jacobi_kernel<NP, JACOBI_FINISH4>), dim3(grid), dim3(BLOCK), 0, s, a);
+    return;
+  }
   if (rows && (a.mode == JACOBI_SWEEP || a.mode == JACOBI_FINISH)) {
     const int64_t nr = n / a.geo.w;
     const int g = (int)(nr < grid ? nr : grid);   // partials hold >= grid entries

@@ -145,3 +145,29 @@ def tiled_vs_sequential(device, h=150, w=300, omegas=(1.0, 1.3, 1.2, 1.25, 1.22)
         K.reg_sweep(n, u, v, cur, None, nxt, gamma, mask, N, geo=geo, z_prev=prev if c else None, omega=om)
         prev, cur = cur, nxt
     return (zo[:, :N].cpu(), zpo[:, :N].cpu()), (cur[:, :N].cpu(), prev[:, :N].cpu())
+
+
+def dense_finish(device, h_total=30, w=44, ranks=3, rank=1, n=7, j0=6, out=True, seed=9):
+    """reg_finish on a dense strip of a ``ranks``-strip partition (halo rows
+    above/below) with the output dump; returns (x_out, mean, unc) on the CPU.
+    On the device with w % 4 == 0 this takes the 16-byte path (FINISH4)."""
+    from kafka_inferenceengine_amd.parallel import StripPartition
+    rng = np.random.default_rng(seed)
+    part = StripPartition(np.ones((h_total, w), bool), rank, ranks)
+    geo = part.dense_geometry()
+    N = part.N
+    lay = part.halo_layout()
+    cols = N + lay["n_up"] + lay["n_down"]
+    ld = N + 12
+    mk = lambda r, c, lo=-1.0, hi=1.0: torch.tensor(rng.uniform(lo, hi, size=(r, c)), dtype=torch.float32,
+                                                   device=device)
+    u, v, xr = mk(n, ld), mk(n, ld, 0.0, 0.2), mk(n, ld)
+    z = mk(1, cols)
+    a_prec = mk(n * (n + 1) // 2, ld, 0.5, 4.0)
+    xo = torch.zeros(n, ld, device=device)
+    part_buf = torch.zeros(4096, dtype=torch.float64, device=device)
+    mean = torch.zeros(n, N, device=device)
+    unc = torch.zeros(n, N, device=device)
+    K.reg_finish(n, u, v, z, None, xr, xo, 0.8, 1 << j0, N, partials=part_buf, geo=geo,
+                 out=(mean, unc, None) if out else None, a_prec=a_prec if out else None)
+    return xo[:, :N].cpu(), mean.cpu(), unc.cpu(), float(part_buf.sum())

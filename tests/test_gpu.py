@@ -346,3 +346,16 @@ def test_spatial_tiled_sweeps_equal_per_sweep_launches_on_device(cuda):
     b, nb = _spatial_dense_run(cuda, False, size=(200, 300))
     assert na > 0 and nb == 0
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("rank,out", [(0, True), (1, True), (2, False), (1, False)])
+def test_dense_finish_vectorised_equals_host(cuda, rank, out):
+    """The 16-byte finish (4 pixels of a row per thread) equals the host's
+    per-pixel finish bit for bit (x, output mean), halo rows included;
+    the norm partials agree to rounding (different summation order)."""
+    d = C.dense_finish(cuda, rank=rank, out=out)
+    h = C.dense_finish("cpu", rank=rank, out=out)
+    assert torch.equal(d[0], h[0]) and torch.equal(d[1], h[1])
+    # 1/sqrt(diag A): the device's rsqrt differs from the host's in the last bit
+    assert torch.allclose(d[2], h[2], rtol=2e-7, atol=0)
+    assert abs(d[3] - h[3]) <= 1e-5 * abs(h[3])
