@@ -290,6 +290,44 @@ KF_HD int64_t opaque_lane(int64_t v) {
   return v;
 }
 
+// Pixel p of an SoA row: `row` (array + r * ld) is wave-uniform and p's byte
+// offset is formed in 32 bits, so gfx950 addresses the element as SGPR base +
+// 32-bit VGPR offset (global_load/store saddr form) -- one offset VGPR shared
+// by every row instead of a 64-bit VGPR address (2 VALU, 2 VGPRs) per access.
+// Valid while N * sizeof(T) < 2^32: the host wrappers (ops/kernels.py) bound
+// N, out_plane < 2^30.
+// The row base goes through an SGPR asm operand (as a global-address-space
+// pointer, so the access stays a global_* instruction) so the optimiser cannot
+// fold it and the lane offset into one 64-bit VGPR sum: every row passed here
+// must be wave-uniform (kernel arguments, BandDesc fields, uniform row indices).
+template <typename T>
+KF_HD T* pxp(T* row, int64_t p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __attribute__((address_space(1))) char* g = (__attribute__((address_space(1))) char*)row;
+  asm volatile("" : "+s"(g));
+  return (T*)(g + (uint32_t)((uint32_t)p * (uint32_t)sizeof(T)));
+#else
+  return (T*)((char*)row + (uint32_t)((uint32_t)p * (uint32_t)sizeof(T)));
+#endif
+}
+template <typename T>
+KF_HD const T* pxp(const T* row, int64_t p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __attribute__((address_space(1))) char* g = (const __attribute__((address_space(1))) char*)row;
+  asm volatile("" : "+s"(g));
+  return (const T*)(g + (uint32_t)((uint32_t)p * (uint32_t)sizeof(T)));
+#else
+  return (const T*)((const char*)row + (uint32_t)((uint32_t)p * (uint32_t)sizeof(T)));
+#endif
+}
+// KF_PXS: the SGPR-base form (pxp); KF_PX: plain 64-bit indexing.  The SGPR
+// form is used where the row bases are short-lived (the analysis epilogue's
+// stores, after the GP loop): applied to every access it kept ~60 row bases
+// live in SGPRs across the fused Gauss-Newton loop and spilled them to VGPR
+// lanes (186 spill slots, 171 VGPRs: one wave per SIMD fewer).
+#define KF_PXS(base, off, p) (*::kf::pxp((base) + (off), (p)))
+#define KF_PX(base, off, p) ((base)[(off) + (p)])
+
 // In-place packed Cholesky A = U^T U (U upper, stored in A's packed slots).
 // Convention: the diagonal slots hold 1 / U_jj (what the solves multiply by);
 // only chol_solve / chol_inverse read a factor.
@@ -376,7 +414,7 @@ KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y_out, float& w_out)
   // references made the compiler spill (y, w) to scratch in generic kernels
   float y = 0.f, w = 0.f;
   if (FOBS == OBS_DN16 || (FOBS == 0 && bd.obs == OBS_DN16)) {
-    const uint16_t dn = bd.dn[p];
+    const uint16_t dn = KF_PX(bd.dn, 0, p);
     const float yd = (float)dn * bd.scale;
     const float sig = fmaxf(bd.rel_unc * yd, bd.unc_floor);
     const bool ok = dn > 0 && sig > 0.f;
@@ -385,14 +423,14 @@ KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y_out, float& w_out)
   } else if (FOBS == OBS_F32 || FOBS == OBS_BF16 || (FOBS == 0 && (bd.obs == OBS_F32 || bd.obs == OBS_BF16))) {
     float yv, wv;
     if (FOBS == OBS_F32 || (FOBS == 0 && bd.obs == OBS_F32)) {
-      yv = bd.y[p];
-      wv = bd.w[p];
+      yv = KF_PX(bd.y, 0, p);
+      wv = KF_PX(bd.w, 0, p);
     } else {
       // bf16 (y, w) pairs: half the ingest bytes of f32; math stays f32
       yv = bf16_to_f32(reinterpret_cast<const uint16_t*>(bd.y)[p]);
       wv = bf16_to_f32(reinterpret_cast<const uint16_t*>(bd.w)[p]);
     }
-    const bool keep = (!bd.mask || bd.mask[p]) && (wv > 0.f) && finitef(wv) && finitef(yv);
+    const bool keep = (!bd.mask || KF_PX(bd.mask, 0, p)) && (wv > 0.f) && finitef(wv) && finitef(yv);
     y = keep ? yv : 0.f;
     w = keep ? wv : 0.f;
   } else if (FOBS == OBS_BF16Y || (FOBS == 0 && bd.obs == OBS_BF16Y)) {
@@ -400,7 +438,7 @@ KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y_out, float& w_out)
     // weight follows the relative-uncertainty model of the DN16 path
     const float yv = bf16_to_f32(reinterpret_cast<const uint16_t*>(bd.y)[p]);
     const float sig = fmaxf(bd.rel_unc * fabsf(yv), bd.unc_floor);
-    const bool keep = (!bd.mask || bd.mask[p]) && finitef(yv) && sig > 0.f;
+    const bool keep = (!bd.mask || KF_PX(bd.mask, 0, p)) && finitef(yv) && sig > 0.f;
     y = keep ? yv : 0.f;
     w = keep ? kf_rcp(sig * sig) : 0.f;
   }
@@ -576,7 +614,7 @@ KF_HD bool sar_eval(const BandDesc& bd, int64_t p, const float (&x)[NP], float& 
   const float V = gather_state<NP>(x, bd.map[0]);
   const float SM = gather_state<NP>(x, bd.map[1]);
   const float A = bd.coef[0], B = bd.coef[1], C = bd.coef[2], Dc = bd.coef[3], E = bd.coef[4];
-  const float th = bd.aux ? bd.aux[p] : bd.coef[5];
+  const float th = bd.aux ? KF_PX(bd.aux, 0, p) : bd.coef[5];
   const float mu = cosf(th * DEG2RAD);
   const bool ok = (V > 0.f) && (SM > 0.f);
   const float Vs = ok ? V : 1.f;
@@ -625,9 +663,9 @@ KF_HD bool eval_operator(const BandDesc& bd, int64_t p, int64_t ld, const float 
       H0 = t;
     } break;
     default: {  // OP_PRECOMP
-      H0 = bd.pre_h0[p];
+      H0 = KF_PX(bd.pre_h0, 0, p);
 #pragma unroll
-      for (int j = 0; j < NP; ++j) h[j] = bd.pre_h[j * bd.pre_ld + p];
+      for (int j = 0; j < NP; ++j) h[j] = KF_PX(bd.pre_h, j * bd.pre_ld, p);
     }
   }
   bool fin = finitef(H0);
@@ -648,7 +686,7 @@ template <int NP>
 KF_HD void forecast_partial_mean(const KF_CONST_AS PropArgs* a, int64_t p, float (&xf)[NP]) {
 #pragma unroll
   for (int j = 0; j < NP; ++j)
-    xf[j] = ((a->prop_mask >> j) & 1u) ? a->m[j] * a->x_a[j * a->ld + p] : a->reset_mean[j];
+    xf[j] = ((a->prop_mask >> j) & 1u) ? a->m[j] * KF_PX(a->x_a, j * a->ld, p) : a->reset_mean[j];
 }
 
 template <int NP>
@@ -659,8 +697,8 @@ KF_HD void forecast_partial_precision(const KF_CONST_AS PropArgs* a, int64_t p, 
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
     if ((a->prop_mask >> j) & 1u) {
-      const float q = a->q_pix ? a->q_pix[j * ld + p] : a->q[j];
-      P[tri(NP, j, j)] = kf_rcp(kf_rcp(a->p_a[tri(NP, j, j) * ld + p]) + q);
+      const float q = a->q_pix ? KF_PX(a->q_pix, j * ld, p) : a->q[j];
+      P[tri(NP, j, j)] = kf_rcp(kf_rcp(KF_PX(a->p_a, tri(NP, j, j) * ld, p)) + q);
     }
   }
 }
@@ -680,7 +718,7 @@ KF_HD uint8_t forecast_pixel(const PropArgs& a, int64_t p, float (&xf)[NP], floa
   uint8_t st = 0;
   float q[NP];
 #pragma unroll
-  for (int j = 0; j < NP; ++j) q[j] = a.q_pix ? a.q_pix[j * ld + p] : a.q[j];
+  for (int j = 0; j < NP; ++j) q[j] = a.q_pix ? KF_PX(a.q_pix, j * ld, p) : a.q[j];
 
   switch (a.mode) {
     case PROP_PRIOR: {
@@ -695,31 +733,31 @@ KF_HD uint8_t forecast_pixel(const PropArgs& a, int64_t p, float (&xf)[NP], floa
 #pragma unroll
       for (int j = 0; j < NP; ++j) {
         const bool pj = (a.prop_mask >> j) & 1u;
-        xf[j] = pj ? a.m[j] * a.x_a[j * ld + p] : a.reset_mean[j];
+        xf[j] = pj ? a.m[j] * KF_PX(a.x_a, j * ld, p) : a.reset_mean[j];
         if (pj) {
-          const float pa = a.p_a[tri(NP, j, j) * ld + p];
+          const float pa = KF_PX(a.p_a, tri(NP, j, j) * ld, p);
           P[tri(NP, j, j)] = kf_rcp(kf_rcp(pa) + q[j]);   // same rounding as forecast_partial
         }
       }
     } break;
     case PROP_INFO_APPROX: {
 #pragma unroll
-      for (int j = 0; j < NP; ++j) xf[j] = a.m[j] * a.x_a[j * ld + p];
+      for (int j = 0; j < NP; ++j) xf[j] = a.m[j] * KF_PX(a.x_a, j * ld, p);
 #pragma unroll
       for (int t = 0; t < NT; ++t) P[t] = 0.f;
 #pragma unroll
       for (int j = 0; j < NP; ++j) {
-        const float d = a.p_a[tri(NP, j, j) * ld + p];
+        const float d = KF_PX(a.p_a, tri(NP, j, j) * ld, p);
         P[tri(NP, j, j)] = d / (1.f + d * q[j]);
       }
     } break;
     case PROP_INFO_EXACT: {
       // P_f^-1 = (I + P_a^-1 Q)^-1 P_a^-1 = (P_a + Q)^-1
 #pragma unroll
-      for (int j = 0; j < NP; ++j) xf[j] = a.m[j] * a.x_a[j * ld + p];
+      for (int j = 0; j < NP; ++j) xf[j] = a.m[j] * KF_PX(a.x_a, j * ld, p);
       float U[NT];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) U[t] = a.p_a[t * ld + p];
+      for (int t = 0; t < NT; ++t) U[t] = KF_PX(a.p_a, t * ld, p);
       bool ok = chol_packed<NP>(U);
       float C[NT];
       chol_inverse<NP>(U, C);
@@ -731,17 +769,17 @@ KF_HD uint8_t forecast_pixel(const PropArgs& a, int64_t p, float (&xf)[NP], floa
     } break;
     case PROP_STANDARD: {
 #pragma unroll
-      for (int j = 0; j < NP; ++j) xf[j] = a.m[j] * a.x_a[j * ld + p];
+      for (int j = 0; j < NP; ++j) xf[j] = a.m[j] * KF_PX(a.x_a, j * ld, p);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) P[t] = a.p_a[t * ld + p];
+      for (int t = 0; t < NT; ++t) P[t] = KF_PX(a.p_a, t * ld, p);
 #pragma unroll
       for (int j = 0; j < NP; ++j) P[tri(NP, j, j)] += q[j];
     } break;
     default: {  // PROP_IDENTITY
 #pragma unroll
-      for (int j = 0; j < NP; ++j) xf[j] = a.m[j] * a.x_a[j * ld + p];
+      for (int j = 0; j < NP; ++j) xf[j] = a.m[j] * KF_PX(a.x_a, j * ld, p);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) P[t] = a.p_a[t * ld + p];
+      for (int t = 0; t < NT; ++t) P[t] = KF_PX(a.p_a, t * ld, p);
     }
   }
 
@@ -749,9 +787,9 @@ KF_HD uint8_t forecast_pixel(const PropArgs& a, int64_t p, float (&xf)[NP], floa
     // Gaussian product of forecast (xf, P) with prior (mu, C^-1) (kf_tools.py:75-96).
     float mu[NP], Ci[NT];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) mu[j] = a.blend_mean_pix ? a.blend_mean_pix[j * ld + p] : a.blend_mean[j];
+    for (int j = 0; j < NP; ++j) mu[j] = a.blend_mean_pix ? KF_PX(a.blend_mean_pix, j * ld, p) : a.blend_mean[j];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) Ci[t] = a.blend_cinv_pix ? a.blend_cinv_pix[t * ld + p] : a.blend_cinv[t];
+    for (int t = 0; t < NT; ++t) Ci[t] = a.blend_cinv_pix ? KF_PX(a.blend_cinv_pix, t * ld, p) : a.blend_cinv[t];
     float b1[NP], b2[NP];
     if (a.quirk_blend) {  // reference operand swap (kf_tools.py:90)
       symv<NP>(P, mu, b1);
@@ -780,10 +818,10 @@ KF_HD void pixel_propagate(const PropArgs& a, int64_t p) {
   float xf[NP], P[NT];
   const uint8_t st = forecast_pixel<NP>(a, p, xf, P);
 #pragma unroll
-  for (int j = 0; j < NP; ++j) a.x_f[j * ld + p] = xf[j];
+  for (int j = 0; j < NP; ++j) KF_PX(a.x_f, j * ld, p) = xf[j];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) a.p_f[t * ld + p] = P[t];
-  if (a.status) a.status[p] |= st;
+  for (int t = 0; t < NT; ++t) KF_PX(a.p_f, t * ld, p) = P[t];
+  if (a.status) KF_PX(a.status, 0, p) |= st;
 }
 
 // Full-form right-hand side b = r + A x0 from the correction form r (DELTA).
@@ -814,7 +852,7 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
   const int64_t ld = a->ld;
   if (store && a->x0_out) {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) a->x0_out[j * ld + p] = x0[j];
+    for (int j = 0; j < NP; ++j) KF_PXS(a->x0_out, j * ld, p) = x0[j];
   }
   if (DELTA && (a->reg_v || a->b_out)) delta_to_full<NP>(A, x0, b);
   if (a->reg_v) {
@@ -832,7 +870,7 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
       if ((a->reg_mask >> j) & 1u) A[tri(NP, j, j)] += gd;
     if (a->a_out) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = A[t];
+      for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = A[t];
     }
     const bool spd = chol_packed<NP>(A);
     chol_solve<NP>(A, b);
@@ -851,17 +889,17 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
         forecast_partial<NP>(opaque(cptr(a->prop)), p, b, Af);
       } else {
 #pragma unroll
-        for (int j = 0; j < NP; ++j) b[j] = a->x_f[j * ld + p];
+        for (int j = 0; j < NP; ++j) b[j] = KF_PXS(a->x_f, j * ld, p);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) Af[t] = a->pf_inv[t * ld + p];
+        for (int t = 0; t < NT; ++t) Af[t] = KF_PXS(a->pf_inv, t * ld, p);
       }
       if (a->a_out) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = Af[t];
+        for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = Af[t];
       }
     }
 #pragma unroll
-    for (int j = 0; j < NP; ++j) a->x_out[j * ld + p] = b[j];
+    for (int j = 0; j < NP; ++j) KF_PXS(a->x_out, j * ld, p) = b[j];
     int c = 0;
 #pragma unroll
     for (int r = 0; r < NP; ++r) {
@@ -871,20 +909,20 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
         for (int j = 0; j < NP; ++j) e[j] = (j == r) ? 1.f : 0.f;
         chol_solve<NP>(A, e);
 #pragma unroll
-        for (int j = 0; j < NP; ++j) a->reg_v[((int64_t)c * NP + j) * ld + p] = bad ? 0.f : e[j];
+        for (int j = 0; j < NP; ++j) KF_PXS(a->reg_v, ((int64_t)c * NP + j) * ld, p) = bad ? 0.f : e[j];
         ++c;
       }
     }
-    if (a->status) a->status[p] = st;
+    if (a->status) KF_PXS(a->status, 0, p) = st;
     return 0.f;
   }
   if (store && a->a_out) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = A[t];
+    for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = A[t];
   }
   if (store && a->b_out) {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) a->b_out[j * ld + p] = b[j];
+    for (int j = 0; j < NP; ++j) KF_PXS(a->b_out, j * ld, p) = b[j];
   }
   float dn = 0.f;
   if (a->solve) {
@@ -907,35 +945,35 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
         forecast_partial<NP>(opaque(cptr(a->prop)), p, b, A);   // rare path: recompute instead of keeping it live
       } else {
 #pragma unroll
-        for (int j = 0; j < NP; ++j) b[j] = a->x_f[j * ld + p];
+        for (int j = 0; j < NP; ++j) b[j] = KF_PXS(a->x_f, j * ld, p);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) A[t] = a->pf_inv[t * ld + p];
+        for (int t = 0; t < NT; ++t) A[t] = KF_PXS(a->pf_inv, t * ld, p);
       }
 #pragma unroll
       for (int j = 0; j < NP; ++j) dA[j] = A[tri(NP, j, j)];
       if (store && a->a_out) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) a->a_out[t * ld + p] = A[t];
+        for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = A[t];
       }
     }
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      if (store) a->x_out[j * ld + p] = b[j];
+      if (store) KF_PXS(a->x_out, j * ld, p) = b[j];
       const float d = b[j] - x0[j];
       dn = fmaf(d, d, dn);
     }
     if (store && a->out_mean) {
       // fused output dump: the unpack pass's work without re-reading x and A
-      const int64_t r = a->out_idx ? a->out_idx[p] : p;
+      const int64_t r = a->out_idx ? KF_PXS(a->out_idx, 0, p) : p;
       const int64_t pl = a->out_plane;
 #pragma unroll
       for (int j = 0; j < NP; ++j) {
-        a->out_mean[j * pl + r] = b[j];
-        a->out_unc[j * pl + r] = kf_rsqrt(dA[j]);
+        KF_PXS(a->out_mean, j * pl, r) = b[j];
+        KF_PXS(a->out_unc, j * pl, r) = kf_rsqrt(dA[j]);
       }
     }
   }
-  if (store && a->status) a->status[p] = st;
+  if (store && a->status) KF_PXS(a->status, 0, p) = st;
   return dn;
 }
 
@@ -972,7 +1010,7 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
   float x0[NP], A[NT], b[NP];
   if (a.x_prev) {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
+    for (int j = 0; j < NP; ++j) x0[j] = KF_PX(a.x_prev, j * ld, p);
   }
   dn_first = 0.f;
   for (int it = 0;; ++it) {
@@ -991,9 +1029,9 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
   } else if (a.a_in) {
     // band-chunked accumulation: continue from a previous chunk's (A, b)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) A[t] = a.a_in[t * ld + p];
+    for (int t = 0; t < NT; ++t) A[t] = KF_PX(a.a_in, t * ld, p);
 #pragma unroll
-    for (int j = 0; j < NP; ++j) b[j] = a.b_in[j * ld + p];
+    for (int j = 0; j < NP; ++j) b[j] = KF_PX(a.b_in, j * ld, p);
     if (DELTA) {
       float t[NP];
       symv<NP>(A, x0, t);
@@ -1003,9 +1041,9 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
   } else {
     float xf[NP];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) xf[j] = a.x_f[j * ld + p];
+    for (int j = 0; j < NP; ++j) xf[j] = KF_PX(a.x_f, j * ld, p);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) A[t] = a.pf_inv[t * ld + p];
+    for (int t = 0; t < NT; ++t) A[t] = KF_PX(a.pf_inv, t * ld, p);
     prior_rhs<NP, DELTA>(A, xf, x0, b);
   }
   int nobs = 0;
@@ -1014,7 +1052,7 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
     float y, w;
     decode_obs<FOBS>(bd, p, y, w);
     if (!(w > 0.f)) {
-      if (bd.h0_out) bd.h0_out[p] = 0.f;
+      if (bd.h0_out) KF_PX(bd.h0_out, 0, p) = 0.f;
       continue;
     }
     float H0, h[NP];
@@ -1030,11 +1068,11 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
       for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);
     } else if constexpr (FD == FD_PRECOMP) {
       // precomputed operator (split GP path / host factories): H0, h from HBM
-      H0 = bd.pre_h0[p];
+      H0 = KF_PX(bd.pre_h0, 0, p);
       ok = finitef(H0);
 #pragma unroll
       for (int j = 0; j < NP; ++j) {
-        h[j] = bd.pre_h[j * bd.pre_ld + p];
+        h[j] = KF_PX(bd.pre_h, j * bd.pre_ld, p);
         ok = ok && finitef(h[j]);
       }
     } else if constexpr (FD == FD_LINEAR) {
@@ -1051,7 +1089,7 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (FD > 0) h0o = opaque(cptr(a.bands + bi))->h0_out;   // not live across the GP loop
 #endif
-    if (h0o) h0o[p] = H0;
+    if (h0o) KF_PX(h0o, 0, p) = H0;
     if (!ok) { st |= ST_BAD_OP; continue; }
     ++nobs;
     float yp;
@@ -1108,11 +1146,11 @@ KF_HD bool pixel_invert(const float* src, float* dst, int64_t ld, int64_t p) {
   constexpr int NT = ntri(NP);
   float U[NT], R[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) U[t] = src[t * ld + p];
+  for (int t = 0; t < NT; ++t) U[t] = KF_PX(src, t * ld, p);
   const bool ok = chol_packed<NP>(U);
   chol_inverse<NP>(U, R);
 #pragma unroll
-  for (int t = 0; t < NT; ++t) dst[t * ld + p] = R[t];
+  for (int t = 0; t < NT; ++t) KF_PX(dst, t * ld, p) = R[t];
   return ok;
 }
 
@@ -1162,13 +1200,13 @@ KF_HD uint8_t forecast_partial_cov(const KF_CONST_AS PropArgs* a, int64_t p, flo
   if (a->prop_mask) {
     float U[NT], Pi[NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) U[t] = a->p_a[t * ld + p];
+    for (int t = 0; t < NT; ++t) U[t] = KF_PX(a->p_a, t * ld, p);
     if (!chol_packed<NP>(U)) st |= ST_NONSPD;
     chol_inverse<NP>(U, Pi);
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
       if ((a->prop_mask >> j) & 1u) {
-        const float q = a->q_pix ? a->q_pix[j * ld + p] : a->q[j];
+        const float q = a->q_pix ? KF_PX(a->q_pix, j * ld, p) : a->q[j];
         C[tri(NP, j, j)] = kf_rcp(kf_rcp(Pi[tri(NP, j, j)]) + q);
       }
     }
@@ -1224,13 +1262,13 @@ KF_HD float pixel_gain(const GainArgs& a, int64_t p) {
     st |= forecast_partial_cov<NP>(opaque(cptr(a.prop)), p, x, P);
   } else {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) x[j] = a.x_f[j * ld + p];
+    for (int j = 0; j < NP; ++j) x[j] = KF_PX(a.x_f, j * ld, p);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) P[t] = a.p_f[t * ld + p];
+    for (int t = 0; t < NT; ++t) P[t] = KF_PX(a.p_f, t * ld, p);
   }
   if (a.x_prev) {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
+    for (int j = 0; j < NP; ++j) x0[j] = KF_PX(a.x_prev, j * ld, p);
   } else {
 #pragma unroll
     for (int j = 0; j < NP; ++j) x0[j] = x[j];
@@ -1240,7 +1278,7 @@ KF_HD float pixel_gain(const GainArgs& a, int64_t p) {
     const BandDesc bd = cptr(a.bands)[bi];
     float y, w;
     decode_obs<FOBS>(bd, p, y, w);
-    if (!(w > 0.f)) { if (bd.h0_out) bd.h0_out[p] = 0.f; continue; }
+    if (!(w > 0.f)) { if (bd.h0_out) KF_PX(bd.h0_out, 0, p) = 0.f; continue; }
     float H0, h[NP];
     bool ok;
     if constexpr (FD > 0) {
@@ -1259,7 +1297,7 @@ KF_HD float pixel_gain(const GainArgs& a, int64_t p) {
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (FD > 0) h0o = opaque(cptr(a.bands + bi))->h0_out;
 #endif
-    if (h0o) h0o[p] = H0;
+    if (h0o) KF_PX(h0o, 0, p) = H0;
     if (!ok) { st |= ST_BAD_OP; continue; }
     ++nobs;
     gain_band_update<NP>(P, x, x0, h, H0, y, w, a.joseph != 0);
@@ -1285,21 +1323,21 @@ KF_HD float gain_finish(const GA& a, int64_t p, float (&x)[NP], float (&P)[ntri(
       forecast_partial_cov<NP>(opaque(cptr(a.prop)), p, x, P);
     } else {
 #pragma unroll
-      for (int j = 0; j < NP; ++j) x[j] = a.x_f[j * ld + p];
+      for (int j = 0; j < NP; ++j) x[j] = KF_PX(a.x_f, j * ld, p);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) P[t] = a.p_f[t * ld + p];
+      for (int t = 0; t < NT; ++t) P[t] = KF_PX(a.p_f, t * ld, p);
     }
   }
   float dn = 0.f;
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
-    a.x_out[j * ld + p] = x[j];
+    KF_PX(a.x_out, j * ld, p) = x[j];
     const float d = x[j] - x0[j];
     dn = fmaf(d, d, dn);
   }
   if (a.p_out) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) a.p_out[t * ld + p] = P[t];
+    for (int t = 0; t < NT; ++t) KF_PX(a.p_out, t * ld, p) = P[t];
   }
   if (a.out_mean) {
     // fused output: 1/sqrt(diag P^-1), the information form's uncertainty raster
@@ -1308,15 +1346,15 @@ KF_HD float gain_finish(const GA& a, int64_t p, float (&x)[NP], float (&P)[ntri(
     for (int t = 0; t < NT; ++t) U[t] = P[t];
     if (!chol_packed<NP>(U)) st |= ST_NONSPD;
     chol_inverse<NP>(U, Pi);
-    const int64_t r = a.out_idx ? a.out_idx[p] : p;
+    const int64_t r = a.out_idx ? KF_PX(a.out_idx, 0, p) : p;
     const int64_t pl = a.out_plane;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      a.out_mean[j * pl + r] = x[j];
-      a.out_unc[j * pl + r] = kf_rsqrt(Pi[tri(NP, j, j)]);
+      KF_PX(a.out_mean, j * pl, r) = x[j];
+      KF_PX(a.out_unc, j * pl, r) = kf_rsqrt(Pi[tri(NP, j, j)]);
     }
   }
-  if (a.status) a.status[p] = st;
+  if (a.status) KF_PX(a.status, 0, p) = st;
   return dn;
 }
 
@@ -1394,9 +1432,9 @@ KF_HD float pixel_reg_prepare(const JacobiArgs& a, int64_t p) {
   const int64_t ld = a.ld;
   float A[NT], b[NP];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) A[t] = a.a_in[t * ld + p];
+  for (int t = 0; t < NT; ++t) A[t] = KF_PX(a.a_in, t * ld, p);
 #pragma unroll
-  for (int j = 0; j < NP; ++j) b[j] = a.b_in[j * ld + p];
+  for (int j = 0; j < NP; ++j) b[j] = KF_PX(a.b_in, j * ld, p);
   int deg = 0;
 #pragma unroll
   for (int q4 = 0; q4 < 4; ++q4) deg += jacobi_neighbour(a, p, q4) >= 0 ? 1 : 0;
@@ -1405,7 +1443,7 @@ KF_HD float pixel_reg_prepare(const JacobiArgs& a, int64_t p) {
     if ((a.reg_mask >> j) & 1u) A[tri(NP, j, j)] += a.gamma * (float)deg;
   if (a.a_out) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = A[t];
+    for (int t = 0; t < NT; ++t) KF_PX(a.a_out, t * ld, p) = A[t];
   }
   const bool spd = chol_packed<NP>(A);
   chol_solve<NP>(A, b);
@@ -1415,7 +1453,7 @@ KF_HD float pixel_reg_prepare(const JacobiArgs& a, int64_t p) {
   // unhealthy pixel: decoupled (V = 0) at the reference point (x_ref when
   // given, else 0), so no non-finite value enters the neighbour sums
 #pragma unroll
-  for (int j = 0; j < NP; ++j) a.x_out[j * ld + p] = bad ? (a.x_ref ? a.x_ref[j * ld + p] : 0.f) : b[j];
+  for (int j = 0; j < NP; ++j) KF_PX(a.x_out, j * ld, p) = bad ? (a.x_ref ? KF_PX(a.x_ref, j * ld, p) : 0.f) : b[j];
   int c = 0;
 #pragma unroll
   for (int r = 0; r < NP; ++r) {
@@ -1425,7 +1463,7 @@ KF_HD float pixel_reg_prepare(const JacobiArgs& a, int64_t p) {
       for (int j = 0; j < NP; ++j) e[j] = (j == r) ? 1.f : 0.f;
       chol_solve<NP>(A, e);
 #pragma unroll
-      for (int j = 0; j < NP; ++j) a.v[((int64_t)c * NP + j) * ld + p] = bad ? 0.f : e[j];
+      for (int j = 0; j < NP; ++j) KF_PX(a.v, ((int64_t)c * NP + j) * ld, p) = bad ? 0.f : e[j];
       ++c;
     }
   }
@@ -1445,8 +1483,8 @@ KF_HD float pixel_reg_sweep(const JacobiArgs& a, int64_t p) {
       float z = 0.f;
 #pragma unroll
       for (int c = 0; c < NP; ++c)
-        if (c < a.k) z = fmaf(a.v[((int64_t)c * NP + j) * ld + p], s[c], z);
-      float zn = fmaf(a.gamma, z, a.u[j * ld + p]);
+        if (c < a.k) z = fmaf(KF_PX(a.v, ((int64_t)c * NP + j) * ld, p), s[c], z);
+      float zn = fmaf(a.gamma, z, KF_PX(a.u, j * ld, p));
       if (a.z_prev) {
         const float zp = a.z_prev[r * a.ld_ext + p];
         zn = fmaf(a.omega, zn - zp, zp);
@@ -1470,16 +1508,16 @@ KF_HD float pixel_reg_finish(const JacobiArgs& a, int64_t p) {
     float z = 0.f;
 #pragma unroll
     for (int c = 0; c < NP; ++c)
-      if (c < a.k) z = fmaf(a.v[((int64_t)c * NP + j) * ld + p], s[c], z);
-    const float x = fmaf(a.gamma, z, a.u[j * ld + p]);
-    a.x_out[j * ld + p] = x;
-    const float d = x - a.x_ref[j * ld + p];
+      if (c < a.k) z = fmaf(KF_PX(a.v, ((int64_t)c * NP + j) * ld, p), s[c], z);
+    const float x = fmaf(a.gamma, z, KF_PX(a.u, j * ld, p));
+    KF_PX(a.x_out, j * ld, p) = x;
+    const float d = x - KF_PX(a.x_ref, j * ld, p);
     dn = fmaf(d, d, dn);
     if (a.out_mean) {
-      const int64_t r = a.out_idx ? a.out_idx[p] : p;
+      const int64_t r = a.out_idx ? KF_PX(a.out_idx, 0, p) : p;
       KF_DCHECK(r >= 0 && r < a.out_plane);
-      a.out_mean[j * a.out_plane + r] = x;
-      a.out_unc[j * a.out_plane + r] = kf_rsqrt(a.a_in[tri(NP, j, j) * ld + p]);
+      KF_PX(a.out_mean, j * a.out_plane, r) = x;
+      KF_PX(a.out_unc, j * a.out_plane, r) = kf_rsqrt(KF_PX(a.a_in, tri(NP, j, j) * ld, p));
     }
   }
   return dn;
@@ -1553,14 +1591,14 @@ KF_HD float reg_finish1(const JacobiArgs& a, int64_t i0, int64_t stride, int64_t
     if (i0 + u * stride >= n) continue;
     const int64_t p = pp[u];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) a.x_out[j * ld + p] = x[u][j];
+    for (int j = 0; j < NP; ++j) KF_PX(a.x_out, j * ld, p) = x[u][j];
     if (a.out_mean) {
-      const int64_t r = a.out_idx ? a.out_idx[p] : p;
+      const int64_t r = a.out_idx ? KF_PX(a.out_idx, 0, p) : p;
       KF_DCHECK(r >= 0 && r < a.out_plane);
 #pragma unroll
       for (int j = 0; j < NP; ++j) {
-        a.out_mean[j * a.out_plane + r] = x[u][j];
-        a.out_unc[j * a.out_plane + r] = kf_rsqrt(a.a_in[tri(NP, j, j) * ld + p]);
+        KF_PX(a.out_mean, j * a.out_plane, r) = x[u][j];
+        KF_PX(a.out_unc, j * a.out_plane, r) = kf_rsqrt(KF_PX(a.a_in, tri(NP, j, j) * ld, p));
       }
     }
   }
@@ -1601,9 +1639,9 @@ KF_HD void reg_sweep1d(const JacobiArgs& a, uint32_t r, uint32_t c0, int j0) {
     const uint32_t c = c0 + u * BS < w ? c0 + u * BS : c0;
     const int64_t p = (int64_t)r * w + c;
     pp[u] = p;
-    z[u] = fmaf(a.gamma, a.v[j0 * ld + p] * reg_nsum_dense(a, r, c, p), a.u[j0 * ld + p]);
+    z[u] = fmaf(a.gamma, KF_PX(a.v, j0 * ld, p) * reg_nsum_dense(a, r, c, p), KF_PX(a.u, j0 * ld, p));
     if (a.z_prev) {
-      const float zp = a.z_prev[p];
+      const float zp = KF_PX(a.z_prev, 0, p);
       z[u] = fmaf(a.omega, z[u] - zp, zp);
     }
   }
@@ -1629,8 +1667,8 @@ KF_HD float reg_finish1d(const JacobiArgs& a, uint32_t r, uint32_t c0) {
     float du = 0.f;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      x[u][j] = fmaf(a.gamma, a.v[j * ld + p] * s, a.u[j * ld + p]);
-      const float d = x[u][j] - a.x_ref[j * ld + p];
+      x[u][j] = fmaf(a.gamma, KF_PX(a.v, j * ld, p) * s, KF_PX(a.u, j * ld, p));
+      const float d = x[u][j] - KF_PX(a.x_ref, j * ld, p);
       du = fmaf(d, d, du);
     }
     dn += in ? du : 0.f;
@@ -1640,14 +1678,14 @@ KF_HD float reg_finish1d(const JacobiArgs& a, uint32_t r, uint32_t c0) {
     if (c0 + u * BS >= w) continue;
     const int64_t p = pp[u];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) a.x_out[j * ld + p] = x[u][j];
+    for (int j = 0; j < NP; ++j) KF_PX(a.x_out, j * ld, p) = x[u][j];
     if (a.out_mean) {
-      const int64_t ro = a.out_idx ? a.out_idx[p] : p;
+      const int64_t ro = a.out_idx ? KF_PX(a.out_idx, 0, p) : p;
       KF_DCHECK(ro >= 0 && ro < a.out_plane);
 #pragma unroll
       for (int j = 0; j < NP; ++j) {
-        a.out_mean[j * a.out_plane + ro] = x[u][j];
-        a.out_unc[j * a.out_plane + ro] = kf_rsqrt(a.a_in[tri(NP, j, j) * ld + p]);
+        KF_PX(a.out_mean, j * a.out_plane, ro) = x[u][j];
+        KF_PX(a.out_unc, j * a.out_plane, ro) = kf_rsqrt(KF_PX(a.a_in, tri(NP, j, j) * ld, p));
       }
     }
   }
@@ -1781,9 +1819,9 @@ KF_HD float pixel_jacobi_classic(const JacobiArgs& a, int64_t p) {
   const int64_t ld = a.ld;
   float A[NT], b[NP];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) A[t] = a.a_in[t * ld + p];
+  for (int t = 0; t < NT; ++t) A[t] = KF_PX(a.a_in, t * ld, p);
 #pragma unroll
-  for (int j = 0; j < NP; ++j) b[j] = a.b_in[j * ld + p];
+  for (int j = 0; j < NP; ++j) b[j] = KF_PX(a.b_in, j * ld, p);
   int deg = 0;
   float sx[NP];
 #pragma unroll
@@ -1806,15 +1844,15 @@ KF_HD float pixel_jacobi_classic(const JacobiArgs& a, int64_t p) {
   }
   if (a.a_out) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) a.a_out[t * ld + p] = A[t];
+    for (int t = 0; t < NT; ++t) KF_PX(a.a_out, t * ld, p) = A[t];
   }
   chol_packed<NP>(A);
   chol_solve<NP>(A, b);
   float dn = 0.f;
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
-    a.x_out[j * ld + p] = b[j];
-    const float d = b[j] - a.x_ref[j * ld + p];
+    KF_PX(a.x_out, j * ld, p) = b[j];
+    const float d = b[j] - KF_PX(a.x_ref, j * ld, p);
     dn = fmaf(d, d, dn);
   }
   return dn;

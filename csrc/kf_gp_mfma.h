@@ -409,7 +409,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   float x0[NP], A[NT], b[NP];
   if (a.x_prev) {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
+    for (int j = 0; j < NP; ++j) x0[j] = KF_PX(a.x_prev, j * ld, p);
   }
   dn_first = 0.f;
   // wave-uniform loop over the fused Gauss-Newton iterations (AnalysisArgs.gn_fused)
@@ -427,9 +427,9 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     prior_rhs<NP, true>(A, xf, x0, b);
   } else if (a.a_in) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) A[t] = a.a_in[t * ld + p];
+    for (int t = 0; t < NT; ++t) A[t] = KF_PX(a.a_in, t * ld, p);
 #pragma unroll
-    for (int j = 0; j < NP; ++j) b[j] = a.b_in[j * ld + p];
+    for (int j = 0; j < NP; ++j) b[j] = KF_PX(a.b_in, j * ld, p);
     float t[NP];
     symv<NP>(A, x0, t);
 #pragma unroll
@@ -437,9 +437,9 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   } else {
     float xf[NP];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) xf[j] = a.x_f[j * ld + p];
+    for (int j = 0; j < NP; ++j) xf[j] = KF_PX(a.x_f, j * ld, p);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) A[t] = a.pf_inv[t * ld + p];
+    for (int t = 0; t < NT; ++t) A[t] = KF_PX(a.pf_inv, t * ld, p);
     prior_rhs<NP, true>(A, xf, x0, b);
   }
   int nobs = 0;
@@ -480,7 +480,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     }
     off += nch * gpm_frags_per_chunk(D);
     float* h0o = opaque(bdp)->h0_out;
-    if (act && h0o) h0o[p] = use ? H0 : 0.f;
+    if (act && h0o) KF_PX(h0o, 0, p) = use ? H0 : 0.f;
     if (use && !ok) st |= ST_BAD_OP;
     if (use && ok) {
       ++nobs;
@@ -544,13 +544,13 @@ __device__ __forceinline__ float pixel_gain_mfma(const GainArgs& a, int64_t p, b
     st |= forecast_partial_cov<NP>(opaque(cptr(a.prop)), p, x, P);
   } else {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) x[j] = a.x_f[j * ld + p];
+    for (int j = 0; j < NP; ++j) x[j] = KF_PX(a.x_f, j * ld, p);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) P[t] = a.p_f[t * ld + p];
+    for (int t = 0; t < NT; ++t) P[t] = KF_PX(a.p_f, t * ld, p);
   }
   if (a.x_prev) {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) x0[j] = a.x_prev[j * ld + p];
+    for (int j = 0; j < NP; ++j) x0[j] = KF_PX(a.x_prev, j * ld, p);
   } else {
 #pragma unroll
     for (int j = 0; j < NP; ++j) x0[j] = x[j];
@@ -585,7 +585,7 @@ __device__ __forceinline__ float pixel_gain_mfma(const GainArgs& a, int64_t p, b
     }
     off += nch * gpm_frags_per_chunk(D);
     float* h0o = opaque(bdp)->h0_out;
-    if (act && h0o) h0o[p] = use ? H0 : 0.f;
+    if (act && h0o) KF_PX(h0o, 0, p) = use ? H0 : 0.f;
     if (use && !ok) st |= ST_BAD_OP;
     if (use && ok) {
       ++nobs;
