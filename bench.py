@@ -267,6 +267,12 @@ def main():
         dist.all_gather_object(per_rank, mine)   # every rank of the job (strips x band groups)
     if hasattr(kf, "cache_stats"):
         log(f"host caches: {kf.cache_stats()}")
+    from kafka_inferenceengine_amd.ops import kernels as K
+    if dev.type == "cuda" and hasattr(K.ext(), "phase_clocks"):
+        # measuring build (KAFKA_PROF=1): shader cycles per phase of the fused
+        # analysis kernel, summed over waves, warm-up steps included
+        names = ("prologue", "forecast", "band_in", "gp", "band_out", "solve", "groups")
+        log("phase_clocks " + json.dumps(dict(zip(names, K.ext().phase_clocks(False)))))
     if prof is not None:
         prof.__exit__(None, None, None)
         prof.export_chrome_trace(a.profile)

@@ -118,6 +118,7 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(AnalysisArgs, partials, double*)
       .PTR_FIELD(AnalysisArgs, partials_first, double*)
       .def_readwrite("gn_fused", &AnalysisArgs::gn_fused)
+      .def_readwrite("band_layout", &AnalysisArgs::band_layout)
       .PTR_FIELD(AnalysisArgs, prop, const PropArgs*)
       .PTR_FIELD(AnalysisArgs, out_mean, float*)
       .PTR_FIELD(AnalysisArgs, out_unc, float*)
@@ -210,6 +211,15 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
   m.def("grid", [](int64_t N) { return dev_grid(N); });
   m.def("set_max_blocks", [](int n) { set_max_blocks(n); });
   m.def("get_max_blocks", []() { return get_max_blocks(); });
+#ifdef KF_PHASE_CLOCKS
+  // shader cycles per phase of the 7-parameter matrix-core analysis kernel,
+  // summed over waves (kf_core.h KF_PH_*); reset=True zeroes them after reading
+  m.def("phase_clocks", [](bool reset) {
+    unsigned long long v[KF_PH_NSLOT];
+    check_hip(phase_clocks(v, reset), "phase_clocks");
+    return std::vector<unsigned long long>(v, v + KF_PH_NSLOT);
+  }, py::arg("reset") = false);
+#endif
   m.def("set_gp_unroll", [](int n) { set_gp_unroll(n); });
 
   m.def("analysis", [](int np, const AnalysisArgs& a, int grid, bool device, uintptr_t stream) {

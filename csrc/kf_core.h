@@ -26,6 +26,41 @@
 #define KF_HD inline __attribute__((always_inline))
 #endif
 
+// KF_PHASE_CLOCKS (measuring build, `_build.py --prof` -> module _kafka_hip_prof,
+// selected with KAFKA_PROF=1): the matrix-core analysis kernels add the shader
+// cycles (s_memtime) each wave spends in a phase to kf_phase_clk[slot] (lane 0,
+// one vector atomic per phase boundary); ext.phase_clocks() reads them.  The
+// clock reads drain lgkmcnt, so the build runs a few per cent slower: it
+// attributes time, it does not time the release kernel.
+enum : int {
+  KF_PH_PROLOGUE = 0,   // LDS table staging
+  KF_PH_FORECAST = 1,   // fused forecast + prior right-hand side
+  KF_PH_BAND_IN = 2,    // observation decode, GP inputs
+  KF_PH_GP = 3,         // gp_mfma_sums: operands, chunk loop, extraction
+  KF_PH_BAND_OUT = 4,   // value / Jacobian, normal equations
+  KF_PH_SOLVE = 5,      // analysis_epilogue: factor, solve, stores
+  KF_PH_GROUPS = 6,     // pixel groups (count)
+  KF_PH_NSLOT = 8
+};
+#if defined(KF_PHASE_CLOCKS) && defined(__HIPCC__)
+static __device__ unsigned long long kf_phase_clk[KF_PH_NSLOT];
+#endif
+#if defined(KF_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+#define KF_PHASE_T0 uint64_t kf_t0_ = __builtin_amdgcn_s_memtime();
+#define KF_PHASE(slot)                                                                   \
+  {                                                                                      \
+    const uint64_t t1_ = __builtin_amdgcn_s_memtime();                                   \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&kf_phase_clk[slot], (unsigned long long)(t1_ - kf_t0_)); \
+    kf_t0_ = t1_;                                                                        \
+  }
+#define KF_PHASE_COUNT(slot) \
+  if ((threadIdx.x & 63) == 0) atomicAdd(&kf_phase_clk[slot], 1ull);
+#else
+#define KF_PHASE_T0
+#define KF_PHASE(slot)
+#define KF_PHASE_COUNT(slot)
+#endif
+
 // KF_CHECKED (debug build, `_build.py --checked` -> module _kafka_hip_checked,
 // selected with KAFKA_CHECKED=1): index assertions on the gather / scatter /
 // neighbour paths (SURVEY.md §5.2 "explicit bounds assertions in the debug
@@ -118,6 +153,9 @@ struct BandDesc {
 // matrix-core kernel gathers the GP inputs and updates only the 4 x 4 touched
 // entries of A with these compiled in instead of the runtime map's selects.
 constexpr int GPM_MAP_RUNTIME = 0, GPM_MAP_TIP_VIS = 2, GPM_MAP_TIP_NIR = 3;
+// AnalysisArgs.band_layout: BAND_LAYOUT_TIP = exactly two bands, the JRC-TIP VIS
+// then NIR maps (kafka/inference/utils.py:148-153), 7-parameter state
+constexpr int BAND_LAYOUT_RUNTIME = 0, BAND_LAYOUT_TIP = 1;
 
 struct PropArgs {
   int64_t N, ld;
@@ -195,7 +233,10 @@ struct AnalysisArgs {
   // which can never end the loop (min_iterations = 2, linear_kf.py:297-304),
   // kept in registers: solved, its norm partial to partials_first, and the
   // second linearised at its x; outputs as for one launch of the second)
-  int32_t gn_fused, pad_gn;
+  int32_t gn_fused;
+  // host hint: the bands form a layout known at compile time (BAND_LAYOUT_*),
+  // selecting a kernel with the band loop unrolled over fixed maps; 0: runtime
+  int32_t band_layout;
   double* partials_first;  // per-block sum (x_1 - x_0)^2 of the first fused iteration
 };
 
@@ -1025,7 +1066,13 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
 #pragma unroll
       for (int j = 0; j < NP; ++j) x0[j] = xf[j];
     }
-    prior_rhs<NP, DELTA>(A, xf, x0, b);
+    if (DELTA && !a.x_prev && it == 0) {
+      // correction form linearised at the forecast: P_f^-1 (x_f - x0) = 0
+#pragma unroll
+      for (int j = 0; j < NP; ++j) b[j] = 0.f;
+    } else {
+      prior_rhs<NP, DELTA>(A, xf, x0, b);
+    }
   } else if (a.a_in) {
     // band-chunked accumulation: continue from a previous chunk's (A, b)
 #pragma unroll

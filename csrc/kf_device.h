@@ -90,10 +90,11 @@ __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
 // MINW = 4 waves per SIMD (<= 128 VGPRs, 2 workgroups per CU for two bands'
 // tables) lets the HBM phases (state loads, result stores) of some waves run
 // under the record loops of others; BS = 256 gives 3 waves per SIMD.
-template <int NP, int D, int FOBS, int BS = BLOCK, int MINW = 1>
+template <int NP, int D, int FOBS, int BS = BLOCK, int MINW = 1, int LAYOUT = BAND_LAYOUT_RUNTIME>
 __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   extern __shared__ kf_h8 gpm_lds[];
+  KF_PHASE_T0
   {
     int off = 0;
     for (int bi = 0; bi < a.n_bands; ++bi) {
@@ -106,6 +107,7 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
     if (threadIdx.x == 0) gpm_lds[a.gpm_frags - 1] = kf_h8{};   // shared zero fragment
   }
   __syncthreads();
+  KF_PHASE(KF_PH_PROLOGUE)
   double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BS;
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
     const int64_t p = base + lane;
     const bool act = p < a.N;
     float dn1;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS>(a, act ? p : a.N - 1, act, gpm_lds, dn1);
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT>(a, act ? p : a.N - 1, act, gpm_lds, dn1);
     acc += act ? (double)dn : 0.0;
     acc1 += act ? (double)dn1 : 0.0;
   }
@@ -432,15 +434,33 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
     }
     if (a.gpm_frags > 0 && a.variant != 4 && a.n_bands <= GPM_MAX_BANDS) {
       const size_t lds = (size_t)a.gpm_frags * sizeof(kf_h8);
-#define KF_MFMA_GO(OBS_, BS_, MINW_)                                                                          \
+#define KF_MFMA_GO(OBS_, BS_, MINW_, LAY_)                                                                    \
   {                                                                                                          \
-    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_>, lds);                                       \
-    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_>), dim3(grid), dim3(BS_), lds, s, a);  \
+    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_>, lds);                                 \
+    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_>), dim3(grid), dim3(BS_), lds, s, \
+                       a);                                                                                   \
   }
+      // JRC-TIP band layout (AnalysisArgs.band_layout, checked on the host):
+      // band loop unrolled over the two compile-time maps (variant 10: the
+      // runtime-layout kernel, for A/B)
+      bool tip = false;
+      if constexpr (NP == 7 && FD == 4) tip = a.band_layout == BAND_LAYOUT_TIP && a.n_bands == 2 && a.variant != 10;
       if (a.fast_obs == OBS_DN16) {
-        KF_MFMA_GO(OBS_DN16, BLOCK, 1)
+        if constexpr (NP == 7 && FD == 4) {
+          if (tip) {
+            KF_MFMA_GO(OBS_DN16, BLOCK, 1, BAND_LAYOUT_TIP)
+            return true;
+          }
+        }
+        KF_MFMA_GO(OBS_DN16, BLOCK, 1, BAND_LAYOUT_RUNTIME)
       } else if (a.fast_obs == OBS_F32) {
-        KF_MFMA_GO(OBS_F32, BLOCK, 1)
+        if constexpr (NP == 7 && FD == 4) {
+          if (tip) {
+            KF_MFMA_GO(OBS_F32, BLOCK, 1, BAND_LAYOUT_TIP)
+            return true;
+          }
+        }
+        KF_MFMA_GO(OBS_F32, BLOCK, 1, BAND_LAYOUT_RUNTIME)
       } else {
         return false;
       }

@@ -39,6 +39,7 @@
 // (BandDesc.gpm_scale).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include "kf_core.h"
 
 namespace kf {
@@ -401,10 +402,14 @@ __device__ __forceinline__ void gpm_epilogue(const KF_CONST_AS BandDesc* q, cons
   }
 }
 
-template <int NP, int D, int FOBS, bool GT = false, bool PF = false>
+template <int NP, int D, int FOBS, bool GT = false, bool PF = false, int LAYOUT = BAND_LAYOUT_RUNTIME>
 __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
                                                      const kf_h8* lds, float& dn_first) {
   constexpr int NT = ntri(NP);
+  // LAYOUT == BAND_LAYOUT_TIP: two bands with the JRC-TIP VIS / NIR maps, the
+  // band loop unrolled with both maps compile-time (no runtime map branches
+  // and no register copies at their joins)
+  static_assert(LAYOUT == BAND_LAYOUT_RUNTIME || (NP == 7 && D == 4 && !GT), "JRC-TIP layout: 7 params, 4 inputs");
   const int64_t ld = a.ld;
   float x0[NP], A[NT], b[NP];
   if (a.x_prev) {
@@ -412,6 +417,8 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     for (int j = 0; j < NP; ++j) x0[j] = KF_PX(a.x_prev, j * ld, p);
   }
   dn_first = 0.f;
+  KF_PHASE_T0
+  KF_PHASE_COUNT(KF_PH_GROUPS)
   // wave-uniform loop over the fused Gauss-Newton iterations (AnalysisArgs.gn_fused)
   for (int it = 0;; ++it) {
   p = opaque_lane(p);
@@ -421,10 +428,15 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     float xf[NP];
     forecast_partial<NP>(opaque(cptr(a.prop)), p, xf, A);
     if (!a.x_prev && it == 0) {
+      // linearised at the forecast: the prior part P_f^-1 (x_f - x0) is 0
 #pragma unroll
-      for (int j = 0; j < NP; ++j) x0[j] = xf[j];
+      for (int j = 0; j < NP; ++j) {
+        x0[j] = xf[j];
+        b[j] = 0.f;
+      }
+    } else {
+      prior_rhs<NP, true>(A, xf, x0, b);
     }
-    prior_rhs<NP, true>(A, xf, x0, b);
   } else if (a.a_in) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) A[t] = KF_PX(a.a_in, t * ld, p);
@@ -444,7 +456,10 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   }
   int nobs = 0;
   int off = 0;
-  for (int bi = 0; bi < a.n_bands; ++bi) {
+  // one band: GP sums on the matrix cores, value and Jacobian, normal equations.
+  // MKC: the band's map kind when known at compile time (LAYOUT), else -1
+  auto band = [&](int bi, auto mkc) {
+    constexpr int MKC = decltype(mkc)::value;
     const KF_CONST_AS BandDesc* bdp = cptr(a.bands) + bi;
     float y, w;
     decode_obs<FOBS>(*bdp, p, y, w);
@@ -456,7 +471,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     const int nch = bdp->gpm_nchunk;
     // wave-uniform: a compiled-in JRC-TIP map, or the runtime / identity map
     constexpr bool TIPK = NP == 7 && D == 4;
-    const int mk = TIPK ? bdp->map_kind : GPM_MAP_RUNTIME;
+    const int mk = MKC >= 0 ? MKC : (TIPK ? bdp->map_kind : GPM_MAP_RUNTIME);
     const bool any = __any(use);
     if (any) {
       float xi[D], c = 0.f;
@@ -465,8 +480,10 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
       else gpm_inputs<NP, D>(bdp, x0, xi, c);
       c *= -0.5f * LOG2E;
       float S[D + 1];
+      KF_PHASE(KF_PH_BAND_IN)
       if constexpr (GT) gp_mfma_sums_g<D, PF>(bdp->gpm, nch, xi, c, S);
       else gp_mfma_sums<D>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
+      KF_PHASE(KF_PH_GP)
       const KF_CONST_AS BandDesc* q = opaque(bdp);   // epilogue fields: not live across the chunk loop
       const float sc = q->gpm_scale;
       const float S0 = S[0] * sc;
@@ -514,6 +531,14 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
         }
       }
     }
+    KF_PHASE(KF_PH_BAND_OUT)
+  };
+  KF_PHASE(KF_PH_FORECAST)
+  if constexpr (LAYOUT == BAND_LAYOUT_TIP) {
+    band(0, std::integral_constant<int, GPM_MAP_TIP_VIS>{});
+    band(1, std::integral_constant<int, GPM_MAP_TIP_NIR>{});
+  } else {
+    for (int bi = 0; bi < a.n_bands; ++bi) band(bi, std::integral_constant<int, -1>{});
   }
   if (nobs == 0) st |= ST_NO_OBS;
   const KF_CONST_AS AnalysisArgs* ka =
@@ -524,6 +549,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   // operands and must stay finite
   const bool last = it + 1 >= ka->gn_fused;
   const float dn = analysis_epilogue<NP, true>(ka, p, A, b, x0, st, last && act);
+  KF_PHASE(KF_PH_SOLVE)
   if (last) return act ? dn : 0.f;
   dn_first = dn;
 #pragma unroll

@@ -32,6 +32,7 @@ ARCH = os.environ.get("KAFKA_OFFLOAD_ARCH", "gfx950")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 EXT_PATH = PKG_DIR / f"_kafka_hip{EXT_SUFFIX}"
 CHECKED_EXT_PATH = PKG_DIR / f"_kafka_hip_checked{EXT_SUFFIX}"
+PROF_EXT_PATH = PKG_DIR / f"_kafka_hip_prof{EXT_SUFFIX}"
 
 HEADERS = ["kf_core.h", "kf_launch.h", "kf_stream.h", "kf_device.h", "kf_gp_mfma.h", "kf_tiff.h"]
 # device translation units (compiled concurrently: the NP = 7 / 10 analysis
@@ -68,16 +69,25 @@ def _run(cmd: list[str], verbose: bool) -> None:
         raise RuntimeError(f"build step failed ({r.returncode}): {' '.join(cmd)}\n{msg[-8000:]}")
 
 
-def build(force: bool = False, verbose: bool = False, checked: bool = False) -> Path:
+def build(force: bool = False, verbose: bool = False, checked: bool = False, prof: bool = False) -> Path:
+    """``prof``: the phase-clock variant ``_kafka_hip_prof`` (``-DKF_PHASE_CLOCKS``,
+    loaded with ``KAFKA_PROF=1``): the fused analysis kernels add each phase's
+    shader cycles per wave to a device counter (``ext.phase_clocks``); a
+    measuring tool, not built by ``__graft_entry__.build``."""
     from concurrent.futures import ThreadPoolExecutor
 
-    build_dir = BUILD.with_name("kafka_hip_checked") if checked else BUILD
-    ext_path = CHECKED_EXT_PATH if checked else EXT_PATH
+    if checked and prof:
+        raise ValueError("checked and prof are separate variants")
+    build_dir = BUILD.with_name("kafka_hip_checked") if checked else BUILD.with_name("kafka_hip_prof") if prof \
+        else BUILD
+    ext_path = CHECKED_EXT_PATH if checked else PROF_EXT_PATH if prof else EXT_PATH
     build_dir.mkdir(parents=True, exist_ok=True)
     hdrs = [CSRC / h for h in HEADERS]
     common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}"]
     if checked:
         common += ["-DKF_CHECKED", "-DKF_MODULE_NAME=_kafka_hip_checked"]
+    if prof:
+        common += ["-DKF_PHASE_CLOCKS", "-DKF_MODULE_NAME=_kafka_hip_prof"]
     hip_defs = ["-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}"]
     hipcc = _hipcc()
     jobs, objs = [], []
@@ -125,8 +135,9 @@ def main() -> None:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--checked", action="store_true", help="debug build with index assertions")
+    ap.add_argument("--prof", action="store_true", help="phase-clock build (KAFKA_PROF=1)")
     a = ap.parse_args()
-    p = build(force=a.force, verbose=a.verbose, checked=a.checked)
+    p = build(force=a.force, verbose=a.verbose, checked=a.checked, prof=a.prof)
     print(f"built {p}")
 
 

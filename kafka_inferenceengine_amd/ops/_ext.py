@@ -14,9 +14,12 @@ import torch  # noqa: F401  (must precede the extension import)
 
 _err = None
 CHECKED = os.environ.get("KAFKA_CHECKED", "0") not in ("", "0")
+PROF = os.environ.get("KAFKA_PROF", "0") not in ("", "0")
 try:
     if CHECKED:  # debug build with index assertions (_build.py --checked)
         from .. import _kafka_hip_checked as ext  # type: ignore
+    elif PROF:  # phase-clock build of the JRC-TIP analysis kernel (_build.py --prof)
+        from .. import _kafka_hip_prof as ext  # type: ignore
     else:
         from .. import _kafka_hip as ext  # type: ignore
 except ImportError as e:  # pragma: no cover - exercised only when unbuilt

@@ -89,6 +89,7 @@ class BandTable:
     fast_obs: int = 0
     gpm_frags: int = 0      # > 0: GP on the matrix cores, LDS fragments of all bands (kf_gp_mfma.h)
     gpm_global: bool = False  # GP on the matrix cores, tables read from global memory (too large for LDS)
+    layout: int = 0         # BAND_LAYOUT_*: a band layout the kernels know at compile time (0: runtime)
 
     @property
     def ptr(self) -> int:
@@ -105,6 +106,9 @@ GPM_MAX_LDS = 160 * 1024
 GPM_MAX_BANDS = 4          # kf_gp_mfma.h: bands of the LDS-staged matrix-core path
 GPM_GLOBAL_D = (7, 10)     # full-state GP input counts with a global-table instantiation
 
+# kf_core.h BAND_LAYOUT_TIP: exactly two GP bands with the JRC-TIP VIS then NIR maps
+# (BandDesc.map_kind 2, 3), 4 inputs each: the matrix-core kernel unrolls the band loop
+BAND_LAYOUT_TIP = 1
 FD_PRECOMP = -1   # kf_core.h: fast analysis kernel for all-precomputed operators
 FD_LINEAR = -2    # kf_core.h: fast analysis kernel for all-linear (identity/selection) operators
 # analysis fast-kernel variant (kf_kernels.hip:l_analysis_fast); env override for A/B runs
@@ -185,7 +189,10 @@ def make_band_table(descs: list, device, keepalive=()) -> BandTable:
             # too large for LDS: the global-table kernel (compiled for full-state
             # GPs of 7 and 10 parameters, kf_device.h:analysis_mfma_g_kernel)
             gpm_frags, gpm_global = 0, fast_d in GPM_GLOBAL_D
-    return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs, gpm_frags, gpm_global)
+    layout = 0
+    if fast_d == 4 and gpm_frags > 0 and [d.map_kind for d in descs] == [2, 3]:
+        layout = BAND_LAYOUT_TIP
+    return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs, gpm_frags, gpm_global, layout)
 
 
 # ------------------------------------------------------------------ ops
@@ -268,6 +275,7 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     a.gn_fused = int(gn_fused)
     a.partials_first = _ptr(partials_first) if gn_fused == 2 else 0
     a.fast_d, a.fast_obs = (bands.fast_d, bands.fast_obs) if fast else (0, 0)
+    a.band_layout = int(bands.layout) if (fast and n_params == 7) else 0
     a.variant = DEFAULT_VARIANT if variant is None else int(variant)
     a.gpm_frags = bands.gpm_frags if fast else 0
     a.gpm_global = int(bool(bands.gpm_global) and fast and bands.fast_d == n_params)

@@ -168,3 +168,23 @@ def test_gp_mfma_realistic_tile_matches_valu(cuda, cap):
     for x in outs[variant]:
         d = np.abs(x - ref) / (np.abs(ref) + 0.05)
         assert d.max() < 5e-3, (variant, cap, float(d.max()), np.nonzero(d.max(0) > 5e-3)[0][:8])
+
+
+def test_tip_layout_kernel_bit_identical_to_runtime_layout(cuda):
+    """BAND_LAYOUT_TIP (band loop unrolled over the compile-time VIS / NIR maps,
+    kf_gp_mfma.h) against the runtime-layout kernel (variant 10): the same
+    operations per pixel, so x, A, status and the norm partials are identical."""
+    prob = tip_case(N=64 * 53 + 7, seed=11)
+    tab, xl, al, sl, hl, rl = run(prob, cuda)
+    assert tab.layout == K.BAND_LAYOUT_TIP
+    _, xr, ar, sr, hr, rr = run(prob, cuda, variant=10)
+    assert np.array_equal(xl, xr) and np.array_equal(al, ar) and np.array_equal(sl, sr)
+    for a, b in zip(hl, hr):
+        assert np.array_equal(a, b)
+    assert rl == rr
+    # swapped band order is not the layout: the runtime kernel runs it
+    swapped = dict(prob, specs=prob["specs"][::-1], obs=prob["obs"][::-1], ems=prob["ems"][::-1],
+                   maps=prob["maps"][::-1], bands=prob["bands"][::-1])
+    tab2, xs, *_ = run(swapped, cuda)
+    assert tab2.layout == 0
+    assert np.max(np.abs(xs - xl) / (np.abs(xl) + 0.05)) < 1e-5

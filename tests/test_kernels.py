@@ -416,3 +416,20 @@ def test_reg_sweeps_tiled_rejects_bad_args():
                            [1.0], [True])
     with pytest.raises(ValueError):
         K.reg_sweeps_tiled(7, u, u, z, None, z, torch.zeros(1, 100), 1.0, 4, 100, geo, [1.0], [False])
+
+
+def test_band_layout_detection():
+    """BAND_LAYOUT_TIP (kf_core.h) is set only for two GP bands with the JRC-TIP
+    VIS then NIR maps and matrix-core tables; any other set runs the
+    runtime-layout kernel."""
+    from kafka_inferenceengine_amd.engine.bands import DeviceBand, RecordCache, build_table
+
+    ems = k.make_tip_emulators(n_train=64, seed=1)
+    specs = [k.gp_spec(em, mp) for em, mp in zip(ems, [k.TIP_BAND_MAPPER[0], k.TIP_BAND_MAPPER[1]])]
+    N = 100
+    dbs = [DeviceBand(K.OBS_F32, y=torch.zeros(N), w=torch.ones(N)) for _ in specs]
+    cache = RecordCache()
+    assert build_table(specs, dbs, 7, cache, torch.device("cpu")).layout == K.BAND_LAYOUT_TIP
+    assert build_table(specs[::-1], dbs, 7, cache, torch.device("cpu")).layout == 0
+    assert build_table(specs[:1], dbs[:1], 7, cache, torch.device("cpu")).layout == 0
+    assert build_table(specs + specs[:1], dbs + dbs[:1], 7, cache, torch.device("cpu")).layout == 0
