@@ -913,6 +913,9 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
 #pragma unroll
       for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = A[t];
     }
+    float dA[NP];   // output uncertainty: 1/sqrt(diag) of the regularised precision
+#pragma unroll
+    for (int j = 0; j < NP; ++j) dA[j] = A[tri(NP, j, j)];
     const bool spd = chol_packed<NP>(A);
     chol_solve<NP>(A, b);
     bool fin = true;
@@ -938,6 +941,17 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
 #pragma unroll
         for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = Af[t];
       }
+#pragma unroll
+      for (int j = 0; j < NP; ++j) dA[j] = Af[tri(NP, j, j)];
+    }
+    if (a->out_unc) {
+      // the uncertainty raster of the final iteration (the mean follows in
+      // reg_finish): written here, where diag A is in registers, so the finish
+      // pass does not re-read the precision
+      const int64_t r = a->out_idx ? KF_PXS(a->out_idx, 0, p) : p;
+      const int64_t pl = a->out_plane;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) KF_PXS(a->out_unc, j * pl, r) = kf_rsqrt(dA[j]);
     }
 #pragma unroll
     for (int j = 0; j < NP; ++j) KF_PXS(a->x_out, j * ld, p) = b[j];
@@ -1564,7 +1578,7 @@ KF_HD float pixel_reg_finish(const JacobiArgs& a, int64_t p) {
       const int64_t r = a.out_idx ? KF_PX(a.out_idx, 0, p) : p;
       KF_DCHECK(r >= 0 && r < a.out_plane);
       KF_PX(a.out_mean, j * a.out_plane, r) = x;
-      KF_PX(a.out_unc, j * a.out_plane, r) = kf_rsqrt(KF_PX(a.a_in, tri(NP, j, j) * ld, p));
+      if (a.out_unc) KF_PX(a.out_unc, j * a.out_plane, r) = kf_rsqrt(KF_PX(a.a_in, tri(NP, j, j) * ld, p));
     }
   }
   return dn;
@@ -1645,7 +1659,7 @@ KF_HD float reg_finish1(const JacobiArgs& a, int64_t i0, int64_t stride, int64_t
 #pragma unroll
       for (int j = 0; j < NP; ++j) {
         KF_PX(a.out_mean, j * a.out_plane, r) = x[u][j];
-        KF_PX(a.out_unc, j * a.out_plane, r) = kf_rsqrt(KF_PX(a.a_in, tri(NP, j, j) * ld, p));
+        if (a.out_unc) KF_PX(a.out_unc, j * a.out_plane, r) = kf_rsqrt(KF_PX(a.a_in, tri(NP, j, j) * ld, p));
       }
     }
   }
@@ -1732,7 +1746,7 @@ KF_HD float reg_finish1d(const JacobiArgs& a, uint32_t r, uint32_t c0) {
 #pragma unroll
       for (int j = 0; j < NP; ++j) {
         KF_PX(a.out_mean, j * a.out_plane, ro) = x[u][j];
-        KF_PX(a.out_unc, j * a.out_plane, ro) = kf_rsqrt(KF_PX(a.a_in, tri(NP, j, j) * ld, p));
+        if (a.out_unc) KF_PX(a.out_unc, j * a.out_plane, ro) = kf_rsqrt(KF_PX(a.a_in, tri(NP, j, j) * ld, p));
       }
     }
   }
@@ -1789,7 +1803,7 @@ KF_HD float reg_finish4(const JacobiArgs& a, int64_t p) {
     du4[3] = fmaf(d3, d3, du4[3]);
   }
   F4 dg[NP];
-  if (a.out_mean) {
+  if (a.out_unc) {
 #pragma unroll
     for (int j = 0; j < NP; ++j) dg[j] = ld4(a.a_in + tri(NP, j, j) * ld + p);
   }
@@ -1797,11 +1811,13 @@ KF_HD float reg_finish4(const JacobiArgs& a, int64_t p) {
   for (int j = 0; j < NP; ++j) st4(a.x_out + j * ld + p, x[j]);
   if (a.out_mean) {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      st4(a.out_mean + j * a.out_plane + p, x[j]);
+    for (int j = 0; j < NP; ++j) st4(a.out_mean + j * a.out_plane + p, x[j]);
+  }
+  if (a.out_unc) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
       st4(a.out_unc + j * a.out_plane + p,
           F4{kf_rsqrt(dg[j].x), kf_rsqrt(dg[j].y), kf_rsqrt(dg[j].z), kf_rsqrt(dg[j].w)});
-    }
   }
   return ((du4[0] + du4[1]) + du4[2]) + du4[3];
 }

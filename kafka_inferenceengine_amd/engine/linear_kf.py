@@ -1124,9 +1124,12 @@ class LinearKalman:
                                  for r in (n, k * n, n))
         u, v, x0_buf = self._reg_uv
         x_ref = x_prev if x_prev is not None else x0_buf
+        # the final iteration's uncertainty raster comes from the prepare (diag of
+        # the regularised precision in registers), the mean from reg_finish
         K.analysis(n, table, x_prev, fx, fP, u, A_out, None, status, None, N=N, prop=prop,
                    reg=dict(gamma=gamma, mask=reg.reg_mask, v_out=v, nbr=None if geo else reg.nbr, geo=geo),
-                   x0_out=None if x_prev is not None else x0_buf)
+                   x0_out=None if x_prev is not None else x0_buf,
+                   out=None if out is None else (None, out[1], out[2]))
         nbr = None if geo else reg.nbr
         rho, sweeps = self._reg_schedule(reg, v, rows, k, gamma, sweeps,
                                          self.config.spatial_tol if final else self.config.spatial_tol_first)
@@ -1183,7 +1186,7 @@ class LinearKalman:
                 nxt = reg.fill_halo(nxt)
             prev, cur = cur, nxt
         K.reg_finish(n, u, v, cur, nbr, x_ref, x_out, gamma, reg.reg_mask, N, partials=self._partials, geo=geo,
-                     out=out, a_prec=A_out if out is not None else None)
+                     out=None if out is None else (out[0], None, out[2]))
         # residual of the coupled solve (metrics only): the finish applied one more
         # Jacobi update to the last iterate, x_R - z = J z + f - z (device, read lazily)
         r2 = None

@@ -291,11 +291,18 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     if prop is not None:
         a.prop = _ptr(prop.device_copy())
     if out is not None:
+        # (mean, unc, idx); with ``reg`` the mean is None: the regulariser's
+        # prepare writes the uncertainty raster (1/sqrt of the regularised
+        # precision's diagonal) and reg_finish the mean
         mean, unc, idx = out
         if not solve:
             raise ValueError("fused output needs solve=True")
-        plane = mean.shape[1]
+        if unc is None or (mean is None) != (reg is not None):
+            raise ValueError("out = (mean, unc, idx); mean is None exactly with reg")
+        plane = unc.shape[1]
         for t, nm in ((mean, "out mean"), (unc, "out unc")):
+            if t is None:
+                continue
             _check_soa(t, n_params, 0, nm, device=dev)
             if t.shape[1] != plane:
                 raise ValueError("out mean / unc planes differ")
@@ -316,8 +323,8 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
         if x_out is None or v_out.shape[1] != ld or k == 0:
             raise ValueError("regulariser prepare needs x_out (u), v_out [k*n, ld] and a non-empty mask")
         _check_nbr(reg.get("nbr"), N, reg.get("geo"))
-        if partials is not None or out is not None:
-            raise ValueError("regulariser prepare produces no partials / output")
+        if partials is not None:
+            raise ValueError("regulariser prepare produces no partials (reg_finish does)")
         a.reg_gamma, a.reg_mask = float(reg["gamma"]), int(reg["mask"])
         a.reg_nbr, a.reg_v = _ptr(reg.get("nbr")), _ptr(v_out)
         geo = reg.get("geo")
@@ -559,12 +566,18 @@ def reg_finish(n_params, u, v, z_ext, nbr, x_ref, x_out, gamma, reg_mask, N, par
     a.ld_ext = z_ext.shape[1]
     a.u, a.v, a.x_ext, a.x_ref, a.x_out, a.partials = map(_ptr, (u, v, z_ext, x_ref, x_out, partials))
     if out is not None:
+        # unc None: the analysis (regulariser prepare) already wrote it
         mean, unc, idx = out
-        _check_soa(a_prec, ntri(n_params), N, "a_prec", device=dev)
-        if a_prec.shape[1] != ld:
-            raise ValueError("a_prec must share the leading dimension")
+        if (unc is None) != (a_prec is None):
+            raise ValueError("the uncertainty raster needs a_prec (and only then)")
+        if a_prec is not None:
+            _check_soa(a_prec, ntri(n_params), N, "a_prec", device=dev)
+            if a_prec.shape[1] != ld:
+                raise ValueError("a_prec must share the leading dimension")
         plane = mean.shape[1]
         for t, nm in ((mean, "out mean"), (unc, "out unc")):
+            if t is None:
+                continue
             _check_soa(t, n_params, 0, nm, device=dev)
             if t.shape[1] != plane:
                 raise ValueError("out mean / unc planes differ")

@@ -168,6 +168,8 @@ def dense_finish(device, h_total=30, w=44, ranks=3, rank=1, n=7, j0=6, out=True,
     part_buf = torch.zeros(4096, dtype=torch.float64, device=device)
     mean = torch.zeros(n, N, device=device)
     unc = torch.zeros(n, N, device=device)
+    # out="mean": the mean only (the analysis wrote the uncertainty raster)
     K.reg_finish(n, u, v, z, None, xr, xo, 0.8, 1 << j0, N, partials=part_buf, geo=geo,
-                 out=(mean, unc, None) if out else None, a_prec=a_prec if out else None)
+                 out=(mean, None if out == "mean" else unc, None) if out else None,
+                 a_prec=a_prec if out is True else None)
     return xo[:, :N].cpu(), mean.cpu(), unc.cpu(), float(part_buf.sum())

@@ -348,7 +348,7 @@ def test_spatial_tiled_sweeps_equal_per_sweep_launches_on_device(cuda):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("rank,out", [(0, True), (1, True), (2, False), (1, False)])
+@pytest.mark.parametrize("rank,out", [(0, True), (1, True), (2, False), (1, False), (1, "mean")])
 def test_dense_finish_vectorised_equals_host(cuda, rank, out):
     """The 16-byte finish (4 pixels of a row per thread) equals the host's
     per-pixel finish bit for bit (x, output mean), halo rows included;
@@ -359,3 +359,5 @@ def test_dense_finish_vectorised_equals_host(cuda, rank, out):
     # 1/sqrt(diag A): the device's rsqrt differs from the host's in the last bit
     assert torch.allclose(d[2], h[2], rtol=2e-7, atol=0)
     assert abs(d[3] - h[3]) <= 1e-5 * abs(h[3])
+    if out == "mean":
+        assert torch.equal(d[1], d[0]) and not d[2].any()
