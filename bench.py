@@ -272,7 +272,7 @@ def main():
         # measuring build (KAFKA_PROF=1): shader cycles per phase of the fused
         # analysis kernel, summed over waves, warm-up steps included
         names = ("prologue", "forecast", "band_in", "gp", "band_out", "solve", "groups")
-        log("phase_clocks " + json.dumps(dict(zip(names, K.ext().phase_clocks(False)))))
+        log("phase_clocks " + json.dumps(dict(zip(names, K.ext().phase_clocks(kf.n_params, False)))))
     if prof is not None:
         prof.__exit__(None, None, None)
         prof.export_chrome_trace(a.profile)

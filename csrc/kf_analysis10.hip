@@ -10,4 +10,16 @@ hipError_t dev_analysis_np10(const AnalysisArgs& a, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifdef KF_PHASE_CLOCKS
+// the phase counters of this translation unit's (10-parameter) analysis kernels
+hipError_t phase_clocks_np10(unsigned long long* out, bool reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(kf_phase_clk), sizeof(kf_phase_clk));
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[KF_PH_NSLOT] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(kf_phase_clk), z, sizeof(z));
+  }
+  return e;
+}
+#endif
+
 }  // namespace kf

@@ -12,7 +12,7 @@ hipError_t dev_analysis_np7(const AnalysisArgs& a, int grid, hipStream_t s) {
 
 #ifdef KF_PHASE_CLOCKS
 // the phase counters of this translation unit's (7-parameter) analysis kernels
-hipError_t phase_clocks(unsigned long long* out, bool reset) {
+hipError_t phase_clocks_np7(unsigned long long* out, bool reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(kf_phase_clk), sizeof(kf_phase_clk));
   if (e == hipSuccess && reset) {
     const unsigned long long z[KF_PH_NSLOT] = {};

@@ -212,13 +212,13 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
   m.def("set_max_blocks", [](int n) { set_max_blocks(n); });
   m.def("get_max_blocks", []() { return get_max_blocks(); });
 #ifdef KF_PHASE_CLOCKS
-  // shader cycles per phase of the 7-parameter matrix-core analysis kernel,
+  // shader cycles per phase of the 7- or 10-parameter matrix-core analysis kernels,
   // summed over waves (kf_core.h KF_PH_*); reset=True zeroes them after reading
-  m.def("phase_clocks", [](bool reset) {
+  m.def("phase_clocks", [](int np, bool reset) {
     unsigned long long v[KF_PH_NSLOT];
-    check_hip(phase_clocks(v, reset), "phase_clocks");
+    check_hip(np == 10 ? phase_clocks_np10(v, reset) : phase_clocks_np7(v, reset), "phase_clocks");
     return std::vector<unsigned long long>(v, v + KF_PH_NSLOT);
-  }, py::arg("reset") = false);
+  }, py::arg("n_params") = 7, py::arg("reset") = false);
 #endif
   m.def("set_gp_unroll", [](int n) { set_gp_unroll(n); });
 

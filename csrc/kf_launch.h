@@ -24,7 +24,8 @@ hipError_t dev_analysis(int np, const AnalysisArgs& a, int grid, hipStream_t s);
 hipError_t dev_analysis_np7(const AnalysisArgs& a, int grid, hipStream_t s);
 hipError_t dev_analysis_np10(const AnalysisArgs& a, int grid, hipStream_t s);
 #ifdef KF_PHASE_CLOCKS
-hipError_t phase_clocks(unsigned long long* out, bool reset);
+hipError_t phase_clocks_np7(unsigned long long* out, bool reset);
+hipError_t phase_clocks_np10(unsigned long long* out, bool reset);
 #endif
 hipError_t dev_gain(int np, const GainArgs& a, int grid, hipStream_t s);
 hipError_t dev_jacobi(int np, const JacobiArgs& a, int grid, hipStream_t s);
