@@ -28,9 +28,9 @@
 
 // KF_PHASE_CLOCKS (measuring build, `_build.py --prof` -> module _kafka_hip_prof,
 // selected with KAFKA_PROF=1): the matrix-core analysis kernels add the shader
-// cycles (s_memtime) each wave spends in a phase to kf_phase_clk[slot] (lane 0,
-// one vector atomic per phase boundary); ext.phase_clocks() reads them.  The
-// clock reads drain lgkmcnt, so the build runs a few per cent slower: it
+// cycles (s_memtime) each wave spends in a phase to per-wave counters, summed
+// into kf_phase_clk[slot] at the end of the kernel; ext.phase_clocks() reads
+// them.  The clock reads drain lgkmcnt, so the build runs somewhat slower: it
 // attributes time, it does not time the release kernel.
 enum : int {
   KF_PH_PROLOGUE = 0,   // LDS table staging
@@ -46,19 +46,36 @@ enum : int {
 static __device__ unsigned long long kf_phase_clk[KF_PH_NSLOT];
 #endif
 #if defined(KF_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
-#define KF_PHASE_T0 uint64_t kf_t0_ = __builtin_amdgcn_s_memtime();
-#define KF_PHASE(slot)                                                                   \
-  {                                                                                      \
-    const uint64_t t1_ = __builtin_amdgcn_s_memtime();                                   \
-    if ((threadIdx.x & 63) == 0) atomicAdd(&kf_phase_clk[slot], (unsigned long long)(t1_ - kf_t0_)); \
-    kf_t0_ = t1_;                                                                        \
+// per-wave accumulators in registers, added to kf_phase_clk once per wave at
+// the end of the kernel (per-boundary atomics on 8 shared addresses serialise
+// in one L2 channel and sit in vmcnt ahead of the wave's own loads)
+struct KfPhaseAcc {
+  uint64_t t0;
+  uint64_t acc[KF_PH_NSLOT];
+};
+#define KF_PHASE_PARAM , ::KfPhaseAcc& kf_pc_
+#define KF_PHASE_ARG , kf_pc_
+#define KF_PHASE_KERNEL_BEGIN                                 \
+  ::KfPhaseAcc kf_pc_;                                      \
+  for (int s_ = 0; s_ < KF_PH_NSLOT; ++s_) kf_pc_.acc[s_] = 0; \
+  kf_pc_.t0 = __builtin_amdgcn_s_memtime();
+#define KF_PHASE(slot)                                  \
+  {                                                     \
+    const uint64_t t1_ = __builtin_amdgcn_s_memtime();  \
+    kf_pc_.acc[slot] += t1_ - kf_pc_.t0;                \
+    kf_pc_.t0 = t1_;                                    \
   }
-#define KF_PHASE_COUNT(slot) \
-  if ((threadIdx.x & 63) == 0) atomicAdd(&kf_phase_clk[slot], 1ull);
+#define KF_PHASE_COUNT(slot) kf_pc_.acc[slot] += 1;
+#define KF_PHASE_KERNEL_END                                                                      \
+  if ((threadIdx.x & 63) == 0)                                                                   \
+    for (int s_ = 0; s_ < KF_PH_NSLOT; ++s_) atomicAdd(&kf_phase_clk[s_], (unsigned long long)kf_pc_.acc[s_]);
 #else
-#define KF_PHASE_T0
+#define KF_PHASE_PARAM
+#define KF_PHASE_ARG
+#define KF_PHASE_KERNEL_BEGIN
 #define KF_PHASE(slot)
 #define KF_PHASE_COUNT(slot)
+#define KF_PHASE_KERNEL_END
 #endif
 
 // KF_CHECKED (debug build, `_build.py --checked` -> module _kafka_hip_checked,

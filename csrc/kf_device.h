@@ -94,7 +94,7 @@ template <int NP, int D, int FOBS, int BS = BLOCK, int MINW = 1, int LAYOUT = BA
 __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   extern __shared__ kf_h8 gpm_lds[];
-  KF_PHASE_T0
+  KF_PHASE_KERNEL_BEGIN
   {
     int off = 0;
     for (int bi = 0; bi < a.n_bands; ++bi) {
@@ -115,11 +115,13 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
     const int64_t p = base + lane;
     const bool act = p < a.N;
     float dn1;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT>(a, act ? p : a.N - 1, act, gpm_lds, dn1);
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT>(a, act ? p : a.N - 1, act, gpm_lds,
+                                                                           dn1 KF_PHASE_ARG);
     acc += act ? (double)dn : 0.0;
     acc1 += act ? (double)dn1 : 0.0;
   }
   analysis_partials<BS>(a, acc, acc1);
+  KF_PHASE_KERNEL_END
 #endif
 }
 
@@ -130,6 +132,7 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
 template <int NP, int D, int FOBS, bool PF = false>
 __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  KF_PHASE_KERNEL_BEGIN
   double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
@@ -137,11 +140,12 @@ __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs 
     const int64_t p = base + lane;
     const bool act = p < a.N;
     float dn1;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, true, PF>(a, act ? p : a.N - 1, act, nullptr, dn1);
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, true, PF>(a, act ? p : a.N - 1, act, nullptr, dn1 KF_PHASE_ARG);
     acc += act ? (double)dn : 0.0;
     acc1 += act ? (double)dn1 : 0.0;
   }
   analysis_partials(a, acc, acc1);
+  KF_PHASE_KERNEL_END
 #endif
 }
 

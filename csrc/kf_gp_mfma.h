@@ -404,7 +404,7 @@ __device__ __forceinline__ void gpm_epilogue(const KF_CONST_AS BandDesc* q, cons
 
 template <int NP, int D, int FOBS, bool GT = false, bool PF = false, int LAYOUT = BAND_LAYOUT_RUNTIME>
 __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
-                                                     const kf_h8* lds, float& dn_first) {
+                                                     const kf_h8* lds, float& dn_first KF_PHASE_PARAM) {
   constexpr int NT = ntri(NP);
   // LAYOUT == BAND_LAYOUT_TIP: two bands with the JRC-TIP VIS / NIR maps, the
   // band loop unrolled with both maps compile-time (no runtime map branches
@@ -417,7 +417,6 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     for (int j = 0; j < NP; ++j) x0[j] = KF_PX(a.x_prev, j * ld, p);
   }
   dn_first = 0.f;
-  KF_PHASE_T0
   KF_PHASE_COUNT(KF_PH_GROUPS)
   // wave-uniform loop over the fused Gauss-Newton iterations (AnalysisArgs.gn_fused)
   for (int it = 0;; ++it) {
