@@ -108,10 +108,6 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
   }
   __syncthreads();
   KF_PHASE(KF_PH_PROLOGUE)
-  // LDS-DMA prefetch sink (gpm_prefetch_row): written by every wave, never read
-  __shared__ float pf_sink_buf[64];
-  // variant 11 (A/B): no prefetch
-  const kf_lds_ptr pf_sink = a.variant == 11 ? nullptr : (kf_lds_ptr)pf_sink_buf;
   double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BS;
@@ -119,9 +115,8 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
     const int64_t p = base + lane;
     const bool act = p < a.N;
     float dn1;
-    const int64_t pn = p + stride < a.N ? p + stride : (base + stride < a.N ? a.N - 1 : -1);
     const float dn = pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT>(a, act ? p : a.N - 1, act, gpm_lds,
-                                                                           dn1, pn, pf_sink KF_PHASE_ARG);
+                                                                           dn1 KF_PHASE_ARG);
     acc += act ? (double)dn : 0.0;
     acc1 += act ? (double)dn1 : 0.0;
   }
@@ -138,7 +133,6 @@ template <int NP, int D, int FOBS, bool PF = false>
 __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   KF_PHASE_KERNEL_BEGIN
-  __shared__ float pf_sink_buf[64];   // LDS-DMA prefetch sink (gpm_prefetch_row)
   double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
@@ -146,10 +140,7 @@ __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs 
     const int64_t p = base + lane;
     const bool act = p < a.N;
     float dn1;
-    const int64_t pn = p + stride < a.N ? p + stride : (base + stride < a.N ? a.N - 1 : -1);
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, true, PF>(a, act ? p : a.N - 1, act, nullptr, dn1, pn,
-                                                                a.variant == 11 ? nullptr : (kf_lds_ptr)pf_sink_buf
-                                                                KF_PHASE_ARG);
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, true, PF>(a, act ? p : a.N - 1, act, nullptr, dn1 KF_PHASE_ARG);
     acc += act ? (double)dn : 0.0;
     acc1 += act ? (double)dn1 : 0.0;
   }
@@ -461,19 +452,19 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
       if (a.fast_obs == OBS_DN16) {
         if constexpr (NP == 7 && FD == 4) {
           if (tip) {
-            KF_MFMA_GO(OBS_DN16, BLOCK, 3, BAND_LAYOUT_TIP)
+            KF_MFMA_GO(OBS_DN16, BLOCK, 1, BAND_LAYOUT_TIP)
             return true;
           }
         }
-        KF_MFMA_GO(OBS_DN16, BLOCK, 3, BAND_LAYOUT_RUNTIME)
+        KF_MFMA_GO(OBS_DN16, BLOCK, 1, BAND_LAYOUT_RUNTIME)
       } else if (a.fast_obs == OBS_F32) {
         if constexpr (NP == 7 && FD == 4) {
           if (tip) {
-            KF_MFMA_GO(OBS_F32, BLOCK, 3, BAND_LAYOUT_TIP)
+            KF_MFMA_GO(OBS_F32, BLOCK, 1, BAND_LAYOUT_TIP)
             return true;
           }
         }
-        KF_MFMA_GO(OBS_F32, BLOCK, 3, BAND_LAYOUT_RUNTIME)
+        KF_MFMA_GO(OBS_F32, BLOCK, 1, BAND_LAYOUT_RUNTIME)
       } else {
         return false;
       }

@@ -402,54 +402,9 @@ __device__ __forceinline__ void gpm_epilogue(const KF_CONST_AS BandDesc* q, cons
   }
 }
 
-// L2 prefetch through the LDS-DMA path (global_load_lds): the wave's 64
-// lanes load one row segment into a 256-byte LDS sink that nothing reads, so
-// no VGPR is tied up and the compiler tracks the load (vmcnt) itself.  The
-// data lands in L2 / the vector L1, and the real load of the same line later
-// hits there instead of paying an HBM round trip.  Used for the inputs whose
-// latency the per-pixel phases otherwise expose: the observations of the
-// bands not yet decoded and the next pixel group's forecast inputs and
-// observations (phase clocks, profiles/README.md r3_v11).
-typedef __attribute__((address_space(3))) void* kf_lds_ptr;
-__device__ __forceinline__ void gpm_prefetch_row(const void* row, int64_t p, int bytes, kf_lds_ptr sink) {
-  const char* g = (const char*)row + p * bytes;
-  if (bytes == 2) __builtin_amdgcn_global_load_lds(g, sink, 2, 0, 0);
-  else __builtin_amdgcn_global_load_lds(g, sink, 4, 0, 0);
-}
-
-// The next pixel group's forecast inputs (propagated rows of x_a and the
-// diagonal of p_a: the light fused propagators, forecast_partial) and every
-// band's observations; p_next < 0: no next group.
-template <int NP, int FOBS>
-__device__ __forceinline__ void gpm_prefetch_group(const AnalysisArgs& a, int64_t p_next, int band0,
-                                                   kf_lds_ptr sink) {
-  if (p_next < 0) return;
-  if (FOBS == OBS_DN16 || FOBS == OBS_F32) {
-    for (int bi = band0; bi < a.n_bands; ++bi) {
-      const KF_CONST_AS BandDesc* bdp = cptr(a.bands) + bi;
-      if (FOBS == OBS_DN16) gpm_prefetch_row(bdp->dn, p_next, 2, sink);
-      else gpm_prefetch_row(bdp->y, p_next, 4, sink);
-    }
-  }
-  if (band0 == 0 && a.prop) {
-    const KF_CONST_AS PropArgs* pa = opaque(cptr(a.prop));
-    const uint32_t pm = pa->prop_mask;
-    if (pa->mode == PROP_PRIOR_PARTIAL && __builtin_popcount(pm) <= 2) {
-#pragma unroll
-      for (int j = 0; j < NP; ++j) {
-        if ((pm >> j) & 1u) {
-          gpm_prefetch_row(pa->x_a + j * pa->ld, p_next, 4, sink);
-          gpm_prefetch_row(pa->p_a + tri(NP, j, j) * pa->ld, p_next, 4, sink);
-        }
-      }
-    }
-  }
-}
-
 template <int NP, int D, int FOBS, bool GT = false, bool PF = false, int LAYOUT = BAND_LAYOUT_RUNTIME>
 __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
-                                                     const kf_h8* lds, float& dn_first,
-                                                     int64_t p_next = -1, kf_lds_ptr pf_sink = nullptr KF_PHASE_PARAM) {
+                                                     const kf_h8* lds, float& dn_first KF_PHASE_PARAM) {
   constexpr int NT = ntri(NP);
   // LAYOUT == BAND_LAYOUT_TIP: two bands with the JRC-TIP VIS / NIR maps, the
   // band loop unrolled with both maps compile-time (no runtime map branches
@@ -524,12 +479,6 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
       else gpm_inputs<NP, D>(bdp, x0, xi, c);
       c *= -0.5f * LOG2E;
       float S[D + 1];
-      if (pf_sink && bi == 0 && it == 0) {
-        // under this band's GP loop: the remaining bands of this group, then
-        // the next group (older in vmcnt than every later load of this group)
-        gpm_prefetch_group<NP, FOBS>(a, p, 1, pf_sink);
-        gpm_prefetch_group<NP, FOBS>(a, p_next, 0, pf_sink);
-      }
       KF_PHASE(KF_PH_BAND_IN)
       if constexpr (GT) gp_mfma_sums_g<D, PF>(bdp->gpm, nch, xi, c, S);
       else gp_mfma_sums<D>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
