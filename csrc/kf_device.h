@@ -451,6 +451,12 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
       if constexpr (NP == 7 && FD == 4) tip = a.band_layout == BAND_LAYOUT_TIP && a.n_bands == 2 && a.variant != 10;
       if (a.fast_obs == OBS_DN16) {
         if constexpr (NP == 7 && FD == 4) {
+          if (tip && a.variant == 12) {
+            // (A/B) launch bound of 3 workgroups per CU: the compiler holds the
+            // kernel to 168 VGPRs itself instead of landing there by chance
+            KF_MFMA_GO(OBS_DN16, BLOCK, 3, BAND_LAYOUT_TIP)
+            return true;
+          }
           if (tip) {
             KF_MFMA_GO(OBS_DN16, BLOCK, 1, BAND_LAYOUT_TIP)
             return true;

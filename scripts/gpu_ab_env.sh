@@ -12,13 +12,13 @@ if [ -n "$TESTS" ]; then
   tail -1 gpurun_out/ab_tests.log
 fi
 IFS='|' read -ra SETS <<< "${AB:?set AB}"
-: > gpurun_out/ab_env.jsonl
+OUT=${OUT:-gpurun_out/ab_env.jsonl}; : > $OUT
 for r in $(seq 1 "${ROUNDS:-2}"); do
   for s in "${SETS[@]}"; do
     timeout -k 10 300 env $s python -u bench.py ${BENCH_ARGS} > gpurun_out/ab_run.log 2>&1 \
       || { tail -5 gpurun_out/ab_run.log; echo "!! bench ($s) rc=$?"; exit 1; }
     line=$(tail -1 gpurun_out/ab_run.log)
-    echo "{\"setting\": \"$s\", \"round\": $r, \"result\": $line}" >> gpurun_out/ab_env.jsonl
+    echo "{\"setting\": \"$s\", \"round\": $r, \"result\": $line}" >> $OUT
     echo "$s r$r: $(echo "$line" | python -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["ms_per_step"])')"
   done
 done
