@@ -444,6 +444,11 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
     hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_>), dim3(grid), dim3(BS_), lds, s, \
                        a);                                                                                   \
   }
+      // Launch bound of 3 workgroups per CU (MINW = 3, as the LDS tables
+      // allow) up to 7 parameters: the compiler holds the kernel to <= 168
+      // VGPRs itself (A/B neutral against landing there unconstrained,
+      // profiles/r3_v13_*); 10 parameters would spill, so no bound there.
+      constexpr int MW = NP <= 7 ? 3 : 1;
       // JRC-TIP band layout (AnalysisArgs.band_layout, checked on the host):
       // band loop unrolled over the two compile-time maps (variant 10: the
       // runtime-layout kernel, for A/B)
@@ -451,26 +456,20 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
       if constexpr (NP == 7 && FD == 4) tip = a.band_layout == BAND_LAYOUT_TIP && a.n_bands == 2 && a.variant != 10;
       if (a.fast_obs == OBS_DN16) {
         if constexpr (NP == 7 && FD == 4) {
-          if (tip && a.variant == 12) {
-            // (A/B) launch bound of 3 workgroups per CU: the compiler holds the
-            // kernel to 168 VGPRs itself instead of landing there by chance
+          if (tip) {
             KF_MFMA_GO(OBS_DN16, BLOCK, 3, BAND_LAYOUT_TIP)
             return true;
           }
-          if (tip) {
-            KF_MFMA_GO(OBS_DN16, BLOCK, 1, BAND_LAYOUT_TIP)
-            return true;
-          }
         }
-        KF_MFMA_GO(OBS_DN16, BLOCK, 1, BAND_LAYOUT_RUNTIME)
+        KF_MFMA_GO(OBS_DN16, BLOCK, MW, BAND_LAYOUT_RUNTIME)
       } else if (a.fast_obs == OBS_F32) {
         if constexpr (NP == 7 && FD == 4) {
           if (tip) {
-            KF_MFMA_GO(OBS_F32, BLOCK, 1, BAND_LAYOUT_TIP)
+            KF_MFMA_GO(OBS_F32, BLOCK, 3, BAND_LAYOUT_TIP)
             return true;
           }
         }
-        KF_MFMA_GO(OBS_F32, BLOCK, 1, BAND_LAYOUT_RUNTIME)
+        KF_MFMA_GO(OBS_F32, BLOCK, MW, BAND_LAYOUT_RUNTIME)
       } else {
         return false;
       }

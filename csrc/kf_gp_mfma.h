@@ -189,7 +189,9 @@ __device__ __forceinline__ int gpm_sum_row(int col) {
 }
 
 // One 32-point chunk for both column blocks: exponent, split, packed sums.
-template <int D>
+// FIRST: the first chunk starts the sums from a zero accumulator operand (an
+// inline constant of the MFMA) instead of 32 zeroed registers.
+template <int D, bool FIRST = false>
 __device__ __forceinline__ void gpm_chunk(const kf_h8 (&ea)[gpm_k_steps(D)], const kf_h8 (&sa)[2],
                                           const kf_h8 (&xb)[2][gpm_k_steps(D)], float neg1, kf_f16v (&acc)[2]) {
   constexpr int NK = gpm_k_steps(D);
@@ -203,7 +205,7 @@ __device__ __forceinline__ void gpm_chunk(const kf_h8 (&ea)[gpm_k_steps(D)], con
     for (int q = 0; q < 2; ++q) {
       kf_h8 mh, ml;
       gpm_exp_split(e, 8 * q, neg1, mh, ml);
-      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q], mh, acc[i], 0, 0, 0);
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q], mh, (FIRST && q == 0) ? zero : acc[i], 0, 0, 0);
       acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q], ml, acc[i], 0, 0, 0);
     }
   }
@@ -231,15 +233,26 @@ __device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, cons
   kf_h8 xb[2][NK];
   float cl;
   gpm_operands<D>(xi, c, xb, cl);
-  kf_f16v acc[2] = {{}, {}};
-  for (int ch = 0; ch < nchunk; ++ch) {
+  kf_f16v acc[2];
+  auto load = [&](int ch, kf_h8 (&ea)[NK], kf_h8 (&sa)[2]) {
     const kf_h8* t = tab + ch * FPC;
-    kf_h8 ea[NK], sa[2];
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk) ea[kk] = t[64 * kk + lane];
     const kf_h8* st = sp + ch * sstep;
     sa[0] = st[0];
     sa[1] = st[soff];
+  };
+  // every table has >= 1 chunk (models/gp.py mfma_tables); the first one is
+  // peeled so the sums start from the MFMA's zero operand
+  KF_DCHECK(nchunk >= 1);
+  {
+    kf_h8 ea[NK], sa[2];
+    load(0, ea, sa);
+    gpm_chunk<D, true>(ea, sa, xb, neg1, acc);
+  }
+  for (int ch = 1; ch < nchunk; ++ch) {
+    kf_h8 ea[NK], sa[2];
+    load(ch, ea, sa);
     gpm_chunk<D>(ea, sa, xb, neg1, acc);
   }
   gpm_extract2<D>(acc, S);
@@ -270,7 +283,7 @@ __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, con
   kf_h8 xb[2][NK];
   float cl;
   gpm_operands<D>(xi, c, xb, cl);
-  kf_f16v acc[2] = {{}, {}};
+  kf_f16v acc[2];
   kf_h8 ea[NK], sa[2];
   if constexpr (PF) {
 #pragma unroll
@@ -278,9 +291,10 @@ __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, con
     sa[0] = sp[0];
     sa[1] = sp[soff];
   }
-  for (int ch = 0; ch < nchunk; ++ch) {
-    // PF: prefetch chunk ch + 1 (the last chunk re-reads itself); otherwise
-    // load chunk ch here and leave the latency to the other waves
+  // one chunk: PF prefetches chunk ch + 1 (the last chunk re-reads itself);
+  // otherwise chunk ch is loaded here and the latency left to the other waves.
+  // The first chunk is peeled (sums from the MFMA's zero operand, >= 1 chunk).
+  auto step = [&](int ch, auto first) {
     const int nx = PF ? (ch + 1 < nchunk ? ch + 1 : ch) : ch;
     const kf_gtab t = tab + (int64_t)nx * FPC;
     const kf_gtab st = sp + (int64_t)nx * sstep;
@@ -295,14 +309,17 @@ __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, con
       sa[0] = san[0];
       sa[1] = san[1];
     }
-    gpm_chunk<D>(ea, sa, xb, neg1, acc);
+    gpm_chunk<D, decltype(first)::value>(ea, sa, xb, neg1, acc);
     if constexpr (PF) {
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) ea[kk] = ean[kk];
       sa[0] = san[0];
       sa[1] = san[1];
     }
-  }
+  };
+  KF_DCHECK(nchunk >= 1);
+  step(0, std::true_type{});
+  for (int ch = 1; ch < nchunk; ++ch) step(ch, std::false_type{});
   gpm_extract2<D>(acc, S);
   const float s = kexp2(cl);
 #pragma unroll
