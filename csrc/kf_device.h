@@ -456,12 +456,6 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
       if constexpr (NP == 7 && FD == 4) tip = a.band_layout == BAND_LAYOUT_TIP && a.n_bands == 2 && a.variant != 10;
       if (a.fast_obs == OBS_DN16) {
         if constexpr (NP == 7 && FD == 4) {
-          if (tip && a.variant == 13) {
-            // (A/B) one 768-thread workgroup per CU (3 waves per SIMD): one LDS
-            // table copy per CU, staged once per 12 waves instead of per 4
-            KF_MFMA_GO(OBS_DN16, 768, 1, BAND_LAYOUT_TIP)
-            return true;
-          }
           if (tip) {
             KF_MFMA_GO(OBS_DN16, BLOCK, 3, BAND_LAYOUT_TIP)
             return true;
