@@ -264,9 +264,7 @@ __device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, cons
 // The same sums with the band's table read from global memory (L2-resident:
 // used when the tables of all bands do not fit the 160 KiB of LDS, e.g. ten
 // PROSAIL bands).  PF: the next chunk's fragments are loaded while the current
-// one runs (register double buffer).  tab + nchunk * FPC holds a zero
-// fragment (models/gp.py).
-typedef const __attribute__((address_space(1))) kf_h8* kf_gtab;
+// one runs (register double buffer).
 
 template <int D, bool PF = false>
 __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, const float (&xi)[D], float c,
@@ -274,35 +272,44 @@ __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, con
   static_assert(D >= 1 && D <= GPM_MAX_D, "GP input count for the matrix-core path");
   constexpr int NK = gpm_k_steps(D), NR = gpm_sum_rows(D), FPC = gpm_frags_per_chunk(D);
   const int lane = threadIdx.x & 63, h = lane >> 5;
-  const kf_gtab tab = (kf_gtab)tab_;
+  // The table through a raw buffer resource: per-lane byte offsets fixed for
+  // the whole loop (VGPR), the chunk offset in the scalar soffset, so a chunk
+  // costs no VALU address arithmetic (64-bit pointer adds per load before).
+  // Lanes whose sums row is unused read past num_records: the hardware
+  // returns zeros, the shared zero fragment of the LDS path.
+  const int chunk_bytes = FPC * 16;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(tab_), (short)0, nchunk * chunk_bytes, 0x00020000);
   const int cr = gpm_sum_row<D>(lane & 31);
   const bool ls = cr >= 0;
-  const kf_gtab sp = ls ? tab + 64 * NK + h * NR + cr : tab + (int64_t)nchunk * FPC;
-  const int sstep = ls ? FPC : 0, soff = ls ? 2 * NR : 0;
+  constexpr int OOB = 0x40000000;
+  const int soff0 = ls ? (64 * NK + h * NR + cr) * 16 : OOB;
+  const int soff1 = ls ? soff0 + 2 * NR * 16 : OOB;
   const float neg1 = gpm_neg1();
   kf_h8 xb[2][NK];
   float cl;
   gpm_operands<D>(xi, c, xb, cl);
   kf_f16v acc[2];
   kf_h8 ea[NK], sa[2];
+  auto ld = [&](int voff, int ch) {
+    return __builtin_bit_cast(kf_h8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, ch * chunk_bytes, 0));
+  };
   if constexpr (PF) {
 #pragma unroll
-    for (int kk = 0; kk < NK; ++kk) ea[kk] = tab[64 * kk + lane];
-    sa[0] = sp[0];
-    sa[1] = sp[soff];
+    for (int kk = 0; kk < NK; ++kk) ea[kk] = ld((64 * kk + lane) * 16, 0);
+    sa[0] = ld(soff0, 0);
+    sa[1] = ld(soff1, 0);
   }
   // one chunk: PF prefetches chunk ch + 1 (the last chunk re-reads itself);
   // otherwise chunk ch is loaded here and the latency left to the other waves.
   // The first chunk is peeled (sums from the MFMA's zero operand, >= 1 chunk).
   auto step = [&](int ch, auto first) {
     const int nx = PF ? (ch + 1 < nchunk ? ch + 1 : ch) : ch;
-    const kf_gtab t = tab + (int64_t)nx * FPC;
-    const kf_gtab st = sp + (int64_t)nx * sstep;
     kf_h8 ean[NK], san[2];
 #pragma unroll
-    for (int kk = 0; kk < NK; ++kk) ean[kk] = t[64 * kk + lane];
-    san[0] = st[0];
-    san[1] = st[soff];
+    for (int kk = 0; kk < NK; ++kk) ean[kk] = ld((64 * kk + lane) * 16, nx);
+    san[0] = ld(soff0, nx);
+    san[1] = ld(soff1, nx);
     if constexpr (!PF) {
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) ea[kk] = ean[kk];

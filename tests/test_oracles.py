@@ -338,3 +338,14 @@ def test_gain_fused_forecast_and_output_vs_oracle(dev):
     print(f"gain fused on {dev}: x {ex:.2e} P {ep:.2e} unc {eu:.2e}")
     assert ex < 1e-4 and ep < 2e-4 and eu < 1e-4, (ex, ep, eu)
     assert torch.equal(mean, xo)
+
+
+@pytest.mark.gpu
+def test_global_table_prefetch_variant_bit_identical(cuda):
+    """The global-table matrix-core kernel reads its tables through a raw buffer
+    resource (rows past the table return zeros); the register double-buffered
+    variant (7) loads the same fragments one chunk earlier: identical results."""
+    prob = prosail_problem(N=3000, n_bands=10, seed=31)
+    x0, a0, s0 = run_fused(prob, cuda, variant=0, expect_global=True)
+    x7, a7, s7 = run_fused(prob, cuda, variant=7, expect_global=True)
+    assert np.array_equal(x0, x7) and np.array_equal(a0, a7) and np.array_equal(s0, s7)
