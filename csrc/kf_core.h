@@ -172,7 +172,10 @@ struct BandDesc {
 constexpr int GPM_MAP_RUNTIME = 0, GPM_MAP_TIP_VIS = 2, GPM_MAP_TIP_NIR = 3;
 // AnalysisArgs.band_layout: BAND_LAYOUT_TIP = exactly two bands, the JRC-TIP VIS
 // then NIR maps (kafka/inference/utils.py:148-153), 7-parameter state
-constexpr int BAND_LAYOUT_RUNTIME = 0, BAND_LAYOUT_TIP = 1;
+// BAND_LAYOUT_SHARED_X = every band a full-state GP (identity map, D = NP)
+// with the same centre: the global-table matrix-core kernel builds the
+// exponent operand once per Gauss-Newton iteration (kf_gp_mfma.h)
+constexpr int BAND_LAYOUT_RUNTIME = 0, BAND_LAYOUT_TIP = 1, BAND_LAYOUT_SHARED_X = 2;
 
 struct PropArgs {
   int64_t N, ld;

@@ -267,8 +267,8 @@ __device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, cons
 // one runs (register double buffer).
 
 template <int D, bool PF = false>
-__device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, const float (&xi)[D], float c,
-                                               float (&S)[D + 1]) {
+__device__ __forceinline__ void gp_mfma_sums_g_xb(const void* tab_, int nchunk, const kf_h8 (&xb)[2][gpm_k_steps(D)],
+                                                  float cl, float (&S)[D + 1]) {
   static_assert(D >= 1 && D <= GPM_MAX_D, "GP input count for the matrix-core path");
   constexpr int NK = gpm_k_steps(D), NR = gpm_sum_rows(D), FPC = gpm_frags_per_chunk(D);
   const int lane = threadIdx.x & 63, h = lane >> 5;
@@ -286,9 +286,6 @@ __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, con
   const int soff0 = ls ? (64 * NK + h * NR + cr) * 16 : OOB;
   const int soff1 = ls ? soff0 + 2 * NR * 16 : OOB;
   const float neg1 = gpm_neg1();
-  kf_h8 xb[2][NK];
-  float cl;
-  gpm_operands<D>(xi, c, xb, cl);
   kf_f16v acc[2];
   kf_h8 ea[NK], sa[2];
   auto ld = [&](int voff, int ch) {
@@ -331,6 +328,45 @@ __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, con
   const float s = kexp2(cl);
 #pragma unroll
   for (int f = 0; f <= D; ++f) S[f] *= s;
+}
+
+template <int D, bool PF = false>
+__device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, const float (&xi)[D], float c,
+                                               float (&S)[D + 1]) {
+  kf_h8 xb[2][gpm_k_steps(D)];
+  float cl;
+  gpm_operands<D>(xi, c, xb, cl);
+  gp_mfma_sums_g_xb<D, PF>(tab_, nchunk, xb, cl, S);
+}
+
+// BAND_LAYOUT_SHARED_X: every band is a full-state GP around the same centre,
+// so the exponent operand (split, packed and half-swapped centred inputs,
+// gpm_operands) is built once per Gauss-Newton iteration and each band only
+// patches the K slot 3D + 1 that carries its own constant c.  D even: slots 3D
+// ("1") and 3D + 1 (c) share one packed dword.  Which lanes hold the dword of
+// their own pixel and which their partner's follows gpm_operands.
+template <int D>
+__device__ __forceinline__ void gpm_patch_c(kf_h8 (&xb)[2][gpm_k_steps(D)], float c, float& cl) {
+  static_assert(D % 2 == 0, "slots 3D and 3D + 1 share a dword for even D");
+  constexpr int K = 3 * D + 1, KK = K / 16, W = K % 16, F = W / 8, Q = (W % 8) / 2;
+  const _Float16 ch = (_Float16)fmaxf(c, -6.0e4f);
+  cl = c - (float)ch;
+  const uint32_t own = gpm_pack((_Float16)1.f, ch);
+  const uint32_t par = __builtin_bit_cast(uint32_t, gpm_partner32(__builtin_bit_cast(float, own)));
+  const bool h1 = (threadIdx.x & 32) != 0;
+  // F1 slot: lanes h = 1 hold their own dword in block 1 and the partner's in
+  // block 0; F0 slot: lanes h = 0 their own in block 0, the partner's in block 1
+  const bool mine = F == 1 ? h1 : !h1;
+  kf_u4 b0 = __builtin_bit_cast(kf_u4, xb[0][KK]), b1 = __builtin_bit_cast(kf_u4, xb[1][KK]);
+  if (F == 1) {
+    b1[Q] = mine ? own : b1[Q];
+    b0[Q] = mine ? par : b0[Q];
+  } else {
+    b0[Q] = mine ? own : b0[Q];
+    b1[Q] = mine ? par : b1[Q];
+  }
+  xb[0][KK] = __builtin_bit_cast(kf_h8, b0);
+  xb[1][KK] = __builtin_bit_cast(kf_h8, b1);
 }
 
 #endif
@@ -479,6 +515,22 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   }
   int nobs = 0;
   int off = 0;
+  // BAND_LAYOUT_SHARED_X (global tables, full-state GPs around one centre):
+  // the exponent operand of the centred inputs once per iteration, each band
+  // patches its constant in (gpm_patch_c).  Variant 14: per band (A/B).
+  constexpr bool SXC = GT && D == NP && D % 2 == 0;
+  bool sx = false;
+  kf_h8 sxb[2][gpm_k_steps(D)];
+  if constexpr (SXC) {
+    sx = a.band_layout == BAND_LAYOUT_SHARED_X && a.variant != 14 && a.n_bands > 0;
+    if (sx) {
+      const KF_CONST_AS BandDesc* b0 = cptr(a.bands);
+      float xi0[D], c0;
+#pragma unroll
+      for (int d = 0; d < D; ++d) xi0[d] = x0[d] - b0->center[d];
+      gpm_operands<D>(xi0, 0.f, sxb, c0);
+    }
+  }
   // one band: GP sums on the matrix cores, value and Jacobian, normal equations.
   // MKC: the band's map kind when known at compile time (LAYOUT), else -1
   auto band = [&](int bi, auto mkc) {
@@ -504,8 +556,24 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
       c *= -0.5f * LOG2E;
       float S[D + 1];
       KF_PHASE(KF_PH_BAND_IN)
-      if constexpr (GT) gp_mfma_sums_g<D, PF>(bdp->gpm, nch, xi, c, S);
-      else gp_mfma_sums<D>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
+      if constexpr (SXC) {
+        if (sx) {
+          kf_h8 xb[2][gpm_k_steps(D)];
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int kk = 0; kk < gpm_k_steps(D); ++kk) xb[i][kk] = sxb[i][kk];
+          float cl;
+          gpm_patch_c<D>(xb, c, cl);
+          gp_mfma_sums_g_xb<D, PF>(bdp->gpm, nch, xb, cl, S);
+        } else {
+          gp_mfma_sums_g<D, PF>(bdp->gpm, nch, xi, c, S);
+        }
+      } else if constexpr (GT) {
+        gp_mfma_sums_g<D, PF>(bdp->gpm, nch, xi, c, S);
+      } else {
+        gp_mfma_sums<D>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
+      }
       KF_PHASE(KF_PH_GP)
       const KF_CONST_AS BandDesc* q = opaque(bdp);   // epilogue fields: not live across the chunk loop
       const float sc = q->gpm_scale;

@@ -34,6 +34,7 @@ class GaussianProcessEmulator:
         if self.lam.shape != (self.inputs.shape[1],):
             raise ValueError("lam must have one entry per input dimension")
         self._records = None
+        self._center = None     # set_center: a shared reference point (else the training mean)
 
     # ------------------------------------------------------------------ shape
     @property
@@ -76,7 +77,23 @@ class GaussianProcessEmulator:
 
     # ---------------------------------------------------------- kernel ABI
     def center(self) -> np.ndarray:
-        return self.inputs.mean(0)
+        """Reference point the kernel records are expressed around (inputs are
+        centred on it): the training mean unless ``set_center`` chose one."""
+        return self.inputs.mean(0) if self._center is None else self._center
+
+    def set_center(self, c) -> "GaussianProcessEmulator":
+        """Express the records around ``c`` instead of the training mean (the
+        same predictions up to rounding).  Bands of one state that share a
+        reference point share their centred GP inputs, and the matrix-core
+        kernel then builds the exponent operand once for all of them
+        (kf_gp_mfma.h, BAND_LAYOUT_SHARED_X)."""
+        c = np.asarray(c, dtype=np.float64).reshape(-1)
+        if c.shape != (self.n_inputs,):
+            raise ValueError("center needs one value per input")
+        self._center = c.copy()
+        self._records = None
+        self.__dict__.pop("_spec_cache", None)
+        return self
 
     def records(self) -> np.ndarray:
         """float32 kernel records, training-point pairs field-major:
@@ -153,12 +170,13 @@ class GaussianProcessEmulator:
 
 def pack_emulator_set(ems: dict):
     """{key: emulator} -> (header, float64 buffer): header = [(key, T, D, name)],
-    buffer = per emulator [signal, mean, inputs (T x D), alpha (T), lam (D)]."""
+    buffer = per emulator [signal, mean, inputs (T x D), alpha (T), lam (D), center (D)]."""
     header, parts = [], []
     for key, em in ems.items():
         T, D = em.inputs.shape
         header.append((str(key), int(T), int(D), str(em.name)))
-        parts += [np.array([em.signal, em.mean]), em.inputs.ravel(), em.alpha.ravel(), em.lam.ravel()]
+        parts += [np.array([em.signal, em.mean]), em.inputs.ravel(), em.alpha.ravel(), em.lam.ravel(),
+                  np.asarray(em.center(), dtype=np.float64).ravel()]
     return header, (np.concatenate(parts) if parts else np.zeros(0))
 
 
@@ -173,7 +191,10 @@ def unpack_emulator_set(header, buf) -> dict:
         o += T
         lam = buf[o:o + D]
         o += D
-        out[key] = GaussianProcessEmulator(inputs.copy(), alpha.copy(), lam.copy(), float(sig), float(mu), name=name)
+        center = buf[o:o + D]
+        o += D
+        em = GaussianProcessEmulator(inputs.copy(), alpha.copy(), lam.copy(), float(sig), float(mu), name=name)
+        out[key] = em.set_center(center) if not np.array_equal(center, em.center()) else em
     return out
 
 
@@ -390,6 +411,8 @@ def make_prosail_emulators(n_bands: int = 10, n_train: int = 250, seed: int = 0,
     sig = np.sqrt(np.diag(covar))
     lo = mean - 3 * np.maximum(sig, 0.05)
     hi = mean + 3 * np.maximum(sig, 0.05)
+    # every band's records around the SAIL prior mean (the centre of the design
+    # box): the bands share their centred inputs (BAND_LAYOUT_SHARED_X)
     return [GaussianProcessEmulator.synthetic(prosail_target(b, n_params, hard), lo[:n_params], hi[:n_params],
                                               n_train, seed + b, name=f"prosail_b{b}{'h' if hard else ''}")
-            for b in range(n_bands)]
+            .set_center(mean[:n_params]) for b in range(n_bands)]

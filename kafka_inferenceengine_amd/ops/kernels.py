@@ -109,6 +109,9 @@ GPM_GLOBAL_D = (7, 10)     # full-state GP input counts with a global-table inst
 # kf_core.h BAND_LAYOUT_TIP: exactly two GP bands with the JRC-TIP VIS then NIR maps
 # (BandDesc.map_kind 2, 3), 4 inputs each: the matrix-core kernel unrolls the band loop
 BAND_LAYOUT_TIP = 1
+# kf_core.h BAND_LAYOUT_SHARED_X: every band a full-state GP (identity map) around the
+# same centre, matrix-core tables in global memory: one exponent operand per iteration
+BAND_LAYOUT_SHARED_X = 2
 FD_PRECOMP = -1   # kf_core.h: fast analysis kernel for all-precomputed operators
 FD_LINEAR = -2    # kf_core.h: fast analysis kernel for all-linear (identity/selection) operators
 # analysis fast-kernel variant (kf_kernels.hip:l_analysis_fast); env override for A/B runs
@@ -192,6 +195,9 @@ def make_band_table(descs: list, device, keepalive=()) -> BandTable:
     layout = 0
     if fast_d == 4 and gpm_frags > 0 and [d.map_kind for d in descs] == [2, 3]:
         layout = BAND_LAYOUT_TIP
+    elif (gpm_global and fast_d % 2 == 0 and all(d.map_identity for d in descs)
+          and len({tuple(d.center[:fast_d]) for d in descs}) == 1):
+        layout = BAND_LAYOUT_SHARED_X
     return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs, gpm_frags, gpm_global, layout)
 
 
@@ -275,7 +281,7 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     a.gn_fused = int(gn_fused)
     a.partials_first = _ptr(partials_first) if gn_fused == 2 else 0
     a.fast_d, a.fast_obs = (bands.fast_d, bands.fast_obs) if fast else (0, 0)
-    a.band_layout = int(bands.layout) if (fast and n_params == 7) else 0
+    a.band_layout = int(bands.layout) if (fast and (bands.layout != BAND_LAYOUT_TIP or n_params == 7)) else 0
     a.variant = DEFAULT_VARIANT if variant is None else int(variant)
     a.gpm_frags = bands.gpm_frags if fast else 0
     a.gpm_global = int(bool(bands.gpm_global) and fast and bands.fast_d == n_params)

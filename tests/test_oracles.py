@@ -349,3 +349,18 @@ def test_global_table_prefetch_variant_bit_identical(cuda):
     x0, a0, s0 = run_fused(prob, cuda, variant=0, expect_global=True)
     x7, a7, s7 = run_fused(prob, cuda, variant=7, expect_global=True)
     assert np.array_equal(x0, x7) and np.array_equal(a0, a7) and np.array_equal(s0, s7)
+
+
+@pytest.mark.gpu
+def test_shared_centre_operand_bit_identical(cuda):
+    """PROSAIL emulators share one centre (models/gp.py set_center), so the
+    global-table kernel builds the exponent operand once per iteration and each
+    band patches its constant in (BAND_LAYOUT_SHARED_X); variant 14 builds it per
+    band: identical results."""
+    prob = prosail_problem(N=3000, n_bands=10, seed=33)
+    db = dbands(prob, cuda)
+    tab = build_table(prob["specs"], db, prob["n"], RecordCache(), cuda)
+    assert tab.layout == K.BAND_LAYOUT_SHARED_X
+    xs, as_, ss = run_fused(prob, cuda, variant=0, expect_global=True)
+    xp, ap, sp = run_fused(prob, cuda, variant=14, expect_global=True)
+    assert np.array_equal(xs, xp) and np.array_equal(as_, ap) and np.array_equal(ss, sp)
