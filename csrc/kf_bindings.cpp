@@ -288,27 +288,82 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
     else host_lut_nearest(P<const float>(lut), M, D, P<const float>(x), N, ld, P<int32_t>(out));
   });
 
+  // omega non-empty: host schedule (nsweep = len(omega)); else the device
+  // schedule (sched / omega_tab, at most nsweep sweeps from s_base)
   m.def("reg_tiled", [](int64_t ld, int w, int h, int j0, uint32_t prev_mask, float gamma,
                         const std::vector<float>& omega, uintptr_t u, uintptr_t v, uintptr_t z, uintptr_t zp,
-                        uintptr_t z_out, uintptr_t zp_out, bool device, uintptr_t stream) {
+                        uintptr_t z_out, uintptr_t zp_out, bool device, uintptr_t stream, int nsweep, int hu, int hd,
+                        uintptr_t halo_up, uintptr_t halo_dn, int64_t halo_plane, int ty0, int ty1, uintptr_t sched,
+                        uintptr_t omega_tab, int s_base) {
     RegTileArgs a{};
     a.ld = ld;
     a.w = w;
     a.h = h;
     a.j0 = j0;
-    a.nsweep = (int32_t)omega.size();
+    if (!omega.empty()) {
+      a.nsweep = (int32_t)omega.size();
+      if (sched) throw std::runtime_error("reg_tiled: host omegas and a device schedule");
+      set_arr(a.omega, omega, "omega");
+    } else {
+      a.nsweep = nsweep;
+      if (!sched || !omega_tab) throw std::runtime_error("reg_tiled: no omegas and no device schedule");
+    }
     if (a.nsweep < 1 || a.nsweep > REG_TILE_MAX_SWEEPS) throw std::runtime_error("reg_tiled: 1..8 sweeps");
     a.prev_mask = prev_mask;
     a.gamma = gamma;
-    set_arr(a.omega, omega, "omega");
     a.u = P<const float>(u);
     a.v = P<const float>(v);
     a.z = P<const float>(z);
     a.zp = P<const float>(zp);
     a.z_out = P<float>(z_out);
     a.zp_out = P<float>(zp_out);
+    a.hu = hu;
+    a.hd = hd;
+    a.halo_up = P<const float>(halo_up);
+    a.halo_dn = P<const float>(halo_dn);
+    a.halo_plane = halo_plane;
+    a.ty0 = ty0;
+    a.ty1 = ty1;
+    a.sched = P<const int32_t>(sched);
+    a.omega_tab = P<const float>(omega_tab);
+    a.s_base = s_base;
     if (device) check_hip(dev_reg_tiled(a, (hipStream_t)stream), "reg_tiled");
     else if (host_reg_tiled(a) != 0) throw std::runtime_error("reg_tiled: bad arguments");
+  }, py::arg("ld"), py::arg("w"), py::arg("h"), py::arg("j0"), py::arg("prev_mask"), py::arg("gamma"),
+     py::arg("omega"), py::arg("u"), py::arg("v"), py::arg("z"), py::arg("zp"), py::arg("z_out"),
+     py::arg("zp_out"), py::arg("device"), py::arg("stream"), py::arg("nsweep") = 0, py::arg("hu") = 0,
+     py::arg("hd") = 0, py::arg("halo_up") = 0, py::arg("halo_dn") = 0, py::arg("halo_plane") = 0,
+     py::arg("ty0") = 0, py::arg("ty1") = 0, py::arg("sched") = 0, py::arg("omega_tab") = 0,
+     py::arg("s_base") = 0);
+  m.def("reg_rho_blocks", [](int64_t N) { return reg_rho_blocks(N); });
+  // rho = gamma * max_p v_RR(p) deg(p) of one field on a dense strip -> rho[0] (f64)
+  m.def("reg_rho", [](uintptr_t vrow, int64_t w, int h, int halo, int64_t N, uintptr_t pmax, int npart, float gamma,
+                      uintptr_t rho, bool device, uintptr_t stream) {
+    StripGeo g{};
+    g.w = w;
+    g.h = h;
+    g.halo = halo;
+    g.n_up = (halo & 1) ? w : 0;
+    if (w <= 0 || (int64_t)h * w != N) throw std::runtime_error("reg_rho: dense geometry w * h != N");
+    RegScheduleArgs a{};
+    a.pmax = P<const float>(pmax);
+    a.npart = npart;
+    a.gamma = gamma;
+    a.rho = P<double>(rho);
+    if (device) check_hip(dev_reg_rho(P<const float>(vrow), g, N, a, (hipStream_t)stream), "reg_rho");
+    else if (host_reg_rho(P<const float>(vrow), g, N, a) != 0) throw std::runtime_error("reg_rho: bad arguments");
+  });
+  m.def("reg_schedule", [](uintptr_t rho, double tol, int max_sweeps, uintptr_t sched, uintptr_t omega_tab,
+                           uintptr_t info, bool device, uintptr_t stream) {
+    RegScheduleArgs a{};
+    a.rho = P<double>(rho);
+    a.tol = tol;
+    a.max_sweeps = max_sweeps;
+    a.sched = P<int32_t>(sched);
+    a.omega_tab = P<float>(omega_tab);
+    a.info = P<double>(info);
+    if (device) check_hip(dev_reg_schedule(a, (hipStream_t)stream), "reg_schedule");
+    else if (host_reg_schedule(a) != 0) throw std::runtime_error("reg_schedule: bad arguments");
   });
 
   bind_stream(m);

@@ -1855,17 +1855,105 @@ constexpr int REG_TILE_MAX_SWEEPS = 8;
 struct RegTileArgs {
   int64_t ld;                // u / v leading dimension
   int32_t w, h;              // strip geometry (w * h local pixels)
-  int32_t j0, nsweep;        // regularised row of u / v; sweeps in this pass
+  int32_t j0, nsweep;        // regularised row of u / v; sweeps in this pass (at most)
   uint32_t prev_mask;        // bit s: sweep s is a Chebyshev step against the iterate before
   float gamma;
   float omega[REG_TILE_MAX_SWEEPS];
   const float* u;            // [NP][ld]  (row j0 used)
   const float* v;            // [k*NP][ld] (row j0 used)
   const float* z;            // [w*h] current iterate
-  const float* zp;           // [w*h] the iterate before (read when bit 0 of prev_mask is set)
-  float* z_out;              // iterate after nsweep sweeps
+  const float* zp;           // [w*h] the iterate before (read when the first sweep is a Chebyshev step)
+  float* z_out;              // iterate after the pass's sweeps
   float* zp_out;             // the iterate before that
+  // Deep halo (tile-DP strips with neighbours; C2 once per pass instead of once
+  // per sweep): rows -hu..-1 above and h..h+hd-1 below the strip, each side 4
+  // planes of halo_plane floats -- u, v, z, zp -- row-major from its first row
+  // (row -hu, row h).  The ring of the strip's edge tiles reads them; a pass of
+  // ns <= min(hu, hd) sweeps (hu / hd > 0) leaves every strip row exact because
+  // the values that go stale at the halo's outer edge move one row per sweep.
+  int32_t hu, hd;
+  const float* halo_up;
+  const float* halo_dn;
+  int64_t halo_plane;
+  int32_t ty0, ty1;          // tile rows [ty0, ty1) of this launch (ty1 = 0: every tile row)
+  // Device-resident schedule (RegSchedule, no host read-back before the pass):
+  // sched[0] = sweeps of this GN iteration's coupled solve before the finish,
+  // omega_tab[s] = the Chebyshev weight of sweep s (0: a plain Jacobi sweep).
+  // This pass runs sweeps s_base .. s_base + min(nsweep, sched[0] - s_base) - 1
+  // (none: the outputs are copies of the inputs).  Null: nsweep / prev_mask / omega.
+  const int32_t* sched;
+  const float* omega_tab;
+  int32_t s_base;
 };
+
+// sweeps this pass runs and the weight of its sweep s (cheb: a Chebyshev step)
+KF_HD int reg_tile_nsweep(const RegTileArgs& a) {
+  if (!a.sched) return a.nsweep;
+  const int left = a.sched[0] - a.s_base;
+  return left < 0 ? 0 : (left < a.nsweep ? left : a.nsweep);
+}
+KF_HD float reg_tile_omega(const RegTileArgs& a, int s, bool& cheb) {
+  if (a.sched) {
+    const float om = a.omega_tab[a.s_base + s];
+    cheb = om != 0.f;
+    return om;
+  }
+  cheb = (a.prev_mask >> s) & 1u;
+  return a.omega[s];
+}
+
+// Chebyshev schedule of a GN iteration's coupled solve (K9) from the all-rank
+// Jacobi bound rho (Gershgorin, linear_kf.py:_reg_schedule): S sweeps in all
+// (the last is the finish) cut the error by tol at the Chebyshev rate
+// sigma = rho / (1 + sqrt(1 - rho^2)); rho >= 1 (or NaN): max_sweeps plain
+// Jacobi sweeps; rho <= 0: one.  omega[it] for it < S - 1 (0: plain Jacobi,
+// the first sweep always).  Double precision, one thread: the device kernel
+// and the host runner evaluate the same expressions.
+KF_HD int reg_cheb_schedule(double rho, double tol, int max_sweeps, float* omega, double* rho_used) {
+  int S;
+  double r = rho;
+  if (!(r < 1.0)) {
+    r = 0.0;
+    S = max_sweeps;
+  } else if (r <= 0.0) {
+    r = 0.0;
+    S = 1;
+  } else {
+    const double sigma = r / (1.0 + sqrt(fmax(0.0, 1.0 - r * r)));
+    const double need = ceil(log(2.0 / tol) / log(1.0 / sigma));
+    S = (int)fmin(fmax(1.0, need), (double)max_sweeps);
+  }
+  double om = 1.0;
+  for (int it = 0; it < S - 1; ++it) {
+    const bool cheb = r > 0.0 && it > 0;
+    if (cheb) om = it == 1 ? 1.0 / (1.0 - 0.5 * r * r) : 1.0 / (1.0 - 0.25 * r * r * om);
+    omega[it] = cheb ? (float)om : 0.f;
+  }
+  *rho_used = r;
+  return S;
+}
+
+struct RegScheduleArgs {
+  const float* pmax;         // per-block maxima of v_RR * deg (reg_rho pass), npart of them
+  int32_t npart;
+  float gamma;
+  double* rho;               // [1] g * max: written by the rho pass, all-reduced (max) over ranks in between
+  double tol;
+  int32_t max_sweeps;
+  int32_t* sched;            // [1] sweeps before the finish (S - 1)
+  float* omega_tab;          // [max_sweeps]
+  double* info;              // [2] rho used, S (read back by the host, asynchronously)
+};
+
+// per-pixel term of the Jacobi bound for one regularised field on a dense strip:
+// V_RR * deg (deg from the index, halo rows included)
+KF_HD float reg_rho_term(const float* vrow, const StripGeo& g, int64_t p) {
+  const uint32_t w = (uint32_t)g.w;
+  const uint32_t r = (uint32_t)p / w, c = (uint32_t)p - r * w;
+  const int deg = ((r > 0 || (g.halo & 1)) ? 1 : 0) + ((r + 1 < (uint32_t)g.h || (g.halo & 2)) ? 1 : 0) +
+                  (c > 0 ? 1 : 0) + (c + 1 < w ? 1 : 0);
+  return vrow[p] * (float)deg;
+}
 
 // neighbour sum in reg_nsum_dense's order (up, down, left, right; missing ones skipped)
 KF_HD float reg_tile_nsum(const float* z, int64_t p, int64_t w, bool up, bool dn, bool lf, bool rt) {
@@ -1879,7 +1967,9 @@ KF_HD float reg_tile_nsum(const float* z, int64_t p, int64_t w, bool up, bool dn
 
 KF_HD float reg_tile_step(const RegTileArgs& a, int s, float s_nb, float u, float v, float zp) {
   float z = fmaf(a.gamma, v * s_nb, u);
-  if ((a.prev_mask >> s) & 1u) z = fmaf(a.omega[s], z - zp, zp);
+  bool cheb;
+  const float om = reg_tile_omega(a, s, cheb);
+  if (cheb) z = fmaf(om, z - zp, zp);
   return z;
 }
 

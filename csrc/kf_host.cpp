@@ -192,27 +192,80 @@ int host_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, 
   return 0;
 }
 
-// RegTileArgs on the host: the same sweeps over the whole strip, one at a time
-// (two scratch planes), so a host run equals the device's tiled pass.
+// RegTileArgs on the host: the same sweeps over the whole domain (strip plus
+// deep halo rows), one at a time (scratch planes), then the strip rows of the
+// launch's tile rows are written -- a host run equals the device's tiled pass.
 int host_reg_tiled(const RegTileArgs& a) {
-  const int64_t w = a.w, n = (int64_t)a.w * a.h;
-  if (a.nsweep < 1 || a.nsweep > REG_TILE_MAX_SWEEPS || n <= 0) return 1;
-  std::vector<float> cur(a.z, a.z + n), prev(n), nxt(n);
-  if (a.prev_mask & 1u) std::copy(a.zp, a.zp + n, prev.begin());
-  const float* u = a.u + a.j0 * a.ld;
-  const float* v = a.v + a.j0 * a.ld;
-  for (int s = 0; s < a.nsweep; ++s) {
+  const int64_t w = a.w;
+  if (a.nsweep < 1 || a.nsweep > REG_TILE_MAX_SWEEPS || a.w <= 0 || a.h <= 0) return 1;
+  if (a.hu < 0 || a.hd < 0 || (a.hu && a.hu < a.nsweep) || (a.hd && a.hd < a.nsweep)) return 1;
+  if ((a.hu && !a.halo_up) || (a.hd && !a.halo_dn) || (a.sched && !a.omega_tab)) return 1;
+  const int K = reg_tile_nsweep(a);
+  bool cheb0 = false;
+  if (K > 0) reg_tile_omega(a, 0, cheb0);
+  const int H = a.hu + a.h + a.hd;          // domain rows, row 0 = strip row -hu
+  const int64_t n = (int64_t)H * w;
+  std::vector<float> cur(n), prev(n, 0.f), nxt(n), u(n), v(n);
+  const float* ug = a.u + a.j0 * a.ld;
+  const float* vg = a.v + a.j0 * a.ld;
+  for (int R = 0; R < H; ++R) {
+    const int gr = R - a.hu;
+    const float *su = ug, *sv = vg, *sz = a.z, *szp = a.zp;
+    int64_t off = (int64_t)gr * w;
+    if (gr < 0) {
+      off = (int64_t)(gr + a.hu) * w;
+      su = a.halo_up, sv = a.halo_up + a.halo_plane, sz = a.halo_up + 2 * a.halo_plane;
+      szp = a.halo_up + 3 * a.halo_plane;
+    } else if (gr >= a.h) {
+      off = (int64_t)(gr - a.h) * w;
+      su = a.halo_dn, sv = a.halo_dn + a.halo_plane, sz = a.halo_dn + 2 * a.halo_plane;
+      szp = a.halo_dn + 3 * a.halo_plane;
+    }
+    for (int64_t c = 0; c < w; ++c) {
+      const int64_t q = (int64_t)R * w + c;
+      cur[q] = sz[off + c];
+      u[q] = su[off + c];
+      v[q] = sv[off + c];
+      if ((cheb0 || K == 0) && szp) prev[q] = szp[off + c];
+    }
+  }
+  for (int s = 0; s < K; ++s) {
 #pragma omp parallel for schedule(static)
-    for (int64_t p = 0; p < n; ++p) {
-      const int64_t r = p / w, c = p - r * w;
-      const float sn = reg_tile_nsum(cur.data(), p, w, r > 0, r + 1 < a.h, c > 0, c + 1 < w);
-      nxt[p] = reg_tile_step(a, s, sn, u[p], v[p], prev[p]);
+    for (int64_t q = 0; q < n; ++q) {
+      const int64_t r = q / w, c = q - r * w;
+      const float sn = reg_tile_nsum(cur.data(), q, w, r > 0, r + 1 < H, c > 0, c + 1 < w);
+      nxt[q] = reg_tile_step(a, s, sn, u[q], v[q], prev[q]);
     }
     std::swap(prev, cur);
     std::swap(cur, nxt);
   }
-  std::copy(cur.begin(), cur.end(), a.z_out);
-  std::copy(prev.begin(), prev.end(), a.zp_out);
+  const int tiles_y = (a.h + 63) / 64;
+  const int ty0 = a.ty1 == 0 ? 0 : a.ty0, ty1 = a.ty1 == 0 ? tiles_y : a.ty1;
+  if (ty0 < 0 || ty1 > tiles_y || ty0 > ty1) return 1;
+  const int64_t r_lo = (int64_t)ty0 * 64, r_hi = std::min<int64_t>((int64_t)ty1 * 64, a.h);
+  for (int64_t r = r_lo; r < r_hi; ++r) {
+    const int64_t src = (r + a.hu) * w;
+    std::copy(cur.begin() + src, cur.begin() + src + w, a.z_out + r * w);
+    std::copy(prev.begin() + src, prev.begin() + src + w, a.zp_out + r * w);
+  }
+  return 0;
+}
+
+int host_reg_rho(const float* vrow, const StripGeo& g, int64_t N, const RegScheduleArgs& a) {
+  if (N <= 0 || g.w <= 0) return 1;
+  float m = 0.f;
+  for (int64_t p = 0; p < N; ++p) m = std::max(m, reg_rho_term(vrow, g, p));
+  a.rho[0] = (double)(m * a.gamma);
+  return 0;
+}
+
+int host_reg_schedule(const RegScheduleArgs& a) {
+  if (a.max_sweeps < 1 || !a.sched || !a.omega_tab || !a.info || !a.rho) return 1;
+  double used;
+  const int S = reg_cheb_schedule(a.rho[0], a.tol, a.max_sweeps, a.omega_tab, &used);
+  a.sched[0] = S - 1;
+  a.info[0] = used;
+  a.info[1] = (double)S;
   return 0;
 }
 

@@ -46,6 +46,9 @@ hipError_t dev_gather(int elem_bytes, const void* src, const int64_t* idx, void*
 hipError_t dev_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out,
                            hipStream_t s);
 hipError_t dev_reg_tiled(const RegTileArgs& a, hipStream_t s);
+int reg_rho_blocks(int64_t N);
+hipError_t dev_reg_rho(const float* vrow, const StripGeo& g, int64_t N, const RegScheduleArgs& a, hipStream_t s);
+hipError_t dev_reg_schedule(const RegScheduleArgs& a, hipStream_t s);
 
 // Host runner: the same per-pixel code over OpenMP; the block partition
 // mirrors the device grid-stride mapping so partials have the same meaning.
@@ -64,5 +67,7 @@ int host_unpack(int np, const float* x, const float* a, int64_t N, int64_t ld, c
                 float* unc, int64_t plane);
 int host_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out);
 int host_reg_tiled(const RegTileArgs& a);
+int host_reg_rho(const float* vrow, const StripGeo& g, int64_t N, const RegScheduleArgs& a);
+int host_reg_schedule(const RegScheduleArgs& a);
 
 }  // namespace kf

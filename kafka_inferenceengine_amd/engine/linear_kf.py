@@ -1131,60 +1131,12 @@ class LinearKalman:
                    x0_out=None if x_prev is not None else x0_buf,
                    out=None if out is None else (None, out[1], out[2]))
         nbr = None if geo else reg.nbr
-        rho, sweeps = self._reg_schedule(reg, v, rows, k, gamma, sweeps,
-                                         self.config.spatial_tol if final else self.config.spatial_tol_first)
-        z = reg.z_buffers(k)
-        for i, r in enumerate(rows):
-            z[0][i, :N].copy_(x_ref[r, :N])
-        cur = reg.fill_halo(z[0])
-        prev = None
-        # Chebyshev semi-iterative weights (omega_1 = 1: the first step is Jacobi)
-        sched, omega = [], 1.0
-        for it in range(sweeps - 1):
-            if rho > 0 and it > 0:
-                omega = 1.0 / (1.0 - 0.5 * rho * rho) if it == 1 else 1.0 / (1.0 - 0.25 * rho * rho * omega)
-            sched.append((omega, rho > 0 and it > 0))
-        # C2 overlap (dense or masked strips): the rows the neighbours need first,
-        # their exchange posted, then the interior while the rows are on the wire
-        overlap = self.comm.distributed and reg.split is not None
-        sa, sb = reg.split if overlap else (0, 0)
-        tiled = (self.config.spatial_tiled and not overlap and k == 1 and geo is not None
-                 and int(geo["halo"]) == 0 and N > 0)
-        if tiled and sched:
-            if self._reg_z4 is None or self._reg_z4.shape != z[0].shape:
-                self._reg_z4 = torch.zeros_like(z[0])
-            spare = [b for b in (*z, self._reg_z4) if b is not cur]
-            prev = spare.pop()
-            for c0 in range(0, len(sched), K.REG_TILE_MAX_SWEEPS):
-                part = sched[c0:c0 + K.REG_TILE_MAX_SWEEPS]
-                o_cur, o_prev = spare[0], spare[1]
-                K.reg_sweeps_tiled(n, u, v, cur, prev, o_cur, o_prev, gamma, reg.reg_mask, N, geo,
-                                   [o for o, _ in part], [c for _, c in part])
-                spare = [cur, prev]
-                cur, prev = o_cur, o_prev
-            self.reg_tiled_launches += -(-len(sched) // K.REG_TILE_MAX_SWEEPS)
-            sched = []
-        for omega, use_prev in sched:
-            nxt = next(b for b in z if b is not cur and b is not prev)
-            zp = prev if use_prev else None
-            if overlap:
-                with self.timer.phase("reg_boundary"):
-                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(0, sa), z_prev=zp,
-                                omega=omega)
-                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(N - sb, sb),
-                                z_prev=zp, omega=omega)
-                with self.timer.phase("halo"):
-                    pend = reg.start_fill(nxt)
-                with self.timer.phase("reg_interior"):
-                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(sa, N - sa - sb),
-                                z_prev=zp, omega=omega)
-                with self.timer.phase("halo"):
-                    nxt = reg.finish_fill(pend, nxt)
-                self.reg_overlapped_sweeps += 1
-            else:
-                K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, z_prev=zp, omega=omega)
-                nxt = reg.fill_halo(nxt)
-            prev, cur = cur, nxt
+        tol = self.config.spatial_tol if final else self.config.spatial_tol_first
+        depth = self._reg_tiled_depth(k)
+        if depth:
+            cur, rho, sweeps = self._reg_tiled_solve(reg, geo, u, v, x_ref, rows[0], gamma, tol, depth, sweeps)
+        else:
+            cur, rho, sweeps = self._reg_sweep_solve(reg, geo, nbr, u, v, x_ref, rows, gamma, tol, sweeps)
         K.reg_finish(n, u, v, cur, nbr, x_ref, x_out, gamma, reg.reg_mask, N, partials=self._partials, geo=geo,
                      out=None if out is None else (out[0], None, out[2]))
         # residual of the coupled solve (metrics only): the finish applied one more
@@ -1196,18 +1148,29 @@ class LinearKalman:
         self._reg_log.append({"solver": self.config.spatial_solver, "rho": rho, "sweeps": sweeps, "r2": r2,
                               "count": k * self.n_total})
 
-    def _reg_schedule(self, reg, v, rows, k, gamma, sweeps, tol):
-        """(rho, sweeps) of this GN iteration's coupled solve.  Chebyshev: rho =
-        max over pixels of g deg ||V_RR||_inf, a Gershgorin bound of the Jacobi
-        matrix's spectral radius (its spectrum is real: J is similar to a
-        symmetric matrix), max-reduced over the ranks; the sweeps cut the error
-        by ``spatial_tol`` at the Chebyshev rate sigma = rho / (1 + sqrt(1 -
-        rho^2)) (plain Jacobi: rho).  ``tol``: spatial_tol for an iteration that
-        can end the GN loop, spatial_tol_first before.  One host read-back per
-        GN iteration."""
-        cfg = self.config
-        if cfg.spatial_solver != "chebyshev":
-            return 0.0, sweeps
+    def _reg_tiled_depth(self, k: int) -> int:
+        """Sweeps per temporal-blocking pass of the coupled solve, 0 for the
+        per-sweep path.  Rank-uniform (every rank sees the whole state mask and
+        the strip bounds): one regularised field on a fully active raster, a
+        pass as deep as the shallowest strip (its deep halo comes from one
+        neighbour) and at most REG_TILE_MAX_SWEEPS."""
+        if not self.config.spatial_tiled or k != 1:
+            return 0
+        dense = getattr(self, "_mask_dense", None)
+        if dense is None:
+            dense = self._mask_dense = bool(self.state_mask.size) and bool(self.state_mask.all())
+        if not dense:
+            return 0
+        h_min = min(b - a for a, b in self.partition.bounds)
+        return int(min(K.REG_TILE_MAX_SWEEPS, h_min))
+
+    def _reg_rho_async(self, reg, v, rows, k, gamma):
+        """Chebyshev bound rho = max over pixels of g deg ||V_RR||_inf, a
+        Gershgorin bound of the Jacobi matrix's spectral radius (its spectrum is
+        real: J is similar to a symmetric matrix), max-reduced over the ranks
+        on the stream; returns a pending read-back (PendingSum, element 0)."""
+        from ..parallel.comm import PendingSum
+
         n, N = self.n_params, self.N
         if N and k == 1:
             # V row (c * n + r_j): component r_j of column c (kf_core.h JacobiArgs); one
@@ -1218,15 +1181,188 @@ class LinearKalman:
             rho_t = (gamma * blk.amax(0) * reg.degrees).amax().reshape(1).double()
         else:
             rho_t = torch.zeros(1, dtype=torch.float64, device=self.device)
-        rho = float(self.comm.all_reduce_(rho_t, op="max").item())
+        return PendingSum(self.comm.all_reduce_(rho_t, op="max"), 1, 1)
+
+    def _reg_sweeps_for(self, rho: float, tol: float):
+        """(rho, sweeps) of the coupled solve: the sweeps (the finish included)
+        cut the error by ``tol`` at the Chebyshev rate sigma = rho / (1 + sqrt(1
+        - rho^2)); the same expressions as the device schedule
+        (kf_core.h:reg_cheb_schedule).  ``tol``: spatial_tol for an iteration
+        that can end the GN loop, spatial_tol_first before."""
+        cfg = self.config
         if not rho < 1.0:
             LOG.warning("spatial prior: Jacobi bound rho=%.4f >= 1, plain Jacobi sweeps", rho)
             return 0.0, max(1, int(cfg.spatial_max_sweeps))
         if rho <= 0.0:
             return 0.0, 1
         sigma = rho / (1.0 + math.sqrt(max(0.0, 1.0 - rho * rho)))
-        need = math.log(2.0 / tol) / math.log(1.0 / sigma)
-        return rho, int(min(max(1, math.ceil(need)), int(cfg.spatial_max_sweeps)))
+        need = math.ceil(math.log(2.0 / tol) / math.log(1.0 / sigma))
+        return rho, int(min(max(1, need), int(cfg.spatial_max_sweeps)))
+
+    @staticmethod
+    def _cheb_weights(rho: float, n_sweeps: int):
+        """Chebyshev semi-iterative weights of the sweeps before the finish:
+        (omega, Chebyshev step?) -- the first step is plain Jacobi."""
+        sched, omega = [], 1.0
+        for it in range(n_sweeps):
+            if rho > 0 and it > 0:
+                omega = 1.0 / (1.0 - 0.5 * rho * rho) if it == 1 else 1.0 / (1.0 - 0.25 * rho * rho * omega)
+            sched.append((omega, rho > 0 and it > 0))
+        return sched
+
+    def _reg_sweep_solve(self, reg, geo, nbr, u, v, x_ref, rows, gamma, tol, sweeps):
+        """Coupled solve, one launch per sweep (masked strips, several fields).
+        The first sweep is plain Jacobi whatever rho is, so it is queued before
+        rho is read back: the host waits while the GPU runs it.  (With rho <= 0
+        the schedule has no sweep before the finish; V_RR deg = 0 everywhere
+        then, so that extra sweep leaves z = u and the finish unchanged.)  C2
+        overlap on distributed strips: each sweep's boundary rows, their
+        exchange posted, the interior rows under it."""
+        cfg = self.config
+        n, N = self.n_params, self.N
+        k = len(rows)
+        cheb = cfg.spatial_solver == "chebyshev"
+        pend = self._reg_rho_async(reg, v, rows, k, gamma) if cheb else None
+        rho = 0.0
+        z = reg.z_buffers(k)
+        for i, r in enumerate(rows):
+            z[0][i, :N].copy_(x_ref[r, :N])
+        cur = reg.fill_halo(z[0])
+        prev = None
+        overlap = self.comm.distributed and reg.split is not None
+        sa, sb = reg.split if overlap else (0, 0)
+        sched = [(1.0, False)] if cheb else self._cheb_weights(0.0, sweeps - 1)
+        it = 0
+        while it < len(sched):
+            omega, use_prev = sched[it]
+            nxt = next(b for b in z if b is not cur and b is not prev)
+            zp = prev if use_prev else None
+            if overlap:
+                with self.timer.phase("reg_boundary"):
+                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(0, sa), z_prev=zp,
+                                omega=omega)
+                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(N - sb, sb),
+                                z_prev=zp, omega=omega)
+                with self.timer.phase("halo"):
+                    hp = reg.start_fill(nxt)
+                with self.timer.phase("reg_interior"):
+                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(sa, N - sa - sb),
+                                z_prev=zp, omega=omega)
+                with self.timer.phase("halo"):
+                    nxt = reg.finish_fill(hp, nxt)
+                self.reg_overlapped_sweeps += 1
+            else:
+                K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, z_prev=zp, omega=omega)
+                nxt = reg.fill_halo(nxt)
+            prev, cur = cur, nxt
+            it += 1
+            if pend is not None:
+                # the first sweep is queued: read rho while the GPU runs it
+                rho, sweeps = self._reg_sweeps_for(pend.result(0), tol)
+                pend = None
+                sched = self._cheb_weights(rho, max(sweeps - 1, 1))
+        return cur, rho, sweeps
+
+    def _reg_tiled_solve(self, reg, geo, u, v, x_ref, j0, gamma, tol, depth, sweeps):
+        """Coupled solve of one regularised field on dense strips, `depth`
+        sweeps per pass out of LDS (kf_reg_tiled.hip).
+
+        * The schedule lives on the device: rho (one max pass over V_RR deg),
+          its all-rank max, then the sweep count and Chebyshev weights
+          (RegSchedule).  The first pass is queued at once and reads them; the
+          host reads the sweep count back while the GPU runs that pass, then
+          queues the rest (no host wait between the prepare and the sweeps).
+        * Tile-DP (C2): once per GN iteration the neighbours' u, v and initial
+          iterate rows, then once per pass the last two iterates -- `depth`
+          rows each -- instead of one row per sweep.  A pass runs its boundary
+          tile rows, posts their exchange and runs the interior under it.  The
+          finish reads the neighbours' adjacent row of the final iterate from
+          the last pass's exchange (no extra exchange).
+        Bit-identical to one launch per sweep, at any rank count."""
+        from ..parallel.comm import PendingSum
+
+        cfg = self.config
+        n, N = self.n_params, self.N
+        dist_ = self.comm.distributed
+        z = reg.z_buffers(1)
+        if self._reg_z4 is None or self._reg_z4.shape != z[0].shape:
+            self._reg_z4 = torch.zeros_like(z[0])
+        bufs = [z[0], z[1], z[2], self._reg_z4]
+        cur, prev = bufs[0], bufs[1]
+        cur[0, :N].copy_(x_ref[j0, :N])
+        cheb = cfg.spatial_solver == "chebyshev"
+        pend, rs, rho = None, None, 0.0
+        if cheb:
+            rs = getattr(self, "_reg_sched", None)
+            if rs is None or rs.max_sweeps != int(cfg.spatial_max_sweeps):
+                rs = self._reg_sched = K.RegSchedule(N, cfg.spatial_max_sweeps, self.device)
+            with self.timer.phase("reg_schedule"):
+                rs.rho_pass(v[j0], geo, N, gamma)
+                self.comm.all_reduce_(rs.rho, op="max")
+                rs.schedule(tol)
+                pend = PendingSum(rs.info, 1, 2)
+            n_sched = None
+        else:
+            n_sched = max(1, int(sweeps)) - 1
+            if n_sched == 0:
+                return reg.fill_halo(cur), 0.0, 1
+        halo, rows_b = None, None
+        if dist_:
+            if getattr(reg, "depth", None) != depth:
+                reg.deep_setup(depth)
+            with self.timer.phase("halo"):
+                reg.deep_finish(reg.deep_start({0: u[j0], 1: v[j0], 2: cur[0]}))
+            halo = reg.deep_halo()
+            T = K.reg_tile_rows(geo["h"])
+            ta, tb = K.reg_boundary_tile_rows(geo["h"], depth, halo[0] > 0, halo[1] > 0)
+            rows_b = ((0, ta), (tb, T), (ta, tb))
+        s_base = 0
+        while True:
+            o_cur, o_prev = [b for b in bufs if b is not cur and b is not prev]
+            if cheb:
+                kw = dict(sched=(rs.sched, rs.omega), s_base=s_base, nsweep=depth)
+            else:
+                ns = min(depth, n_sched - s_base)
+                part = self._cheb_weights(0.0, n_sched)[s_base:s_base + ns]
+                kw = dict(omegas=[o for o, _ in part], chebyshev=[c for _, c in part])
+
+            def launch(tr):
+                K.reg_sweeps_tiled(n, u, v, cur, prev, o_cur, o_prev, gamma, reg.reg_mask, N, geo, halo=halo,
+                                   tile_rows=tr, **kw)
+            if dist_:
+                with self.timer.phase("reg_boundary"):
+                    launch(rows_b[0])
+                    launch(rows_b[1])
+                with self.timer.phase("halo"):
+                    hp = reg.deep_start({2: o_cur[0], 3: o_prev[0]})
+                with self.timer.phase("reg_interior"):
+                    launch(rows_b[2])
+                with self.timer.phase("halo"):
+                    reg.deep_finish(hp)
+                self.reg_overlapped_sweeps += 1
+            else:
+                launch(None)
+            self.reg_tiled_launches += 1
+            cur, prev = o_cur, o_prev
+            s_base += depth
+            if n_sched is None:
+                # the first pass is queued: read the schedule while the GPU runs it
+                rho = pend.result(0)
+                sweeps = int(pend.result(1))
+                n_sched = sweeps - 1
+                if not rho < 1.0:
+                    LOG.warning("spatial prior: Jacobi bound rho=%.4f >= 1, plain Jacobi sweeps", rho)
+            if s_base >= n_sched:
+                break
+        if dist_:
+            # the finish's one-row halo: the neighbours' adjacent rows of the final iterate
+            w = int(geo["w"])
+            if halo[2] is not None:
+                cur[0, N:N + w].copy_(halo[2][2, (depth - 1) * w:depth * w])
+            if halo[3] is not None:
+                off = N + reg.n_up
+                cur[0, off:off + w].copy_(halo[3][2, :w])
+        return cur, rho, sweeps
 
     # ------------------------------------------------ band-parallel (TP-like)
     def _band_parallel_iteration(self, table, x_prev, fc: KFState, x_out, A_out, status):

@@ -514,40 +514,144 @@ def reg_sweep(n_params, u, v, z_ext, nbr, z_out, gamma, reg_mask, N, geo=None, r
 REG_TILE_MAX_SWEEPS = 8
 
 
-def reg_sweeps_tiled(n_params, u, v, z, z_prev, z_out, zp_out, gamma, reg_mask, N, geo, omegas, chebyshev):
-    """K9 temporal blocking (csrc/kf_reg_tiled.hip): ``len(omegas)`` (<= 8) sweeps
-    of the one regularised field of a dense strip without halo rows in one
-    launch.  Sweep s is ``reg_sweep(..., z_prev=previous iterate,
-    omega=omegas[s])`` when ``chebyshev[s]``, the plain Jacobi sweep otherwise;
-    bit-identical to those launches.  Writes the last iterate to ``z_out`` and
-    the one before to ``zp_out`` (local parts, [1, >= N])."""
+REG_TILE_ROWS = 64    # kf_reg_tiled.hip RT_TH: strip rows per tile row
+
+
+def reg_tile_rows(h: int) -> int:
+    """Tile rows of the tiled sweep kernel over a strip of ``h`` rows."""
+    return -(-int(h) // REG_TILE_ROWS)
+
+
+def reg_boundary_tile_rows(h: int, depth: int, up: bool, down: bool):
+    """``(a, b)``: the tile rows [0, a) and [b, tiles) hold the strip rows the
+    neighbours need ([0, depth) with a neighbour above, [h - depth, h) with one
+    below); [a, b) is the interior a pass can run while they are on the wire."""
+    ty = reg_tile_rows(h)
+    a = reg_tile_rows(min(depth, h)) if up else 0
+    b = (max(h - depth, 0) // REG_TILE_ROWS) if down else ty
+    a = min(a, ty)
+    return a, max(a, b)
+
+
+def reg_sweeps_tiled(n_params, u, v, z, z_prev, z_out, zp_out, gamma, reg_mask, N, geo, omegas=None,
+                     chebyshev=None, *, sched=None, s_base=0, nsweep=None, halo=None, tile_rows=None):
+    """K9 temporal blocking (csrc/kf_reg_tiled.hip): up to 8 sweeps of the one
+    regularised field of a dense strip in one launch.  Sweep s is
+    ``reg_sweep(..., z_prev=previous iterate, omega=omegas[s])`` when
+    ``chebyshev[s]``, the plain Jacobi sweep otherwise; bit-identical to those
+    launches.  Writes the last iterate to ``z_out`` and the one before to
+    ``zp_out`` (local parts, [1, >= N]).
+
+    ``sched = (sched_i32, omega_tab)``: the device schedule of :func:`reg_schedule`
+    instead of host weights -- the pass runs sweeps ``s_base ..`` of it, at most
+    ``nsweep`` (none left: the outputs are copies of the inputs).
+    ``halo = (hu, hd, up, dn)``: deep halo of a tile-DP strip, ``up`` / ``dn``
+    [4, >= depth * w] planes (u, v, z, zp rows) of the rows above / below, row-
+    major from the outermost row (``HaloExchanger.deep_*``).  ``tile_rows = (ty0,
+    ty1)``: only those tile rows (boundary-first C2 overlap)."""
     check_np(n_params)
     dev = u.device
     if bin(int(reg_mask)).count("1") != 1:
         raise ValueError("reg_sweeps_tiled: one regularised field")
-    if geo is None or int(geo["halo"]) != 0:
-        raise ValueError("reg_sweeps_tiled: dense strip geometry without halo rows")
-    ns = len(omegas)
-    if not 1 <= ns <= REG_TILE_MAX_SWEEPS or len(chebyshev) != ns:
-        raise ValueError(f"reg_sweeps_tiled: 1..{REG_TILE_MAX_SWEEPS} sweeps, one flag per sweep")
+    if geo is None:
+        raise ValueError("reg_sweeps_tiled: dense strip geometry needed")
+    hu, hd, up, dn = halo if halo is not None else (0, 0, None, None)
+    gh = int(geo["halo"])
+    if bool(hu) != bool(gh & 1) or bool(hd) != bool(gh & 2):
+        raise ValueError("reg_sweeps_tiled: the deep halo must match the strip's halo rows")
+    if sched is None:
+        if omegas is None or chebyshev is None:
+            raise ValueError("reg_sweeps_tiled: host weights or a device schedule")
+        ns = len(omegas)
+        if not 1 <= ns <= REG_TILE_MAX_SWEEPS or len(chebyshev) != ns:
+            raise ValueError(f"reg_sweeps_tiled: 1..{REG_TILE_MAX_SWEEPS} sweeps, one flag per sweep")
+        mask = sum(1 << s for s, c in enumerate(chebyshev) if c)
+        if mask & 1 and z_prev is None:
+            raise ValueError("reg_sweeps_tiled: the first sweep is a Chebyshev step but z_prev is None")
+    else:
+        if omegas is not None:
+            raise ValueError("reg_sweeps_tiled: host weights and a device schedule")
+        ns = int(nsweep or 0)
+        if not 1 <= ns <= REG_TILE_MAX_SWEEPS:
+            raise ValueError(f"reg_sweeps_tiled: 1..{REG_TILE_MAX_SWEEPS} sweeps per pass")
+        mask = 0
+        sch, om = sched
+        if sch.dtype != torch.int32 or om.dtype != torch.float32 or sch.device != dev or om.device != dev:
+            raise ValueError("reg_sweeps_tiled: schedule tensors (int32, float32) on the operands' device")
+        # the kernel reads omega_tab[s] only for s < sched[0] <= omega_tab.numel() - 1
+        if s_base < 0:
+            raise ValueError("reg_sweeps_tiled: negative first sweep")
+        if z_prev is None and s_base > 0:
+            raise ValueError("reg_sweeps_tiled: a later pass needs the previous iterate")
+    w, h = int(geo["w"]), int(geo["h"])
+    for d in (hu, hd):
+        if d and not ns <= d <= REG_TILE_MAX_SWEEPS:
+            raise ValueError(f"reg_sweeps_tiled: halo depth {d} must cover the pass's {ns} sweeps")
+    plane = 0
+    for t, d, nm in ((up, hu, "halo up"), (dn, hd, "halo down")):
+        if d:
+            if t is None or t.dim() != 2 or t.shape[0] != 4 or t.shape[1] < d * w or not t.is_contiguous():
+                raise ValueError(f"reg_sweeps_tiled: {nm} must be contiguous [4, >= {d * w}]")
+            if t.device != dev or t.dtype != torch.float32:
+                raise ValueError(f"reg_sweeps_tiled: {nm} float32 on {dev}")
+            if plane and plane != t.shape[1]:
+                raise ValueError("reg_sweeps_tiled: halo planes differ in size")
+            plane = t.shape[1]
     _check_soa(u, n_params, N, "u", device=dev)
     _check_soa(v, n_params, N, "v", device=dev)
     if v.shape[1] != u.shape[1]:
         raise ValueError("v must share u's leading dimension")
     for t, nm in ((z, "z"), (z_out, "z_out"), (zp_out, "zp_out")):
         _check_soa(t, 1, N, nm, device=dev)
-    mask = sum(1 << s for s, c in enumerate(chebyshev) if c)
-    if mask & 1:
-        if z_prev is None:
-            raise ValueError("reg_sweeps_tiled: the first sweep is a Chebyshev step but z_prev is None")
+    if z_prev is not None:
         _check_soa(z_prev, 1, N, "z_prev", device=dev)
     ptrs = {t.data_ptr() for t in (z, z_out, zp_out)}
     if len(ptrs) != 3 or (z_prev is not None and z_prev.data_ptr() in (z_out.data_ptr(), zp_out.data_ptr())):
         raise ValueError("reg_sweeps_tiled: outputs must not alias the inputs")
     _set_geo(ext().JacobiArgs(), geo, N)   # validates w * h == N
+    ty0, ty1 = tile_rows if tile_rows is not None else (0, 0)
+    if tile_rows is not None:
+        if not 0 <= ty0 <= ty1 <= reg_tile_rows(h):
+            raise ValueError(f"reg_sweeps_tiled: tile rows {tile_rows} outside [0, {reg_tile_rows(h)}]")
+        if ty0 == ty1:
+            return
     j0 = (int(reg_mask) & -int(reg_mask)).bit_length() - 1
-    ext().reg_tiled(u.shape[1], int(geo["w"]), int(geo["h"]), j0, mask, float(gamma), [float(o) for o in omegas],
-                    _ptr(u), _ptr(v), _ptr(z), _ptr(z_prev), _ptr(z_out), _ptr(zp_out), _dev(u), _stream(u))
+    ext().reg_tiled(u.shape[1], w, h, j0, mask, float(gamma), [] if sched is not None else [float(o) for o in omegas],
+                    _ptr(u), _ptr(v), _ptr(z), _ptr(z_prev), _ptr(z_out), _ptr(zp_out), _dev(u), _stream(u),
+                    nsweep=ns, hu=int(hu), hd=int(hd), halo_up=_ptr(up), halo_dn=_ptr(dn), halo_plane=plane,
+                    ty0=int(ty0), ty1=int(ty1), sched=_ptr(sched[0]) if sched is not None else 0,
+                    omega_tab=_ptr(sched[1]) if sched is not None else 0, s_base=int(s_base))
+
+
+class RegSchedule:
+    """Device-resident schedule of one GN iteration's coupled solve (K9): rho
+    (Gershgorin bound of the Jacobi matrix, all-rank max), the sweep count and
+    the Chebyshev weights, computed on the device so the host can queue the
+    first tiled pass without reading rho back (kf_reg_tiled.hip)."""
+
+    def __init__(self, N: int, max_sweeps: int, device):
+        self.device = torch.device(device)
+        self.max_sweeps = int(max_sweeps)
+        self.npart = int(ext().reg_rho_blocks(max(int(N), 1))) if self.device.type == "cuda" else 1
+        self.pmax = torch.zeros(self.npart, dtype=torch.float32, device=self.device)
+        self.rho = torch.zeros(1, dtype=torch.float64, device=self.device)
+        self.sched = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.omega = torch.zeros(max(self.max_sweeps, 1), dtype=torch.float32, device=self.device)
+        self.info = torch.zeros(2, dtype=torch.float64, device=self.device)
+
+    def rho_pass(self, v_row: torch.Tensor, geo, N: int, gamma: float):
+        """rho[0] = gamma * max_p v_row[p] * deg(p) over a dense strip."""
+        if v_row.dtype != torch.float32 or v_row.device != self.device or v_row.numel() < N:
+            raise ValueError("reg rho: float32 v row of >= N entries on the schedule's device")
+        if not v_row.is_contiguous():
+            raise ValueError("reg rho: contiguous v row")
+        ext().reg_rho(_ptr(v_row), int(geo["w"]), int(geo["h"]), int(geo["halo"]), int(N), _ptr(self.pmax),
+                      self.npart, float(gamma), _ptr(self.rho), _dev(v_row), _stream(v_row))
+
+    def schedule(self, tol: float):
+        """sched[0] = sweeps before the finish, omega[:] their weights, info = (rho, S)."""
+        ext().reg_schedule(_ptr(self.rho), float(tol), self.max_sweeps, _ptr(self.sched), _ptr(self.omega),
+                           _ptr(self.info), _dev(self.rho), _stream(self.rho))
 
 
 def reg_finish(n_params, u, v, z_ext, nbr, x_ref, x_out, gamma, reg_mask, N, partials=None, geo=None, out=None,

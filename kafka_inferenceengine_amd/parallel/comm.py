@@ -268,31 +268,44 @@ class Comm:
         stream (the pack kernels); ``wait()`` makes the current stream wait for
         them (no host block), so kernels queued in between overlap the
         transfer."""
+        return self.exchange_fields_async([send_up], [send_down], [recv_up], [recv_down])
+
+    def exchange_fields_async(self, send_up, send_down, recv_up, recv_down) -> "PendingP2P":
+        """C2 with several fields per direction in one batch (the deep halo of
+        the tiled sweeps: u, v, z, zp rows).  Field i sent up is received by
+        rank - 1 as its field i from below (same order on both sides); None or
+        empty entries are skipped consistently on both sides."""
         if not self.distributed:
             return PendingP2P([])
-        dev = next((t for t in (send_up, send_down, recv_up, recv_down) if t is not None and t.numel()), None)
-        if dev is not None and dev.is_cuda and dist.get_backend(self.group) != "nccl":
+        every = [t for ts in (send_up, send_down, recv_up, recv_down) for t in ts if t is not None and t.numel()]
+        if every and every[0].is_cuda and dist.get_backend(self.group) != "nccl":
             # gloo P2P has no device-stream ordering (one-GPU rehearsals): stage
             # through host memory so the sends see the finished pack kernels and
             # the device sees the received rows in stream order (no overlap).
-            h = [None if t is None else t.cpu() for t in (send_up, send_down)]
-            r = [None if t is None else torch.empty(t.shape, dtype=t.dtype) for t in (recv_up, recv_down)]
-            self.exchange_halo(h[0], h[1], r[0], r[1])
-            for dst, src in ((recv_up, r[0]), (recv_down, r[1])):
+            h_up = [None if t is None else t.cpu() for t in send_up]
+            h_dn = [None if t is None else t.cpu() for t in send_down]
+            r_up = [None if t is None else torch.empty(t.shape, dtype=t.dtype) for t in recv_up]
+            r_dn = [None if t is None else torch.empty(t.shape, dtype=t.dtype) for t in recv_down]
+            self.exchange_fields_async(h_up, h_dn, r_up, r_dn).wait()
+            for dst, src in zip(list(recv_up) + list(recv_down), r_up + r_dn):
                 if dst is not None and dst.numel():
                     dst.copy_(src)
             return PendingP2P([])
         ops = []
         if self.rank > 0:
-            if send_up is not None and send_up.numel():
-                ops.append(dist.P2POp(dist.isend, send_up.contiguous(), self.ranks[self.rank - 1], group=self.group))
-            if recv_up is not None and recv_up.numel():
-                ops.append(dist.P2POp(dist.irecv, recv_up, self.ranks[self.rank - 1], group=self.group))
+            peer = self.ranks[self.rank - 1]
+            for s, r in zip(send_up, recv_up):
+                if s is not None and s.numel():
+                    ops.append(dist.P2POp(dist.isend, s.contiguous(), peer, group=self.group))
+                if r is not None and r.numel():
+                    ops.append(dist.P2POp(dist.irecv, r, peer, group=self.group))
         if self.rank < self.world - 1:
-            if send_down is not None and send_down.numel():
-                ops.append(dist.P2POp(dist.isend, send_down.contiguous(), self.ranks[self.rank + 1], group=self.group))
-            if recv_down is not None and recv_down.numel():
-                ops.append(dist.P2POp(dist.irecv, recv_down, self.ranks[self.rank + 1], group=self.group))
+            peer = self.ranks[self.rank + 1]
+            for s, r in zip(send_down, recv_down):
+                if s is not None and s.numel():
+                    ops.append(dist.P2POp(dist.isend, s.contiguous(), peer, group=self.group))
+                if r is not None and r.numel():
+                    ops.append(dist.P2POp(dist.irecv, r, peer, group=self.group))
         return PendingP2P(dist.batch_isend_irecv(ops) if ops else [])
 
     def gather_object(self, obj):

@@ -112,3 +112,65 @@ class HaloExchanger:
     def fill_halo(self, z_ext: torch.Tensor) -> torch.Tensor:
         """Blocking C2 (start + finish)."""
         return self.finish_fill(self.start_fill(z_ext), z_ext)
+
+    # --------------------------------------------------------- deep halo
+    # The tiled sweeps (kf_reg_tiled.hip) run up to `depth` sweeps per pass on
+    # a dense strip; the ring of the edge tiles reads `depth` rows of each
+    # neighbour -- u and v once per GN iteration, the iterate and the one
+    # before it once per pass -- instead of one row per sweep.  A neighbour's
+    # rows are contiguous slices of its row-major local arrays, so nothing is
+    # packed: its first / last `depth` rows go straight on the wire into this
+    # rank's planes.
+    def deep_setup(self, depth: int):
+        """Allocate the [4, depth * w] planes (u, v, z, zp) of each neighbour
+        side; ``depth`` <= every strip's height (rank-uniform)."""
+        geo = self.partition.dense_geometry()
+        if geo is None:
+            raise ValueError("deep halo: dense strips only")
+        w, h = int(geo["w"]), int(geo["h"])
+        if not 1 <= depth <= h:
+            raise ValueError(f"deep halo depth {depth} outside [1, {h}]")
+        self.deep_w, self.deep_h, self.depth = w, h, int(depth)
+        up = bool(int(geo["halo"]) & 1)
+        dn = bool(int(geo["halo"]) & 2)
+        mk = lambda: torch.zeros((4, depth * w), dtype=torch.float32, device=self._device)  # noqa: E731
+        self.deep_up = mk() if up else None
+        self.deep_dn = mk() if dn else None
+        self.deep_exchanges = 0
+        return self
+
+    def deep_halo(self):
+        """``(hu, hd, up, dn)`` for :func:`ops.kernels.reg_sweeps_tiled`."""
+        return (self.depth if self.deep_up is not None else 0, self.depth if self.deep_dn is not None else 0,
+                self.deep_up, self.deep_dn)
+
+    def _edge_rows(self, t: torch.Tensor):
+        """My first / last ``depth`` rows of a local row-major field (views)."""
+        d, w, h = self.depth, self.deep_w, self.deep_h
+        return t[:d * w], t[(h - d) * w:h * w]
+
+    def deep_start(self, fields: dict):
+        """Post the exchange of ``{plane: local field [>= N]}`` (plane 0 u, 1 v,
+        2 z, 3 zp): my first rows go to rank - 1's lower planes, my last rows to
+        rank + 1's upper planes, theirs come into mine.  Returns a handle for
+        :meth:`deep_finish` (None on one rank)."""
+        if not self.comm.distributed:
+            return None
+        keys = sorted(fields)
+        su, sd, ru, rd = [], [], [], []
+        for kp in keys:
+            first, last = self._edge_rows(fields[kp].reshape(-1))
+            su.append(first if self.deep_up is not None else None)
+            sd.append(last if self.deep_dn is not None else None)
+            ru.append(self.deep_up[kp] if self.deep_up is not None else None)
+            rd.append(self.deep_dn[kp] if self.deep_dn is not None else None)
+        pending = self.comm.exchange_fields_async(su, sd, ru, rd)
+        self.bytes_sent += 4 * sum(t.numel() for t in su + sd if t is not None)
+        self.exchanges += 1
+        self.deep_exchanges += 1
+        return pending
+
+    def deep_finish(self, handle):
+        """The compute stream waits for the posted deep exchange (no host block on RCCL)."""
+        if handle is not None:
+            handle.wait()

@@ -147,6 +147,72 @@ def tiled_vs_sequential(device, h=150, w=300, omegas=(1.0, 1.3, 1.2, 1.25, 1.22)
     return (zo[:, :N].cpu(), zpo[:, :N].cpu()), (cur[:, :N].cpu(), prev[:, :N].cpu())
 
 
+def deep_halo_vs_full(device, h_total=200, w=150, r0=70, r1=150, depth=8, omegas=(1.0, 1.3, 1.2, 1.25, 1.22, 1.21),
+                      cheb=None, device_sched=False, split=False, n=7, j0=6, seed=11, rho=None):
+    """K9 deep halo: a tiled pass over strip rows [r0, r1) of a dense raster,
+    with `depth` rows of u, v, z, zp of each neighbour in halo planes (as the
+    engine receives them), against the same pass over the whole raster (no
+    halo).  ``device_sched``: the weights come from a RegSchedule (``rho``) and
+    the pass from its table; ``split``: boundary tile rows, then the interior
+    (the C2 overlap order).  Returns ((z, zp) strip, (z, zp) full rows r0..r1)."""
+    rng = np.random.default_rng(seed)
+    Nf = h_total * w
+    ld = Nf + 32
+    t = lambda a: torch.tensor(a, dtype=torch.float32, device=device)  # noqa: E731
+    u = t(rng.normal(size=(n, ld)))
+    v = t(rng.uniform(0.0, 0.2, size=(n, ld)))
+    z0 = t(rng.normal(size=(1, ld)))
+    zm1 = t(rng.normal(size=(1, ld)))
+    gamma, mask = 0.9, 1 << j0
+    kw_host = {}
+    if device_sched:
+        rs = K.RegSchedule(Nf, 32, device)
+        rs.rho.fill_(0.8 if rho is None else rho)
+        rs.schedule(1e-3)
+        kw = dict(sched=(rs.sched, rs.omega), s_base=1, nsweep=len(omegas))
+        kw_host = kw
+    else:
+        cheb = [s > 0 for s in range(len(omegas))] if cheb is None else list(cheb)
+        kw = dict(omegas=list(omegas), chebyshev=cheb)
+        kw_host = kw
+    geo_full = {"w": w, "h": h_total, "halo": 0, "n_up": 0}
+    zo, zpo = (torch.zeros(1, ld, device=device) for _ in range(2))
+    K.reg_sweeps_tiled(n, u, v, z0, zm1, zo, zpo, gamma, mask, Nf, geo_full, **kw_host)
+    # the strip's own arrays and its neighbours' rows
+    h = r1 - r0
+    N = h * w
+    lds = N + 16
+
+    def rows_of(a, ra, rb):
+        return a[..., ra * w:rb * w]
+    us = torch.zeros(n, lds, device=device)
+    vs = torch.zeros(n, lds, device=device)
+    us[:, :N] = rows_of(u, r0, r1)
+    vs[:, :N] = rows_of(v, r0, r1)
+    zs = torch.zeros(1, lds, device=device)
+    zps = torch.zeros(1, lds, device=device)
+    zs[:, :N] = rows_of(z0, r0, r1)
+    zps[:, :N] = rows_of(zm1, r0, r1)
+    hu = depth if r0 > 0 else 0
+    hd = depth if r1 < h_total else 0
+    up = dn = None
+    if hu:
+        up = torch.stack([rows_of(f[j], r0 - hu, r0) for f, j in ((u, j0), (v, j0), (z0, 0), (zm1, 0))]).contiguous()
+    if hd:
+        dn = torch.stack([rows_of(f[j], r1, r1 + hd) for f, j in ((u, j0), (v, j0), (z0, 0), (zm1, 0))]).contiguous()
+    geo = {"w": w, "h": h, "halo": (1 if hu else 0) | (2 if hd else 0), "n_up": w if hu else 0}
+    so, spo = (torch.zeros(1, lds, device=device) for _ in range(2))
+    halo = (hu, hd, up, dn)
+    if split:
+        T = K.reg_tile_rows(h)
+        a, b = K.reg_boundary_tile_rows(h, depth, hu > 0, hd > 0)
+        for tr in ((0, a), (b, T), (a, b)):
+            K.reg_sweeps_tiled(n, us, vs, zs, zps, so, spo, gamma, mask, N, geo, halo=halo, tile_rows=tr, **kw)
+    else:
+        K.reg_sweeps_tiled(n, us, vs, zs, zps, so, spo, gamma, mask, N, geo, halo=halo, **kw)
+    return ((so[:, :N].cpu(), spo[:, :N].cpu()), (rows_of(zo, r0, r1).cpu(), rows_of(zpo, r0, r1).cpu()))
+
+
 def dense_finish(device, h_total=30, w=44, ranks=3, rank=1, n=7, j0=6, out=True, seed=9):
     """reg_finish on a dense strip of a ``ranks``-strip partition (halo rows
     above/below) with the output dump; returns (x_out, mean, unc) on the CPU.

@@ -52,7 +52,11 @@ def _run(world, rank, cfg, out_q):
     grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
     st = kf.run(grid, x0, None, Pinv)
     norms = [r["norms"] for r in kf.metrics.records if r.get("event") == "date"]
-    out_q.put((rank, part.offset, st.x.numpy().copy(), st.P.numpy().copy(), norms, kf.reg_overlapped_sweeps))
+    sweeps = [[e["sweeps"] for e in r.get("spatial", [])] for r in kf.metrics.records if r.get("event") == "date"]
+    reg = kf._reg
+    out_q.put((rank, part.offset, st.x.numpy().copy(), st.P.numpy().copy(), norms, kf.reg_overlapped_sweeps,
+               {"tiled": kf.reg_tiled_launches, "exchanges": reg.exchanges if reg is not None else 0,
+                "sweeps": sweeps, "depth": kf._reg_tiled_depth(1)}))
 
 
 def _worker(rank, world, port, cfg, q):
@@ -83,6 +87,7 @@ def _gather(world, cfg):
     x = np.concatenate([r[2] for r in res], 1)
     P = np.concatenate([r[3] for r in res], 1)
     _gather.overlapped = [r[5] for r in res]
+    _gather.reg = [r[6] for r in res]
     return x, P, [r[4] for r in res]
 
 
@@ -127,6 +132,7 @@ def test_eight_ranks_equal_one_rank(cfg):
     6 interior strips exchange halos with two neighbours) give the 1-rank
     result and the same global convergence decisions on every rank."""
     x1, P1, n1 = _gather(1, cfg)
+    reg1 = _gather.reg[0]
     x8, P8, n8 = _gather(8, cfg)
     assert x1.shape == x8.shape
     assert np.allclose(x1, x8, rtol=1e-5, atol=1e-6)
@@ -135,6 +141,37 @@ def test_eight_ranks_equal_one_rank(cfg):
     assert [len(a) for a in n1[0]] == [len(a) for a in n8[0]]
     if cfg.get("spatial_gamma"):
         assert all(c > 0 for c in _gather.overlapped), _gather.overlapped
+        _check_deep_halo(x1, P1, reg1, x8, P8, _gather.reg)
+
+
+def _check_deep_halo(x1, P1, reg1, xw, Pw, regw):
+    """Communication-avoiding coupled solve (K9 + C2 deep halo): every rank
+    runs the LDS-tiled passes, the state equals one rank's bit for bit, and the
+    halo exchanges per GN iteration are one per pass plus the initial u, v, z
+    one (the finish takes its row from the last pass's exchange)."""
+    assert reg1["tiled"] > 0
+    assert all(r["tiled"] > 0 for r in regw), regw
+    assert np.array_equal(x1, xw) and np.array_equal(P1, Pw)
+    for r in regw:
+        depth = r["depth"]
+        per_it = [s for date in r["sweeps"] for s in date]
+        assert per_it and per_it == [s for date in reg1["sweeps"] for s in date]
+        # sweeps before the finish, `depth` per pass; + 1: the u, v, z0 exchange
+        bound = sum(max(1, -(-(s - 1) // depth)) + 1 for s in per_it)
+        assert 0 < r["exchanges"] <= bound, (r["exchanges"], bound, per_it, depth)
+        assert r["exchanges"] <= sum(-(-s // 8) + 1 for s in per_it) or depth < 8
+
+
+def test_four_ranks_deep_halo_passes_of_eight():
+    """Strips of 16 rows: passes of the full 8 sweeps, interior strips read a
+    deep halo from both neighbours; equal to one rank bit for bit."""
+    cfg = {"_rows": 64, "_dense": True, "spatial_gamma": 30.0, "spatial_params": [6]}
+    x1, P1, n1 = _gather(1, cfg)
+    reg1 = _gather.reg[0]
+    x4, P4, n4 = _gather(4, cfg)
+    assert all(r["depth"] == 8 for r in _gather.reg)
+    assert all(n == n4[0] for n in n4[1:])
+    _check_deep_halo(x1, P1, reg1, x4, P4, _gather.reg)
 
 
 def test_strip_partition_balances_active_pixels():

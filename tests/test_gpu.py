@@ -340,6 +340,46 @@ def test_reg_sweeps_tiled_equals_sequential_on_device(cuda, case):
     assert torch.equal(zt, ht) and torch.equal(zpt, hpt)
 
 
+@pytest.mark.parametrize("case", [dict(split=True), dict(r0=0, r1=90), dict(device_sched=True, split=True),
+                                  dict(device_sched=True, rho=0.0), dict(h_total=1400, w=1000, r0=600, r1=1290,
+                                                                         split=True, device_sched=True)])
+def test_reg_sweeps_tiled_deep_halo_on_device(cuda, case):
+    """Deep-halo pass of a strip (C2 once per pass) on gfx950: equal to the
+    whole-raster pass's rows and to the host runner, bit for bit."""
+    (zs, zps), (zf, zpf) = C.deep_halo_vs_full(cuda, **case)
+    assert torch.equal(zs, zf) and torch.equal(zps, zpf)
+    (hs, hps), _ = C.deep_halo_vs_full("cpu", **case)
+    assert torch.equal(zs, hs) and torch.equal(zps, hps)
+
+
+def test_reg_schedule_on_device_matches_host(cuda):
+    """The device schedule kernel and the host runner agree (count and weights)."""
+    for rho in (0.833, 0.5, 0.97, 0.0, 1.5):
+        out = []
+        for dev in (cuda, "cpu"):
+            rs = K.RegSchedule(1000, 64, dev)
+            rs.rho.fill_(rho)
+            rs.schedule(1e-3)
+            out.append((rs.info.cpu(), rs.sched.cpu(), rs.omega.cpu()))
+        assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+        assert torch.equal(out[0][2], out[1][2])
+
+
+def test_reg_rho_pass_on_device(cuda):
+    """rho = gamma max v deg over a dense strip with halo rows (device = torch)."""
+    h, w = 300, 257
+    N = h * w
+    v = torch.rand(N + 10, device=cuda)
+    geo = {"w": w, "h": h, "halo": 1, "n_up": w}
+    rs = K.RegSchedule(N, 64, cuda)
+    rs.rho_pass(v, geo, N, 2.5)
+    rr = torch.arange(N, device=cuda) // w
+    cc = torch.arange(N, device=cuda) % w
+    deg = (1 + (rr + 1 < h).int() + (cc > 0).int() + (cc + 1 < w).int()).float()
+    ref = float(torch.amax(v[:N] * deg) * 2.5)
+    assert float(rs.rho) == ref
+
+
 def test_spatial_tiled_sweeps_equal_per_sweep_launches_on_device(cuda):
     from test_engine import _spatial_dense_run
     a, na = _spatial_dense_run(cuda, True, size=(200, 300))

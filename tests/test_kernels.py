@@ -401,6 +401,45 @@ def test_reg_sweeps_tiled_equals_sequential(case):
     assert torch.equal(zt, zs) and torch.equal(zpt, zps)
 
 
+DEEP_HALO_CASES = [dict(), dict(split=True), dict(r0=0, r1=90), dict(r0=120, r1=200, split=True),
+                   dict(depth=6, omegas=(1.0,) * 6, cheb=(False,) * 6, split=True),
+                   dict(device_sched=True, split=True), dict(device_sched=True, rho=0.3),
+                   dict(device_sched=True, rho=0.0), dict(h_total=40, w=33, r0=9, r1=17, depth=8)]
+
+
+@pytest.mark.parametrize("case", DEEP_HALO_CASES)
+def test_reg_sweeps_tiled_deep_halo_equals_full_domain(case):
+    """A strip's pass with the neighbours' rows in deep-halo planes equals the
+    same rows of a pass over the whole raster: the ring's stale values never
+    reach the strip (tile-DP C2 once per pass)."""
+    (zs, zps), (zf, zpf) = C.deep_halo_vs_full("cpu", **case)
+    assert torch.equal(zs, zf) and torch.equal(zps, zpf)
+
+
+def test_reg_schedule_matches_host_formula():
+    """The device-side Chebyshev schedule (kf_core.h:reg_cheb_schedule) gives
+    the engine's host schedule: sweep count and weights."""
+    kf = k.LinearKalman.__new__(k.LinearKalman)
+    kf.config = k.EngineConfig(spatial_max_sweeps=40)
+    for rho, tol in ((0.833, 1e-3), (0.2, 1e-1), (0.0, 1e-3), (0.99999, 1e-3), (1.2, 1e-3), (float("nan"), 1e-3)):
+        rs = K.RegSchedule(100, 40, "cpu")
+        rs.rho.fill_(rho)
+        rs.schedule(tol)
+        S = int(rs.info[1])
+        r_h, S_h = kf._reg_sweeps_for(rho, tol)
+        assert S == S_h and int(rs.sched[0]) == S - 1
+        w = kf._cheb_weights(r_h, S - 1)
+        assert [float(np.float32(o)) if c else 0.0 for o, c in w] == rs.omega[:S - 1].tolist()
+
+
+def test_reg_boundary_tile_rows():
+    assert K.reg_boundary_tile_rows(1373, 8, True, True) == (1, 21)
+    assert K.reg_boundary_tile_rows(1373, 8, False, True) == (0, 21)
+    assert K.reg_boundary_tile_rows(1373, 8, True, False) == (1, 22)
+    assert K.reg_boundary_tile_rows(70, 8, True, True) == (1, 1)     # two tile rows, both boundary
+    assert K.reg_boundary_tile_rows(6, 6, True, True) == (1, 1)
+
+
 def test_reg_sweeps_tiled_rejects_bad_args():
     u = torch.zeros(7, 100)
     z = torch.zeros(1, 100)
