@@ -161,6 +161,9 @@ def main():
                          "the default re-uploads every date from pinned host memory)")
     ap.add_argument("--no-telemetry", action="store_true",
                     help="no per-phase hipEvent timers (the per_rank record then has no phase times)")
+    ap.add_argument("--dump-state", default=None, metavar="PREFIX",
+                    help="after the timed region, write each strip's final state x [n_p, N] to "
+                         "PREFIX.strip<r>.npy (band slot 0 only; rehearsal checks against one rank)")
     a = ap.parse_args()
     if a.watchdog > 0:
         import faulthandler
@@ -255,6 +258,8 @@ def main():
     ph1 = kf.timer.cumulative()
     phases = {kk: round(v - ph0.get(kk, 0.0), 3) for kk, v in ph1.items()}
     mine = {"rank": g_rank, "strip_rank": rank, "N": int(part.N), "wall_ms": round(1e3 * t_local, 3),
+            "device": str(dev), "host": socket_name(),
+            "local_rank": int(__import__("os").environ.get("LOCAL_RANK", "0")),
             "analysis_ms": phases.get("analysis", 0.0), "c1_ms": phases.get("converge", 0.0),
             "halo_ms": round(phases.get("halo", 0.0) + phases.get("band_allreduce", 0.0), 3),
             "ingest_ms": phases.get("ingest", 0.0), "phases_ms": phases,
@@ -279,6 +284,8 @@ def main():
     # numerical health over the WHOLE job: finite everywhere (min over ranks) and
     # the fraction of pixels whose solve fell back to the forecast (should be ~0)
     ok_local = bool(torch.isfinite(state.x[:, :state.N]).all().item())
+    if a.dump_state and (comm.band is None or comm.band.rank == 0):
+        np.save(f"{a.dump_state}.strip{rank}.npy", state.x[:, :state.N].cpu().numpy())
     st_last = getattr(kf, "last_status", None)
     n_fb = 0 if st_last is None or not state.N else int(((st_last[:state.N] & 16) > 0).sum().item())
     ok = comm.max_float(0.0 if ok_local else 1.0) == 0.0
@@ -314,6 +321,15 @@ def main():
                           "finite": ok, "fallback_frac": round(fallback, 6), "ingest_bytes_per_step": ingest,
                           "baseline_updates_per_s": c["baseline"]}}
         rec["per_rank"] = sorted(per_rank, key=lambda r: r["rank"])
+        # what torch.distributed saw: the driver can confirm from the record alone
+        # that the N-GPU line came from N RCCL ranks on N distinct devices
+        import torch.distributed as dist
+        rec["dist"] = {"initialized": dist.is_initialized(),
+                       "backend": dist.get_backend() if dist.is_initialized() else None,
+                       "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+                       "devices": [r["device"] for r in rec["per_rank"]],
+                       "hosts": sorted({r["host"] for r in rec["per_rank"]}),
+                       "distinct_devices": n_dev}
         if n_dev != n_ranks:
             rec["rehearsal"] = f"{n_ranks} ranks on {n_dev} device(s): logic rehearsal, not a scaling point"
         print(json.dumps(rec), flush=True)

@@ -212,6 +212,58 @@ def test_bench_torchrun_gloo_two_ranks(extra):
         assert len(r["gn_iterations"]) == 2
 
 
+SCALE_CASES = [("tip7", []), ("spatial", []), ("prosail10", []), ("identity7", []), ("multisensor", []),
+               ("multisensor", ["--band-parallel", "2"])]
+
+
+def _bench(nproc, config, extra, prefix, size=256):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", KAFKA_DIST_BACKEND="gloo")
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--steps", "2", "--warmup", "1", "--size",
+            str(size), "--n-train", "24", "--device", "cpu", "--config", config, "--dump-state", prefix] + extra
+    if nproc > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}"] + args
+    else:
+        cmd = [sys.executable] + args
+        env["OMP_NUM_THREADS"] = "8"
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("config,extra", SCALE_CASES,
+                         ids=[c + ("-bp2" if e else "") for c, e in SCALE_CASES])
+def test_bench_eight_rank_rehearsal(tmp_path, config, extra):
+    """The driver's SCALE run, rehearsed on the CPU: bench.py under
+    torch.distributed.run with 8 ranks (gloo) at 256^2 -- one JSON line with 8
+    per-rank records, what torch.distributed saw (backend, world size, the
+    devices), the same GN iterations on every rank, and a final state equal to
+    a one-rank run (reference analogue: the dask farm of
+    kafka_test_Py36.py:241-255)."""
+    one = _bench(1, config, [], str(tmp_path / "one"))
+    rec = _bench(8, config, extra, str(tmp_path / "eight"))
+    assert rec["n_gpus"] == 8 and rec["value"] > 0 and rec["config"]["finite"]
+    assert rec["config"]["fallback_frac"] < 0.01
+    d = rec["dist"]
+    assert d["initialized"] and d["backend"] == "gloo" and d["world_size"] == 8
+    assert len(d["devices"]) == 8 and d["distinct_devices"] == 8
+    pr = rec["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(8))
+    assert all(r["gn_iterations"] == pr[0]["gn_iterations"] for r in pr)
+    assert pr[0]["gn_iterations"] == one["per_rank"][0]["gn_iterations"]
+    assert sorted(r["local_rank"] for r in pr) == list(range(8))
+    S = 4 if extra else 8
+    x8 = np.concatenate([np.load(tmp_path / f"eight.strip{s}.npy") for s in range(S)], axis=1)
+    x1 = np.load(tmp_path / "one.strip0.npy")
+    assert x8.shape == x1.shape
+    assert np.allclose(x8, x1, rtol=1e-5, atol=1e-5), float(np.abs(x8 - x1).max())
+    if config == "spatial":
+        assert np.array_equal(x8, x1)   # deep-halo tiled passes: bit-identical at any rank count
+
+
 def _bp_worker(rank, world, port, B, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
