@@ -27,6 +27,7 @@ from __future__ import annotations
 import argparse
 import datetime as dt
 import json
+import os
 import sys
 import time
 
@@ -156,6 +157,8 @@ def main():
                     help="override an EngineConfig field (A/B runs), e.g. --set gp_split=never")
     ap.add_argument("--band-parallel", type=int, default=1,
                     help="ranks per band group (strips x band groups; multi-band configs)")
+    ap.add_argument("--band-parallel-force", action="store_true",
+                    help="keep --band-parallel even where the cost model says strips are faster")
     ap.add_argument("--resident", action="store_true",
                     help="keep the synthetic observation pool in HBM (compute-only: no per-step H2D; "
                          "the default re-uploads every date from pinned host memory)")
@@ -177,6 +180,20 @@ def main():
 
     from kafka_inferenceengine_amd.engine.config import EngineConfig
 
+    # band-parallel only where its C5 all-reduce pays (parallel/policy.py); else pure strips
+    from kafka_inferenceengine_amd.parallel.policy import band_parallel_decision
+    c0 = CONFIGS[a.config]
+    dev_type = (a.device or ("cuda" if torch.cuda.is_available() else "cpu")).split(":")[0]
+    nb, npar = {"tip7": (2, 7), "spatial": (2, 7), "identity7": (7, 7), "prosail10": (10, 10),
+                "prosail10_hard": (10, 10), "multisensor": (34, 10)}[a.config]
+    T = 0 if a.config == "identity7" else (a.n_train or c0["n_train"])
+    bp_req = a.band_parallel
+    a.band_parallel, bp_why = band_parallel_decision(npar, nb, T, a.band_parallel, dev_type,
+                                                     force=a.band_parallel_force)
+    if bp_why:
+        log(bp_why)
+    if a.band_parallel_force:
+        a.set.append("band_parallel_force=true")
     comm = Comm.from_env(device=a.device, band_parallel=a.band_parallel, timeout_s=EngineConfig().comm_timeout_s)
     if comm.distributed or comm.band is not None:
         dev = comm.device
@@ -230,11 +247,7 @@ def main():
                                                           torch.profiler.ProfilerActivity.CUDA])
                 prof.__enter__()
         t0 = time.perf_counter()
-        # the next step's first GN iteration may be queued inside this one
-        # (EngineConfig.speculate) -- never across the timed-region boundaries
-        j = i + 1
-        nxt = steps[j][:2] if (j < a.warmup + a.steps and j != a.warmup) else None
-        state = kf.step(t, loc, state, advance=not first, all_dates=dates, next_step=nxt)
+        state = kf.step(t, loc, state, advance=not first, all_dates=dates)
         first = False
         if dev.type == "cuda" and i == a.warmup - 1:
             torch.cuda.synchronize()
@@ -259,7 +272,7 @@ def main():
     phases = {kk: round(v - ph0.get(kk, 0.0), 3) for kk, v in ph1.items()}
     mine = {"rank": g_rank, "strip_rank": rank, "N": int(part.N), "wall_ms": round(1e3 * t_local, 3),
             "device": str(dev), "host": socket_name(),
-            "local_rank": int(__import__("os").environ.get("LOCAL_RANK", "0")),
+            "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
             "analysis_ms": phases.get("analysis", 0.0), "c1_ms": phases.get("converge", 0.0),
             "halo_ms": round(phases.get("halo", 0.0) + phases.get("band_allreduce", 0.0), 3),
             "ingest_ms": phases.get("ingest", 0.0), "phases_ms": phases,
@@ -330,6 +343,8 @@ def main():
                        "devices": [r["device"] for r in rec["per_rank"]],
                        "hosts": sorted({r["host"] for r in rec["per_rank"]}),
                        "distinct_devices": n_dev}
+        if bp_why:
+            rec["band_parallel_fallback"] = {"requested": bp_req, "reason": bp_why}
         if n_dev != n_ranks:
             rec["rehearsal"] = f"{n_ranks} ranks on {n_dev} device(s): logic rehearsal, not a scaling point"
         print(json.dumps(rec), flush=True)

@@ -62,6 +62,10 @@ static void l_jacobi(const JacobiArgs& a, int grid, hipStream_t s) {
   if (rows && (a.mode == JACOBI_SWEEP || a.mode == JACOBI_FINISH)) {
     const int64_t nr = n / a.geo.w;
     const int g = (int)(nr < grid ? nr : grid);   // partials hold >= grid entries
+    // the norm sums all `grid` partials: blocks g.. do not exist here, so their
+    // entries are cleared (nothing written earlier into the buffer leaks in)
+    if (a.mode == JACOBI_FINISH && a.partials && g < grid)
+      (void)hipMemsetAsync(a.partials + g, 0, sizeof(double) * (size_t)(grid - g), s);
     if (a.mode == JACOBI_SWEEP)
       hipLaunchKernelGGL((jacobi_kernel<NP, JACOBI_SWEEP1D>), dim3(g), dim3(BLOCK), 0, s, a);
     else

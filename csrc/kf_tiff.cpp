@@ -295,17 +295,21 @@ void read_window(const std::string& path, int band, void* dst, uint64_t r0, uint
     const uint64_t cid = per_band * (uint64_t)band + id;
     const uint64_t rows = in.tiled ? ch : std::min<uint64_t>(ch, in.H - ty * ch);
     const uint64_t raw = rows * cw * (uint64_t)bps;
-    std::vector<uint8_t> comp(in.cnt[cid]), buf(raw);
+    // some writers pad a compressed last strip to the full RowsPerStrip: room
+    // for a whole strip, of which the rows inside the raster are used
+    const uint64_t room = ch * cw * (uint64_t)bps;
+    std::vector<uint8_t> comp(in.cnt[cid]), buf(room);
     f.read_at(comp.data(), comp.size(), in.off[cid]);
     if (in.comp == 1) {
       if (comp.size() < raw) throw std::runtime_error("truncated TIFF chunk " + std::to_string(cid) + " in " + path);
       std::memcpy(buf.data(), comp.data(), raw);
     } else {
-      // only a complete stream that fills the chunk exactly is a good chunk
-      // (Z_BUF_ERROR = truncated / corrupt input or output overflow)
-      uLongf dl = (uLongf)raw;
+      // a good chunk is a complete stream that fills at least the rows inside
+      // the raster and at most a whole strip / tile (Z_BUF_ERROR = truncated or
+      // corrupt input, or more data than a chunk holds)
+      uLongf dl = (uLongf)room;
       const int rc = uncompress(buf.data(), &dl, comp.data(), (uLong)comp.size());
-      if (rc != Z_OK || dl != (uLongf)raw)
+      if (rc != Z_OK || dl < (uLongf)raw)
         throw std::runtime_error("inflate failed (zlib " + std::to_string(rc) + ", " + std::to_string(dl) + " of " +
                                  std::to_string(raw) + " bytes) for chunk " + std::to_string(cid) + " in " + path);
     }

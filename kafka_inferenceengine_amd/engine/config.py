@@ -59,6 +59,10 @@ class EngineConfig:
     # band-parallel (TP-like) decomposition: ranks = strips x band_parallel;
     # the B ranks of a strip split the bands and all-reduce the normal equations
     band_parallel: int = 1
+    # band-parallel costs one all-reduce of the per-pixel [A | b] per GN iteration;
+    # on a GPU the engine refuses it when that costs > 25 % of the per-rank analysis
+    # (parallel/policy.py) unless forced
+    band_parallel_force: bool = False
     # runtime
     device: str | None = None                 # 'cuda', 'cuda:1', 'cpu' (default: cuda if present)
     prefetch: bool = True                     # overlap next date's ingest with compute
@@ -66,8 +70,6 @@ class EngineConfig:
     fuse_propagation: bool = True             # evaluate the forecast inside the analysis kernel
     fuse_gn: bool = True                      # GN iterations 1 and 2 in one launch (iteration 1 can never
                                               # end the loop, linear_kf.py:297-304); plain fused path only
-    speculate: bool = True                    # unfused path: queue the next step's first GN iteration before
-                                              # the convergence read-back (discarded if it was not the last)
     fuse_output: bool = True                  # device outputs written by the final analysis iteration
     return_innovations: bool = False
     metrics_path: str | None = None           # JSONL metrics (per date / timestep)

@@ -45,8 +45,6 @@ LOG = logging.getLogger(__name__ + ".linear_kf")
 Metadata = namedtuple("Metadata", "mask uncertainty")
 Previous_State = namedtuple("Previous_State", "timestamp x_vect cov_m icov_mv")
 AssimilationResult = namedtuple("AssimilationResult", "state n_iter norms innovations")
-# first GN iteration of the next step, queued ahead of the convergence read-back
-_Speculation = namedtuple("_Speculation", "ts date cand forecast table prop x P status pend")
 
 
 def _resolve_device(device):
@@ -140,13 +138,8 @@ class LinearKalman:
                                 enabled=self.metrics.enabled or self.config.phase_timing)
         self._lookahead_fn = None       # host prep of the next date, run under the last GN iteration
         self._prepared = None           # (date, bands, table) made by it
-        self._next_step = None          # (timestep, locate_times) of the caller's next step
-        self._speculate_fn = None       # queues that step's first GN iteration (see _speculate)
-        self._spec = None               # the queued iteration, adopted or dropped by the next step
-        self._spec_predict = True       # last date converged at min_iterations
         self._lazy_norms = []           # (norms, pending 1, pending 2, len_x, n_bands) of static convergence
         self._reg_log = []              # per GN iteration of the spatial prior: rho, sweeps, residual
-        self.spec_stats = {"queued": 0, "adopted": 0}
         self._split_chunk = {}          # split path: bands per chunk, per band count
         self._reg = None
         self._reg_uv = None             # affine regulariser: u = A_reg^-1 b, V = A_reg^-1 E_R, x0
@@ -278,9 +271,7 @@ class LinearKalman:
             if resume_t is not None and timestep <= resume_t:
                 continue
             advance = analysis is not None and (not is_first or resume_t is not None)
-            nxt = steps[step_i + 1][:2] if step_i + 1 < len(steps) else None
-            analysis = self.step(timestep, locate_times, analysis if advance else forecast, advance, all_dates,
-                                 next_step=nxt)
+            analysis = self.step(timestep, locate_times, analysis if advance else forecast, advance, all_dates)
             if ckpt is not None and self.config.checkpoint_every and (step_i + 1) % self.config.checkpoint_every == 0:
                 with self.timer.phase("checkpoint"):
                     ckpt.save(timestep, analysis)
@@ -302,44 +293,25 @@ class LinearKalman:
             return all_dates[bisect.bisect_left(all_dates, first):]
         return [d for d in all_dates if d >= first]
 
-    def step(self, timestep, locate_times, state: KFState, advance: bool = True, all_dates=None,
-             next_step=None) -> KFState:
+    def step(self, timestep, locate_times, state: KFState, advance: bool = True, all_dates=None) -> KFState:
         """One time-grid step: advance (unless ``advance`` is False, i.e. ``state``
         already is the forecast), assimilate every date in ``locate_times``,
-        dump.  Returns the analysis state.
-
-        ``next_step``: ``(timestep, locate_times)`` of the step the caller runs
-        next (advancing from this step's analysis).  With ``config.speculate`` the
-        first Gauss-Newton iteration of its first date is queued on the stream
-        before this step's convergence norm is read back, so the GPU does not idle
-        through the host's read-back, decision and next-step launch; if this
-        step's date needs one more iteration the queued one is dropped."""
+        dump.  Returns the analysis state."""
         self.current_timestep = timestep
         t0 = time.perf_counter()
         forecast = state
-        spec, self._spec = self._spec, None
         if advance:
             if LOG.isEnabledFor(logging.INFO):
                 LOG.info("Advancing state, %s" % timestep.strftime("%Y-%m-%d"))
-            if (spec is not None and spec.ts == timestep and len(locate_times) and spec.date == locate_times[0]
-                    and spec.cand.x is state.x and spec.cand.P is state.P):
-                forecast = spec.forecast
-                self._spec = spec
-            else:
-                forecast = self.advance_state(state, timestep, lazy=self.config.fuse_propagation)
-        self._next_step = next_step if (self.config.speculate and next_step is not None
-                                        and len(next_step[1])) else None
-        try:
-            if len(locate_times) == 0:
-                analysis = self._materialize(forecast)
-                LOG.info("No observations in this time")
-                info = {"n_dates": 0}
-            else:
-                all_dates = list(self.observations.dates) if all_dates is None else all_dates
-                upcoming = self._upcoming(all_dates, locate_times[0])
-                analysis, info = self._assimilate_dates(locate_times, forecast, upcoming)
-        finally:
-            self._next_step = None
+            forecast = self.advance_state(state, timestep, lazy=self.config.fuse_propagation)
+        if len(locate_times) == 0:
+            analysis = self._materialize(forecast)
+            LOG.info("No observations in this time")
+            info = {"n_dates": 0}
+        else:
+            all_dates = list(self.observations.dates) if all_dates is None else all_dates
+            upcoming = self._upcoming(all_dates, locate_times[0])
+            analysis, info = self._assimilate_dates(locate_times, forecast, upcoming)
         LOG.info("Dumping results to disk")
         self._dump(timestep, analysis)
         rec = {"event": "timestep", "timestep": timestep.isoformat(), "wall_s": time.perf_counter() - t0,
@@ -443,8 +415,7 @@ class LinearKalman:
     def cache_stats(self) -> dict:
         """Host-side reuse counters (band tables, fused-argument blocks)."""
         return {"table_hits": self._tables.hits, "table_misses": self._tables.misses,
-                "prop_hits": self._prop_bufs.get("_hits", 0), "prop_misses": self._prop_bufs.get("_misses", 0),
-                **{f"spec_{k}": v for k, v in self.spec_stats.items()}}
+                "prop_hits": self._prop_bufs.get("_hits", 0), "prop_misses": self._prop_bufs.get("_misses", 0)}
 
     def _remember_prop(self, key, kind, d, keep):
         if len(self._prop_dicts) > 32:
@@ -559,15 +530,11 @@ class LinearKalman:
                         self.observations.prefetch(d_ahead)
                 if nxt and self.config.lookahead:
                     self._lookahead_fn = lambda d=nxt[0]: self._prepare_date(d)
-                    ns = self._next_step
-                    if i == len(locate_times) - 1 and ns is not None and ns[1][0] == nxt[0]:
-                        self._speculate_fn = lambda cand, ts=ns[0], d=nxt[0]: self._speculate(cand, ts, d)
                 try:
                     res = self.do_all_bands_state(step, bands, forecast,
                                                   table=prep[2] if (prep is not None and prep[1] is bands) else None)
                 finally:
                     self._lookahead_fn = None
-                    self._speculate_fn = None
             forecast = res.state
             info["gn_iterations"].append(res.n_iter)
             info["norms"].append(res.norms[-1] if res.norms else None)
@@ -594,39 +561,6 @@ class LinearKalman:
                 self._split_plan_kind(specs) is None:
             table = self._tables.get(specs, [d for _, d in bands], self.n_params, self._cache, self.device)
         self._prepared = (date, bands, table)
-
-    def _speculate(self, cand: KFState, ts, date):
-        """Queue the first Gauss-Newton iteration of ``date`` (first date of the
-        next time step ``ts``) from the candidate analysis ``cand`` of the current
-        date's latest iteration, before the host reads that iteration's
-        convergence norm.  Only the fused plain path (lazy propagation, table
-        built by the lookahead) is speculated; the first iteration never ends the
-        loop (``min_iterations >= 2``), so it writes neither the precision nor the
-        output rasters.  Its x / P / status buffers are fresh and the reduction
-        slot (1) differs from the pending one (>= 2), so dropping it is free."""
-        prep = self._prepared
-        # every condition is rank-independent: all ranks queue the same collective
-        if prep is None or prep[0] != date or prep[2] is None or self.config.min_iterations < 2:
-            return
-        fc = self.advance_state(cand, ts, lazy=True)
-        if not isinstance(fc, LazyForecast):
-            return
-        prop = fc.handle()
-        x1 = torch.empty_like(cand.x)
-        P1 = torch.empty_like(cand.P)
-        status = torch.empty(max(self.N, 1), dtype=torch.uint8, device=self.device)   # written per pixel
-        red = self._red_hist[1:2]
-        with self.timer.phase("analysis"):
-            if self.N:
-                K.analysis(self.n_params, prep[2], None, None, None, x1, None, None, status, self._partials,
-                           N=self.N, prop=prop, out=None)
-                K.reduce_partials(self._partials, red)
-            else:
-                red.zero_()
-        with self.timer.phase("converge"):
-            pend = self.comm.sum_f64_async(red)
-        self._spec = _Speculation(ts, date, cand, fc, prep[2], prop, x1, P1, status, pend)
-        self.spec_stats["queued"] += 1
 
     def _health_metrics(self, wall_s: float) -> dict:
         """Per-date structured metrics: rank-local pixel updates/s,
@@ -794,6 +728,8 @@ class LinearKalman:
         bp = self.band_comm is not None
         if bp and (gain or cfg.spatial_gamma > 0 or cfg.hessian_correction):
             raise ValueError("band_parallel runs the information form without regulariser / Hessian correction")
+        if bp and not getattr(self, "_bp_checked", False):
+            self._band_parallel_check(specs)
         split = None if (precomp or gain or bp or cfg.spatial_gamma > 0) else self._split_plan(specs, dbs, h0_outs)
         if precomp or split:
             table = None
@@ -824,16 +760,6 @@ class LinearKalman:
         norms = []
         deferred = []
         n_iter = 1
-        spec, self._spec = self._spec, None
-        if (spec is not None and (prop is not None or not N) and spec.date == timestep
-                and forecast is spec.forecast and table is spec.table and h0_outs is None):
-            # the previous step queued this date's first iteration (_speculate);
-            # rank-independent test (an empty strip adopts too: same collectives)
-            prop = spec.prop if N else None
-            x_prev, x_new, P_out, status = spec.x, x_new, spec.P, spec.status
-            deferred.append((1, spec.pend))
-            n_iter = 2
-            self.spec_stats["adopted"] += 1
         len_x = float(n * self.n_total)
         # fused output: an output with device rasters is written by the analysis
         # kernel itself in every iteration that can end the loop (the last one wins)
@@ -928,12 +854,6 @@ class LinearKalman:
                 # host preparation of the next date runs under this iteration's kernels
                 self._lookahead_fn()
                 self._lookahead_fn = None
-            if (self._speculate_fn is not None and plain and h0_outs is None
-                    and self._spec_predict and not cfg.fuse_gn):
-                # queue the next step's first iteration from this candidate analysis
-                # before the read-back below blocks the host
-                self._speculate_fn(KFState(x_prev, P_out, PRECISION, N))
-                self._speculate_fn = None
             self._resolve_lazy_norms()
             for it, pd in deferred:
                 norms.append(self._log_norm(pd.result(), len_x, len(bands), it))
@@ -942,7 +862,6 @@ class LinearKalman:
             norms.append(convergence_norm)
             if convergence_norm < cfg.convergence_tolerance and n_iter >= cfg.min_iterations:
                 break
-            self._spec = None   # not the last iteration: the queued next-step iteration is stale
             if n_iter > cfg.max_iterations:
                 LOG.warning("Bailing out after 25 iterations!!!!!!")
                 break
@@ -950,11 +869,6 @@ class LinearKalman:
         if ld != x_prev.shape[1]:
             raise RuntimeError("leading dimension changed")
         state = KFState(x_prev, P_out, COVARIANCE if gain else PRECISION, N)
-        # predictor: speculate on the next date only while dates converge at the
-        # first iteration allowed to end the loop
-        self._spec_predict = n_iter <= cfg.min_iterations
-        if self._spec is not None and not (self._spec.cand.x is state.x and self._spec.cand.P is state.P):
-            self._spec = None
         self._output_written = state if out_t is not None else None
         if cfg.hessian_correction and not gain and N:
             with self.timer.phase("hessian"):
@@ -985,8 +899,13 @@ class LinearKalman:
         return out
 
     def _norms_needed_now(self) -> bool:
-        """Per-date metrics and INFO logs report the norms as they happen."""
-        return self.metrics.enabled or LOG.isEnabledFor(logging.INFO)
+        """Per-date metrics report the norms as they happen.  Rank-uniform on
+        purpose (the metrics path is part of the shared config): the answer
+        decides whether this rank queues another collective, so a per-process
+        setting such as the log level (INFO often on rank 0 only) must not
+        enter it -- INFO lines of statically converged dates are logged when
+        the deferred norms resolve."""
+        return bool(self.metrics.enabled)
 
     def _resolve_lazy_norms(self):
         """Fill in the deferred norms of statically converged dates (linear
@@ -1390,6 +1309,21 @@ class LinearKalman:
         if N:
             K.analysis(n, self._bp_solve_tab, x_prev, fc.x, fc.P, x_out, A_out, None, self._bp_status,
                        self._partials, N=N, a_in=A_part, b_in=b_part)
+
+    def _band_parallel_check(self, specs):
+        """Refuse band-parallel where its C5 all-reduce dwarfs the analysis it
+        splits (parallel/policy.py; rank-uniform: every rank of a group sees the
+        same band count and emulators).  ``specs``: this rank's bands."""
+        from ..parallel.policy import band_parallel_decision
+
+        self._bp_checked = True
+        B = self.band_comm.world
+        n_bands = len(specs) * B
+        n_train = max([int(getattr(s.emulator, "n_train", 0) or 0) for s in specs] or [0])
+        B_eff, why = band_parallel_decision(self.n_params, n_bands, n_train, B, self.device.type,
+                                            force=self.config.band_parallel_force)
+        if B_eff != B:
+            raise ValueError(why + " (set band_parallel_force to run it anyway)")
 
     def _band_parallel_status(self, status):
         """Combine per-rank band flags (BAD_OP any, NO_OBS all) with the solve flags."""

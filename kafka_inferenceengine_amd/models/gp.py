@@ -391,18 +391,19 @@ TIP_RANGES = {
 }
 
 
-def make_tip_emulators(n_train: int = 500, seed: int = 0):
-    """Two JRC-TIP band emulators (VIS, NIR), 4 inputs each."""
+def make_tip_emulators(n_train: int = 500, seed: int = 0, noise: float = 1e-3):
+    """Two JRC-TIP band emulators (VIS, NIR), 4 inputs each.  ``noise``: the
+    nugget (1e-5: near-interpolating weights that cancel, |alpha| >> |f|)."""
     ems = []
     for band in (0, 1):
         lo, hi = TIP_RANGES[band]
         ems.append(GaussianProcessEmulator.synthetic(tip_bhr_target(band), lo, hi, n_train, seed + band,
-                                                     name=f"tip_{'vis' if band == 0 else 'nir'}"))
+                                                     noise=noise, name=f"tip_{'vis' if band == 0 else 'nir'}"))
     return ems
 
 
 def make_prosail_emulators(n_bands: int = 10, n_train: int = 250, seed: int = 0, n_params: int = 10,
-                           hard: bool = False):
+                           hard: bool = False, noise: float = 1e-3):
     """Per-band PROSAIL-like emulators over the 10 transformed parameters
     (``hard``: the strongly non-linear targets of :func:`prosail_target`)."""
     from .priors import sail_prior
@@ -414,5 +415,6 @@ def make_prosail_emulators(n_bands: int = 10, n_train: int = 250, seed: int = 0,
     # every band's records around the SAIL prior mean (the centre of the design
     # box): the bands share their centred inputs (BAND_LAYOUT_SHARED_X)
     return [GaussianProcessEmulator.synthetic(prosail_target(b, n_params, hard), lo[:n_params], hi[:n_params],
-                                              n_train, seed + b, name=f"prosail_b{b}{'h' if hard else ''}")
+                                              n_train, seed + b, noise=noise,
+                                              name=f"prosail_b{b}{'h' if hard else ''}")
             .set_center(mean[:n_params]) for b in range(n_bands)]

@@ -134,26 +134,31 @@ def _run_emulator_device(gp, x, lut_threshold, lut_size, seed):
     """run_emulator for a resident (N, D) tensor: the unique-row pass and the
     LUT assignment stay on x's device (torch.unique, K7 ``lut_nearest``); only
     the emulator itself runs on the host, over at most ``lut_size`` rows or the
-    unique rows.  Returns (H (N,), dH (N, D)) float32 tensors on x's device."""
+    unique rows.  Rows are deduplicated in x's own precision (float64 input:
+    rows that differ only below float32 precision stay distinct, as on the
+    host path, utils.py:72-84); the LUT nearest search runs in float32 (K7).
+    Returns (H (N,), dH (N, D)) in x's float dtype (float64 or float32) on x's
+    device."""
     from ..ops import kernels as K
     dev = x.device
+    dt = torch.float64 if x.dtype == torch.float64 else torch.float32
     if x.shape[0] == 0:
-        return (torch.zeros(0, device=dev), torch.zeros_like(x, dtype=torch.float32))
-    x32 = x.to(torch.float32)
-    uniq, inv = torch.unique(x32, dim=0, return_inverse=True)
+        return (torch.zeros(0, dtype=dt, device=dev), torch.zeros_like(x, dtype=dt))
+    xin = x.to(dt)
+    uniq, inv = torch.unique(xin, dim=0, return_inverse=True)
     if uniq.shape[0] > lut_threshold:
         LOG.info("Clustering parameter space")
-        xd = x32.double()
+        xd = xin.double()
         mean = xd.mean(0)
         xc = xd - mean
         cov = (xc.T @ xc) / max(x.shape[0] - 1, 1)
         rng = np.random.default_rng(seed)
         lut = rng.multivariate_normal(mean.cpu().numpy(), cov.cpu().numpy(), lut_size)
-        uniq = torch.as_tensor(lut, dtype=torch.float32, device=dev)
-        inv = K.lut_nearest(uniq, x32.T.contiguous()).long()
+        uniq = torch.as_tensor(lut, dtype=dt, device=dev)
+        inv = K.lut_nearest(uniq.to(torch.float32), xin.to(torch.float32).T.contiguous()).long()
     out = gp.predict(uniq.double().cpu().numpy(), do_unc=False)
-    H_ = torch.as_tensor(np.asarray(out[0]), dtype=torch.float32, device=dev)
-    dH_ = torch.as_tensor(np.asarray(out[-1]), dtype=torch.float32, device=dev)
+    H_ = torch.as_tensor(np.asarray(out[0]), dtype=dt, device=dev)
+    dH_ = torch.as_tensor(np.asarray(out[-1]), dtype=dt, device=dev)
     return H_[inv], dH_[inv]
 
 

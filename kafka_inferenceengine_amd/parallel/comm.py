@@ -63,7 +63,7 @@ class PendingSum:
         if vals.is_cuda:
             # async copy into a pinned mailbox slot + an event: result() waits for
             # THIS value only, not for work queued on the stream after it (the
-            # next step's speculatively queued iteration)
+            # next date's launches, the spatial prior's remaining sweep passes)
             key = (vals.device.index, vals.numel())
             box = _MAILBOXES.get(key)
             if box is None:

@@ -28,7 +28,7 @@ def wrap(obj, name, label=None):
         try: return fn(*a, **kw)
         finally: acc[label] += time.perf_counter() - t; cnt[label] += 1
     setattr(obj, name, w)
-for nm in ["advance_state", "_device_bands", "_prepare_date", "_speculate", "do_all_bands_state", "_dump", "_assimilate_dates"]:
+for nm in ["advance_state", "_device_bands", "_prepare_date", "do_all_bands_state", "_dump", "_assimilate_dates"]:
     wrap(L.LinearKalman, nm)
 wrap(K, "analysis", "K.analysis"); wrap(K, "reduce_partials", "K.reduce"); wrap(S.LazyForecast, "handle")
 import kafka_inferenceengine_amd.engine.linear_kf as LL
@@ -52,8 +52,7 @@ steps = list(iterate_time_grid(grid, dates))
 def run(lo, hi, st):
     for i in range(lo, hi):
         t, loc, first = steps[i]
-        nxt = steps[i + 1][:2] if i + 1 < hi else None
-        st = kf.step(t, loc, st, advance=i > 0, all_dates=dates, next_step=nxt)
+        st = kf.step(t, loc, st, advance=i > 0, all_dates=dates)
     return st
 state = run(0, 20, state); acc.clear(); cnt.clear()
 if DEV == "cuda":

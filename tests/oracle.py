@@ -15,7 +15,9 @@ from kafka_inferenceengine_amd.inference import (iterate_time_grid, propagate_an
 
 
 def oracle_run(obs, state_mask, factory, n_params, time_grid, x0, Pinv0, propagator=None, prior=None, Q=None,
-               tol=1e-3, min_iterations=2, max_iterations=25):
+               tol=1e-3, min_iterations=2, max_iterations=25, on_step=None):
+    """``on_step(timestep, x_a, P_a^-1)``: called after every time-grid step
+    (the state the engine's output writer sees, linear_kf.py:211-212)."""
     state_mask = np.asarray(state_mask).astype(bool)
     N = int(state_mask.sum())
     M = sp.eye(n_params * N, format="csr")
@@ -29,6 +31,8 @@ def oracle_run(obs, state_mask, factory, n_params, time_grid, x0, Pinv0, propaga
                                                      state_propagator=propagator, date=timestep)
         if len(locate) == 0:
             x_a, Pi_a = x_f, Pi_f
+            if on_step is not None:
+                on_step(timestep, x_a, Pi_a)
             continue
         for date in locate:
             data = [obs.get_band_data(date, b) for b in range(obs.bands_per_observation[date])]
@@ -50,4 +54,103 @@ def oracle_run(obs, state_mask, factory, n_params, time_grid, x0, Pinv0, propaga
             iters.append(n_iter)
             x_f, Pi_f = xa, A
         x_a, Pi_a = x_f, Pi_f
+        if on_step is not None:
+            on_step(timestep, x_a, Pi_a)
     return x_a, Pi_a, iters
+
+
+def gp_predict64(em, X, chunk=16384):
+    """float64 RBF GP value and gradient through GEMMs (an implementation
+    independent of the emulator's ``predict``): with centred inputs, d2 =
+    |x|^2_lam + |t|^2_lam - 2 x lam t^T, k = s exp(-d2 / 2), f = mean + k alpha,
+    df/dx_d = -lam_d (x_d (k alpha) - k (alpha t_d))."""
+    X = np.atleast_2d(np.asarray(X, dtype=np.float64))
+    T = np.asarray(em.inputs, dtype=np.float64)
+    c = T.mean(0)
+    Tc = T - c
+    lam = np.asarray(em.lam, dtype=np.float64)
+    alpha = np.asarray(em.alpha, dtype=np.float64)
+    tt = np.einsum("td,td,d->t", Tc, Tc, lam)
+    B = np.concatenate([alpha[:, None], alpha[:, None] * Tc], axis=1)       # [T, 1 + D]
+    H = np.empty(X.shape[0])
+    dH = np.empty_like(X)
+    for s in range(0, X.shape[0], chunk):
+        Xc = X[s:s + chunk] - c
+        xx = np.einsum("nd,nd,d->n", Xc, Xc, lam)
+        d2 = xx[:, None] + tt[None, :] - 2.0 * (Xc * lam[None, :]) @ Tc.T
+        k = em.signal * np.exp(-0.5 * np.maximum(d2, 0.0))
+        S = k @ B
+        H[s:s + chunk] = em.mean + S[:, 0]
+        dH[s:s + chunk] = -lam[None, :] * (Xc * S[:, :1] - S[:, 1:])
+    return H, dH
+
+
+def oracle_run_blocks(obs, state_mask, maps, time_grid, prior_mean, prior_cinv, propagated=(6,), q=None,
+                      tol=1e-3, min_iterations=2, max_iterations=25, on_step=None, x0=None, A0=None):
+    """The same run loop with every matrix held as its per-pixel n x n blocks,
+    all in float64 (no float32 cast of the normal equations): the GP value and
+    gradient from :func:`gp_predict64` on each band's input subset ``maps[b]``,
+    ``analysis_blocks`` for the analysis and the partial prior-reset
+    propagation of ``propagate_information_filter_LAI`` (kf_tools.py:292-314:
+    every parameter back to the prior except ``propagated``, whose precision
+    is inflated by q).  Fast enough for 256^2 tiles; checked against
+    :func:`oracle_run` on small tiles (tests/test_mvp.py).
+
+    Returns (x [N, n], A [N, n, n], iters); ``on_step(timestep, x, A)``."""
+    from kafka_inferenceengine_amd.inference import analysis_blocks
+
+    sm = np.asarray(state_mask).astype(bool)
+    N = int(sm.sum())
+    mu = np.asarray(prior_mean, dtype=np.float64)
+    ci = np.asarray(prior_cinv, dtype=np.float64)
+    n = mu.size
+    q = np.zeros(n) if q is None else np.asarray(q, dtype=np.float64)
+    # initial state: the given per-pixel constants (x0 [n], A0 [n, n]), else the prior
+    x_f = np.broadcast_to(mu if x0 is None else np.asarray(x0, np.float64), (N, n)).copy()
+    A_f = np.broadcast_to(ci if A0 is None else np.asarray(A0, np.float64), (N, n, n)).copy()
+    x_a, A_a = None, None
+    iters = []
+    for timestep, locate, is_first in iterate_time_grid(time_grid, obs.dates):
+        if not is_first:
+            x_f = np.broadcast_to(mu, (N, n)).copy()
+            A_f = np.broadcast_to(ci, (N, n, n)).copy()
+            for kk in propagated:
+                x_f[:, kk] = x_a[:, kk]
+                A_f[:, kk, kk] = 1.0 / (1.0 / A_a[:, kk, kk] + q[kk])
+        if len(locate) == 0:
+            x_a, A_a = x_f, A_f
+            if on_step is not None:
+                on_step(timestep, x_a, A_a)
+            continue
+        for date in locate:
+            data = [obs.get_band_data(date, b) for b in range(obs.bands_per_observation[date])]
+            raw = []
+            for d in data:
+                m = np.asarray(d.mask)[sm]
+                w = np.asarray(d.uncertainty.diagonal())[sm.ravel()] if sp.issparse(d.uncertainty) else \
+                    np.asarray(d.uncertainty)[sm]
+                w = np.where(m & np.isfinite(w), w, 0.0)
+                raw.append((np.where(m, np.asarray(d.observations)[sm], 0.0), w, d.emulator))
+            x_prev = x_f.copy()
+            n_iter = 1
+            while True:
+                bands = []
+                for b, (y, w, em) in enumerate(raw):
+                    H0, dH = gp_predict64(em, x_prev[:, maps[b]])
+                    h = np.zeros((N, n))
+                    h[:, maps[b]] = dH
+                    bands.append((H0, h, y, w))
+                xa, A = analysis_blocks(x_prev, x_f, A_f, bands)
+                norm = np.linalg.norm((xa - x_prev).ravel()) / float(N * n)
+                x_prev = xa
+                if norm < tol and n_iter >= min_iterations:
+                    break
+                if n_iter > max_iterations:
+                    break
+                n_iter += 1
+            iters.append(n_iter)
+            x_f, A_f = xa, A
+        x_a, A_a = x_f, A_f
+        if on_step is not None:
+            on_step(timestep, x_a, A_a)
+    return x_a, A_a, iters

@@ -93,7 +93,7 @@ def _gather(world, cfg):
 
 @pytest.mark.parametrize("cfg", [{}, {"spatial_gamma": 30.0, "spatial_params": [6], "jacobi_sweeps": 5},
                                  {"convergence_tolerance": 1e-7, "max_iterations": 4}],
-                         ids=["independent", "regularised-halo", "speculation-dropped"])
+                         ids=["independent", "regularised-halo", "extra-iterations"])
 def test_two_ranks_equal_one_rank(cfg):
     x1, P1, n1 = _gather(1, cfg)
     x2, P2, n2 = _gather(2, cfg)

@@ -345,34 +345,6 @@ def test_identity_operator_engine_matches_oracle(encoding):
 
 
 @pytest.mark.parametrize("tol", [1e-3, 1e-9])
-def test_speculative_next_step_equals_sequential(tol):
-    """EngineConfig.speculate: the next step's first GN iteration queued before
-    the convergence read-back gives the same run; with a tolerance that forces
-    extra iterations the queued iteration is dropped (and the predictor stops
-    queueing)."""
-    mask, obs, prior, x0, Pinv, Q = _setup(seed=7)
-    grid = _grid(6)
-    res = []
-    for spec in (False, True):
-        out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
-        kf = _engine(mask, obs, Q, out=out, speculate=spec, convergence_tolerance=tol, max_iterations=4,
-                     fuse_gn=False)
-        st = kf.run(grid, x0, None, Pinv)
-        res.append((st, out, [h["gn_iterations"] for h in kf.history], [h["norms"] for h in kf.history],
-                    dict(kf.spec_stats)))
-    (a, oa, ia, na, sa), (b, ob, ib, nb, sb) = res
-    assert ia == ib and na == nb
-    assert torch.equal(a.x, b.x) and torch.equal(a.P, b.P)
-    for t in oa.history:
-        assert torch.equal(oa.history[t][0], ob.history[t][0])
-    assert sa == {"queued": 0, "adopted": 0}
-    if tol == 1e-3:
-        assert sb["queued"] >= sb["adopted"] >= len(grid) - 3
-    else:
-        assert sb["adopted"] == 0 and sb["queued"] <= 1
-
-
-@pytest.mark.parametrize("tol", [1e-3, 1e-9])
 def test_fused_gn_iterations_equal_separate_launches(tol):
     """EngineConfig.fuse_gn: Gauss-Newton iterations 1 and 2 in one launch
     (iteration 1 kept in registers) give bit-identical states, outputs,
@@ -383,7 +355,7 @@ def test_fused_gn_iterations_equal_separate_launches(tol):
     res = []
     for fuse in (False, True):
         out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
-        kf = _engine(mask, obs, Q, out=out, fuse_gn=fuse, speculate=False, convergence_tolerance=tol,
+        kf = _engine(mask, obs, Q, out=out, fuse_gn=fuse, convergence_tolerance=tol,
                      max_iterations=4)
         st = kf.run(grid, x0, None, Pinv)
         res.append((st, out, [h["gn_iterations"] for h in kf.history], [h["norms"] for h in kf.history]))
@@ -407,7 +379,7 @@ def test_linear_operator_converges_statically():
         obs = k.SyntheticIdentityObservations(mask, dates=dates, device="cpu", seed=3, stream=False)
         kf = k.LinearKalman(obs, None, mask, k.create_linear_observation_operator, k.TIP_PARAMETERS,
                             state_propagation=k.propagate_information_filter_LAI, device="cpu",
-                            config=k.EngineConfig(fuse_gn=fuse, speculate=False))
+                            config=k.EngineConfig(fuse_gn=fuse))
         kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
         prior = k.JRCPrior(k.TIP_PARAMETERS, mask)
         x0, Pi = prior.process_prior(None)

@@ -252,7 +252,7 @@ def test_fused_gn_launch_equals_separate_launches_gpu(cuda, op):
             fac = k.create_linear_observation_operator
         kf = k.LinearKalman(obs, out, mask, fac, k.TIP_PARAMETERS, device=cuda,
                             state_propagation=k.propagate_information_filter_LAI,
-                            config=k.EngineConfig(fuse_gn=fuse, speculate=False))
+                            config=k.EngineConfig(fuse_gn=fuse))
         kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
         st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
         outs.append((st.x.cpu(), st.P.cpu(), [h.get("gn_iterations") for h in kf.history],
@@ -350,6 +350,30 @@ def test_reg_sweeps_tiled_deep_halo_on_device(cuda, case):
     assert torch.equal(zs, zf) and torch.equal(zps, zpf)
     (hs, hps), _ = C.deep_halo_vs_full("cpu", **case)
     assert torch.equal(zs, hs) and torch.equal(zps, hps)
+
+
+def test_reg_finish_rows_clears_stale_partials(cuda):
+    """The row-loop finish launches fewer blocks than the partials buffer has
+    entries (w > 256: rows < grid); stale values in the unused entries must not
+    reach the convergence norm."""
+    h, w, n, j0 = 10, 300, 7, 6
+    N = h * w
+    rng = np.random.default_rng(3)
+    geo = {"w": w, "h": h, "halo": 0, "n_up": 0}
+    res = []
+    for dev in (cuda, "cpu"):
+        t = lambda a: torch.tensor(a, dtype=torch.float32, device=dev)  # noqa: E731
+        u = t(rng.normal(size=(n, N)))
+        v = t(rng.uniform(0, 0.2, size=(n, N)))
+        z = t(rng.normal(size=(1, N)))
+        xr = t(rng.normal(size=(n, N)))
+        xo = torch.zeros((n, N), device=dev)
+        part = K.partials_buffer(N, dev)
+        part.fill_(1e30)
+        K.reg_finish(n, u, v, z, None, xr, xo, 0.9, 1 << j0, N, partials=part, geo=geo)
+        res.append(float(K.reduce_partials(part).cpu()))
+        rng = np.random.default_rng(3)
+    assert res[0] < 1e20 and abs(res[0] - res[1]) <= 1e-5 * abs(res[1]), res
 
 
 def test_reg_schedule_on_device_matches_host(cuda):

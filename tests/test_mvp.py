@@ -1,0 +1,121 @@
+"""SURVEY.md §7.3 minimum end-to-end slice against a float64 oracle: JRC-TIP
+7-parameter, 2-band assimilation, T = 500 random-init GP emulators, 10 dates,
+``propagate_information_filter_LAI`` with Q[6] = 0.04 (kafka_test.py:156-217,
+Q at :207-208), the default fused engine path, run loop of
+kafka/linear_kf.py:171-212.
+
+Acceptance: x within 5e-4 and the packed analysis
+precision within 1e-3 of the oracle (relative to each parameter's / packed
+entry's largest magnitude over the tile), the same Gauss-Newton iteration
+counts, and the per-date drift reported (docs/PARITY.md records it).
+"""
+import datetime as dt
+import json
+
+import numpy as np
+import pytest
+
+import kafka_inferenceengine_amd as k
+from kafka_inferenceengine_amd.utils.blocks import interleaved_to_soa, pack_blocks, sparse_to_blocks
+
+from oracle import oracle_run, oracle_run_blocks
+
+Q6 = 0.04
+X_TOL, P_TOL = 5e-4, 1e-3
+
+
+def _grid(n_dates):
+    dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(n_dates)]
+    return dates, [dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in dates]
+
+
+def _rel(a, b):
+    """max |a - b| per row over the row's largest |b| (a, b: [rows, N])."""
+    return np.abs(a - b).max(1) / (np.abs(b).max(1) + 1e-12)
+
+
+def mvp(device, size, n_dates=10, n_train=500):
+    """Run the engine and the float64 block oracle; returns the per-date drift
+    records and the final (x, packed P) errors."""
+    mask = np.ones((size, size), bool)
+    dates, grid = _grid(n_dates)
+    jp = k.JRCPrior(k.TIP_PARAMETERS, mask)
+    obs = k.SyntheticBHRObservations(mask, dates=dates, n_train=n_train, device=device, stream=True,
+                                     n_pool=n_dates)
+    out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
+    kf = k.LinearKalman(obs, out, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS,
+                        state_propagation=k.propagate_information_filter_LAI, device=device)
+    kf.set_trajectory_model()
+    kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, Q6]))
+    st = kf.run(grid, kf.state_from_prior(jp), None, None)
+    gn = [h["gn_iterations"][0] for h in kf.history]
+    N = st.N
+    # oracle on the host, fed the very observations the engine assimilated (the
+    # source's reference records decode its uint16 DN rasters; a source made on
+    # another device would quantise its own operator values to DN, and one DN
+    # step flipped is 1e-4 of reflectance)
+    mu, _, ci = k.tip_prior()
+    steps = []
+    xo, Ao, iters = oracle_run_blocks(obs, mask, k.TIP_BAND_MAPPER, grid, mu, ci, q=[0, 0, 0, 0, 0, 0, Q6],
+                                      x0=jp.mean, A0=jp.inv_covar,
+                                      on_step=lambda t, x, A: steps.append((t, x.copy(), A.copy())))
+    drift = []
+    for t, x, A in steps:
+        mean, unc = out.history[t]
+        xm = mean[:, :N].cpu().numpy().astype(np.float64)
+        um = unc[:, :N].cpu().numpy().astype(np.float64)
+        uo = 1.0 / np.sqrt(np.einsum("nii->in", A))
+        drift.append({"date": t.date().isoformat(), "x_rel": float(_rel(xm, x.T).max()),
+                      "x_rel_per_param": [float(v) for v in _rel(xm, x.T)],
+                      "unc_rel": float(_rel(um, uo).max())})
+    Ps = st.P[:, :N].cpu().numpy().astype(np.float64)
+    Po = pack_blocks(Ao).astype(np.float64)
+    if Po.shape != Ps.shape:
+        Po = Po.T
+    x_err = float(_rel(st.x[:, :N].cpu().numpy().astype(np.float64), xo.T).max())
+    p_err = float(_rel(Ps, Po).max())
+    return {"size": size, "n_dates": n_dates, "n_train": n_train, "gn": gn, "gn_oracle": iters,
+            "x_rel": x_err, "P_rel": p_err, "drift": drift}
+
+
+def test_block_oracle_equals_reference_api_oracle():
+    """The float64 block oracle (no float32 cast) reproduces the reference-API
+    oracle (sparse operators, variational_kalman_multiband with its float32
+    cast, propagate_and_blend_prior) to the cast's precision."""
+    mask = np.ones((24, 20), bool)
+    mask[:3, :4] = False
+    dates, grid = _grid(4)
+    obs = k.SyntheticBHRObservations(mask, dates=dates, n_train=100, device="cpu", stream=True, n_pool=4)
+    jp = k.JRCPrior(k.TIP_PARAMETERS, mask)
+    x0, Pinv = jp.process_prior(None)
+    Q = np.zeros_like(x0)
+    Q[6::7] = Q6
+    xr, Pr, it_r = oracle_run(obs, mask, k.create_nonlinear_observation_operator, 7, grid, x0, Pinv,
+                              propagator=k.propagate_information_filter_LAI, Q=Q)
+    mu, _, ci = k.tip_prior()
+    xb, Ab, it_b = oracle_run_blocks(obs, mask, k.TIP_BAND_MAPPER, grid, mu, ci, q=[0, 0, 0, 0, 0, 0, Q6],
+                                     x0=jp.mean, A0=jp.inv_covar)
+    assert it_r == it_b
+    assert np.abs(interleaved_to_soa(xr, 7).T - xb).max() < 1e-4
+    Ar = sparse_to_blocks(Pr, 7, check=False)
+    assert np.abs(Ar - Ab).max() / np.abs(Ab).max() < 1e-4   # the reference propagator casts to f32
+
+
+def test_mvp_slice_host_runner():
+    """The slice on the host runner (the kernels' per-pixel source over
+    OpenMP, f32 VALU GP) at 48^2."""
+    r = mvp("cpu", 48)
+    print(json.dumps(r))
+    assert r["gn"] == r["gn_oracle"]
+    assert r["x_rel"] < X_TOL and r["P_rel"] < P_TOL, r
+
+
+@pytest.mark.gpu
+def test_mvp_slice_on_device(cuda):
+    """The slice on one MI355X at 256^2 (65,536 px, 10 dates, T = 500): the
+    fused matrix-core kernel (split-f16 GP on MFMA, fused forecast and GN 1+2)."""
+    r = mvp(cuda, 256)
+    print("MVP " + json.dumps(r), flush=True)
+    assert r["gn"] == r["gn_oracle"]
+    assert r["x_rel"] < X_TOL, r
+    assert r["P_rel"] < P_TOL, r

@@ -352,6 +352,66 @@ def _ifd_entries(b):
     return out
 
 
+def _strip_tiff(path, img, rps, pad_last=True):
+    """A hand-made DEFLATE strip TIFF (float32) whose last strip, when
+    ``pad_last``, is compressed padded to a full RowsPerStrip (as some writers
+    do)."""
+    import struct
+    import zlib
+    H, W = img.shape
+    strips = []
+    for r in range(0, H, rps):
+        blk = img[r:r + rps]
+        if pad_last and blk.shape[0] < rps:
+            blk = np.vstack([blk, np.zeros((rps - blk.shape[0], W), np.float32)])
+        strips.append(zlib.compress(np.ascontiguousarray(blk, "<f4").tobytes()))
+    n = len(strips)
+    entries = [(256, 4, 1, W), (257, 4, 1, H), (258, 3, 1, 32), (259, 3, 1, 8), (262, 3, 1, 1),
+               (273, 4, n, None), (277, 3, 1, 1), (278, 4, 1, rps), (279, 4, n, None), (339, 3, 1, 3)]
+    ifd_size = 2 + 12 * len(entries) + 4
+    arr_off = 8 + ifd_size
+    data_off = arr_off + 8 * n
+    offs, o = [], data_off
+    for s in strips:
+        offs.append(o)
+        o += len(s)
+    out = bytearray(b"II*\x00" + struct.pack("<I", 8) + struct.pack("<H", len(entries)))
+    for tag, typ, cnt, val in entries:
+        if tag == 273:
+            val = arr_off if n > 1 else offs[0]
+        elif tag == 279:
+            val = arr_off + 4 * n if n > 1 else len(strips[0])
+        if typ == 3 and cnt == 1:
+            out += struct.pack("<HHIHH", tag, typ, cnt, val, 0)
+        else:
+            out += struct.pack("<HHII", tag, typ, cnt, val)
+    out += struct.pack("<I", 0)
+    out += b"".join(struct.pack("<I", v) for v in offs) + b"".join(struct.pack("<I", len(s)) for s in strips)
+    out += b"".join(strips)
+    path.write_bytes(bytes(out))
+
+
+def test_native_reader_accepts_padded_last_strip(tmp_path):
+    """a compressed last strip padded to the full RowsPerStrip
+    decodes (libtiff reads such files); one that stops short is refused."""
+    from kafka_inferenceengine_amd.input_output.tiff import read_tiff_window
+    img = np.random.default_rng(2).random((7, 10)).astype(np.float32)
+    for pad in (True, False):
+        p = tmp_path / f"s{int(pad)}.tif"
+        _strip_tiff(p, img, 4, pad_last=pad)
+        got = read_tiff_window(p, out=np.zeros((7, 10), np.float32))
+        assert np.array_equal(got, img), pad
+    # a last strip short of the raster's rows: refused
+    p = tmp_path / "short.tif"
+    _strip_tiff(p, img[:6], 4, pad_last=False)
+    b = bytearray(p.read_bytes())
+    import struct
+    b[8 + 2 + 12 * 1 + 8:8 + 2 + 12 * 1 + 12] = struct.pack("<I", 7)   # ImageLength 6 -> 7
+    (tmp_path / "short7.tif").write_bytes(bytes(b))
+    with pytest.raises(RuntimeError, match="inflate failed"):
+        read_tiff_window(tmp_path / "short7.tif", out=np.zeros((7, 10), np.float32))
+
+
 def test_native_reader_rejects_bad_inputs(tmp_path):
     """the native reader must refuse (not overflow, zero-fill or
     index out of range on) a sample-size mismatch, a truncated DEFLATE stream,

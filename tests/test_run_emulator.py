@@ -48,3 +48,22 @@ def test_run_emulator_lut_branch_device_equals_host(device):
     pred = np.asarray(gp.predict(lut, do_unc=False)[0])
     np.testing.assert_allclose(H, pred[near], rtol=1e-12)
     assert dHt.shape == (4000, 4) and np.isfinite(dHt.cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_run_emulator_float64_rows_that_collide_in_float32(device):
+    """float64 rows that differ only below float32 precision stay
+    distinct on the tensor path (deduplicated in the input's precision, as on
+    the host path), and the results come back in float64."""
+    gp = _gp()
+    rng = np.random.default_rng(4)
+    base = rng.uniform(0.2, 0.8, (20, 4))
+    x = np.repeat(base, 3, axis=0)
+    x[1::3, 0] += 1e-11          # same float32 row, a different float64 row
+    x[2::3, 2] -= 3e-12
+    assert len(np.unique(x.astype(np.float32), axis=0)) == 20 and len(np.unique(x, axis=0)) == 60
+    H, dH = run_emulator(gp, x)
+    Ht, dHt = run_emulator(gp, torch.as_tensor(x, device=device))
+    assert Ht.dtype == torch.float64 and dHt.dtype == torch.float64
+    np.testing.assert_allclose(Ht.cpu().numpy(), H, rtol=1e-13, atol=1e-14)
+    np.testing.assert_allclose(dHt.cpu().numpy(), dH, rtol=1e-12, atol=1e-13)
