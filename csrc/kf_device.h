@@ -90,7 +90,7 @@ __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
 // MINW = 4 waves per SIMD (<= 128 VGPRs, 2 workgroups per CU for two bands'
 // tables) lets the HBM phases (state loads, result stores) of some waves run
 // under the record loops of others; BS = 256 gives 3 waves per SIMD.
-template <int NP, int D, int FOBS, int BS = BLOCK, int MINW = 1, int LAYOUT = BAND_LAYOUT_RUNTIME>
+template <int NP, int D, int FOBS, int BS = BLOCK, int MINW = 1, int LAYOUT = BAND_LAYOUT_RUNTIME, bool IL = false>
 __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   extern __shared__ kf_h8 gpm_lds[];
@@ -115,8 +115,8 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
     const int64_t p = base + lane;
     const bool act = p < a.N;
     float dn1;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT>(a, act ? p : a.N - 1, act, gpm_lds,
-                                                                           dn1 KF_PHASE_ARG);
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT, IL>(a, act ? p : a.N - 1, act, gpm_lds,
+                                                                               dn1 KF_PHASE_ARG);
     acc += act ? (double)dn : 0.0;
     acc1 += act ? (double)dn1 : 0.0;
   }
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
 // (gp_mfma_sums_g): many-band GP states (PROSAIL: ten bands, 358-716 KiB of
 // tables) whose tables exceed the LDS.  No LDS, so the waves per SIMD follow
 // the VGPR count alone.
-template <int NP, int D, int FOBS, bool PF = false>
+template <int NP, int D, int FOBS, bool PF = false, bool IL = false>
 __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   KF_PHASE_KERNEL_BEGIN
@@ -140,7 +140,8 @@ __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs 
     const int64_t p = base + lane;
     const bool act = p < a.N;
     float dn1;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, true, PF>(a, act ? p : a.N - 1, act, nullptr, dn1 KF_PHASE_ARG);
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, true, PF, BAND_LAYOUT_RUNTIME, IL>(a, act ? p : a.N - 1, act,
+                                                                                         nullptr, dn1 KF_PHASE_ARG);
     acc += act ? (double)dn : 0.0;
     acc1 += act ? (double)dn1 : 0.0;
   }
@@ -438,11 +439,17 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
     }
     if (a.gpm_frags > 0 && a.variant != 4 && a.n_bands <= GPM_MAX_BANDS) {
       const size_t lds = (size_t)a.gpm_frags * sizeof(kf_h8);
-#define KF_MFMA_GO(OBS_, BS_, MINW_, LAY_)                                                                    \
-  {                                                                                                          \
-    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_>, lds);                                 \
-    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_>), dim3(grid), dim3(BS_), lds, s, \
-                       a);                                                                                   \
+#define KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_)                                                                  \
+  {                                                                                                              \
+    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_, IL_>, lds);                                \
+    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_, IL_>), dim3(grid), dim3(BS_), lds, s, \
+                       a);                                                                                       \
+  }
+      // variant 16 (A/B): both column blocks' exponent MFMAs issued first (gpm_chunk IL)
+#define KF_MFMA_GO(OBS_, BS_, MINW_, LAY_)                 \
+  {                                                       \
+    if (a.variant == 16) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, true) \
+    else KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, false)        \
   }
       // Launch bound of 3 workgroups per CU (MINW = 3, as the LDS tables
       // allow) up to 7 parameters: the compiler holds the kernel to <= 168
@@ -474,6 +481,7 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
         return false;
       }
 #undef KF_MFMA_GO
+#undef KF_MFMA_GO1
       return true;
     }
     if constexpr (FD == NP && NP >= 7) {
@@ -483,6 +491,8 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
         // the default leaves the latency to the other wave
         if (a.fast_obs == OBS_DN16 && a.variant == 7)
           hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, true>), dim3(grid), dim3(BLOCK), 0, s, a);
+        else if (a.fast_obs == OBS_DN16 && a.variant == 16)   // interleaved exponent MFMAs (A/B)
+          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, false, true>), dim3(grid), dim3(BLOCK), 0, s, a);
         else if (a.fast_obs == OBS_DN16)
           hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
         else if (a.fast_obs == OBS_F32)

@@ -191,11 +191,34 @@ __device__ __forceinline__ int gpm_sum_row(int col) {
 // One 32-point chunk for both column blocks: exponent, split, packed sums.
 // FIRST: the first chunk starts the sums from a zero accumulator operand (an
 // inline constant of the MFMA) instead of 32 zeroed registers.
-template <int D, bool FIRST = false>
+// IL: both column blocks' exponent MFMAs are issued first, so the second
+// block's exponent runs on the matrix cores under the first block's
+// exponentials and split (one more 16-register accumulator live).
+template <int D, bool FIRST = false, bool IL = false>
 __device__ __forceinline__ void gpm_chunk(const kf_h8 (&ea)[gpm_k_steps(D)], const kf_h8 (&sa)[2],
                                           const kf_h8 (&xb)[2][gpm_k_steps(D)], float neg1, kf_f16v (&acc)[2]) {
   constexpr int NK = gpm_k_steps(D);
   const kf_f16v zero = {};
+  if constexpr (IL) {
+    kf_f16v e[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      e[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[0], xb[i][0], zero, 0, 0, 0);
+#pragma unroll
+      for (int kk = 1; kk < NK; ++kk) e[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[kk], xb[i][kk], e[i], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        kf_h8 mh, ml;
+        gpm_exp_split(e[i], 8 * q, neg1, mh, ml);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q], mh, (FIRST && q == 0) ? zero : acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[q], ml, acc[i], 0, 0, 0);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     kf_f16v e = __builtin_amdgcn_mfma_f32_32x32x16_f16(ea[0], xb[i][0], zero, 0, 0, 0);
@@ -216,7 +239,7 @@ __device__ __forceinline__ void gpm_chunk(const kf_h8 (&ea)[gpm_k_steps(D)], con
 // fragment.  Returns the lane's S[0] = sum sgn m, S[1 + d] = sum sgn m B_d,
 // unscaled (gpm_scale not applied; 2^cl is).  Every lane of the wave must call
 // it (MFMA); lanes without an observation pass any finite x.
-template <int D>
+template <int D, bool IL = false>
 __device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, const kf_h8* __restrict__ zf, int nchunk,
                                              const float (&xi)[D], float c, float (&S)[D + 1]) {
   static_assert(D >= 1 && D <= GPM_MAX_D, "GP input count for the matrix-core path");
@@ -248,12 +271,12 @@ __device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, cons
   {
     kf_h8 ea[NK], sa[2];
     load(0, ea, sa);
-    gpm_chunk<D, true>(ea, sa, xb, neg1, acc);
+    gpm_chunk<D, true, IL>(ea, sa, xb, neg1, acc);
   }
   for (int ch = 1; ch < nchunk; ++ch) {
     kf_h8 ea[NK], sa[2];
     load(ch, ea, sa);
-    gpm_chunk<D>(ea, sa, xb, neg1, acc);
+    gpm_chunk<D, false, IL>(ea, sa, xb, neg1, acc);
   }
   gpm_extract2<D>(acc, S);
   const float s = kexp2(cl);
@@ -266,7 +289,7 @@ __device__ __forceinline__ void gp_mfma_sums(const kf_h8* __restrict__ tab, cons
 // PROSAIL bands).  PF: the next chunk's fragments are loaded while the current
 // one runs (register double buffer).
 
-template <int D, bool PF = false>
+template <int D, bool PF = false, bool IL = false>
 __device__ __forceinline__ void gp_mfma_sums_g_xb(const void* tab_, int nchunk, const kf_h8 (&xb)[2][gpm_k_steps(D)],
                                                   float cl, float (&S)[D + 1]) {
   static_assert(D >= 1 && D <= GPM_MAX_D, "GP input count for the matrix-core path");
@@ -313,7 +336,7 @@ __device__ __forceinline__ void gp_mfma_sums_g_xb(const void* tab_, int nchunk, 
       sa[0] = san[0];
       sa[1] = san[1];
     }
-    gpm_chunk<D, decltype(first)::value>(ea, sa, xb, neg1, acc);
+    gpm_chunk<D, decltype(first)::value, IL>(ea, sa, xb, neg1, acc);
     if constexpr (PF) {
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) ea[kk] = ean[kk];
@@ -330,13 +353,13 @@ __device__ __forceinline__ void gp_mfma_sums_g_xb(const void* tab_, int nchunk, 
   for (int f = 0; f <= D; ++f) S[f] *= s;
 }
 
-template <int D, bool PF = false>
+template <int D, bool PF = false, bool IL = false>
 __device__ __forceinline__ void gp_mfma_sums_g(const void* tab_, int nchunk, const float (&xi)[D], float c,
                                                float (&S)[D + 1]) {
   kf_h8 xb[2][gpm_k_steps(D)];
   float cl;
   gpm_operands<D>(xi, c, xb, cl);
-  gp_mfma_sums_g_xb<D, PF>(tab_, nchunk, xb, cl, S);
+  gp_mfma_sums_g_xb<D, PF, IL>(tab_, nchunk, xb, cl, S);
 }
 
 // BAND_LAYOUT_SHARED_X: every band is a full-state GP around the same centre,
@@ -462,7 +485,8 @@ __device__ __forceinline__ void gpm_epilogue(const KF_CONST_AS BandDesc* q, cons
   }
 }
 
-template <int NP, int D, int FOBS, bool GT = false, bool PF = false, int LAYOUT = BAND_LAYOUT_RUNTIME>
+template <int NP, int D, int FOBS, bool GT = false, bool PF = false, int LAYOUT = BAND_LAYOUT_RUNTIME,
+          bool IL = false>
 __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
                                                      const kf_h8* lds, float& dn_first KF_PHASE_PARAM) {
   constexpr int NT = ntri(NP);
@@ -565,14 +589,14 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
             for (int kk = 0; kk < gpm_k_steps(D); ++kk) xb[i][kk] = sxb[i][kk];
           float cl;
           gpm_patch_c<D>(xb, c, cl);
-          gp_mfma_sums_g_xb<D, PF>(bdp->gpm, nch, xb, cl, S);
+          gp_mfma_sums_g_xb<D, PF, IL>(bdp->gpm, nch, xb, cl, S);
         } else {
-          gp_mfma_sums_g<D, PF>(bdp->gpm, nch, xi, c, S);
+          gp_mfma_sums_g<D, PF, IL>(bdp->gpm, nch, xi, c, S);
         }
       } else if constexpr (GT) {
-        gp_mfma_sums_g<D, PF>(bdp->gpm, nch, xi, c, S);
+        gp_mfma_sums_g<D, PF, IL>(bdp->gpm, nch, xi, c, S);
       } else {
-        gp_mfma_sums<D>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
+        gp_mfma_sums<D, IL>(lds + off, lds + a.gpm_frags - 1, nch, xi, c, S);
       }
       KF_PHASE(KF_PH_GP)
       const KF_CONST_AS BandDesc* q = opaque(bdp);   // epilogue fields: not live across the chunk loop

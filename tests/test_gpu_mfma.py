@@ -119,6 +119,18 @@ def test_gp_mfma_analysis_vs_oracle_and_valu(cuda, case):
     assert abs(rm - rv) / rv < 1e-2
 
 
+@pytest.mark.parametrize("case", ["tip", "prosail"])
+def test_interleaved_exponent_variant_bit_identical(cuda, case):
+    """Variant 16 issues both column blocks' exponent MFMAs before the first
+    block's exponentials (gpm_chunk IL): the same operations per block, so the
+    same bits."""
+    prob = tip_case(N=5000) if case == "tip" else prosail_case(N=3000)
+    _, x0, a0, s0, h0, r0 = run(prob, cuda)
+    _, x1, a1, s1, h1, r1 = run(prob, cuda, variant=16)
+    assert np.array_equal(x0, x1) and np.array_equal(a0, a1) and np.array_equal(s0, s1)
+    assert all(np.array_equal(p, q) for p, q in zip(h0, h1)) and r0 == r1
+
+
 # The cancelling regime (ADVICE r3): near-interpolating emulators (1e-5 nugget,
 # |alpha| >> |f|) are the stress case of the f16 hi/lo split.  Round 2's bounds,
 # measured on such emulators, still hold for the round-3 packed operand.
