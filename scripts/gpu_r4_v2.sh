@@ -11,6 +11,11 @@ O=gpurun_out/r4v2
 stop() { echo "!! $1 rc=$2"; exit ${2:-1}; }
 run() { local n=$1 log=$2 to=$3; shift 3; timeout -k 10 $to "$@" > $log 2>&1; local rc=$?; \
         if [ $rc -ne 0 ]; then tail -30 $log; stop $n $rc; fi; }
+# kernel trace of the spatial step (where its 1.34x over tip7 goes)
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/$O/trace_spatial" -o run \
+    --output-format csv -- python "$R/bench.py" --config spatial --steps 3 --warmup 1 > "$R/$O/trace_spatial.log" 2>&1) \
+  || { tail -5 $O/trace_spatial.log; stop trace_spatial 1; }
+echo trace-spatial-done
 if [ -z "$SKIP_PROBE" ]; then
   (cd scripts/probes && hipcc --offload-arch=gfx950 -O3 -Wno-unused-value -o issue_overlap_probe issue_overlap_probe.hip) || stop build_probe 1
   run probe $O/issue_overlap_probe.jsonl 300 ./scripts/probes/issue_overlap_probe
