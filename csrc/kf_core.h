@@ -902,21 +902,26 @@ KF_HD void delta_to_full(const float (&A)[ntri(NP)], const float (&x0)[NP], floa
 // the f32 solve error scales with |x - x0| instead of |x|); b_out and the
 // regulariser get the full form.
 // store = false: a fused intermediate Gauss-Newton iteration (AnalysisArgs.
-// gn_fused) -- the same solve and health fallback, x left in b, nothing stored.
+// gn_fused) or a tail lane -- the same solve and health fallback, x left in b,
+// nothing stored.  final_it = false: an intermediate iteration, which takes the
+// plain solve even when the launch carries the regulariser (reg_v: the fused
+// spatial launch, a plain first iteration and the regularised prepare of the
+// second).
 // The fused kernels reach this function from ONE call site for both kinds of
 // iteration, so the intermediate x is bit-identical to a separate launch's
 // (two inlined copies of the solve may be scheduled / contracted differently).
 template <int NP, bool DELTA = false, typename AP>
 KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[NP], const float (&x0)[NP],
-                              uint8_t st, bool store = true) {
+                              uint8_t st, bool store = true, bool final_it = true) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a->ld;
   if (store && a->x0_out) {
 #pragma unroll
     for (int j = 0; j < NP; ++j) KF_PXS(a->x0_out, j * ld, p) = x0[j];
   }
-  if (DELTA && (a->reg_v || a->b_out)) delta_to_full<NP>(A, x0, b);
-  if (a->reg_v) {
+  const bool reg = a->reg_v && final_it;
+  if (DELTA && (reg || a->b_out)) delta_to_full<NP>(A, x0, b);
+  if (reg) {
     int deg = 0;
     if (a->reg_geo.w > 0) {
 #pragma unroll
@@ -929,7 +934,7 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
 #pragma unroll
     for (int j = 0; j < NP; ++j)
       if ((a->reg_mask >> j) & 1u) A[tri(NP, j, j)] += gd;
-    if (a->a_out) {
+    if (store && a->a_out) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = A[t];
     }
@@ -957,14 +962,14 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
 #pragma unroll
         for (int t = 0; t < NT; ++t) Af[t] = KF_PXS(a->pf_inv, t * ld, p);
       }
-      if (a->a_out) {
+      if (store && a->a_out) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = Af[t];
       }
 #pragma unroll
       for (int j = 0; j < NP; ++j) dA[j] = Af[tri(NP, j, j)];
     }
-    if (a->out_unc) {
+    if (store && a->out_unc) {
       // the uncertainty raster of the final iteration (the mean follows in
       // reg_finish): written here, where diag A is in registers, so the finish
       // pass does not re-read the precision
@@ -973,6 +978,7 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
 #pragma unroll
       for (int j = 0; j < NP; ++j) KF_PXS(a->out_unc, j * pl, r) = kf_rsqrt(dA[j]);
     }
+    if (!store) return 0.f;
 #pragma unroll
     for (int j = 0; j < NP; ++j) KF_PXS(a->x_out, j * ld, p) = b[j];
     int c = 0;
@@ -1031,9 +1037,12 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
         for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = A[t];
       }
     }
+    if (store) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) KF_PXS(a->x_out, j * ld, p) = b[j];
+    }
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      if (store) KF_PXS(a->x_out, j * ld, p) = b[j];
       const float d = b[j] - x0[j];
       dn = fmaf(d, d, dn);
     }
@@ -1205,13 +1214,13 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
     const KF_CONST_AS AnalysisArgs* ka =
         opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
     const bool last = it + 1 >= ka->gn_fused;
-    dn = analysis_epilogue<NP, DELTA>(ka, p, A, b, x0, st, last);
+    dn = analysis_epilogue<NP, DELTA>(ka, p, A, b, x0, st, last, last);
     if (last) return dn;
   } else
 #endif
   {
     const bool last = it + 1 >= a.gn_fused;
-    dn = analysis_epilogue<NP, DELTA>(&a, p, A, b, x0, st, last);
+    dn = analysis_epilogue<NP, DELTA>(&a, p, A, b, x0, st, last, last);
     if (last) return dn;
   }
   // fused intermediate iteration: x_1 (left in b) becomes the linearisation point

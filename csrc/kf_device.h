@@ -422,6 +422,19 @@ inline int grid_for(int64_t N, int max_blocks) {
     default: return hipErrorInvalidValue;         \
   }
 
+// Interleaved exponent MFMAs (gpm_chunk IL: both column blocks' exponent
+// MFMAs before the first block's exponentials) by default where the second
+// live block costs no waves per SIMD and no scratch (ISA lint,
+// tests/test_isa_lint.py): the JRC-TIP layout kernel (156 -> 168 VGPRs, 3
+// waves either way) and 10-parameter states (2 waves either way); +0.5% tip7,
+// +1.0% prosail10 interleaved on one box (profiles/r4_v2_ab_fixed_tip7T.jsonl).
+// Elsewhere (7-parameter runtime layout: 8-24 B scratch; 3-4 parameters: 4 ->
+// 3 waves) the block-by-block order stays.
+template <int NP, int LAYOUT>
+constexpr bool gpm_il_default() {
+  return (NP == 7 && LAYOUT == BAND_LAYOUT_TIP) || NP >= 10;
+}
+
 template <int NP, int FD>
 static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
   // GP on the matrix cores when the host attached split-f16 tables to every band
@@ -445,11 +458,13 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
     hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_, IL_>), dim3(grid), dim3(BS_), lds, s, \
                        a);                                                                                       \
   }
-      // variant 16 (A/B): both column blocks' exponent MFMAs issued first (gpm_chunk IL)
-#define KF_MFMA_GO(OBS_, BS_, MINW_, LAY_)                 \
-  {                                                       \
-    if (a.variant == 16) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, true) \
-    else KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, false)        \
+      // Both column blocks' exponent MFMAs issued before the first block's
+      // exponentials (gpm_chunk IL) where that costs no occupancy
+      // (gpm_il_default); variant 16 (A/B): the other order
+#define KF_MFMA_GO(OBS_, BS_, MINW_, LAY_)                                   \
+  {                                                                         \
+    if (gpm_il_default<NP, LAY_>() != (a.variant == 16)) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, true) \
+    else KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, false)                          \
   }
       // Launch bound of 3 workgroups per CU (MINW = 3, as the LDS tables
       // allow) up to 7 parameters: the compiler holds the kernel to <= 168
@@ -491,12 +506,13 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
         // the default leaves the latency to the other wave
         if (a.fast_obs == OBS_DN16 && a.variant == 7)
           hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, true>), dim3(grid), dim3(BLOCK), 0, s, a);
-        else if (a.fast_obs == OBS_DN16 && a.variant == 16)   // interleaved exponent MFMAs (A/B)
+        else if (a.fast_obs == OBS_DN16 && (a.variant == 16) != gpm_il_default<NP, BAND_LAYOUT_RUNTIME>())
           hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, false, true>), dim3(grid), dim3(BLOCK), 0, s, a);
         else if (a.fast_obs == OBS_DN16)
           hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
         else if (a.fast_obs == OBS_F32)
-          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_F32>), dim3(grid), dim3(BLOCK), 0, s, a);
+          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_F32, false, gpm_il_default<NP, BAND_LAYOUT_RUNTIME>()>),
+                             dim3(grid), dim3(BLOCK), 0, s, a);
         else
           return false;
         return true;

@@ -663,7 +663,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   // too but store nothing: their x0 only feeds the next iteration's MFMA
   // operands and must stay finite
   const bool last = it + 1 >= ka->gn_fused;
-  const float dn = analysis_epilogue<NP, true>(ka, p, A, b, x0, st, last && act);
+  const float dn = analysis_epilogue<NP, true>(ka, p, A, b, x0, st, last && act, last);
   KF_PHASE(KF_PH_SOLVE)
   if (last) return act ? dn : 0.f;
   dn_first = dn;

@@ -39,6 +39,12 @@ class EngineConfig:
     # (n_iter < min_iterations) only needs a linearisation point, so its coupled
     # solve stops at this looser tolerance (the final iteration uses spatial_tol)
     spatial_tol_first: float = 1e-1
+    # with fuse_gn: the first Gauss-Newton iteration (which only supplies the
+    # second's linearisation point) is the plain per-pixel solve, fused into
+    # the launch that prepares the regularised second iteration -- one analysis
+    # pass and no coupled solve saved per date (False: both iterations coupled,
+    # the first to spatial_tol_first)
+    spatial_first_plain: bool = True
     spatial_max_sweeps: int = 64
     # one field on a dense strip without halo rows (one rank, or no strip
     # neighbours): up to 8 sweeps per launch out of LDS (kf_reg_tiled.hip),

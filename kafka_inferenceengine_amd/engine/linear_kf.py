@@ -778,6 +778,10 @@ class LinearKalman:
         # iteration 1 exactly and its norm is 0 -- converged without a read-back
         static_conv = (fuse2 and cfg.convergence_tolerance > 0 and bool(specs)
                        and all(s.kind == OP_LINEAR for s in specs))
+        # spatial prior: a plain first iteration (config.spatial_first_plain; it
+        # cannot end the loop), fused with the regularised prepare of the second
+        first_plain = spatial and cfg.spatial_first_plain and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
+        fuse_sp = first_plain and cfg.fuse_gn
         while True:
             # the analysis precision is only needed from the iteration that can
             # end the loop on: skip its 4*ntri B/px store before min_iterations
@@ -786,21 +790,26 @@ class LinearKalman:
             if precomp:
                 pre = self._precompute_host(specs, dbs, x_prev)
                 table = build_table(specs, dbs, n, self._cache, self.device, h0_outs, pre)
-            if fuse2:
+            if fuse2 or fuse_sp:
                 # iterations 1 + 2 in one launch: outputs of iteration 2 (which can end the loop)
                 red2 = self._red_hist[1:3]
                 with self.timer.phase("analysis"):
                     if N:
-                        K.analysis(n, table, x_prev, None if prop is not None else fc.x,
-                                   None if prop is not None else fc.P, x_new, P_out, None, status, self._partials,
-                                   N=N, prop=prop, out=out_t, gn_fused=2, partials_first=self._partials1)
+                        if fuse_sp:
+                            self._regularised_iteration(table, x_prev, fc, x_new, P_out, status, prop, out_t,
+                                                        final=True, partials_first=self._partials1)
+                        else:
+                            K.analysis(n, table, x_prev, None if prop is not None else fc.x,
+                                       None if prop is not None else fc.P, x_new, P_out, None, status,
+                                       self._partials, N=N, prop=prop, out=out_t, gn_fused=2,
+                                       partials_first=self._partials1)
                         K.reduce_partials(self._partials1, red2[0:1])
                         K.reduce_partials(self._partials, red2[1:2])
                     else:
                         red2.zero_()
                 with self.timer.phase("converge"):
                     pend2 = self.comm.sum_f64_async(red2)
-                fuse2 = False
+                fuse2 = fuse_sp = False
                 deferred.append((1, pend2.column(0)))
                 pend = pend2.column(1)
                 n_iter = 2
@@ -822,6 +831,13 @@ class LinearKalman:
                         if gain:
                             K.gain(n, table, x_prev, None if prop else fc.x, None if prop else fc.P, x_new, A_keep,
                                    status, self._partials, N=N, joseph=cfg.joseph, prop=prop, out=out_now)
+                        elif first_plain and n_iter == 1:
+                            # the unfused form of fuse_sp's first iteration (same kernel path)
+                            K.analysis(n, table, x_prev, None if prop is not None else fc.x,
+                                       None if prop is not None else fc.P, x_new, None, None, status,
+                                       self._partials, N=N, prop=prop)
+                            self._reg_log.append({"solver": "plain", "rho": 0.0, "sweeps": 0, "r2": None,
+                                                  "count": 0})
                         elif cfg.spatial_gamma > 0:
                             self._regularised_iteration(table, x_prev, fc, x_new, A_keep, status, prop, out_now,
                                                         final=n_iter >= cfg.min_iterations)
@@ -1010,7 +1026,7 @@ class LinearKalman:
                 prev = (A_c, b_c)
 
     def _regularised_iteration(self, table, x_prev, fc: KFState | None, x_out, A_out, status, prop=None, out=None,
-                               final=True):
+                               final=True, partials_first=None):
         """GMRF spatial prior (K9 + C2), affine block-Jacobi form (kf_core.h):
         the analysis kernel assembles (A, b) and, instead of solving, factors
         A_reg = A + g deg E_R once and writes u = A_reg^-1 b and V = A_reg^-1 E_R;
@@ -1020,7 +1036,10 @@ class LinearKalman:
         block-Jacobi sweeps of (A_reg) x = b + g E_R sum_q x_q.  The analysis
         precision includes the smoother's diagonal.  With ``prop`` the forecast
         is fused as in the plain path (first iteration: x0 = forecast, written
-        for the norm and the first sweep)."""
+        for the norm and the first sweep).  ``partials_first``: the launch runs
+        the plain first Gauss-Newton iteration in registers (its norm there)
+        and prepares the regularised second, linearised at x_1 (written to the
+        x0 buffer, the finish's reference for the norm)."""
         from ..parallel.halo import HaloExchanger
 
         if self._reg is None:
@@ -1033,8 +1052,10 @@ class LinearKalman:
         sweeps = max(1, int(self.config.jacobi_sweeps))
         rows = reg.reg_rows()
         fx, fP = (fc.x, fc.P) if fc is not None else (None, None)
+        fused = partials_first is not None
         if not rows:   # nothing regularised: plain analysis
-            K.analysis(n, table, x_prev, fx, fP, x_out, A_out, None, status, self._partials, N=N, prop=prop, out=out)
+            K.analysis(n, table, x_prev, fx, fP, x_out, A_out, None, status, self._partials, N=N, prop=prop, out=out,
+                       gn_fused=2 if fused else 1, partials_first=partials_first)
             return
         k = len(rows)
         ld = x_out.shape[1]
@@ -1042,13 +1063,16 @@ class LinearKalman:
             self._reg_uv = tuple(torch.empty((r, ld), dtype=torch.float32, device=self.device)
                                  for r in (n, k * n, n))
         u, v, x0_buf = self._reg_uv
-        x_ref = x_prev if x_prev is not None else x0_buf
+        x_ref = x_prev if (x_prev is not None and not fused) else x0_buf
         # the final iteration's uncertainty raster comes from the prepare (diag of
         # the regularised precision in registers), the mean from reg_finish
         K.analysis(n, table, x_prev, fx, fP, u, A_out, None, status, None, N=N, prop=prop,
                    reg=dict(gamma=gamma, mask=reg.reg_mask, v_out=v, nbr=None if geo else reg.nbr, geo=geo),
-                   x0_out=None if x_prev is not None else x0_buf,
-                   out=None if out is None else (None, out[1], out[2]))
+                   x0_out=None if x_ref is x_prev else x0_buf,
+                   out=None if out is None else (None, out[1], out[2]),
+                   gn_fused=2 if fused else 1, partials_first=partials_first)
+        if fused:
+            self._reg_log.append({"solver": "plain", "rho": 0.0, "sweeps": 0, "r2": None, "count": 0})
         nbr = None if geo else reg.nbr
         tol = self.config.spatial_tol if final else self.config.spatial_tol_first
         depth = self._reg_tiled_depth(k)

@@ -244,7 +244,10 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     ``reg = dict(gamma, mask, v_out, nbr=None, geo=None)`` replaces the solve by
     the K9 regulariser prepare (kf_core.h): a_out <- A + g deg E_R, x_out <- u =
     A_reg^-1 b, v_out [k*n, ld] <- A_reg^-1 E_R; no partials.  ``x0_out``
-    receives the linearisation point (the fused forecast when x_prev is None)."""
+    receives the linearisation point (the fused forecast when x_prev is None).
+    With ``gn_fused=2`` the first iteration is the plain solve (its norm to
+    ``partials_first``) and the regulariser prepares the second, linearised
+    at x_1 (written to ``x0_out``)."""
     check_np(n_params)
     ref = next(t for t in (x_prev, x_f, x_out, a_out) if t is not None)
     N = int(ref.shape[1] if N is None else N)
@@ -272,8 +275,10 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
         raise ValueError("partials must be float64 with >= grid_for(N) entries")
     if gn_fused not in (1, 2):
         raise ValueError("gn_fused must be 1 or 2")
-    if gn_fused == 2 and (reg is not None or a_in is not None or not solve):
-        raise ValueError("gn_fused=2 runs the plain solve path only (no regulariser, band chunks or solve=False)")
+    if gn_fused == 2 and (a_in is not None or not solve):
+        raise ValueError("gn_fused=2 runs the solve path only (no band chunks or solve=False)")
+    if gn_fused == 2 and reg is not None and x0_out is None:
+        raise ValueError("gn_fused=2 with reg needs x0_out (x_1, the second iteration's linearisation point)")
     if partials_first is not None and (partials_first.dtype != torch.float64 or partials_first.numel() < grid_for(N)):
         raise ValueError("partials_first must be float64 with >= grid_for(N) entries")
     a = ext().AnalysisArgs()

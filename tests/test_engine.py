@@ -366,6 +366,31 @@ def test_fused_gn_iterations_equal_separate_launches(tol):
         assert torch.equal(oa.history[t][0], ob.history[t][0]) and torch.equal(oa.history[t][1], ob.history[t][1])
 
 
+@pytest.mark.parametrize("tol", [1e-3, 1e-9])
+def test_fused_spatial_first_iteration_equals_separate_launches(tol):
+    """Spatial prior with spatial_first_plain: the plain first Gauss-Newton
+    iteration fused with the regularised prepare of the second (one launch)
+    is bit-identical to a plain launch followed by the prepare launch --
+    states, output rasters, iteration counts and norms, also when the
+    tolerance forces more (regularised) iterations after the fused pair."""
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=9)
+    grid = _grid(5)
+    res = []
+    for fuse in (False, True):
+        out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
+        kf = _engine(mask, obs, Q, out=out, fuse_gn=fuse, convergence_tolerance=tol, max_iterations=4,
+                     spatial_gamma=5.0, spatial_params=[6], metrics_path=None)
+        st = kf.run(grid, x0, None, Pinv)
+        res.append((st, out, [h["gn_iterations"] for h in kf.history], [h["norms"] for h in kf.history]))
+    (a, oa, ia, na), (b, ob, ib, nb) = res
+    assert ia == ib and na == nb
+    if tol < 1e-6:
+        assert max(n for g in ib for n in g) > 2
+    assert torch.equal(a.x, b.x) and torch.equal(a.P, b.P)
+    for t in oa.history:
+        assert torch.equal(oa.history[t][0], ob.history[t][0]) and torch.equal(oa.history[t][1], ob.history[t][1])
+
+
 def test_linear_operator_converges_statically():
     """Identity operator: y' = y - offset does not depend on the linearisation
     point, so the fused second iteration reproduces the first exactly (norm 0)

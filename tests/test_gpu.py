@@ -264,6 +264,32 @@ def test_fused_gn_launch_equals_separate_launches_gpu(cuda, op):
         assert torch.equal(ha[t][0], hb[t][0]) and torch.equal(ha[t][1], hb[t][1])
 
 
+def test_fused_spatial_first_iteration_equals_separate_launches_gpu(cuda):
+    """spatial_first_plain on the device (matrix-core TIP kernel): the plain
+    first Gauss-Newton iteration fused with the regularised prepare of the
+    second is bit-identical to the two launches (states, output rasters,
+    iteration counts, norms)."""
+    mask = np.ones((96, 160), bool)
+    mask[5:20, 30:70] = False
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
+    outs = []
+    for fuse in (False, True):
+        out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
+        obs = k.SyntheticBHRObservations(mask, n_train=500, device=cuda, stream=False, n_pool=3, field_cell=8)
+        kf = k.LinearKalman(obs, out, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device=cuda,
+                            state_propagation=k.propagate_information_filter_LAI,
+                            config=k.EngineConfig(fuse_gn=fuse, spatial_gamma=5.0, spatial_params=[6]))
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
+        outs.append((st.x.cpu(), st.P.cpu(), [h.get("gn_iterations") for h in kf.history],
+                     [h.get("norms") for h in kf.history], {t: (m.cpu(), u.cpu()) for t, (m, u) in out.history.items()}))
+    (xa, Pa, ia, na, ha), (xb, Pb, ib, nb, hb) = outs
+    assert ia == ib and na == nb
+    assert torch.equal(xa, xb) and torch.equal(Pa, Pb)
+    for t in ha:
+        assert torch.equal(ha[t][0], hb[t][0]) and torch.equal(ha[t][1], hb[t][1])
+
+
 @pytest.mark.parametrize("spatial", [False, True])
 def test_fused_output_gpu(cuda, spatial):
     """Fused output (analysis kernel, or the regulariser finish pass with a

@@ -121,9 +121,9 @@ def test_gp_mfma_analysis_vs_oracle_and_valu(cuda, case):
 
 @pytest.mark.parametrize("case", ["tip", "prosail"])
 def test_interleaved_exponent_variant_bit_identical(cuda, case):
-    """Variant 16 issues both column blocks' exponent MFMAs before the first
-    block's exponentials (gpm_chunk IL): the same operations per block, so the
-    same bits."""
+    """The default issues both column blocks' exponent MFMAs before the first
+    block's exponentials (gpm_chunk IL); variant 16 keeps the round-3
+    block-by-block order: the same operations per block, so the same bits."""
     prob = tip_case(N=5000) if case == "tip" else prosail_case(N=3000)
     _, x0, a0, s0, h0, r0 = run(prob, cuda)
     _, x1, a1, s1, h1, r1 = run(prob, cuda, variant=16)

@@ -46,8 +46,8 @@ def test_built_code_objects_have_no_mfma_operand_hazards():
 # before it was caught (row addresses hoisted out of the fused GN loop:
 # 256 VGPRs, one wave per SIMD).
 HOT = {   # kernel: (min waves per SIMD, max scratch bytes per lane)
-    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb0EEEvNS_12AnalysisArgsE": (3, 0),   # tip7 headline (TIP layout)
-    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb1EEEvNS_12AnalysisArgsE": (3, 0),   # its interleaved-exponent variant
+    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb0EEEvNS_12AnalysisArgsE": (3, 0),   # tip7 block-by-block variant (A/B)
+    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb1EEEvNS_12AnalysisArgsE": (3, 0),   # tip7 headline (TIP layout, interleaved exponents)
     "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi0ELb0EEEvNS_12AnalysisArgsE": (3, 0),   # runtime band layout
     "_ZN2kf15analysis_kernelILi7ELi4ELi2ELi4ELb0EEEvNS_12AnalysisArgsE": (3, 0),           # TIP VALU loop
     "_ZN2kf15analysis_kernelILi7ELin2ELi4ELi4ELb0EEEvNS_12AnalysisArgsE": (3, 0),          # identity7 (bf16 y)

@@ -90,6 +90,8 @@ def test_spatial_residual_logged_per_gn_iteration(tmp_path):
     dates = [r for r in kf.metrics.records if r.get("event") == "date"]
     sp_rec = dates[-1]["spatial"]
     assert len(sp_rec) == dates[-1]["n_iter"]
-    for r in sp_rec:
+    # the first GN iteration is the plain per-pixel solve (spatial_first_plain)
+    assert sp_rec[0]["solver"] == "plain" and sp_rec[0]["sweeps"] == 0
+    for r in sp_rec[1:]:
         assert r["solver"] == "chebyshev" and 0 < r["rho"] < 1 and r["sweeps"] >= 1
         assert np.isfinite(r["residual_rms"]) and r["residual_rms"] < 1e-2
