@@ -217,6 +217,13 @@ KF_HD int32_t geo_neighbour(const StripGeo& g, int64_t N, int64_t p, int k) {
   }
 }
 
+// Compile-time launch specialisations of the fused analysis (analysis_epilogue
+// / pixel_analysis_mfma SPEC): with the forecast fused (AnalysisArgs.prop set)
+// the explicit-forecast and band-chunk paths are dropped, and without the
+// regulariser its prepare; the cold code no longer holds SGPRs across the
+// hot path (TIP kernel: 89 -> 18 SGPR spill slots).
+constexpr int SPEC_ANY = 0, SPEC_PROP = 1, SPEC_PROP_REG = 2;
+
 struct AnalysisArgs {
   int64_t N, ld;
   int32_t n_bands, solve;
@@ -910,16 +917,20 @@ KF_HD void delta_to_full(const float (&A)[ntri(NP)], const float (&x0)[NP], floa
 // The fused kernels reach this function from ONE call site for both kinds of
 // iteration, so the intermediate x is bit-identical to a separate launch's
 // (two inlined copies of the solve may be scheduled / contracted differently).
-template <int NP, bool DELTA = false, typename AP>
+// SPEC (kf_device.h SPEC_*): the launch's forecast / regulariser known at
+// compile time -- SPEC_PROP: fused forecast, no regulariser; SPEC_PROP_REG:
+// fused forecast and regulariser; SPEC_ANY: decided from the arguments.
+template <int NP, bool DELTA = false, int SPEC = SPEC_ANY, typename AP>
 KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[NP], const float (&x0)[NP],
                               uint8_t st, bool store = true, bool final_it = true) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a->ld;
+  const bool has_prop = SPEC != SPEC_ANY || a->prop;
   if (store && a->x0_out) {
 #pragma unroll
     for (int j = 0; j < NP; ++j) KF_PXS(a->x0_out, j * ld, p) = x0[j];
   }
-  const bool reg = a->reg_v && final_it;
+  const bool reg = (SPEC == SPEC_PROP_REG || (SPEC == SPEC_ANY && a->reg_v)) && final_it;
   if (DELTA && (reg || a->b_out)) delta_to_full<NP>(A, x0, b);
   if (reg) {
     int deg = 0;
@@ -954,7 +965,7 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
     if (bad) {
       st |= (!spd ? ST_NONSPD : 0) | (!fin ? ST_NONFINITE : 0) | ST_FALLBACK;
       float Af[NT];
-      if (a->prop) {
+      if (has_prop) {
         forecast_partial<NP>(opaque(cptr(a->prop)), p, b, Af);
       } else {
 #pragma unroll
@@ -1022,7 +1033,7 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
     if (!spd || !fin) {
       // Health fallback: keep the forecast (prior) for this pixel.
       st |= (!spd ? ST_NONSPD : 0) | (!fin ? ST_NONFINITE : 0) | ST_FALLBACK;
-      if (a->prop) {
+      if (has_prop) {
         forecast_partial<NP>(opaque(cptr(a->prop)), p, b, A);   // rare path: recompute instead of keeping it live
       } else {
 #pragma unroll

@@ -90,7 +90,8 @@ __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
 // MINW = 4 waves per SIMD (<= 128 VGPRs, 2 workgroups per CU for two bands'
 // tables) lets the HBM phases (state loads, result stores) of some waves run
 // under the record loops of others; BS = 256 gives 3 waves per SIMD.
-template <int NP, int D, int FOBS, int BS = BLOCK, int MINW = 1, int LAYOUT = BAND_LAYOUT_RUNTIME, bool IL = false>
+template <int NP, int D, int FOBS, int BS = BLOCK, int MINW = 1, int LAYOUT = BAND_LAYOUT_RUNTIME, bool IL = false,
+          int SPEC = SPEC_ANY>
 __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   extern __shared__ kf_h8 gpm_lds[];
@@ -115,8 +116,8 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
     const int64_t p = base + lane;
     const bool act = p < a.N;
     float dn1;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT, IL>(a, act ? p : a.N - 1, act, gpm_lds,
-                                                                               dn1 KF_PHASE_ARG);
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT, IL, SPEC>(a, act ? p : a.N - 1, act,
+                                                                                     gpm_lds, dn1 KF_PHASE_ARG);
     acc += act ? (double)dn : 0.0;
     acc1 += act ? (double)dn1 : 0.0;
   }
@@ -452,19 +453,29 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
     }
     if (a.gpm_frags > 0 && a.variant != 4 && a.n_bands <= GPM_MAX_BANDS) {
       const size_t lds = (size_t)a.gpm_frags * sizeof(kf_h8);
-#define KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_)                                                                  \
+#define KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_)                                                           \
   {                                                                                                              \
-    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_, IL_>, lds);                                \
-    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_, IL_>), dim3(grid), dim3(BS_), lds, s, \
-                       a);                                                                                       \
+    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_, IL_, SPEC_>, lds);                         \
+    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_, IL_, SPEC_>), dim3(grid), dim3(BS_),  \
+                       lds, s, a);                                                                               \
   }
       // Both column blocks' exponent MFMAs issued before the first block's
       // exponentials (gpm_chunk IL) where that costs no occupancy
       // (gpm_il_default); variant 16 (A/B): the other order
 #define KF_MFMA_GO(OBS_, BS_, MINW_, LAY_)                                   \
   {                                                                         \
-    if (gpm_il_default<NP, LAY_>() != (a.variant == 16)) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, true) \
-    else KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, false)                          \
+    if (gpm_il_default<NP, LAY_>() != (a.variant == 16)) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, true, SPEC_ANY) \
+    else KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, false, SPEC_ANY)                \
+  }
+      // JRC-TIP layout with the forecast fused (every date after the first):
+      // the launch's paths fixed at compile time (SPEC_PROP / SPEC_PROP_REG,
+      // kf_core.h); variant 18 (A/B): the generic kernel
+#define KF_MFMA_GO_SPEC(OBS_, BS_, MINW_, LAY_)                                                  \
+  {                                                                                             \
+    constexpr bool IL_ = gpm_il_default<NP, LAY_>();                                            \
+    if (!a.prop || a.variant == 16 || a.variant == 18) KF_MFMA_GO(OBS_, BS_, MINW_, LAY_)       \
+    else if (a.reg_v) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP_REG)                  \
+    else KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP)                                    \
   }
       // Launch bound of 3 workgroups per CU (MINW = 3, as the LDS tables
       // allow) up to 7 parameters: the compiler holds the kernel to <= 168
@@ -479,7 +490,7 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
       if (a.fast_obs == OBS_DN16) {
         if constexpr (NP == 7 && FD == 4) {
           if (tip) {
-            KF_MFMA_GO(OBS_DN16, BLOCK, 3, BAND_LAYOUT_TIP)
+            KF_MFMA_GO_SPEC(OBS_DN16, BLOCK, 3, BAND_LAYOUT_TIP)
             return true;
           }
         }
@@ -495,6 +506,7 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
       } else {
         return false;
       }
+#undef KF_MFMA_GO_SPEC
 #undef KF_MFMA_GO
 #undef KF_MFMA_GO1
       return true;

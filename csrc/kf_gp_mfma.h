@@ -486,7 +486,7 @@ __device__ __forceinline__ void gpm_epilogue(const KF_CONST_AS BandDesc* q, cons
 }
 
 template <int NP, int D, int FOBS, bool GT = false, bool PF = false, int LAYOUT = BAND_LAYOUT_RUNTIME,
-          bool IL = false>
+          bool IL = false, int SPEC = SPEC_ANY>
 __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
                                                      const kf_h8* lds, float& dn_first KF_PHASE_PARAM) {
   constexpr int NT = ntri(NP);
@@ -507,7 +507,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   p = opaque_lane(p);
   uint8_t st = 0;
   // correction form throughout (kf_core.h analysis_epilogue, DELTA)
-  if (a.prop) {
+  if (SPEC != SPEC_ANY || a.prop) {
     float xf[NP];
     forecast_partial<NP>(opaque(cptr(a.prop)), p, xf, A);
     if (!a.x_prev && it == 0) {
@@ -663,7 +663,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   // too but store nothing: their x0 only feeds the next iteration's MFMA
   // operands and must stay finite
   const bool last = it + 1 >= ka->gn_fused;
-  const float dn = analysis_epilogue<NP, true>(ka, p, A, b, x0, st, last && act, last);
+  const float dn = analysis_epilogue<NP, true, SPEC>(ka, p, A, b, x0, st, last && act, last);
   KF_PHASE(KF_PH_SOLVE)
   if (last) return act ? dn : 0.f;
   dn_first = dn;

@@ -69,32 +69,41 @@ def _run(cmd: list[str], verbose: bool) -> None:
         raise RuntimeError(f"build step failed ({r.returncode}): {' '.join(cmd)}\n{msg[-8000:]}")
 
 
-def build(force: bool = False, verbose: bool = False, checked: bool = False, prof: bool = False) -> Path:
+def build(force: bool = False, verbose: bool = False, checked: bool = False, prof: bool = False,
+          exp: str | None = None, exp_csrc: str | None = None) -> Path:
     """``prof``: the phase-clock variant ``_kafka_hip_prof`` (``-DKF_PHASE_CLOCKS``,
     loaded with ``KAFKA_PROF=1``): the fused analysis kernels add each phase's
     shader cycles per wave to a device counter (``ext.phase_clocks``); a
-    measuring tool, not built by ``__graft_entry__.build``."""
+    measuring tool, not built by ``__graft_entry__.build``.
+
+    ``exp``: an A/B experiment module ``_kafka_hip_<exp>`` built from the
+    sources in ``exp_csrc`` (a patched copy of ``csrc/``), loaded with
+    ``KAFKA_EXT=<exp>``; never part of the release build."""
     from concurrent.futures import ThreadPoolExecutor
 
-    if checked and prof:
-        raise ValueError("checked and prof are separate variants")
+    if sum(map(bool, (checked, prof, exp))) > 1:
+        raise ValueError("checked, prof and exp are separate variants")
+    csrc = Path(exp_csrc) if exp else CSRC
     build_dir = BUILD.with_name("kafka_hip_checked") if checked else BUILD.with_name("kafka_hip_prof") if prof \
-        else BUILD
-    ext_path = CHECKED_EXT_PATH if checked else PROF_EXT_PATH if prof else EXT_PATH
+        else BUILD.with_name(f"kafka_hip_{exp}") if exp else BUILD
+    ext_path = CHECKED_EXT_PATH if checked else PROF_EXT_PATH if prof else \
+        PKG_DIR / f"_kafka_hip_{exp}{EXT_SUFFIX}" if exp else EXT_PATH
     build_dir.mkdir(parents=True, exist_ok=True)
-    hdrs = [CSRC / h for h in HEADERS]
-    common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}"]
+    hdrs = [csrc / h for h in HEADERS]
+    common = ["-O3", "-fPIC", "-std=c++17", f"-I{csrc}"]
     if checked:
         common += ["-DKF_CHECKED", "-DKF_MODULE_NAME=_kafka_hip_checked"]
     if prof:
         common += ["-DKF_PHASE_CLOCKS", "-DKF_MODULE_NAME=_kafka_hip_prof"]
+    if exp:
+        common += [f"-DKF_MODULE_NAME=_kafka_hip_{exp}"]
     hip_defs = ["-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}"]
     hipcc = _hipcc()
     jobs, objs = [], []
 
     # 1. device kernels (gfx950 code objects embedded in the host objects)
     for name in HIP_SOURCES:
-        src, obj = CSRC / name, build_dir / (Path(name).stem + ".o")
+        src, obj = csrc / name, build_dir / (Path(name).stem + ".o")
         if force or _stale(obj, [src] + hdrs):
             # MFMA results straight into VGPRs (no v_accvgpr_read per exponent in kf_gp_mfma.h)
             # -fno-slp-vectorize: keeps the GP hi/lo split scalar so hipcc selects
@@ -104,7 +113,7 @@ def build(force: bool = False, verbose: bool = False, checked: bool = False, pro
         objs.append(obj)
 
     # 2. host runner of the same per-pixel code (g++, OpenMP)
-    src, obj = CSRC / "kf_host.cpp", build_dir / "kf_host.o"
+    src, obj = csrc / "kf_host.cpp", build_dir / "kf_host.o"
     if force or _stale(obj, [src] + hdrs):
         jobs.append(["g++", *common, *hip_defs, "-fopenmp", "-mavx2", "-mfma", "-ffp-contract=fast", "-c", str(src),
                      "-o", str(obj)])
@@ -112,7 +121,7 @@ def build(force: bool = False, verbose: bool = False, checked: bool = False, pro
 
     # 3. bindings + ingest runtime (host code, HIP runtime API)
     for name in ("kf_bindings.cpp", "kf_stream.cpp", "kf_tiff.cpp"):
-        src, obj = CSRC / name, build_dir / (Path(name).stem + ".o")
+        src, obj = csrc / name, build_dir / (Path(name).stem + ".o")
         if force or _stale(obj, [src] + hdrs):
             jobs.append(["g++", *common, *hip_defs, *_pybind_includes(), "-fvisibility=hidden", "-c", str(src),
                          "-o", str(obj)])
@@ -136,8 +145,12 @@ def main() -> None:
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--checked", action="store_true", help="debug build with index assertions")
     ap.add_argument("--prof", action="store_true", help="phase-clock build (KAFKA_PROF=1)")
+    ap.add_argument("--exp", default=None, help="A/B experiment module _kafka_hip_<EXP> (KAFKA_EXT=<EXP>)")
+    ap.add_argument("--exp-csrc", default=None, help="patched copy of csrc/ for --exp")
     a = ap.parse_args()
-    p = build(force=a.force, verbose=a.verbose, checked=a.checked, prof=a.prof)
+    if bool(a.exp) != bool(a.exp_csrc):
+        ap.error("--exp and --exp-csrc go together")
+    p = build(force=a.force, verbose=a.verbose, checked=a.checked, prof=a.prof, exp=a.exp, exp_csrc=a.exp_csrc)
     print(f"built {p}")
 
 

@@ -15,8 +15,13 @@ import torch  # noqa: F401  (must precede the extension import)
 _err = None
 CHECKED = os.environ.get("KAFKA_CHECKED", "0") not in ("", "0")
 PROF = os.environ.get("KAFKA_PROF", "0") not in ("", "0")
+EXP = os.environ.get("KAFKA_EXT", "")   # A/B experiment module (_build.py --exp)
 try:
-    if CHECKED:  # debug build with index assertions (_build.py --checked)
+    if EXP:
+        import importlib
+
+        ext = importlib.import_module(f"kafka_inferenceengine_amd._kafka_hip_{EXP}")
+    elif CHECKED:  # debug build with index assertions (_build.py --checked)
         from .. import _kafka_hip_checked as ext  # type: ignore
     elif PROF:  # phase-clock build of the JRC-TIP analysis kernel (_build.py --prof)
         from .. import _kafka_hip_prof as ext  # type: ignore

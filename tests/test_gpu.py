@@ -291,6 +291,38 @@ def test_fused_spatial_first_iteration_equals_separate_launches_gpu(cuda):
 
 
 @pytest.mark.parametrize("spatial", [False, True])
+def test_specialised_tip_kernel_equals_generic_gpu(cuda, spatial):
+    """The JRC-TIP kernels specialised for the fused forecast (SPEC_PROP, and
+    SPEC_PROP_REG with the spatial prior: explicit-forecast / regulariser code
+    compiled out) give the same bits as the generic kernel (variant 18)."""
+    from kafka_inferenceengine_amd.ops import kernels as K
+    mask = np.ones((96, 160), bool)
+    mask[5:20, 30:70] = False
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
+    reg = dict(spatial_gamma=5.0, spatial_params=[6]) if spatial else {}
+    outs = []
+    old = K.DEFAULT_VARIANT
+    try:
+        for variant in (0, 18):
+            K.DEFAULT_VARIANT = variant
+            out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
+            obs = k.SyntheticBHRObservations(mask, n_train=500, device=cuda, stream=False, n_pool=3, field_cell=8)
+            kf = k.LinearKalman(obs, out, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS,
+                                device=cuda, state_propagation=k.propagate_information_filter_LAI,
+                                config=k.EngineConfig(**reg))
+            kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+            st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
+            outs.append((st.x.cpu(), st.P.cpu(), [h.get("norms") for h in kf.history],
+                         {t: (m.cpu(), u.cpu()) for t, (m, u) in out.history.items()}))
+    finally:
+        K.DEFAULT_VARIANT = old
+    (xa, Pa, na, ha), (xb, Pb, nb, hb) = outs
+    assert na == nb and torch.equal(xa, xb) and torch.equal(Pa, Pb)
+    for t in ha:
+        assert torch.equal(ha[t][0], hb[t][0]) and torch.equal(ha[t][1], hb[t][1])
+
+
+@pytest.mark.parametrize("spatial", [False, True])
 def test_fused_output_gpu(cuda, spatial):
     """Fused output (analysis kernel, or the regulariser finish pass with a
     spatial prior) equals the separate unpack kernel on the device."""

@@ -46,9 +46,11 @@ def test_built_code_objects_have_no_mfma_operand_hazards():
 # before it was caught (row addresses hoisted out of the fused GN loop:
 # 256 VGPRs, one wave per SIMD).
 HOT = {   # kernel: (min waves per SIMD, max scratch bytes per lane)
-    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb0EEEvNS_12AnalysisArgsE": (3, 0),   # tip7 block-by-block variant (A/B)
-    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb1EEEvNS_12AnalysisArgsE": (3, 0),   # tip7 headline (TIP layout, interleaved exponents)
-    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi0ELb0EEEvNS_12AnalysisArgsE": (3, 0),   # runtime band layout
+    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb1ELi1EEEvNS_12AnalysisArgsE": (3, 0),   # tip7 headline (TIP layout, fused forecast)
+    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb1ELi2EEEvNS_12AnalysisArgsE": (3, 0),   # spatial (+ regulariser prepare)
+    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb1ELi0EEEvNS_12AnalysisArgsE": (3, 0),   # generic TIP layout (first date)
+    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb0ELi0EEEvNS_12AnalysisArgsE": (3, 0),   # block-by-block variant (A/B)
+    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi0ELb0ELi0EEEvNS_12AnalysisArgsE": (3, 0),   # runtime band layout
     "_ZN2kf15analysis_kernelILi7ELi4ELi2ELi4ELb0EEEvNS_12AnalysisArgsE": (3, 0),           # TIP VALU loop
     "_ZN2kf15analysis_kernelILi7ELin2ELi4ELi4ELb0EEEvNS_12AnalysisArgsE": (3, 0),          # identity7 (bf16 y)
     # PROSAIL (55-float packed A per lane): 2 waves/SIMD, no scratch since the
