@@ -110,9 +110,11 @@ class PendingP2P:
 
 
 class Comm:
-    def __init__(self, rank: int = 0, world: int = 1, device=None, group=None, ranks=None, band=None):
+    def __init__(self, rank: int = 0, world: int = 1, device=None, group=None, ranks=None, band=None,
+                 forced: bool = False):
         self.rank = rank
         self.world = world
+        self.forced = forced   # KAFKA_FORCE_DIST: the collective code paths at world 1
         self.group = group
         self.ranks = list(ranks) if ranks is not None else list(range(world))   # global rank of each member
         self.band = band                                                       # band-parallel sub-comm (C5)
@@ -129,7 +131,12 @@ class Comm:
         """Initialise from torchrun env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*).
         ``band_parallel`` > 1 splits the world into strips x band groups."""
         world = int(os.environ.get("WORLD_SIZE", "1"))
-        if world <= 1 and not dist.is_initialized():
+        # KAFKA_FORCE_DIST=1: a one-rank job still initialises the process group
+        # and runs every collective through it (RCCL on a one-GPU box: the
+        # device code paths of C1/C3/C4 and the barrier, which several-rank
+        # runs need and gloo rehearsals do not take)
+        forced = os.environ.get("KAFKA_FORCE_DIST", "0") not in ("", "0")
+        if world <= 1 and not dist.is_initialized() and not forced:
             return cls.single(device)
         rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -151,7 +158,7 @@ class Comm:
         rank, world = dist.get_rank(), dist.get_world_size()
         B = int(band_parallel)
         if B <= 1:
-            return cls(rank, world, device)
+            return cls(rank, world, device, forced=forced and world == 1)
         if world % B:
             raise ValueError(f"world size {world} is not a multiple of band_parallel={B}")
         S = world // B
@@ -166,7 +173,7 @@ class Comm:
 
     @property
     def distributed(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.forced
 
     # ----------------------------------------------------- collectives
     def sum_f64(self, local: torch.Tensor) -> float:

@@ -212,6 +212,32 @@ def test_bench_torchrun_gloo_two_ranks(extra):
         assert len(r["gn_iterations"]) == 2
 
 
+@pytest.mark.parametrize("config", ["tip7", "spatial"])
+def test_forced_one_rank_process_group_equals_single_process(tmp_path, config):
+    """KAFKA_FORCE_DIST=1 under torch.distributed.run with one rank: the
+    collectives run through the process group (gloo here, RCCL on a GPU box,
+    tests/test_gpu.py) and the state equals the plain single-process run."""
+    args = ["--config", config, "--size", "64", "--n-train", "24", "--steps", "2", "--warmup", "1", "--device", "cpu"]
+    recs = []
+    for forced in (False, True):
+        env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
+        if forced:
+            env["KAFKA_FORCE_DIST"] = "1"
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                   "--master-addr=127.0.0.1", f"--master-port={_free_port()}"] + cmd[1:]
+        cmd += ["--dump-state", str(tmp_path / f"f{int(forced)}")]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        import json
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1
+        recs.append(json.loads(lines[0]))
+    assert recs[1]["dist"]["initialized"] and recs[1]["dist"]["world_size"] == 1
+    assert not recs[0]["dist"]["initialized"]
+    assert np.array_equal(np.load(tmp_path / "f0.strip0.npy"), np.load(tmp_path / "f1.strip0.npy"))
+
+
 SCALE_CASES = [("tip7", []), ("spatial", []), ("prosail10", []), ("identity7", []), ("multisensor", []),
                ("multisensor", ["--band-parallel", "2"])]
 

@@ -366,6 +366,46 @@ def test_identity_linear_fast_path_gpu_matches_cpu(cuda):
     assert close(outs[0][0], outs[1][0], 1e-4) and close(outs[0][1], outs[1][1], 1e-4, floor=1.0)
 
 
+@pytest.mark.parametrize("config", ["tip7", "spatial"])
+def test_bench_rccl_one_rank_equals_single_process(cuda, tmp_path, config):
+    """bench.py under torch.distributed.run with KAFKA_FORCE_DIST=1: a one-rank
+    job whose collectives (C1 all-gather of the norms, the per-rank record
+    gather, C4 broadcasts, device barriers) go through RCCL ("nccl") on the
+    GPU -- the code the driver's multi-GPU runs take and the gloo rehearsals
+    do not.  The final state equals the plain single-process run bit for bit."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = str(Path(__file__).resolve().parents[1])
+    args = [os.path.join(root, "bench.py"), "--config", config, "--size", "512", "--steps", "2", "--warmup", "1"]
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    recs = []
+    for forced in (False, True):
+        env = dict(os.environ, PYTHONPATH=root)
+        cmd = [sys.executable] + args
+        if forced:
+            env["KAFKA_FORCE_DIST"] = "1"
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                   "--master-addr=127.0.0.1", f"--master-port={port}"] + args
+        cmd += ["--dump-state", str(tmp_path / f"f{int(forced)}")]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=100, env=env, cwd=root)
+        assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, r.stdout[-2000:]
+        recs.append(json.loads(lines[0]))
+    assert recs[1]["dist"]["backend"] == "nccl" and recs[1]["dist"]["world_size"] == 1, recs[1]["dist"]
+    assert recs[0]["dist"]["initialized"] is False
+    a = np.load(tmp_path / "f0.strip0.npy")
+    b = np.load(tmp_path / "f1.strip0.npy")
+    assert np.array_equal(a, b)
+
+
 def test_checked_build_smoke_on_device(cuda):
     """The debug variant (KF_CHECKED index assertions in the gfx950 kernels) runs the
     smoke step on the GPU without a failed check."""
