@@ -98,13 +98,14 @@ def test_gp_mfma_analysis_vs_oracle_and_valu(cuda, case):
     scale = np.abs(xr) + 0.05
     err_m = np.max(np.abs(xm - xr) / scale)
     err_v = np.max(np.abs(xv - xr) / scale)
-    # SURVEY.md §7.3 asks 1e-4 relative on x against float64.  PROSAIL meets it;
-    # for TIP both f32 device paths sit at ~1.5e-4 (measured: MFMA 1.47e-4,
-    # VALU 1.73e-4), set by the f32 accumulation of the GP sums (H0 to ~3e-5
-    # of max|H0|, test_gp_mfma_operator_value_vs_float64) amplified on the
-    # small-magnitude TIP parameters -- the reference's own f32 cast of A, b
-    # (solvers.py:127-128) is at the same 1e-4 level
-    tol = 1e-4 if case == "prosail" else 2e-4
+    # SURVEY.md §7.3 asks 1e-4 relative on x against float64.  Both cases meet
+    # it on the matrix cores since the tables alternate the two alpha-sign
+    # groups (models/gp.py mfma_point_order: the f32 running sums stay near
+    # the result).  Measured: TIP MFMA 5.4e-5 (1.47e-4 with the sign groups
+    # one after the other), the f32 VALU record loop (grouped order) 1.73e-4;
+    # PROSAIL 1.5e-5 -- the reference's own f32 cast of A, b
+    # (solvers.py:127-128) is at the 1e-4 level
+    tol = 1e-4
     print(f"x err mfma {err_m:.2e} valu {err_v:.2e}")
     from kafka_inferenceengine_amd.utils.blocks import unpack_blocks
     n = prob["n"]
