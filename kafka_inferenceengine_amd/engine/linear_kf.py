@@ -339,78 +339,79 @@ class LinearKalman:
         precision-form forecast, return a :class:`LazyForecast` instead; the
         fused analysis kernel then computes the forecast per pixel and it is
         never written to memory."""
-        with self.timer.phase("propagate"):
-            prop = self._state_propagator
-            spec = getattr(prop, "device_spec", None) if prop is not None else None
-            prior_dev = self.prior.device_prior(date) if (self.prior is not None and
-                                                          hasattr(self.prior, "device_prior")) else None
-            if (prop is not None and spec is None) or (self.prior is not None and prior_dev is None):
+        # device passes are timed in _run_propagate / _advance_host ("propagate")
+        prop = self._state_propagator
+        spec = getattr(prop, "device_spec", None) if prop is not None else None
+        prior_dev = self.prior.device_prior(date) if (self.prior is not None and
+                                                      hasattr(self.prior, "device_prior")) else None
+        if (prop is not None and spec is None) or (self.prior is not None and prior_dev is None):
+            with self.timer.phase("propagate"):
                 return self._advance_host(analysis, date)
-            n = self.n_params
-            memo_key = (id(spec), id(prior_dev) if prior_dev is not None else None, id(self._m), id(self._q),
-                        bool(self.config.reference_quirks), self._analysis_kind(), analysis.kind)
-            memo = self._prop_dicts.get(memo_key)
-            if memo is not None and lazy:
-                # same propagator / prior / Q objects as an earlier step: reuse the
-                # (immutable) argument dict, so the fused argument block is reused too
-                kind, d = memo[0], memo[1]
-                if kind == "lazy":
-                    return self._lazy(d, self._as_kind(analysis, PRECISION), None)
-                if kind == "lazy_cov":
-                    return self._lazy_cov(d, analysis)
-            d = {"m": self._m, "q": self._q}
-            d["_key"] = memo_key
-            keep = (spec, prior_dev, self._m, self._q)
-            if prop is None and self.prior is None:
-                spec = PropagatorSpec(PROP_IDENTITY)
-            elif prop is None and prior_dev.constant:
-                # prior only (kf_tools.py:165-166): reset to the prior, no blend needed
-                d.update(mode=PROP_PRIOR, prop_mask=0, reset_mean=np.asarray(prior_dev.mean),
-                         reset_cinv=pack_matrix(np.asarray(prior_dev.cinv)))
-                if lazy and self._analysis_kind() == PRECISION and analysis.kind == PRECISION:
-                    self._remember_prop(memo_key, "lazy", d, keep)
-                    return self._lazy(d, analysis, None)
-                if lazy and analysis.kind == COVARIANCE:
-                    self._remember_prop(memo_key, "lazy_cov", d, keep)
-                    return self._lazy_cov(d, analysis)
-                out = self._run_propagate(d, analysis, None, PRECISION)
-                return self._as_kind(out, self._analysis_kind())
-            elif prop is None:
-                spec = PropagatorSpec(PROP_PRIOR, reset_mean=np.zeros(n), reset_cinv=np.zeros((n, n)))
-            d["mode"] = spec.mode
-            mask = 0
-            for k in spec.propagated:
-                mask |= 1 << int(k)
-            d["prop_mask"] = mask
-            if spec.reset_mean is not None:
-                d["reset_mean"] = np.asarray(spec.reset_mean)
-                d["reset_cinv"] = pack_matrix(np.asarray(spec.reset_cinv))
-            in_kind = COVARIANCE if spec.mode == PROP_STANDARD else PRECISION
-            out_kind = COVARIANCE if spec.output == "covariance" else PRECISION
-            if (lazy and self.prior is None and in_kind == PRECISION and out_kind == PRECISION
-                    and analysis.kind == COVARIANCE and self._analysis_kind() == COVARIANCE):
-                # gain form: the K1g kernel evaluates this forecast from the analysis covariance
+        n = self.n_params
+        memo_key = (id(spec), id(prior_dev) if prior_dev is not None else None, id(self._m), id(self._q),
+                    bool(self.config.reference_quirks), self._analysis_kind(), analysis.kind)
+        memo = self._prop_dicts.get(memo_key)
+        if memo is not None and lazy:
+            # same propagator / prior / Q objects as an earlier step: reuse the
+            # (immutable) argument dict, so the fused argument block is reused too
+            kind, d = memo[0], memo[1]
+            if kind == "lazy":
+                return self._lazy(d, self._as_kind(analysis, PRECISION), None)
+            if kind == "lazy_cov":
+                return self._lazy_cov(d, analysis)
+        d = {"m": self._m, "q": self._q}
+        d["_key"] = memo_key
+        keep = (spec, prior_dev, self._m, self._q)
+        if prop is None and self.prior is None:
+            spec = PropagatorSpec(PROP_IDENTITY)
+        elif prop is None and prior_dev.constant:
+            # prior only (kf_tools.py:165-166): reset to the prior, no blend needed
+            d.update(mode=PROP_PRIOR, prop_mask=0, reset_mean=np.asarray(prior_dev.mean),
+                     reset_cinv=pack_matrix(np.asarray(prior_dev.cinv)))
+            if lazy and self._analysis_kind() == PRECISION and analysis.kind == PRECISION:
+                self._remember_prop(memo_key, "lazy", d, keep)
+                return self._lazy(d, analysis, None)
+            if lazy and analysis.kind == COVARIANCE:
                 self._remember_prop(memo_key, "lazy_cov", d, keep)
                 return self._lazy_cov(d, analysis)
-            src = self._as_kind(analysis, in_kind)
-            blend_pix = (None, None)
-            if self.prior is not None:
-                if out_kind == COVARIANCE:
-                    # covariance-form propagator + prior: blend in precision form afterwards
-                    fc = self._run_propagate(d, src, None, COVARIANCE)
-                    fc = self._as_kind(fc, PRECISION)
-                    d2 = {"mode": PROP_IDENTITY, "m": np.ones(n), "q": np.zeros(n)}
-                    self._fill_blend(d2, prior_dev)
-                    out = self._run_propagate(d2, fc, self._blend_pix(prior_dev), PRECISION)
-                    return self._as_kind(out, self._analysis_kind())
-                self._fill_blend(d, prior_dev)
-                blend_pix = self._blend_pix(prior_dev)
-            if lazy and out_kind == PRECISION and self._analysis_kind() == PRECISION:
-                if blend_pix == (None, None) and src.kind == PRECISION:
-                    self._remember_prop(memo_key, "lazy", d, keep)
-                return self._lazy(d, src, blend_pix)
-            out = self._run_propagate(d, src, blend_pix, out_kind)
+            out = self._run_propagate(d, analysis, None, PRECISION)
             return self._as_kind(out, self._analysis_kind())
+        elif prop is None:
+            spec = PropagatorSpec(PROP_PRIOR, reset_mean=np.zeros(n), reset_cinv=np.zeros((n, n)))
+        d["mode"] = spec.mode
+        mask = 0
+        for k in spec.propagated:
+            mask |= 1 << int(k)
+        d["prop_mask"] = mask
+        if spec.reset_mean is not None:
+            d["reset_mean"] = np.asarray(spec.reset_mean)
+            d["reset_cinv"] = pack_matrix(np.asarray(spec.reset_cinv))
+        in_kind = COVARIANCE if spec.mode == PROP_STANDARD else PRECISION
+        out_kind = COVARIANCE if spec.output == "covariance" else PRECISION
+        if (lazy and self.prior is None and in_kind == PRECISION and out_kind == PRECISION
+                and analysis.kind == COVARIANCE and self._analysis_kind() == COVARIANCE):
+            # gain form: the K1g kernel evaluates this forecast from the analysis covariance
+            self._remember_prop(memo_key, "lazy_cov", d, keep)
+            return self._lazy_cov(d, analysis)
+        src = self._as_kind(analysis, in_kind)
+        blend_pix = (None, None)
+        if self.prior is not None:
+            if out_kind == COVARIANCE:
+                # covariance-form propagator + prior: blend in precision form afterwards
+                fc = self._run_propagate(d, src, None, COVARIANCE)
+                fc = self._as_kind(fc, PRECISION)
+                d2 = {"mode": PROP_IDENTITY, "m": np.ones(n), "q": np.zeros(n)}
+                self._fill_blend(d2, prior_dev)
+                out = self._run_propagate(d2, fc, self._blend_pix(prior_dev), PRECISION)
+                return self._as_kind(out, self._analysis_kind())
+            self._fill_blend(d, prior_dev)
+            blend_pix = self._blend_pix(prior_dev)
+        if lazy and out_kind == PRECISION and self._analysis_kind() == PRECISION:
+            if blend_pix == (None, None) and src.kind == PRECISION:
+                self._remember_prop(memo_key, "lazy", d, keep)
+            return self._lazy(d, src, blend_pix)
+        out = self._run_propagate(d, src, blend_pix, out_kind)
+        return self._as_kind(out, self._analysis_kind())
 
     def cache_stats(self) -> dict:
         """Host-side reuse counters (band tables, fused-argument blocks)."""
@@ -423,11 +424,8 @@ class LinearKalman:
         self._prop_dicts[key] = (kind, d, keep)
 
     def _lazy(self, d, src: KFState, blend_pix):
-        timer = self.timer
-
         def materialize():
-            with timer.phase("propagate"):
-                return self._run_propagate(d, src, blend_pix, PRECISION)
+            return self._run_propagate(d, src, blend_pix, PRECISION)
         if not K.prop_is_light(d["mode"], d.get("blend", False)):
             return materialize()
         return LazyForecast(src, d, blend_pix, self._q_pix, materialize, cache=self._prop_bufs)
@@ -437,11 +435,8 @@ class LinearKalman:
         held as a covariance, evaluated per pixel by the K1g kernel
         (kf_core.h:forecast_partial_cov) instead of invert + propagate + invert
         passes; other consumers materialise it through those passes."""
-        timer = self.timer
-
         def materialize():
-            with timer.phase("propagate"):
-                out = self._run_propagate(d, self._as_kind(src, PRECISION), None, PRECISION)
+            out = self._run_propagate(d, self._as_kind(src, PRECISION), None, PRECISION)
             return self._as_kind(out, COVARIANCE)
         if not K.prop_is_light(d["mode"], d.get("blend", False)):
             return materialize()
@@ -466,8 +461,9 @@ class LinearKalman:
         out = KFState.empty(self.n_params, self.N, self.device, out_kind, ld=src.x.shape[1])
         bm, bc = blend_pix if blend_pix else (None, None)
         if self.N:
-            K.propagate(self.n_params, d, src.x, src.P, out.x, out.P, N=self.N, q_pix=self._q_pix,
-                        blend_mean_pix=bm, blend_cinv_pix=bc)
+            with self.timer.phase("propagate"):
+                K.propagate(self.n_params, d, src.x, src.P, out.x, out.P, N=self.N, q_pix=self._q_pix,
+                            blend_mean_pix=bm, blend_cinv_pix=bc)
         return out
 
     def _advance_host(self, analysis: KFState, date) -> KFState:
@@ -1426,10 +1422,11 @@ class LinearKalman:
     def _dump(self, timestep, state: KFState):
         if self.output is None:
             return
+        if getattr(self, "_output_written", None) is state:
+            # written by the analysis kernel: bookkeeping only (no device work to time)
+            self.output.mark_written(timestep, state, self)
+            return
         with self.timer.phase("output"):
-            if getattr(self, "_output_written", None) is state:
-                self.output.mark_written(timestep, state, self)   # written by the analysis kernel
-                return
             if hasattr(self.output, "dump_state"):
                 self.output.dump_state(timestep, state, self)
                 return

@@ -61,6 +61,7 @@ class PhaseTimer:
         self.sync = sync
         self.enabled = bool(enabled or sync)
         self._pending = []
+        self._free = []                        # resolved event pairs, re-recorded (no hipEventCreate per phase)
         self.totals = defaultdict(float)
         self.run_totals = defaultdict(float)   # over the whole run (snapshots reset `totals`)
 
@@ -72,8 +73,12 @@ class PhaseTimer:
     @contextlib.contextmanager
     def _phase(self, name: str):
         if self.cuda:
-            s = torch.cuda.Event(enable_timing=True)
-            e = torch.cuda.Event(enable_timing=True)
+            if not self._free and len(self._pending) > 32:
+                self._reap()
+            if self._free:
+                s, e = self._free.pop()
+            else:
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             try:
                 yield
@@ -89,6 +94,17 @@ class PhaseTimer:
             finally:
                 self.totals[name] += 1e3 * (time.perf_counter() - t0)
 
+    def _reap(self):
+        """Account the oldest pending phases whose end event has completed
+        (non-blocking query) and recycle their event pairs."""
+        done = 0
+        while done < len(self._pending) and done < 32 and self._pending[done][2].query():
+            name, s, e = self._pending[done]
+            self.totals[name] += s.elapsed_time(e)
+            self._free.append((s, e))
+            done += 1
+        del self._pending[:done]
+
     def cumulative(self) -> dict:
         """Per-phase ms over the whole run (pending events included)."""
         cur = self.snapshot(reset=True)
@@ -100,6 +116,7 @@ class PhaseTimer:
             self._pending[-1][2].synchronize()
             for name, s, e in self._pending:
                 self.totals[name] += s.elapsed_time(e)
+                self._free.append((s, e))
             self._pending = []
         out = {k: round(v, 3) for k, v in self.totals.items()}
         if reset:

@@ -1,7 +1,8 @@
-"""Per-step host-time breakdown of the identity7 engine loop (wall time of the
-main engine methods; --noop replaces the kernels by no-ops to isolate Python).
+"""Per-step host-time breakdown of the identity7 (default) or tip7 (--tip7)
+engine loop (wall time of the main engine methods; --noop replaces the
+kernels by no-ops to isolate Python).
 
-    SIZE=1024 python scripts/host_breakdown.py [--noop]
+    SIZE=1024 python scripts/host_breakdown.py [--noop] [--tip7]
 """
 import os, sys, time, datetime as dt, collections, functools
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
@@ -37,14 +38,40 @@ from kafka_inferenceengine_amd.inference import iterate_time_grid
 SIZE = int(os.environ.get("SIZE", "1024" if torch.cuda.is_available() else "32"))
 DEV = "cuda" if torch.cuda.is_available() else "cpu"
 mask = np.ones((SIZE, SIZE), bool)
-dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(400)]
-obs = k.SyntheticIdentityObservations(mask, dates=dates, device=DEV, n_pool=3, stream=True, cloud_fraction=0.2)
-kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_linear_observation_operator,
+TIP = "--tip7" in sys.argv
+NSTEP = int(os.environ.get("NSTEP", "400" if not TIP else "60"))
+dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(NSTEP)]
+if TIP:
+    obs = k.SyntheticBHRObservations(mask, dates=dates, device=DEV, n_pool=3, stream=True, cloud_fraction=0.2,
+                                     n_train=500)
+    fac = k.create_nonlinear_observation_operator
+else:
+    obs = k.SyntheticIdentityObservations(mask, dates=dates, device=DEV, n_pool=3, stream=True, cloud_fraction=0.2)
+    fac = k.create_linear_observation_operator
+kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, fac,
                     k.TIP_PARAMETERS, state_propagation=k.propagate_information_filter_LAI)
 wrap(kf.comm, "sum_f64_async", "comm.sum_f64_async")
 import kafka_inferenceengine_amd.parallel.comm as CM
 for cls in [c for c in vars(CM).values() if isinstance(c, type) and hasattr(c, "result")]:
     wrap(cls, "result", f"{cls.__name__}.result (host wait)")
+# host latency from the last norm read-back of a date to the next analysis launch
+_last = [None]
+def _mark(obj, name):
+    fn = getattr(obj, name)
+    @functools.wraps(fn)
+    def w(*a, **kw):
+        try: return fn(*a, **kw)
+        finally: _last[0] = time.perf_counter()
+    setattr(obj, name, w)
+for cls in [c for c in vars(CM).values() if isinstance(c, type) and hasattr(c, "result")]:
+    _mark(cls, "result")
+_an = K.analysis
+def _an_w(*a, **kw):
+    if _last[0] is not None:
+        acc["readback -> next analysis launch"] += time.perf_counter() - _last[0]; cnt["readback -> next analysis launch"] += 1
+        _last[0] = None
+    return _an(*a, **kw)
+K.analysis = _an_w
 kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
 state = kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask))
 grid = [dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in dates]
@@ -54,13 +81,15 @@ def run(lo, hi, st):
         t, loc, first = steps[i]
         st = kf.step(t, loc, st, advance=i > 0, all_dates=dates)
     return st
-state = run(0, 20, state); acc.clear(); cnt.clear()
+W = NSTEP // 20
+state = run(0, W, state); acc.clear(); cnt.clear()
 if DEV == "cuda":
     torch.cuda.synchronize()
-t0 = time.perf_counter(); state = run(20, 380, state)
+M = NSTEP - 2 * W
+t0 = time.perf_counter(); state = run(W, W + M, state)
 if DEV == "cuda":
     torch.cuda.synchronize()
-T = (time.perf_counter() - t0) / 360 * 1e6
+T = (time.perf_counter() - t0) / M * 1e6
 print(f"step {T:.0f} us")
-for k_, v in acc.most_common(): print(f"{k_:34s} {v/360*1e6:7.1f} us/step  ({cnt[k_]/360:.1f} calls)")
+for k_, v in acc.most_common(): print(f"{k_:34s} {v/M*1e6:7.1f} us/step  ({cnt[k_]/M:.1f} calls)")
 print("caches", kf.cache_stats())
