@@ -130,7 +130,7 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
 // (gp_mfma_sums_g): many-band GP states (PROSAIL: ten bands, 358-716 KiB of
 // tables) whose tables exceed the LDS.  No LDS, so the waves per SIMD follow
 // the VGPR count alone.
-template <int NP, int D, int FOBS, bool PF = false, bool IL = false>
+template <int NP, int D, int FOBS, bool PF = false, bool IL = false, int SPEC = SPEC_ANY>
 __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   KF_PHASE_KERNEL_BEGIN
@@ -141,8 +141,8 @@ __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs 
     const int64_t p = base + lane;
     const bool act = p < a.N;
     float dn1;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, true, PF, BAND_LAYOUT_RUNTIME, IL>(a, act ? p : a.N - 1, act,
-                                                                                         nullptr, dn1 KF_PHASE_ARG);
+    const float dn = pixel_analysis_mfma<NP, D, FOBS, true, PF, BAND_LAYOUT_RUNTIME, IL, SPEC>(
+        a, act ? p : a.N - 1, act, nullptr, dn1 KF_PHASE_ARG);
     acc += act ? (double)dn : 0.0;
     acc1 += act ? (double)dn1 : 0.0;
   }
@@ -518,6 +518,11 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
         // the default leaves the latency to the other wave
         if (a.fast_obs == OBS_DN16 && a.variant == 7)
           hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, true>), dim3(grid), dim3(BLOCK), 0, s, a);
+        else if (a.fast_obs == OBS_DN16 && a.prop && !a.reg_v && a.variant == 0 &&
+                 gpm_il_default<NP, BAND_LAYOUT_RUNTIME>())
+          // fused forecast, no regulariser: the launch's paths fixed at compile time (SPEC_PROP)
+          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, false, true, SPEC_PROP>), dim3(grid), dim3(BLOCK),
+                             0, s, a);
         else if (a.fast_obs == OBS_DN16 && (a.variant == 16) != gpm_il_default<NP, BAND_LAYOUT_RUNTIME>())
           hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, false, true>), dim3(grid), dim3(BLOCK), 0, s, a);
         else if (a.fast_obs == OBS_DN16)

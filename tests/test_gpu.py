@@ -290,6 +290,31 @@ def test_fused_spatial_first_iteration_equals_separate_launches_gpu(cuda):
         assert torch.equal(ha[t][0], hb[t][0]) and torch.equal(ha[t][1], hb[t][1])
 
 
+def test_specialised_prosail_kernel_equals_generic_gpu(cuda):
+    """PROSAIL (global-table matrix-core kernel) with the fused forecast: the
+    SPEC_PROP kernel gives the same bits as the generic one (variant 18)."""
+    from kafka_inferenceengine_amd.ops import kernels as K
+    mask = np.ones((64, 80), bool)
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=5 * i) for i in range(4)]
+    outs = []
+    old = K.DEFAULT_VARIANT
+    try:
+        for variant in (0, 18):
+            K.DEFAULT_VARIANT = variant
+            obs = k.SyntheticS2Observations(mask, dates=grid, n_bands=10, n_train=250, device=cuda, stream=False,
+                                            n_pool=2)
+            prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
+            kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
+                                state_propagation=None, prior=prior, device=cuda)
+            st = kf.run([grid[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in grid],
+                        kf.state_from_prior(prior), None, None)
+            outs.append((st.x.cpu(), st.P.cpu(), [h.get("norms") for h in kf.history]))
+    finally:
+        K.DEFAULT_VARIANT = old
+    assert outs[0][2] == outs[1][2]
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("spatial", [False, True])
 def test_specialised_tip_kernel_equals_generic_gpu(cuda, spatial):
     """The JRC-TIP kernels specialised for the fused forecast (SPEC_PROP, and

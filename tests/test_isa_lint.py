@@ -55,8 +55,9 @@ HOT = {   # kernel: (min waves per SIMD, max scratch bytes per lane)
     "_ZN2kf15analysis_kernelILi7ELin2ELi4ELi4ELb0EEEvNS_12AnalysisArgsE": (3, 0),          # identity7 (bf16 y)
     # PROSAIL (55-float packed A per lane): 2 waves/SIMD, no scratch since the
     # epilogue stores use SGPR row bases (kf_core.h pxp; was 36 B, 2.5 % slower)
-    "_ZN2kf22analysis_mfma_g_kernelILi10ELi10ELi2ELb0ELb0EEEvNS_12AnalysisArgsE": (2, 0),
-    "_ZN2kf22analysis_mfma_g_kernelILi10ELi10ELi2ELb0ELb1EEEvNS_12AnalysisArgsE": (2, 0),
+    "_ZN2kf22analysis_mfma_g_kernelILi10ELi10ELi2ELb0ELb0ELi0EEEvNS_12AnalysisArgsE": (2, 0),
+    "_ZN2kf22analysis_mfma_g_kernelILi10ELi10ELi2ELb0ELb1ELi0EEEvNS_12AnalysisArgsE": (2, 0),
+    "_ZN2kf22analysis_mfma_g_kernelILi10ELi10ELi2ELb0ELb1ELi1EEEvNS_12AnalysisArgsE": (2, 0),   # prosail10 (fused forecast)
 }
 
 
