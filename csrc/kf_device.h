@@ -132,6 +132,7 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
 // the VGPR count alone.
 template <int NP, int D, int FOBS, bool PF = false, bool IL = false, int SPEC = SPEC_ANY>
 __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs a) {
+  static_assert(BLOCK / 64 == GPM_G_WAVES, "per-wave LDS transpose buffers of gp_mfma_sums_g_xb");
 #if defined(__HIP_DEVICE_COMPILE__)
   KF_PHASE_KERNEL_BEGIN
   double acc = 0.0, acc1 = 0.0;

@@ -60,6 +60,9 @@ KF_HD constexpr int gpm_frags_per_chunk(int D) { return 64 * gpm_k_steps(D) + 4 
 constexpr int GPM_MAX_D = 10;
 // bands whose sums are held across the record loops (larger tables fall back to VALU)
 constexpr int GPM_MAX_BANDS = 4;
+// waves per workgroup of the global-table kernels (analysis_mfma_g_kernel,
+// BLOCK = 256): the sizes of their per-wave LDS transpose buffers
+constexpr int GPM_G_WAVES = 4;
 
 #if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ uint32_t gpm_pack(_Float16 a, _Float16 b) {
@@ -154,6 +157,46 @@ __device__ __forceinline__ void gpm_extract2(const kf_f16v (&acc)[2], float (&S)
     const float recv = gpm_partner32(send);
     S[f] = (((f >> 2) & 1) == (h1 ? 1 : 0)) ? own : recv;
   }
+}
+
+// gpm_extract2 through LDS, for the global-table kernels (whose LDS is
+// otherwise unused): each lane adds its own hi and lo rows (the same adds) and
+// stores its fields of both column blocks, [block][column][field], then reads
+// its own pixel's D + 1 fields back -- 2 G ds_write_b128 + ceil((D+1)/4)
+// ds_read_b128 per band instead of ~6 VALU per field (own/partner selects and
+// the wave-half swap).  Bit-identical to gpm_extract2.  LDS of one wave: the
+// ds ops of a wave execute in order, so the wave barriers (no instruction:
+// they only stop the compiler moving the accesses across) suffice.
+template <int D>
+__device__ __forceinline__ void gpm_extract_lds(const kf_f16v (&acc)[2], float (&S)[D + 1], float* wbuf) {
+  constexpr int LR = gpm_lo_row(D) / 2;
+  constexpr int G = (D + 1 + 7) / 8;   // 8-row groups holding fields 0..D
+  const int lane = threadIdx.x & 63, n = lane & 31, q = lane >> 5;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      // fields 8g + 4q + i of column n sit in register 4g + i (hi row) and
+      // 4g + i + LR (lo row) of this lane
+      f4 v;
+      v.x = acc[blk][4 * g + 0] + acc[blk][4 * g + 0 + LR];
+      v.y = acc[blk][4 * g + 1] + acc[blk][4 * g + 1 + LR];
+      v.z = acc[blk][4 * g + 2] + acc[blk][4 * g + 2 + LR];
+      v.w = acc[blk][4 * g + 3] + acc[blk][4 * g + 3 + LR];
+      *(f4*)(wbuf + (blk * 32 + n) * 16 + 8 * g + 4 * q) = v;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  const f4* src = (const f4*)(wbuf + (q * 32 + n) * 16);   // own pixel 32 q + n: column n of block q
+#pragma unroll
+  for (int f4i = 0; f4i < (D + 4) / 4; ++f4i) {
+    const f4 v = src[f4i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (4 * f4i + i <= D) S[4 * f4i + i] = v[i];
+  }
+  __builtin_amdgcn_wave_barrier();
 }
 
 // m = 2^e for 8 accumulator registers, split into f16 hi (round toward zero)
@@ -347,7 +390,9 @@ __device__ __forceinline__ void gp_mfma_sums_g_xb(const void* tab_, int nchunk, 
   KF_DCHECK(nchunk >= 1);
   step(0, std::true_type{});
   for (int ch = 1; ch < nchunk; ++ch) step(ch, std::false_type{});
-  gpm_extract2<D>(acc, S);
+  __shared__ float gpm_xbuf[GPM_G_WAVES * 2 * 32 * 16];
+  KF_DCHECK((int)(threadIdx.x >> 6) < GPM_G_WAVES);
+  gpm_extract_lds<D>(acc, S, gpm_xbuf + (threadIdx.x >> 6) * (2 * 32 * 16));
   const float s = kexp2(cl);
 #pragma unroll
   for (int f = 0; f <= D; ++f) S[f] *= s;
