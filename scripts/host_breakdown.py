@@ -20,14 +20,16 @@ if "--noop" in sys.argv:      # host-only: kernels replaced by no-ops (CPU)
 import kafka_inferenceengine_amd as k
 import kafka_inferenceengine_amd.engine.linear_kf as L
 import kafka_inferenceengine_amd.engine.state as S
-acc = collections.Counter(); cnt = collections.Counter()
+acc = collections.Counter(); cnt = collections.Counter(); mx = collections.Counter()
 def wrap(obj, name, label=None):
     fn = getattr(obj, name); label = label or name
     @functools.wraps(fn)
     def w(*a, **kw):
         t = time.perf_counter()
         try: return fn(*a, **kw)
-        finally: acc[label] += time.perf_counter() - t; cnt[label] += 1
+        finally:
+            dt_ = time.perf_counter() - t
+            acc[label] += dt_; cnt[label] += 1; mx[label] = max(mx[label], dt_)
     setattr(obj, name, w)
 for nm in ["advance_state", "_device_bands", "_prepare_date", "do_all_bands_state", "_dump", "_assimilate_dates"]:
     wrap(L.LinearKalman, nm)
@@ -76,10 +78,18 @@ kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
 state = kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask))
 grid = [dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in dates]
 steps = list(iterate_time_grid(grid, dates))
+import gc
+_gc = []
+gc.callbacks.append(lambda phase, info: _gc.append((phase, info.get("generation"), time.perf_counter())))
+step_t = []
 def run(lo, hi, st):
     for i in range(lo, hi):
         t, loc, first = steps[i]
+        t0_ = time.perf_counter()
+        segs = torch.cuda.memory_stats().get("segment.all.allocated", 0) if DEV == "cuda" else 0
         st = kf.step(t, loc, st, advance=i > 0, all_dates=dates)
+        segs2 = torch.cuda.memory_stats().get("segment.all.allocated", 0) if DEV == "cuda" else 0
+        step_t.append((i, time.perf_counter() - t0_, segs2 - segs))
     return st
 W = NSTEP // 20
 state = run(0, W, state); acc.clear(); cnt.clear()
@@ -91,5 +101,8 @@ if DEV == "cuda":
     torch.cuda.synchronize()
 T = (time.perf_counter() - t0) / M * 1e6
 print(f"step {T:.0f} us")
-for k_, v in acc.most_common(): print(f"{k_:34s} {v/M*1e6:7.1f} us/step  ({cnt[k_]/M:.1f} calls)")
+for k_, v in acc.most_common(): print(f"{k_:34s} {v/M*1e6:7.1f} us/step  ({cnt[k_]/M:.1f} calls, max {mx[k_]*1e6:.0f} us)")
+slow = sorted(step_t, key=lambda r: -r[1])[:5]
+print("slowest steps (index, ms, new allocator segments):", [(i, round(t_ * 1e3, 2), sg) for i, t_, sg in slow])
+print("gc events in the timed steps:", len(_gc))
 print("caches", kf.cache_stats())

@@ -238,6 +238,29 @@ def test_forced_one_rank_process_group_equals_single_process(tmp_path, config):
     assert np.array_equal(np.load(tmp_path / "f0.strip0.npy"), np.load(tmp_path / "f1.strip0.npy"))
 
 
+def _comm_one_rank(env):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "comm_one_rank.py")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=dict(env, KAFKA_FORCE_DIST="1"), cwd=ROOT)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    import json
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["sum_f64"] == 1.25 and out["sum_f64_async"] == [0.5, 2.0] and out["sum_int"] == 7
+    assert out["max_float"] == 3.5 and out["all_reduce"] == [0.0, 1.0, 2.0, 3.0, 4.0, 5.0]
+    assert out["broadcast_packed"] == [[["k", 3]], [0.0, 1.0, 2.0]] and out["broadcast_object"] == {"a": 1}
+    assert out["gather_object"] == [{"r": 0}] and out["gather_to_root"] == [2, 3]
+    return out
+
+
+def test_comm_collectives_one_rank_process_group():
+    """Every Comm collective through a one-rank process group (gloo here;
+    tests/test_gpu.py runs the same script over RCCL on the device)."""
+    out = _comm_one_rank(dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES=""))
+    assert out["backend"] == "gloo"
+
+
 SCALE_CASES = [("tip7", []), ("spatial", []), ("prosail10", []), ("identity7", []), ("multisensor", []),
                ("multisensor", ["--band-parallel", "2"])]
 

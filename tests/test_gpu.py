@@ -431,6 +431,22 @@ def test_bench_rccl_one_rank_equals_single_process(cuda, tmp_path, config):
     assert np.array_equal(a, b)
 
 
+def test_comm_collectives_one_rank_rccl(cuda):
+    """Every Comm collective (C1 sums, band all-reduce, C3 gather, C4
+    broadcasts, object gathers, device barrier, empty C2 batch) through a
+    one-rank RCCL process group with device tensors."""
+    import os
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent))
+    from test_distributed import _comm_one_rank
+
+    root = str(Path(__file__).resolve().parents[1])
+    out = _comm_one_rank(dict(os.environ, PYTHONPATH=root))
+    assert out["backend"] == "nccl" and out["device"].startswith("cuda"), out
+
+
 def test_checked_build_smoke_on_device(cuda):
     """The debug variant (KF_CHECKED index assertions in the gfx950 kernels) runs the
     smoke step on the GPU without a failed check."""
