@@ -55,6 +55,11 @@ class HostRing {
       }
     }
     for (int t = 0; t < std::max(1, n_threads); ++t) workers_.emplace_back([this] { work(); });
+    if (device_) {
+      done_seq_.assign(n_slots, 0);
+      want_seq_.assign(n_slots, 0);
+      submitter_ = std::thread([this] { submit_loop(); });
+    }
   }
 
   ~HostRing() {
@@ -64,6 +69,15 @@ class HostRing {
     }
     cv_.notify_all();
     for (auto& t : workers_) t.join();
+    if (submitter_.joinable()) {
+      {
+        std::lock_guard<std::mutex> g(sub_mu_);
+        sub_stop_ = true;
+      }
+      sub_cv_.notify_all();
+      submitter_.join();
+    }
+    for (hipEvent_t e : dep_pool_) (void)hipEventDestroy(e);
     for (size_t i = 0; i < slots_.size(); ++i) {
       if (device_ && events_[i]) {
         (void)hipEventSynchronize(events_[i]);
@@ -153,14 +167,44 @@ class HostRing {
     if (hipEventRecord(events_[s], st) != hipSuccess) throw std::runtime_error("HostRing: hipEventRecord failed");
   }
 
+  // h2d from a dedicated submitter thread: the copy follows everything queued
+  // on after_stream so far (an event recorded here, on the calling thread)
+  // and is issued on copy_stream by the submitter.  hipMemcpyAsync can block
+  // its calling thread for milliseconds (a one-off runtime stall of ~6 ms on
+  // MI355X, scripts/probes/copy_stall_probe.py); issued here it blocks the
+  // submitter, not the thread that launches the next kernel.  stream_wait /
+  // host_wait of the slot first wait (on the host) until the copy is issued.
+  void h2d_async(int s, uintptr_t dst, size_t nbytes, size_t slot_off, uintptr_t copy_stream,
+                 uintptr_t after_stream) {
+    if (!device_) {
+      h2d(s, dst, nbytes, slot_off, copy_stream);
+      return;
+    }
+    check_range(s, slot_off, nbytes);
+    wait_reads(s);
+    hipEvent_t dep = take_dep_event();
+    if (hipEventRecord(dep, reinterpret_cast<hipStream_t>(after_stream)) != hipSuccess)
+      throw std::runtime_error("HostRing: hipEventRecord failed");
+    {
+      std::lock_guard<std::mutex> g(sub_mu_);
+      SubmitJob j{s, dst, nbytes, slot_off, copy_stream, dep, ++sub_seq_};
+      want_seq_[s] = j.seq;
+      sub_q_.push_back(j);
+    }
+    sub_cv_.notify_one();
+  }
+
   void stream_wait(int s, uintptr_t stream) {
     if (!device_) return;
+    wait_submitted(s);
     if (hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), events_.at(s), 0) != hipSuccess)
       throw std::runtime_error("HostRing: hipStreamWaitEvent failed");
   }
 
   void host_wait(int s) {
-    if (device_) (void)hipEventSynchronize(events_.at(s));
+    if (!device_) return;
+    wait_submitted(s);
+    (void)hipEventSynchronize(events_.at(s));
   }
 
   void write_slot(int s, py::buffer b, size_t slot_off) {
@@ -175,6 +219,69 @@ class HostRing {
     if (s < 0 || s >= (int)slots_.size()) throw std::runtime_error("HostRing: bad slot");
     if (off + n > slot_bytes_) throw std::runtime_error("HostRing: range exceeds slot");
   }
+  struct SubmitJob {
+    int s;
+    uintptr_t dst;
+    size_t nbytes, slot_off;
+    uintptr_t stream;
+    hipEvent_t dep;
+    uint64_t seq;
+  };
+
+  hipEvent_t take_dep_event() {
+    {
+      std::lock_guard<std::mutex> g(sub_mu_);
+      if (!dep_free_.empty()) {
+        hipEvent_t e = dep_free_.back();
+        dep_free_.pop_back();
+        return e;
+      }
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      throw std::runtime_error("HostRing: hipEventCreate failed");
+    std::lock_guard<std::mutex> g(sub_mu_);
+    dep_pool_.push_back(e);
+    return e;
+  }
+
+  void wait_submitted(int s) {
+    std::unique_lock<std::mutex> lk(sub_mu_);
+    sub_done_cv_.wait(lk, [&] { return done_seq_.at(s) >= want_seq_.at(s); });
+    if (!sub_error_.empty()) {
+      std::string e = sub_error_;
+      sub_error_.clear();
+      throw std::runtime_error("HostRing: " + e);
+    }
+  }
+
+  void submit_loop() {
+    for (;;) {
+      SubmitJob j;
+      {
+        std::unique_lock<std::mutex> lk(sub_mu_);
+        sub_cv_.wait(lk, [this] { return sub_stop_ || !sub_q_.empty(); });
+        if (sub_q_.empty()) return;
+        j = sub_q_.front();
+        sub_q_.pop_front();
+      }
+      hipStream_t st = reinterpret_cast<hipStream_t>(j.stream);
+      std::string err;
+      if (hipStreamWaitEvent(st, j.dep, 0) != hipSuccess) err = "hipStreamWaitEvent failed";
+      else if (hipMemcpyAsync(reinterpret_cast<void*>(j.dst), slots_[j.s] + j.slot_off, j.nbytes,
+                              hipMemcpyHostToDevice, st) != hipSuccess)
+        err = "hipMemcpyAsync failed";
+      else if (hipEventRecord(events_[j.s], st) != hipSuccess) err = "hipEventRecord failed";
+      {
+        std::lock_guard<std::mutex> g(sub_mu_);
+        dep_free_.push_back(j.dep);   // the wait above has taken the record it needs
+        done_seq_[j.s] = std::max(done_seq_[j.s], j.seq);
+        if (!err.empty()) sub_error_ = err;
+      }
+      sub_done_cv_.notify_all();
+    }
+  }
+
   void work() {
     for (;;) {
       std::function<void()> job;
@@ -198,6 +305,16 @@ class HostRing {
   std::mutex mu_, err_mu_;
   std::condition_variable cv_;
   std::deque<std::function<void()>> q_;
+  // h2d_async submitter
+  std::thread submitter_;
+  std::mutex sub_mu_;
+  std::condition_variable sub_cv_, sub_done_cv_;
+  std::deque<SubmitJob> sub_q_;
+  std::vector<uint64_t> done_seq_, want_seq_;
+  uint64_t sub_seq_ = 0;
+  bool sub_stop_ = false;
+  std::string sub_error_;
+  std::vector<hipEvent_t> dep_pool_, dep_free_;
   std::vector<std::thread> workers_;
 };
 
@@ -214,7 +331,8 @@ void bind_stream(py::module_& m) {
       .def("read_tiff_async", &HostRing::read_tiff_async)
       .def("wait_reads", &HostRing::wait_reads, py::call_guard<py::gil_scoped_release>())
       .def("h2d", &HostRing::h2d)
-      .def("stream_wait", &HostRing::stream_wait)
+      .def("h2d_async", &HostRing::h2d_async)
+      .def("stream_wait", &HostRing::stream_wait, py::call_guard<py::gil_scoped_release>())
       .def("host_wait", &HostRing::host_wait, py::call_guard<py::gil_scoped_release>())
       .def("write_slot", &HostRing::write_slot);
 }

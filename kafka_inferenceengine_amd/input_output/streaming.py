@@ -73,6 +73,18 @@ class DateStreamer:
             self.ring.h2d(r % self.n_pool, self.bufs[b].data_ptr(), self.entry_bytes, 0, int(self.stream.cuda_stream))
             self.ring.stream_wait(r % self.n_pool, int(cur.cuda_stream))
         torch.cuda.synchronize(self.device)
+        # then the steady-state cycle itself (acquire one date, prefetch the next
+        # n_bufs - 1, a short kernel): the runtime stalls one hipMemcpyAsync of
+        # this pattern for ~6 ms once per process, a few cycles in (probe:
+        # scripts/probes/copy_stall_probe.py) -- here, not in the time steps
+        for r in range(12):
+            buf = self.acquire(r % self.n_pool, key=("warm", r))
+            for j in range(1, self.n_bufs):
+                self.prefetch((r + j) % self.n_pool, key=("warm", r + j))
+            scratch.mul_(0.5)
+            scratch[:1].add_(buf.reshape(-1)[:1].float())
+        torch.cuda.synchronize(self.device)
+        self._current = None
         del scratch
         self._inflight = []
         self.loaded = [None] * self.n_bufs
@@ -109,9 +121,11 @@ class DateStreamer:
             # runtime's command backlog grow until it stalls for milliseconds
             while len(self._inflight) >= self.n_bufs - 1:
                 self.ring.host_wait(self._inflight.pop(0))
-            # the buffer's previous consumer is everything queued so far on the compute stream
-            self.stream.wait_stream(torch.cuda.current_stream(self.device))
-            self.ring.h2d(k, dst.data_ptr(), self.entry_bytes, 0, int(self.stream.cuda_stream))
+            # the buffer's previous consumer is everything queued so far on the
+            # compute stream; the copy itself is issued by the ring's submitter
+            # thread (hipMemcpyAsync can stall its caller for milliseconds)
+            self.ring.h2d_async(k, dst.data_ptr(), self.entry_bytes, 0, int(self.stream.cuda_stream),
+                                int(torch.cuda.current_stream(self.device).cuda_stream))
             self._inflight.append(k)
         else:
             self.ring.h2d(k, dst.data_ptr(), self.entry_bytes, 0, 0)
