@@ -158,6 +158,29 @@ def test_engine_gpu_matches_cpu_and_oracle(cuda):
     assert np.max(np.abs(Ps - Po) / (np.abs(Po).max(axis=1, keepdims=True) + 1e-6)) < 2e-3
 
 
+def test_streamer_async_copies_keep_stream_order(cuda):
+    """DateStreamer copies issued by the HostRing submitter thread (h2d_async)
+    under running kernels: every acquired buffer holds its own date's entry,
+    and no copy overwrites a buffer a queued kernel still reads (each step's
+    kernel reduces the acquired buffer after a slow kernel in front of it)."""
+    from kafka_inferenceengine_amd.input_output.streaming import DateStreamer
+    s = DateStreamer(3, (4, 1 << 18), torch.int16, cuda, n_bufs=3)
+    for kk in range(3):
+        s.host_view(kk).fill_(kk + 1)
+    s.warm()
+    x = torch.ones(1 << 22, device=cuda)
+    sums = []
+    for i in range(30):
+        buf = s.acquire(i % 3, key=i)
+        s.prefetch((i + 1) % 3, key=i + 1)
+        s.prefetch((i + 2) % 3, key=i + 2)
+        for _ in range(20):
+            x.mul_(1.0000001)       # keep the compute stream busy ahead of the read
+        sums.append(buf.float().sum())
+    got = [int(v.item()) for v in sums]
+    assert got == [((i % 3) + 1) * 4 * (1 << 18) for i in range(30)]
+
+
 def test_streamer_pinned_and_overlaps(cuda):
     from kafka_inferenceengine_amd.input_output.streaming import DateStreamer
     s = DateStreamer(3, (2, 1 << 20), torch.int16, cuda)
