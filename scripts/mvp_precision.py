@@ -33,7 +33,7 @@ def main():
         runs.append(("cpu", 0))
     for dev, v in runs:
         K.DEFAULT_VARIANT = v
-        r = mvp(torch.device("cuda", 0) if dev == "cuda" else "cpu", a.size, n_dates=a.n_dates)
+        r = mvp(torch.device("cuda", 0) if dev == "cuda" else "cpu", a.size, n_dates=a.n_dates, progress=True)
         r.update(device=dev, variant=v)
         print(json.dumps(r), flush=True)
 

@@ -34,7 +34,7 @@ def _rel(a, b):
     return np.abs(a - b).max(1) / (np.abs(b).max(1) + 1e-12)
 
 
-def mvp(device, size, n_dates=10, n_train=500):
+def mvp(device, size, n_dates=10, n_train=500, progress=False):
     """Run the engine and the float64 block oracle; returns the per-date drift
     records and the final (x, packed P) errors."""
     mask = np.ones((size, size), bool)
@@ -58,7 +58,9 @@ def mvp(device, size, n_dates=10, n_train=500):
     steps = []
     xo, Ao, iters = oracle_run_blocks(obs, mask, k.TIP_BAND_MAPPER, grid, mu, ci, q=[0, 0, 0, 0, 0, 0, Q6],
                                       x0=jp.mean, A0=jp.inv_covar,
-                                      on_step=lambda t, x, A: steps.append((t, x.copy(), A.copy())))
+                                      on_step=lambda t, x, A: (steps.append((t, x.copy(), A.copy())),
+                                                               progress and print(f"oracle {t.date()} done",
+                                                                                  flush=True)))
     drift = []
     for t, x, A in steps:
         mean, unc = out.history[t]
@@ -72,10 +74,22 @@ def mvp(device, size, n_dates=10, n_train=500):
     Po = pack_blocks(Ao).astype(np.float64)
     if Po.shape != Ps.shape:
         Po = Po.T
-    x_err = float(_rel(st.x[:, :N].cpu().numpy().astype(np.float64), xo.T).max())
+    xs = st.x[:, :N].cpu().numpy().astype(np.float64)
+    x_err = float(_rel(xs, xo.T).max())
     p_err = float(_rel(Ps, Po).max())
+    # per-pixel view: max over parameters of |dx| / max|x_param| -- how many
+    # pixels carry the tail of the max-norm error, and their status flags
+    pix = (np.abs(xs - xo.T) / (np.abs(xo.T).max(1, keepdims=True) + 1e-12)).max(0)
+    status = kf.last_status[:N].cpu().numpy() if getattr(kf, "last_status", None) is not None else None
+    worst = np.argsort(-pix)[:5]
+    tail = {"p50": float(np.percentile(pix, 50)), "p99": float(np.percentile(pix, 99)),
+            "p99.9": float(np.percentile(pix, 99.9)), "p99.99": float(np.percentile(pix, 99.99)),
+            "n_over_5e-4": int((pix > 5e-4).sum()), "n_over_1e-3": int((pix > 1e-3).sum()),
+            "worst": [{"pixel": int(i), "rel": float(pix[i]), "status": None if status is None else int(status[i]),
+                       "x": [round(float(v), 5) for v in xs[:, i]], "x_oracle": [round(float(v), 5) for v in xo[i]]}
+                      for i in worst]}
     return {"size": size, "n_dates": n_dates, "n_train": n_train, "gn": gn, "gn_oracle": iters,
-            "x_rel": x_err, "P_rel": p_err, "drift": drift}
+            "x_rel": x_err, "P_rel": p_err, "pixel_tail": tail, "drift": drift}
 
 
 def test_block_oracle_equals_reference_api_oracle():
