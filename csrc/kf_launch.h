@@ -9,10 +9,13 @@
 #include <hip/hip_runtime_api.h>
 #endif
 
-// Grid cap for the grid-stride kernels: 256 CUs x 8 resident blocks x 8
-// (A/B, scripts/gpu_grid.sh: 16384 is 3 % faster than 4096 at 15M and 120M px;
-// more blocks finish closer together, one pixel per thread is slower).
-#define KF_MAX_BLOCKS 16384
+// Grid cap for the grid-stride kernels (A/B, scripts/gpu_grid.sh: 16384 is 3 %
+// faster than 4096 at 15M and 120M px; round 4, scripts/gpu_r4_v22.sh at 120M
+// px: 768 persistent blocks 45.6 ms, 16384 42.2, 32768-131072 41.9, one pixel
+// per thread 42.8 -- the cloud skip makes blocks uneven, so more blocks finish
+// closer together, up to the point where the per-block LDS table staging and
+// dispatch cost more).
+#define KF_MAX_BLOCKS 65536
 
 namespace kf {
 
