@@ -117,6 +117,7 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(AnalysisArgs, status, uint8_t*)
       .PTR_FIELD(AnalysisArgs, partials, double*)
       .PTR_FIELD(AnalysisArgs, partials_first, double*)
+      .PTR_FIELD(AnalysisArgs, order, const int32_t*)
       .def_readwrite("gn_fused", &AnalysisArgs::gn_fused)
       .def_readwrite("band_layout", &AnalysisArgs::band_layout)
       .PTR_FIELD(AnalysisArgs, prop, const PropArgs*)
@@ -280,6 +281,16 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
                      int64_t src_ld, int64_t dst_ld, uintptr_t stream) {
     check_hip(dev_gather(elem_bytes, P<const void>(src), P<const int64_t>(idx), P<void>(dst), n, rows, src_ld,
                          dst_ld, (hipStream_t)stream), "gather");
+  });
+  // pixels with an observation in any band first (AnalysisArgs.order);
+  // counts: obs_order_chunks(N) + 1 int32 scratch (device only)
+  m.def("obs_order_chunks", &obs_order_chunks);
+  m.def("obs_order", [](uintptr_t bands, int nb, int64_t N, uintptr_t counts, uintptr_t order, bool device,
+                        uintptr_t stream) {
+    if (N > (int64_t)INT32_MAX) throw std::runtime_error("obs_order: N exceeds int32");
+    if (device) check_hip(dev_obs_order(P<const BandDesc>(bands), nb, N, P<int32_t>(counts), P<int32_t>(order),
+                                        (hipStream_t)stream), "obs_order");
+    else host_obs_order(P<const BandDesc>(bands), nb, N, P<int32_t>(order));
   });
   m.def("lut_nearest", [](uintptr_t lut, int M, int D, uintptr_t x, int64_t N, int64_t ld, uintptr_t out,
                           bool device, uintptr_t stream) {

@@ -265,11 +265,19 @@ struct AnalysisArgs {
   // selecting a kernel with the band loop unrolled over fixed maps; 0: runtime
   int32_t band_layout;
   double* partials_first;  // per-block sum (x_1 - x_0)^2 of the first fused iteration
+  // pixel visiting order (null: 0..N-1): the pixels with an observation first
+  // (obs_order), so cloudy pixels fill whole waves that skip the GP -- the
+  // emulator runs on observed pixels only, as in the reference's operator
+  // (utils.py:130-170, run_emulator on x0[mask])
+  const int32_t* order;
 };
 
 
 // ---------------------------------------------------------------------------
 // small helpers
+
+// Pixel of visiting slot q under AnalysisArgs.order (null: the identity).
+KF_HD int64_t visit_px(const int32_t* order, int64_t q) { return order ? (int64_t)order[q] : q; }
 template <int NP>
 KF_HD float gather_state(const float (&x)[NP], int idx) {
   float v = x[0];
@@ -512,6 +520,17 @@ KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y_out, float& w_out)
   }
   y_out = y;
   w_out = w;
+}
+
+// Does pixel p have an observation in any band (obs_order)?
+KF_HD bool any_obs(const BandDesc* bands, int nb, int64_t p) {
+  bool any = false;
+  for (int b = 0; b < nb && !any; ++b) {
+    float y, w;
+    decode_obs<0>(bands[b], p, y, w);
+    any = w > 0.f;
+  }
+  return any;
 }
 
 // ---------------------------------------------------------------------------

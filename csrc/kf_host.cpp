@@ -44,9 +44,9 @@ static int h_analysis(const AnalysisArgs& a, int grid) {
   for (int b = 0; b < grid; ++b) {
     double acc = 0.0, acc1 = 0.0;
     for (int t = 0; t < HBLOCK; ++t)
-      for (int64_t p = (int64_t)b * HBLOCK + t; p < a.N; p += stride) {
+      for (int64_t q = (int64_t)b * HBLOCK + t; q < a.N; q += stride) {
         float dn1;
-        acc += (double)pixel_analysis<NP>(a, p, dn1);
+        acc += (double)pixel_analysis<NP>(a, visit_px(a.order, q), dn1);
         acc1 += (double)dn1;
       }
     if (a.partials) a.partials[b] = acc;
@@ -173,6 +173,14 @@ int host_hessian(int np, const BandDesc* b, int nb, const float* x, float* a, in
 int host_unpack(int np, const float* x, const float* a, int64_t N, int64_t ld, const int64_t* idx, float* mean,
                 float* unc, int64_t plane) {
   KF_HOST_NP_SWITCH(np, h_unpack, x, a, N, ld, idx, mean, unc, plane);
+}
+int host_obs_order(const BandDesc* bands, int nb, int64_t N, int32_t* order) {
+  int64_t k = 0;
+  for (int64_t p = 0; p < N; ++p)
+    if (any_obs(bands, nb, p)) order[k++] = (int32_t)p;
+  for (int64_t p = 0; p < N; ++p)
+    if (!any_obs(bands, nb, p)) order[k++] = (int32_t)p;
+  return 0;
 }
 int host_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out) {
 #pragma omp parallel for schedule(static)

@@ -45,6 +45,10 @@ class EngineConfig:
     # pass and no coupled solve saved per date (False: both iterations coupled,
     # the first to spatial_tol_first)
     spatial_first_plain: bool = True
+    # visit the pixels with an observation first (obs_order): cloudy pixels then
+    # fill whole waves that skip the GP emulator (the reference runs it on the
+    # observed pixels only); each pixel's analysis is unchanged
+    observed_first: bool = True
     spatial_max_sweeps: int = 64
     # one field on a dense strip without halo rows (one rank, or no strip
     # neighbours): up to 8 sweeps per launch out of LDS (kf_reg_tiled.hip),

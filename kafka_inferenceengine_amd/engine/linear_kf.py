@@ -30,7 +30,7 @@ from ..inference.kf_tools import (PROP_IDENTITY, PROP_PRIOR, PROP_STANDARD, Prop
                                   propagate_and_blend_prior, propagate_information_filter_LAI)
 from ..inference.solvers import variational_kalman, variational_kalman_multiband
 from ..inference.utils import iterate_time_grid
-from ..models.operators import OP_LINEAR, OP_PRECOMP, OperatorSpec
+from ..models.operators import OP_GP, OP_LINEAR, OP_PRECOMP, OperatorSpec
 from ..ops import kernels as K
 from ..parallel.comm import Comm
 from ..parallel.partition import StripPartition
@@ -140,6 +140,8 @@ class LinearKalman:
         self._prepared = None           # (date, bands, table) made by it
         self._lazy_norms = []           # (norms, pending 1, pending 2, len_x, n_bands) of static convergence
         self._reg_log = []              # per GN iteration of the spatial prior: rho, sweeps, residual
+        self._order_bufs = None         # (order, scratch) of obs_order, reused across dates
+        self._visit = None              # this date's pixel visiting order (config.observed_first)
         self._split_chunk = {}          # split path: bands per chunk, per band count
         self._reg = None
         self._reg_uv = None             # affine regulariser: u = A_reg^-1 b, V = A_reg^-1 E_R, x0
@@ -774,6 +776,15 @@ class LinearKalman:
         # iteration 1 exactly and its norm is 0 -- converged without a read-back
         static_conv = (fuse2 and cfg.convergence_tolerance > 0 and bool(specs)
                        and all(s.kind == OP_LINEAR for s in specs))
+        # observed pixels first (config.observed_first): one order per date for
+        # every analysis launch of it (GP bands on the fused kernels only)
+        order = None
+        if (cfg.observed_first and table is not None and N and not (gain or precomp or split or bp)
+                and any(s.kind == OP_GP for s in specs)):
+            buf, scratch = self._order_bufs if self._order_bufs is not None else (None, None)
+            order, scratch = K.obs_order(table, N, self.device, buf, scratch)
+            self._order_bufs = (order if buf is None or buf.numel() < N else buf, scratch)
+        self._visit = order
         # spatial prior: a plain first iteration (config.spatial_first_plain; it
         # cannot end the loop), fused with the regularised prepare of the second
         first_plain = spatial and cfg.spatial_first_plain and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
@@ -798,7 +809,7 @@ class LinearKalman:
                             K.analysis(n, table, x_prev, None if prop is not None else fc.x,
                                        None if prop is not None else fc.P, x_new, P_out, None, status,
                                        self._partials, N=N, prop=prop, out=out_t, gn_fused=2,
-                                       partials_first=self._partials1)
+                                       partials_first=self._partials1, order=order)
                         K.reduce_partials(self._partials1, red2[0:1])
                         K.reduce_partials(self._partials, red2[1:2])
                     else:
@@ -831,7 +842,7 @@ class LinearKalman:
                             # the unfused form of fuse_sp's first iteration (same kernel path)
                             K.analysis(n, table, x_prev, None if prop is not None else fc.x,
                                        None if prop is not None else fc.P, x_new, None, None, status,
-                                       self._partials, N=N, prop=prop)
+                                       self._partials, N=N, prop=prop, order=order)
                             self._reg_log.append({"solver": "plain", "rho": 0.0, "sweeps": 0, "r2": None,
                                                   "count": 0})
                         elif cfg.spatial_gamma > 0:
@@ -843,10 +854,10 @@ class LinearKalman:
                             self._split_iteration(split, x_prev, fc, x_new, A_keep, status)
                         elif prop is not None:
                             K.analysis(n, table, x_prev, None, None, x_new, A_keep, None, status, self._partials, N=N,
-                                       prop=prop, out=out_now)
+                                       prop=prop, out=out_now, order=order)
                         else:
                             K.analysis(n, table, x_prev, fc.x, fc.P, x_new, A_keep, None, status, self._partials, N=N,
-                                       out=out_now)
+                                       out=out_now, order=order)
                 red = self._red_hist[min(n_iter, self._red_hist.numel() - 1):][:1]
                 with self.timer.phase("analysis"):
                     if N:
@@ -941,7 +952,7 @@ class LinearKalman:
     # ------------------------------------------------ split GP operator path
     def _split_plan_kind(self, specs):
         """GP input count d when these bands take the split path, else None."""
-        from ..models.operators import OP_GP
+
         cfg = self.config
         if cfg.gp_split == "never" or not specs or any(s.kind != OP_GP for s in specs):
             return None
@@ -1051,7 +1062,7 @@ class LinearKalman:
         fused = partials_first is not None
         if not rows:   # nothing regularised: plain analysis
             K.analysis(n, table, x_prev, fx, fP, x_out, A_out, None, status, self._partials, N=N, prop=prop, out=out,
-                       gn_fused=2 if fused else 1, partials_first=partials_first)
+                       gn_fused=2 if fused else 1, partials_first=partials_first, order=self._visit)
             return
         k = len(rows)
         ld = x_out.shape[1]
@@ -1066,7 +1077,7 @@ class LinearKalman:
                    reg=dict(gamma=gamma, mask=reg.reg_mask, v_out=v, nbr=None if geo else reg.nbr, geo=geo),
                    x0_out=None if x_ref is x_prev else x0_buf,
                    out=None if out is None else (None, out[1], out[2]),
-                   gn_fused=2 if fused else 1, partials_first=partials_first)
+                   gn_fused=2 if fused else 1, partials_first=partials_first, order=self._visit)
         if fused:
             self._reg_log.append({"solver": "plain", "rho": 0.0, "sweeps": 0, "r2": None, "count": 0})
         nbr = None if geo else reg.nbr

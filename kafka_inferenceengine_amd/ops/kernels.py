@@ -224,7 +224,7 @@ def gp_operator_supported(n_params, d) -> bool:
 
 def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=None, b_out=None, status=None,
              partials=None, N=None, solve=True, fast=True, variant=None, a_in=None, b_in=None, prop=None,
-             out=None, reg=None, x0_out=None, gn_fused=1, partials_first=None):
+             out=None, reg=None, x0_out=None, gn_fused=1, partials_first=None, order=None):
     """K1 fused Gauss-Newton analysis (information form).
 
     ``gn_fused=2`` runs two Gauss-Newton iterations in this launch: the first
@@ -247,7 +247,12 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     receives the linearisation point (the fused forecast when x_prev is None).
     With ``gn_fused=2`` the first iteration is the plain solve (its norm to
     ``partials_first``) and the regulariser prepares the second, linearised
-    at x_1 (written to ``x0_out``)."""
+    at x_1 (written to ``x0_out``).
+
+    ``order`` (int32 [N], from :func:`obs_order`): the pixel visiting order --
+    the observed pixels first, so cloudy pixels fill whole waves that skip the
+    GP; each pixel's result is the same in any order (the per-workgroup norm
+    partials sum different pixel sets)."""
     check_np(n_params)
     ref = next(t for t in (x_prev, x_f, x_out, a_out) if t is not None)
     N = int(ref.shape[1] if N is None else N)
@@ -344,9 +349,28 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
                 raise ValueError(f"dense geometry {geo} does not cover N={N} pixels")
             a.geo_w, a.geo_h, a.geo_halo, a.geo_n_up = int(geo["w"]), int(geo["h"]), int(geo["halo"]), \
                 int(geo["n_up"])
+    if order is not None:
+        _check_vec(order, N, "order", torch.int32, dev)
+        a.order = _ptr(order)
     grid = grid_for(N)
     ext().analysis(n_params, a, grid, _dev(ref), _stream(ref))
     return partials
+
+
+def obs_order(bands: BandTable, N: int, device, out=None, scratch=None):
+    """Stable partition of the pixels 0..N-1: those with an observation in any
+    band of ``bands`` first (``AnalysisArgs.order``).  ``out`` int32 [>= N],
+    ``scratch`` int32 [>= obs_order_chunks(N) + 1] (device) may be reused."""
+    dev = torch.device(device)
+    N = int(N)
+    if out is None or out.numel() < N:
+        out = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
+    nc = int(ext().obs_order_chunks(N)) + 1
+    if dev.type == "cuda" and (scratch is None or scratch.numel() < nc):
+        scratch = torch.empty(nc, dtype=torch.int32, device=dev)
+    ext().obs_order(bands.ptr, bands.n, N, _ptr(scratch), _ptr(out), dev.type == "cuda",
+                    int(torch.cuda.current_stream(dev).cuda_stream) if dev.type == "cuda" else 0)
+    return out[:N], scratch
 
 
 def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status=None, partials=None, N=None,

@@ -366,6 +366,53 @@ def test_fused_gn_iterations_equal_separate_launches(tol):
         assert torch.equal(oa.history[t][0], ob.history[t][0]) and torch.equal(oa.history[t][1], ob.history[t][1])
 
 
+@pytest.mark.parametrize("spatial", [False, True])
+def test_observed_first_order_keeps_every_pixel(spatial):
+    """EngineConfig.observed_first: the pixels with an observation are visited
+    first (obs_order, a stable partition), so cloudy pixels fill whole waves
+    that skip the GP.  Every pixel's analysis is unchanged: states and output
+    rasters equal the natural order's bit for bit, and the GN counts match
+    (the norms sum the per-workgroup partials of other pixel sets)."""
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=11)
+    grid = _grid(5)
+    reg = dict(spatial_gamma=5.0, spatial_params=[6]) if spatial else {}
+    res = []
+    for on in (False, True):
+        out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
+        kf = _engine(mask, obs, Q, out=out, observed_first=on, **reg)
+        st = kf.run(grid, x0, None, Pinv)
+        res.append((st, out, [h["gn_iterations"] for h in kf.history], kf._visit))
+    (a, oa, ia, va), (b, ob, ib, vb) = res
+    assert va is None and vb is not None
+    assert ia == ib
+    assert torch.equal(a.x, b.x) and torch.equal(a.P, b.P)
+    for t in oa.history:
+        assert torch.equal(oa.history[t][0], ob.history[t][0]) and torch.equal(oa.history[t][1], ob.history[t][1])
+
+
+def test_obs_order_is_a_stable_partition():
+    """obs_order on the host: observed pixels (any band w > 0) first, each
+    group in increasing pixel order, a permutation of 0..N-1."""
+    from kafka_inferenceengine_amd.ops import kernels as K
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=12)
+    kf = _engine(mask, obs, Q)
+    date = obs.dates[0]
+    bands = kf._device_bands(date)
+    from kafka_inferenceengine_amd.engine.bands import build_table
+    table = build_table([s for s, _ in bands], [d for _, d in bands], kf.n_params, kf._cache, kf.device)
+    order, _ = K.obs_order(table, kf.N, kf.device)
+    o = order.numpy()
+    seen = np.zeros(kf.N, bool)
+    for db in (d for _, d in bands):
+        y, w = db.decode()
+        seen |= (w[:kf.N] > 0).numpy()
+    n_obs = int(seen.sum())
+    assert sorted(o.tolist()) == list(range(kf.N))
+    assert seen[o[:n_obs]].all() and not seen[o[n_obs:]].any()
+    assert (np.diff(o[:n_obs]) > 0).all() and (np.diff(o[n_obs:]) > 0).all()
+    assert 0 < n_obs < kf.N
+
+
 @pytest.mark.parametrize("tol", [1e-3, 1e-9])
 def test_fused_spatial_first_iteration_equals_separate_launches(tol):
     """Spatial prior with spatial_first_plain: the plain first Gauss-Newton

@@ -158,6 +158,63 @@ def test_engine_gpu_matches_cpu_and_oracle(cuda):
     assert np.max(np.abs(Ps - Po) / (np.abs(Po).max(axis=1, keepdims=True) + 1e-6)) < 2e-3
 
 
+@pytest.mark.parametrize("config", ["tip7", "spatial", "prosail"])
+def test_observed_first_order_equals_natural_order_gpu(cuda, config):
+    """EngineConfig.observed_first on the device (matrix-core kernels, obs_order
+    kernels): every pixel's state, precision and output raster equal the
+    natural visiting order's bit for bit, GN counts equal."""
+    mask = np.ones((96, 160), bool)
+    mask[5:20, 30:70] = False
+    outs = []
+    for on in (False, True):
+        out = k.DeviceOutput(k.TIP_PARAMETERS if config != "prosail" else k.SAIL_PARAMETERS, keep_history=True)
+        if config == "prosail":
+            grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=5 * i) for i in range(4)]
+            obs = k.SyntheticS2Observations(mask, dates=grid, n_bands=10, n_train=250, device=cuda, stream=False,
+                                            n_pool=2)
+            prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
+            kf = k.LinearKalman(obs, out, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
+                                state_propagation=None, prior=prior, device=cuda,
+                                config=k.EngineConfig(observed_first=on))
+            st = kf.run([grid[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in grid],
+                        kf.state_from_prior(prior), None, None)
+        else:
+            grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
+            obs = k.SyntheticBHRObservations(mask, n_train=500, device=cuda, stream=False, n_pool=3, field_cell=8)
+            reg = dict(spatial_gamma=5.0, spatial_params=[6]) if config == "spatial" else {}
+            kf = k.LinearKalman(obs, out, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS,
+                                device=cuda, state_propagation=k.propagate_information_filter_LAI,
+                                config=k.EngineConfig(observed_first=on, **reg))
+            kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+            st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
+        assert (kf._visit is not None) == on
+        outs.append((st.x.cpu(), st.P.cpu(), [h.get("gn_iterations") for h in kf.history],
+                     {t: (m.cpu(), u.cpu()) for t, (m, u) in out.history.items()}))
+    (xa, Pa, ia, ha), (xb, Pb, ib, hb) = outs
+    assert ia == ib
+    assert torch.equal(xa, xb) and torch.equal(Pa, Pb)
+    for t in ha:
+        assert torch.equal(ha[t][0], hb[t][0]) and torch.equal(ha[t][1], hb[t][1])
+
+
+def test_obs_order_device_equals_host(cuda):
+    """The three obs_order kernels (count, scan, scatter) give the host
+    runner's stable partition, on a tile spanning many 4096-pixel chunks."""
+    from kafka_inferenceengine_amd.engine.bands import build_table
+    from kafka_inferenceengine_amd.ops import kernels as K
+    mask = np.ones((700, 330), bool)
+    mask[100:180, :] = False
+    res = []
+    for dev in (cuda, torch.device("cpu")):
+        obs = k.SyntheticBHRObservations(mask, n_train=40, device=dev, stream=False, n_pool=1, field_cell=8)
+        kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device=dev)
+        bands = kf._device_bands(obs.dates[0])
+        table = build_table([s for s, _ in bands], [d for _, d in bands], kf.n_params, kf._cache, kf.device)
+        order, _ = K.obs_order(table, kf.N, kf.device)
+        res.append(order.cpu())
+    assert torch.equal(res[0], res[1])
+
+
 def test_streamer_async_copies_keep_stream_order(cuda):
     """DateStreamer copies issued by the HostRing submitter thread (h2d_async)
     under running kernels: every acquired buffer holds its own date's entry,
