@@ -282,15 +282,18 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
     check_hip(dev_gather(elem_bytes, P<const void>(src), P<const int64_t>(idx), P<void>(dst), n, rows, src_ld,
                          dst_ld, (hipStream_t)stream), "gather");
   });
-  // pixels with an observation in any band first (AnalysisArgs.order);
-  // counts: obs_order_chunks(N) + 1 int32 scratch (device only)
+  // stable partition by observation class (AnalysisArgs.order); grp: band
+  // group per band (null: one group), G groups (1..3); counts: (chunks * 2^G
+  // + 1) int32 scratch (device only)
   m.def("obs_order_chunks", &obs_order_chunks);
-  m.def("obs_order", [](uintptr_t bands, int nb, int64_t N, uintptr_t counts, uintptr_t order, bool device,
-                        uintptr_t stream) {
+  m.def("obs_order", [](uintptr_t bands, uintptr_t grp, int nb, int G, int64_t N, uintptr_t counts, uintptr_t order,
+                        bool device, uintptr_t stream) {
     if (N > (int64_t)INT32_MAX) throw std::runtime_error("obs_order: N exceeds int32");
-    if (device) check_hip(dev_obs_order(P<const BandDesc>(bands), nb, N, P<int32_t>(counts), P<int32_t>(order),
-                                        (hipStream_t)stream), "obs_order");
-    else host_obs_order(P<const BandDesc>(bands), nb, N, P<int32_t>(order));
+    if (G < 1 || G > 3) throw std::runtime_error("obs_order: 1 to 3 band groups");
+    if (device) check_hip(dev_obs_order(P<const BandDesc>(bands), P<const int32_t>(grp), nb, G, N, P<int32_t>(counts),
+                                        P<int32_t>(order), (hipStream_t)stream), "obs_order");
+    else if (host_obs_order(P<const BandDesc>(bands), P<const int32_t>(grp), nb, G, N, P<int32_t>(order)) != 0)
+      throw std::runtime_error("obs_order failed");
   });
   m.def("lut_nearest", [](uintptr_t lut, int M, int D, uintptr_t x, int64_t N, int64_t ld, uintptr_t out,
                           bool device, uintptr_t stream) {

@@ -522,15 +522,19 @@ KF_HD void decode_obs(const BandDesc& bd, int64_t p, float& y_out, float& w_out)
   w_out = w;
 }
 
-// Does pixel p have an observation in any band (obs_order)?
-KF_HD bool any_obs(const BandDesc* bands, int nb, int64_t p) {
-  bool any = false;
-  for (int b = 0; b < nb && !any; ++b) {
+// obs_order class of pixel p: the band groups (grp[b], null: one group) with
+// an observation at p, as a bit mask, mapped so that class 0 is "observed in
+// every group" and class 2^G - 1 "in none".
+KF_HD int obs_class(const BandDesc* bands, const int32_t* grp, int nb, int G, int64_t p) {
+  int key = 0;
+  for (int b = 0; b < nb; ++b) {
+    const int g = grp ? grp[b] : 0;
+    if ((key >> g) & 1) continue;
     float y, w;
     decode_obs<0>(bands[b], p, y, w);
-    any = w > 0.f;
+    if (w > 0.f) key |= 1 << g;
   }
-  return any;
+  return ((1 << G) - 1) - key;
 }
 
 // ---------------------------------------------------------------------------

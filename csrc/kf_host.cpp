@@ -174,12 +174,15 @@ int host_unpack(int np, const float* x, const float* a, int64_t N, int64_t ld, c
                 float* unc, int64_t plane) {
   KF_HOST_NP_SWITCH(np, h_unpack, x, a, N, ld, idx, mean, unc, plane);
 }
-int host_obs_order(const BandDesc* bands, int nb, int64_t N, int32_t* order) {
+int host_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int G, int64_t N, int32_t* order) {
+  if (G < 1 || G > 3) return -1;
+  std::vector<uint8_t> cls((size_t)N);
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < N; ++p) cls[p] = (uint8_t)obs_class(bands, grp, nb, G, p);
   int64_t k = 0;
-  for (int64_t p = 0; p < N; ++p)
-    if (any_obs(bands, nb, p)) order[k++] = (int32_t)p;
-  for (int64_t p = 0; p < N; ++p)
-    if (!any_obs(bands, nb, p)) order[k++] = (int32_t)p;
+  for (int c = 0; c < (1 << G); ++c)
+    for (int64_t p = 0; p < N; ++p)
+      if (cls[p] == c) order[k++] = (int32_t)p;
   return 0;
 }
 int host_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out) {

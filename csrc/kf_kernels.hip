@@ -119,99 +119,111 @@ int get_max_blocks() { return g_max_blocks; }
 int dev_grid(int64_t N) { return grid_for(N, g_max_blocks); }
 
 // ---------------------------------------------------------------------------
-// obs_order: a stable partition of 0..N-1, pixels with an observation in any
-// band first (AnalysisArgs.order).  Chunks of ORD_CHUNK pixels: count the
-// observed pixels per chunk, scan the counts (one workgroup), scatter with a
-// workgroup-wide ballot prefix per 256-pixel tile.
+// obs_order: a stable partition of 0..N-1 by observation class (obs_class:
+// pixels observed in every band group first, unobserved last), so each class
+// fills whole waves and a wave skips the GP of the groups it has no data for
+// (AnalysisArgs.order).  Chunks of ORD_CHUNK pixels: class counts per chunk,
+// a scan per class (one workgroup), a scatter with a workgroup-wide ballot
+// prefix per class and 256-pixel tile.
 constexpr int ORD_CHUNK = 4096;
+constexpr int ORD_MAX_CLASSES = 8;   // <= 3 band groups
 
-__global__ __launch_bounds__(BLOCK) void obs_count_kernel(const BandDesc* bands, int nb, int64_t N, int32_t* counts) {
-  __shared__ int red[BLOCK / 64];
-  const int64_t c0 = (int64_t)blockIdx.x * ORD_CHUNK;
-  int n = 0;
-  for (int64_t p = c0 + threadIdx.x; p < N && p < c0 + ORD_CHUNK; p += BLOCK) n += any_obs(bands, nb, p) ? 1 : 0;
-  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = n;
+__global__ __launch_bounds__(BLOCK) void obs_count_kernel(const BandDesc* bands, const int32_t* grp, int nb, int G,
+                                                          int64_t N, int32_t* counts) {
+  __shared__ int red[ORD_MAX_CLASSES];
+  const int K = 1 << G;
+  if (threadIdx.x < ORD_MAX_CLASSES) red[threadIdx.x] = 0;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-    for (int i = 0; i < BLOCK / 64; ++i) t += red[i];
-    counts[blockIdx.x] = t;
+  const int64_t c0 = (int64_t)blockIdx.x * ORD_CHUNK;
+  int n[ORD_MAX_CLASSES] = {};
+  for (int64_t p = c0 + threadIdx.x; p < N && p < c0 + ORD_CHUNK; p += BLOCK) ++n[obs_class(bands, grp, nb, G, p)];
+  for (int c = 0; c < K; ++c) {
+    int v = n[c];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&red[c], v);   // LDS atomics
   }
+  __syncthreads();
+  if (threadIdx.x < K) counts[(int64_t)blockIdx.x * K + threadIdx.x] = red[threadIdx.x];
 }
 
-// exclusive scan of counts[0..nc) in place; counts[nc] = total
-__global__ __launch_bounds__(1024) void obs_scan_kernel(int32_t* counts, int nc) {
+// counts [nc][K] -> exclusive slot offsets in place (class c's pixels start
+// after every pixel of the classes before it); counts[nc * K] = N
+__global__ __launch_bounds__(1024) void obs_scan_kernel(int32_t* counts, int nc, int K) {
   __shared__ int part[1024];
+  __shared__ int cbase;
   const int per = (nc + 1023) / 1024;
   const int i0 = threadIdx.x * per, i1 = min(nc, i0 + per);
-  int s = 0;
-  for (int i = i0; i < i1; ++i) s += counts[i];
-  part[threadIdx.x] = s;
+  if (threadIdx.x == 0) cbase = 0;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int run = 0;
-    for (int i = 0; i < 1024; ++i) {
-      const int v = part[i];
-      part[i] = run;
+  for (int c = 0; c < K; ++c) {
+    int s = 0;
+    for (int i = i0; i < i1; ++i) s += counts[(int64_t)i * K + c];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int run = cbase;
+      for (int i = 0; i < 1024; ++i) {
+        const int v = part[i];
+        part[i] = run;
+        run += v;
+      }
+      cbase = run;
+    }
+    __syncthreads();
+    int run = part[threadIdx.x];
+    for (int i = i0; i < i1; ++i) {
+      const int v = counts[(int64_t)i * K + c];
+      counts[(int64_t)i * K + c] = run;
       run += v;
     }
-    counts[nc] = run;
+    __syncthreads();
   }
-  __syncthreads();
-  int run = part[threadIdx.x];
-  for (int i = i0; i < i1; ++i) {
-    const int v = counts[i];
-    counts[i] = run;
-    run += v;
-  }
+  if (threadIdx.x == 0) counts[(int64_t)nc * K] = cbase;
 }
 
-__global__ __launch_bounds__(BLOCK) void obs_scatter_kernel(const BandDesc* bands, int nb, int64_t N,
-                                                            const int32_t* offs, int nc, int32_t* order) {
-  __shared__ int wave_n[BLOCK / 64];
-  __shared__ int base[2];
+__global__ __launch_bounds__(BLOCK) void obs_scatter_kernel(const BandDesc* bands, const int32_t* grp, int nb, int G,
+                                                            int64_t N, const int32_t* offs, int32_t* order) {
+  __shared__ int wave_n[BLOCK / 64][ORD_MAX_CLASSES];
+  __shared__ int base[ORD_MAX_CLASSES];
+  const int K = 1 << G;
   const int64_t c0 = (int64_t)blockIdx.x * ORD_CHUNK;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (threadIdx.x == 0) {
-    base[0] = offs[blockIdx.x];                          // next observed slot
-    base[1] = offs[nc] + (int)(c0 - offs[blockIdx.x]);   // next unobserved slot
-  }
+  if (threadIdx.x < K) base[threadIdx.x] = offs[(int64_t)blockIdx.x * K + threadIdx.x];
   __syncthreads();
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   for (int64_t t0 = c0; t0 < N && t0 < c0 + ORD_CHUNK; t0 += BLOCK) {
     const int64_t p = t0 + threadIdx.x;
     const bool in = p < N && p < c0 + ORD_CHUNK;
-    const bool f = in && any_obs(bands, nb, p);
-    const uint64_t mo = __ballot(f), mu = __ballot(in && !f);
-    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    if (lane == 0) wave_n[wv] = __popcll(mo) | (__popcll(mu) << 16);
-    __syncthreads();
-    int bo = base[0], bu = base[1];
-    for (int i = 0; i < wv; ++i) {
-      bo += wave_n[i] & 0xffff;
-      bu += wave_n[i] >> 16;
+    const int cls = in ? obs_class(bands, grp, nb, G, p) : -1;
+    int rank = 0;
+    for (int c = 0; c < K; ++c) {
+      const uint64_t m = __ballot(cls == c);
+      if (lane == 0) wave_n[wv][c] = __popcll(m);
+      if (cls == c) rank = __popcll(m & below);
     }
-    if (f) order[bo + __popcll(mo & below)] = (int32_t)p;
-    else if (in) order[bu + __popcll(mu & below)] = (int32_t)p;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int i = 0; i < BLOCK / 64; ++i) {
-        base[0] += wave_n[i] & 0xffff;
-        base[1] += wave_n[i] >> 16;
-      }
+    if (in) {
+      int slot = base[cls] + rank;
+      for (int i = 0; i < wv; ++i) slot += wave_n[i][cls];
+      order[slot] = (int32_t)p;
     }
+    __syncthreads();
+    if (threadIdx.x < K)
+      for (int i = 0; i < BLOCK / 64; ++i) base[threadIdx.x] += wave_n[i][threadIdx.x];
     __syncthreads();
   }
 }
 
 int obs_order_chunks(int64_t N) { return (int)((N + ORD_CHUNK - 1) / ORD_CHUNK); }
 
-hipError_t dev_obs_order(const BandDesc* bands, int nb, int64_t N, int32_t* counts, int32_t* order, hipStream_t s) {
+hipError_t dev_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int G, int64_t N, int32_t* counts,
+                         int32_t* order, hipStream_t s) {
+  if (G < 1 || G > 3) return hipErrorInvalidValue;
   const int nc = obs_order_chunks(N);
   if (N <= 0) return hipSuccess;
-  hipLaunchKernelGGL(obs_count_kernel, dim3(nc), dim3(BLOCK), 0, s, bands, nb, N, counts);
-  hipLaunchKernelGGL(obs_scan_kernel, dim3(1), dim3(1024), 0, s, counts, nc);
-  hipLaunchKernelGGL(obs_scatter_kernel, dim3(nc), dim3(BLOCK), 0, s, bands, nb, N, counts, nc, order);
+  hipLaunchKernelGGL(obs_count_kernel, dim3(nc), dim3(BLOCK), 0, s, bands, grp, nb, G, N, counts);
+  hipLaunchKernelGGL(obs_scan_kernel, dim3(1), dim3(1024), 0, s, counts, nc, 1 << G);
+  hipLaunchKernelGGL(obs_scatter_kernel, dim3(nc), dim3(BLOCK), 0, s, bands, grp, nb, G, N, counts, order);
   return hipGetLastError();
 }
 

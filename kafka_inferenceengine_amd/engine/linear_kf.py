@@ -782,7 +782,11 @@ class LinearKalman:
         if (cfg.observed_first and table is not None and N and not (gain or precomp or split or bp)
                 and any(s.kind == OP_GP for s in specs)):
             buf, scratch = self._order_bufs if self._order_bufs is not None else (None, None)
-            order, scratch = K.obs_order(table, N, self.device, buf, scratch)
+            # band groups: the bands of one sensor share its clouds (multi-sensor sources)
+            groups = self.observations.band_groups(timestep) if hasattr(self.observations, "band_groups") else None
+            if groups is not None and (len(groups) != len(specs) or max(groups) > 2):
+                groups = None
+            order, scratch = K.obs_order(table, N, self.device, buf, scratch, groups=groups)
             self._order_bufs = (order if buf is None or buf.numel() < N else buf, scratch)
         self._visit = order
         # spatial prior: a plain first iteration (config.spatial_first_plain; it

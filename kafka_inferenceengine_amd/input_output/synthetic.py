@@ -469,6 +469,14 @@ class MultiSensorObservations:
         s, b = self._locate(date, band)
         return s.get_band_data(date, b)
 
+    def band_groups(self, date):
+        """Source index of each band of ``date`` (the bands of one sensor
+        share its clouds): the observation classes of the engine's pixel order."""
+        out = []
+        for i, s in enumerate(self.sources):
+            out += [i] * s.bands_per_observation.get(date, 0)
+        return out
+
     def get_device_band_data(self, date, band):
         s, b = self._locate(date, band)
         return s.get_device_band_data(date, b)

@@ -357,18 +357,30 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     return partials
 
 
-def obs_order(bands: BandTable, N: int, device, out=None, scratch=None):
-    """Stable partition of the pixels 0..N-1: those with an observation in any
-    band of ``bands`` first (``AnalysisArgs.order``).  ``out`` int32 [>= N],
-    ``scratch`` int32 [>= obs_order_chunks(N) + 1] (device) may be reused."""
+def obs_order(bands: BandTable, N: int, device, out=None, scratch=None, groups=None):
+    """Stable partition of the pixels 0..N-1 by observation class
+    (``AnalysisArgs.order``): ``groups`` gives each band's group (bands of one
+    sensor share its cloud mask; None: one group, at most 3 groups); pixels
+    observed in every group come first, then the partial classes, the
+    unobserved last -- each class fills whole waves, which skip the GP of the
+    groups they have no data for.  ``out`` int32 [>= N] and ``scratch`` (device
+    int32) may be reused; returns (order [N], scratch)."""
     dev = torch.device(device)
     N = int(N)
     if out is None or out.numel() < N:
         out = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
-    nc = int(ext().obs_order_chunks(N)) + 1
+    grp = None
+    G = 1
+    if groups is not None:
+        groups = [int(g) for g in groups]
+        if len(groups) != bands.n or min(groups) < 0 or max(groups) > 2:
+            raise ValueError("obs_order: one group id in 0..2 per band")
+        G = max(groups) + 1
+        grp = torch.tensor(groups, dtype=torch.int32, device=dev)
+    nc = int(ext().obs_order_chunks(N)) * (1 << G) + 1
     if dev.type == "cuda" and (scratch is None or scratch.numel() < nc):
-        scratch = torch.empty(nc, dtype=torch.int32, device=dev)
-    ext().obs_order(bands.ptr, bands.n, N, _ptr(scratch), _ptr(out), dev.type == "cuda",
+        scratch = torch.empty(max(nc, 9), dtype=torch.int32, device=dev)
+    ext().obs_order(bands.ptr, _ptr(grp), bands.n, G, N, _ptr(scratch), _ptr(out), dev.type == "cuda",
                     int(torch.cuda.current_stream(dev).cuda_stream) if dev.type == "cuda" else 0)
     return out[:N], scratch
 

@@ -413,6 +413,52 @@ def test_obs_order_is_a_stable_partition():
     assert 0 < n_obs < kf.N
 
 
+def test_obs_order_classes_of_two_sensors():
+    """obs_order with band groups (multi-sensor: one group per sensor): a
+    stable partition into the classes observed by both / the first only / the
+    second only / neither, in that order; the engine's multi-sensor states do
+    not depend on the order."""
+    import datetime as dt
+    from kafka_inferenceengine_amd.engine.bands import build_table
+    from kafka_inferenceengine_amd.ops import kernels as K
+    mask = np.ones((30, 26), bool)
+    dates = [dt.datetime(2017, 7, 3) + dt.timedelta(days=2 * i) for i in range(3)]
+    res = []
+    for on in (False, True):
+        s2 = k.SyntheticS2Observations(mask, dates=dates, n_bands=3, n_train=30, device="cpu", n_pool=3,
+                                       stream=False, cloud_fraction=0.3, seed=1)
+        olci = k.SyntheticOLCIObservations(mask, dates=dates, n_bands=2, n_train=30, device="cpu", n_pool=3,
+                                           stream=False, cloud_fraction=0.3, seed=22)
+        obs = k.MultiSensorObservations([s2, olci])
+        prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
+        kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
+                            state_propagation=None, prior=prior, device="cpu",
+                            config=k.EngineConfig(observed_first=on))
+        st = kf.run([dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in dates],
+                    kf.state_from_prior(prior), None, None)
+        res.append((st, [h["gn_iterations"] for h in kf.history]))
+        if on:
+            bands = kf._device_bands(dates[0])
+            table = build_table([sp for sp, _ in bands], [d for _, d in bands], kf.n_params, kf._cache, kf.device)
+            groups = obs.band_groups(dates[0])
+            assert groups == [0, 0, 0, 1, 1]
+            order, _ = K.obs_order(table, kf.N, kf.device, groups=groups)
+            o = order.numpy()
+            seen = np.zeros((2, kf.N), bool)
+            for g, (_, db) in zip(groups, bands):
+                seen[g] |= (db.decode()[1][:kf.N] > 0).numpy()
+            cls = 3 - (seen[0] * 1 + seen[1] * 2)
+            assert sorted(o.tolist()) == list(range(kf.N))
+            c = cls[o]
+            assert (np.diff(c) >= 0).all()
+            for v in range(4):
+                sel = o[c == v]
+                assert (np.diff(sel) > 0).all()
+            assert len(set(c.tolist())) >= 3
+    (a, ia), (b, ib) = res
+    assert ia == ib and torch.equal(a.x, b.x) and torch.equal(a.P, b.P)
+
+
 @pytest.mark.parametrize("tol", [1e-3, 1e-9])
 def test_fused_spatial_first_iteration_equals_separate_launches(tol):
     """Spatial prior with spatial_first_plain: the plain first Gauss-Newton

@@ -212,7 +212,10 @@ def test_obs_order_device_equals_host(cuda):
         table = build_table([s for s, _ in bands], [d for _, d in bands], kf.n_params, kf._cache, kf.device)
         order, _ = K.obs_order(table, kf.N, kf.device)
         res.append(order.cpu())
-    assert torch.equal(res[0], res[1])
+        # band groups (one band per group): the 4-class partition
+        order2, _ = K.obs_order(table, kf.N, kf.device, groups=[0, 1])
+        res.append(order2.cpu())
+    assert torch.equal(res[0], res[2]) and torch.equal(res[1], res[3])
 
 
 def test_streamer_async_copies_keep_stream_order(cuda):
