@@ -19,6 +19,7 @@ from __future__ import annotations
 import bisect
 import logging
 import math
+import os
 import time
 from collections import namedtuple
 
@@ -788,6 +789,8 @@ class LinearKalman:
                 groups = None
             order, scratch = K.obs_order(table, N, self.device, buf, scratch, groups=groups)
             self._order_bufs = (order if buf is None or buf.numel() < N else buf, scratch)
+            if os.environ.get("KAFKA_ORDER_DEBUG") == "identity":   # A/B: the gather without the partition
+                order = torch.arange(N, dtype=torch.int32, device=order.device)
         self._visit = order
         # spatial prior: a plain first iteration (config.spatial_first_plain; it
         # cannot end the loop), fused with the regularised prepare of the second

@@ -357,6 +357,9 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     return partials
 
 
+_GROUP_IDS = {}   # (device, band groups) -> int32 device tensor of obs_order
+
+
 def obs_order(bands: BandTable, N: int, device, out=None, scratch=None, groups=None):
     """Stable partition of the pixels 0..N-1 by observation class
     (``AnalysisArgs.order``): ``groups`` gives each band's group (bands of one
@@ -376,8 +379,12 @@ def obs_order(bands: BandTable, N: int, device, out=None, scratch=None, groups=N
         if len(groups) != bands.n or min(groups) < 0 or max(groups) > 2:
             raise ValueError("obs_order: one group id in 0..2 per band")
         G = max(groups) + 1
-        grp = torch.tensor(groups, dtype=torch.int32, device=dev)
-    nc = int(ext().obs_order_chunks(N)) * (1 << G) + 1
+        key = (str(dev), tuple(groups))
+        grp = _GROUP_IDS.get(key)
+        if grp is None:   # once per layout: a pageable H2D copy waits for the stream
+            grp = _GROUP_IDS[key] = torch.tensor(groups, dtype=torch.int32, device=dev)
+    # [chunks][classes] prefixes, then the class totals
+    nc = (int(ext().obs_order_chunks(N)) + 1) * (1 << G)
     if dev.type == "cuda" and (scratch is None or scratch.numel() < nc):
         scratch = torch.empty(max(nc, 9), dtype=torch.int32, device=dev)
     ext().obs_order(bands.ptr, _ptr(grp), bands.n, G, N, _ptr(scratch), _ptr(out), dev.type == "cuda",

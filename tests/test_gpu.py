@@ -197,16 +197,19 @@ def test_observed_first_order_equals_natural_order_gpu(cuda, config):
         assert torch.equal(ha[t][0], hb[t][0]) and torch.equal(ha[t][1], hb[t][1])
 
 
-def test_obs_order_device_equals_host(cuda):
+@pytest.mark.parametrize("stream", [False, True])
+def test_obs_order_device_equals_host(cuda, stream):
     """The three obs_order kernels (count, scan, scatter) give the host
-    runner's stable partition, on a tile spanning many 4096-pixel chunks."""
+    runner's stable partition, on a tile spanning many 4096-pixel chunks
+    (N = 620 x 331: a partial last chunk and 16-pixel tile).
+    stream: DN16 observations, the kernels' two-vector-load path."""
     from kafka_inferenceengine_amd.engine.bands import build_table
     from kafka_inferenceengine_amd.ops import kernels as K
-    mask = np.ones((700, 330), bool)
+    mask = np.ones((700, 331), bool)
     mask[100:180, :] = False
     res = []
     for dev in (cuda, torch.device("cpu")):
-        obs = k.SyntheticBHRObservations(mask, n_train=40, device=dev, stream=False, n_pool=1, field_cell=8)
+        obs = k.SyntheticBHRObservations(mask, n_train=40, device=dev, stream=stream, n_pool=1, field_cell=8)
         kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device=dev)
         bands = kf._device_bands(obs.dates[0])
         table = build_table([s for s, _ in bands], [d for _, d in bands], kf.n_params, kf._cache, kf.device)
