@@ -283,16 +283,17 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
                          dst_ld, (hipStream_t)stream), "gather");
   });
   // stable partition by observation class (AnalysisArgs.order); grp: band
-  // group per band (null: one group), G groups (1..3); counts: (chunks * 2^G
-  // + 1) int32 scratch (device only)
+  // group per band (null: one group), G groups (1..3); counts: ((chunks + 1)
+  // * 2^G) int32 scratch (device, global partition only); local: each
+  // KF_ORD_CHUNK-pixel chunk partitioned in place
   m.def("obs_order_chunks", &obs_order_chunks);
   m.def("obs_order", [](uintptr_t bands, uintptr_t grp, int nb, int G, int64_t N, uintptr_t counts, uintptr_t order,
-                        bool device, uintptr_t stream) {
+                        bool local, bool device, uintptr_t stream) {
     if (N > (int64_t)INT32_MAX) throw std::runtime_error("obs_order: N exceeds int32");
     if (G < 1 || G > 3) throw std::runtime_error("obs_order: 1 to 3 band groups");
     if (device) check_hip(dev_obs_order(P<const BandDesc>(bands), P<const int32_t>(grp), nb, G, N, P<int32_t>(counts),
-                                        P<int32_t>(order), (hipStream_t)stream), "obs_order");
-    else if (host_obs_order(P<const BandDesc>(bands), P<const int32_t>(grp), nb, G, N, P<int32_t>(order)) != 0)
+                                        P<int32_t>(order), local, (hipStream_t)stream), "obs_order");
+    else if (host_obs_order(P<const BandDesc>(bands), P<const int32_t>(grp), nb, G, N, P<int32_t>(order), local) != 0)
       throw std::runtime_error("obs_order failed");
   });
   m.def("lut_nearest", [](uintptr_t lut, int M, int D, uintptr_t x, int64_t N, int64_t ld, uintptr_t out,

@@ -174,15 +174,20 @@ int host_unpack(int np, const float* x, const float* a, int64_t N, int64_t ld, c
                 float* unc, int64_t plane) {
   KF_HOST_NP_SWITCH(np, h_unpack, x, a, N, ld, idx, mean, unc, plane);
 }
-int host_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int G, int64_t N, int32_t* order) {
+int host_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int G, int64_t N, int32_t* order, bool local) {
   if (G < 1 || G > 3) return -1;
   std::vector<uint8_t> cls((size_t)N);
 #pragma omp parallel for schedule(static)
   for (int64_t p = 0; p < N; ++p) cls[p] = (uint8_t)obs_class(bands, grp, nb, G, p);
-  int64_t k = 0;
-  for (int c = 0; c < (1 << G); ++c)
-    for (int64_t p = 0; p < N; ++p)
-      if (cls[p] == c) order[k++] = (int32_t)p;
+  // local: each KF_ORD_CHUNK-pixel chunk partitioned in place
+  const int64_t span = local ? (int64_t)KF_ORD_CHUNK : N;
+  for (int64_t c0 = 0; c0 < N; c0 += span) {
+    const int64_t c1 = std::min(N, c0 + span);
+    int64_t k = c0;
+    for (int c = 0; c < (1 << G); ++c)
+      for (int64_t p = c0; p < c1; ++p)
+        if (cls[p] == c) order[k++] = (int32_t)p;
+  }
   return 0;
 }
 int host_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out) {

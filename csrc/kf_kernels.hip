@@ -130,6 +130,7 @@ int dev_grid(int64_t N) { return grid_for(N, g_max_blocks); }
 // (r4_v27), these ~0.3 ms.
 constexpr int ORD_PT = 16;
 constexpr int ORD_CHUNK = BLOCK * ORD_PT;
+static_assert(ORD_CHUNK == KF_ORD_CHUNK, "host chunk-local partition (kf_host.cpp)");
 constexpr int ORD_MAX_CLASSES = 8;   // <= 3 band groups
 
 // bit i: pixel p0 + i (< N) has an observation in band bd.  DN16 without
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(BLOCK) void obs_scatter_kernel(const BandDesc* band
   const int64_t p0 = (int64_t)blockIdx.x * ORD_CHUNK + (int64_t)threadIdx.x * ORD_PT;
   const int nv = ord_valid(p0, N);
   const uint64_t cls = nv ? obs_classes<G>(bands, grp, nb, p0, N) : 0;
-  if (threadIdx.x < K) {
+  if (threadIdx.x < K && offs) {
     // the chunk's place in its class, after every pixel of the classes before it
     int g = offs[(int64_t)blockIdx.x * K + threadIdx.x];
     const int32_t* totals = offs + (int64_t)gridDim.x * K;
@@ -317,6 +318,9 @@ __global__ __launch_bounds__(BLOCK) void obs_scatter_kernel(const BandDesc* band
     start[K] = run;
   }
   __syncthreads();
+  // chunk-local partition (offs null): the classes in place, chunk-aligned
+  // (read after the barrier below)
+  if (threadIdx.x < K && !offs) gbase[threadIdx.x] = (int)(blockIdx.x * ORD_CHUNK) + start[threadIdx.x];
   // chunk-local slots in LDS (stable: thread order, then pixel order)
 #pragma unroll
   for (int c = 0; c < K; ++c) {
@@ -340,12 +344,15 @@ __global__ __launch_bounds__(BLOCK) void obs_scatter_kernel(const BandDesc* band
 int obs_order_chunks(int64_t N) { return (int)((N + ORD_CHUNK - 1) / ORD_CHUNK); }
 
 hipError_t dev_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int G, int64_t N, int32_t* counts,
-                         int32_t* order, hipStream_t s) {
+                         int32_t* order, bool local, hipStream_t s) {
   if (G < 1 || G > 3) return hipErrorInvalidValue;
   const int nc = obs_order_chunks(N);
   if (N <= 0) return hipSuccess;
 #define KF_ORD_GO(G_)                                                                                   \
-  {                                                                                                     \
+  if (local) {                                                                                          \
+    hipLaunchKernelGGL(obs_scatter_kernel<G_>, dim3(nc), dim3(BLOCK), 0, s, bands, grp, nb, N,          \
+                       (const int32_t*)nullptr, order);                                                 \
+  } else {                                                                                              \
     hipLaunchKernelGGL(obs_count_kernel<G_>, dim3(nc), dim3(BLOCK), 0, s, bands, grp, nb, N, counts);   \
     hipLaunchKernelGGL(obs_scan_kernel<1 << G_>, dim3(1), dim3(1024), 0, s, counts, nc);                \
     hipLaunchKernelGGL(obs_scatter_kernel<G_>, dim3(nc), dim3(BLOCK), 0, s, bands, grp, nb, N, counts,  \

@@ -68,10 +68,13 @@ int host_gp_operator(int np, const BandDesc* b, int nb, const float* x, int64_t 
                      int64_t ldh);
 int host_unpack(int np, const float* x, const float* a, int64_t N, int64_t ld, const int64_t* idx, float* mean,
                 float* unc, int64_t plane);
+// obs_order chunk: pixels per scatter workgroup; local = 1 partitions each
+// chunk on its own (no count / scan passes, chunk-aligned, see kf_kernels.hip)
+constexpr int KF_ORD_CHUNK = 4096;
 int obs_order_chunks(int64_t N);
 hipError_t dev_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int G, int64_t N, int32_t* counts,
-                         int32_t* order, hipStream_t s);
-int host_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int G, int64_t N, int32_t* order);
+                         int32_t* order, bool local, hipStream_t s);
+int host_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int G, int64_t N, int32_t* order, bool local);
 int host_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out);
 int host_reg_tiled(const RegTileArgs& a);
 int host_reg_rho(const float* vrow, const StripGeo& g, int64_t N, const RegScheduleArgs& a);

@@ -49,6 +49,11 @@ class EngineConfig:
     # fill whole waves that skip the GP emulator (the reference runs it on the
     # observed pixels only); each pixel's analysis is unchanged
     observed_first: bool = True
+    # one global partition (default) or each 4096-pixel chunk in place (True,
+    # A/B: +2.5 % tip7, +7.6 % prosail10, r4_v31 -- the grid stride is a whole
+    # number of chunks, so a wave meets the same in-chunk position, and class,
+    # on every sweep: waves of only observed pixels set the kernel's length)
+    observed_first_local: bool = False
     spatial_max_sweeps: int = 64
     # one field on a dense strip without halo rows (one rank, or no strip
     # neighbours): up to 8 sweeps per launch out of LDS (kf_reg_tiled.hip),

@@ -787,7 +787,8 @@ class LinearKalman:
             groups = self.observations.band_groups(timestep) if hasattr(self.observations, "band_groups") else None
             if groups is not None and (len(groups) != len(specs) or max(groups) > 2):
                 groups = None
-            order, scratch = K.obs_order(table, N, self.device, buf, scratch, groups=groups)
+            order, scratch = K.obs_order(table, N, self.device, buf, scratch, groups=groups,
+                                         local=cfg.observed_first_local)
             self._order_bufs = (order if buf is None or buf.numel() < N else buf, scratch)
             if os.environ.get("KAFKA_ORDER_DEBUG") == "identity":   # A/B: the gather without the partition
                 order = torch.arange(N, dtype=torch.int32, device=order.device)

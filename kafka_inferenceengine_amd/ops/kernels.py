@@ -360,14 +360,16 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
 _GROUP_IDS = {}   # (device, band groups) -> int32 device tensor of obs_order
 
 
-def obs_order(bands: BandTable, N: int, device, out=None, scratch=None, groups=None):
+def obs_order(bands: BandTable, N: int, device, out=None, scratch=None, groups=None, local=False):
     """Stable partition of the pixels 0..N-1 by observation class
     (``AnalysisArgs.order``): ``groups`` gives each band's group (bands of one
     sensor share its cloud mask; None: one group, at most 3 groups); pixels
     observed in every group come first, then the partial classes, the
     unobserved last -- each class fills whole waves, which skip the GP of the
-    groups they have no data for.  ``out`` int32 [>= N] and ``scratch`` (device
-    int32) may be reused; returns (order [N], scratch)."""
+    groups they have no data for.  ``local=False`` (default): one global
+    partition (count, scan, scatter); True: each 4096-pixel chunk (64 waves)
+    partitioned in place, one pass (A/B, EngineConfig.observed_first_local).  ``out`` int32 [>= N] and
+    ``scratch`` (device int32) may be reused; returns (order [N], scratch)."""
     dev = torch.device(device)
     N = int(N)
     if out is None or out.numel() < N:
@@ -385,9 +387,9 @@ def obs_order(bands: BandTable, N: int, device, out=None, scratch=None, groups=N
             grp = _GROUP_IDS[key] = torch.tensor(groups, dtype=torch.int32, device=dev)
     # [chunks][classes] prefixes, then the class totals
     nc = (int(ext().obs_order_chunks(N)) + 1) * (1 << G)
-    if dev.type == "cuda" and (scratch is None or scratch.numel() < nc):
+    if dev.type == "cuda" and not local and (scratch is None or scratch.numel() < nc):
         scratch = torch.empty(max(nc, 9), dtype=torch.int32, device=dev)
-    ext().obs_order(bands.ptr, _ptr(grp), bands.n, G, N, _ptr(scratch), _ptr(out), dev.type == "cuda",
+    ext().obs_order(bands.ptr, _ptr(grp), bands.n, G, N, _ptr(scratch), _ptr(out), bool(local), dev.type == "cuda",
                     int(torch.cuda.current_stream(dev).cuda_stream) if dev.type == "cuda" else 0)
     return out[:N], scratch
 

@@ -413,6 +413,38 @@ def test_obs_order_is_a_stable_partition():
     assert 0 < n_obs < kf.N
 
 
+@pytest.mark.parametrize("groups", [None, [0, 1]])
+def test_obs_order_local_partitions_each_chunk(groups):
+    """obs_order(local=True) (EngineConfig.observed_first_local): every
+    4096-pixel chunk is a stable partition of its own pixels by class
+    (chunk-aligned, so a wave never mixes chunks); the default global partition
+    orders the same classes over the whole tile."""
+    from kafka_inferenceengine_amd.engine.bands import build_table
+    from kafka_inferenceengine_amd.ops import kernels as K
+    mask = np.ones((150, 131), bool)
+    mask[40:60, :] = False
+    obs = k.SyntheticBHRObservations(mask, n_train=20, device="cpu", stream=True, n_pool=1, field_cell=8)
+    kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device="cpu")
+    bands = kf._device_bands(obs.dates[0])
+    table = build_table([s for s, _ in bands], [d for _, d in bands], kf.n_params, kf._cache, kf.device)
+    seen = np.zeros((2, kf.N), bool)
+    for b, (_, db) in enumerate(bands):
+        seen[b if groups else 0] |= (db.decode()[1][:kf.N] > 0).numpy()
+    cls = (3 - (seen[0] * 1 + seen[1] * 2)) if groups else (1 - seen[0] * 1)
+    o = K.obs_order(table, kf.N, kf.device, groups=groups, local=True)[0].numpy()
+    C = 4096
+    assert kf.N > 3 * C
+    for c0 in range(0, kf.N, C):
+        blk = o[c0:c0 + C]
+        assert sorted(blk.tolist()) == list(range(c0, min(kf.N, c0 + C)))
+        kc = cls[blk]
+        assert (np.diff(kc) >= 0).all()
+        for c in np.unique(kc):
+            assert (np.diff(blk[kc == c]) > 0).all()
+    og = K.obs_order(table, kf.N, kf.device, groups=groups, local=False)[0].numpy()
+    assert (np.diff(cls[og]) >= 0).all() and sorted(og.tolist()) == list(range(kf.N))
+
+
 def test_obs_order_classes_of_two_sensors():
     """obs_order with band groups (multi-sensor: one group per sensor): a
     stable partition into the classes observed by both / the first only / the

@@ -199,8 +199,8 @@ def test_observed_first_order_equals_natural_order_gpu(cuda, config):
 
 @pytest.mark.parametrize("stream", [False, True])
 def test_obs_order_device_equals_host(cuda, stream):
-    """The three obs_order kernels (count, scan, scatter) give the host
-    runner's stable partition, on a tile spanning many 4096-pixel chunks
+    """The obs_order kernels (chunk-local: the scatter alone; global: count,
+    scan, scatter) give the host runner's stable partitions, on a tile spanning many 4096-pixel chunks
     (N = 620 x 331: a partial last chunk and 16-pixel tile).
     stream: DN16 observations, the kernels' two-vector-load path."""
     from kafka_inferenceengine_amd.engine.bands import build_table
@@ -213,12 +213,11 @@ def test_obs_order_device_equals_host(cuda, stream):
         kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device=dev)
         bands = kf._device_bands(obs.dates[0])
         table = build_table([s for s, _ in bands], [d for _, d in bands], kf.n_params, kf._cache, kf.device)
-        order, _ = K.obs_order(table, kf.N, kf.device)
-        res.append(order.cpu())
-        # band groups (one band per group): the 4-class partition
-        order2, _ = K.obs_order(table, kf.N, kf.device, groups=[0, 1])
-        res.append(order2.cpu())
-    assert torch.equal(res[0], res[2]) and torch.equal(res[1], res[3])
+        for local in (True, False):
+            res.append(K.obs_order(table, kf.N, kf.device, local=local)[0].cpu())
+            # band groups (one band per group): the 4-class partition
+            res.append(K.obs_order(table, kf.N, kf.device, groups=[0, 1], local=local)[0].cpu())
+    assert all(torch.equal(res[i], res[i + 4]) for i in range(4))
 
 
 def test_streamer_async_copies_keep_stream_order(cuda):
