@@ -133,14 +133,20 @@ constexpr int ORD_CHUNK = BLOCK * ORD_PT;
 static_assert(ORD_CHUNK == KF_ORD_CHUNK, "host chunk-local partition (kf_host.cpp)");
 constexpr int ORD_MAX_CLASSES = 8;   // <= 3 band groups
 
-// bit i: pixel p0 + i (< N) has an observation in band bd.  DN16 without
-// uncertainty overflow (unc_floor > 0: w > 0 <=> dn > 0, decode_obs) on
-// aligned full tiles: two vector loads; anything else: decode_obs per pixel.
+// bit i: pixel p0 + i (< N) has an observation in band bd (p0: this lane's
+// first pixel, lane * ORD_PT past the wave's).  DN16 whose weight is positive
+// exactly when dn > 0 (decode_obs: an uncertainty floor > 0, or a relative
+// uncertainty that cannot underflow; no overflow of sig^2) on aligned full
+// tiles: two vector loads.  Anything else: decode_obs with consecutive lanes on
+// consecutive pixels (coalesced), a ballot per 64 pixels, each lane picking its
+// 16 bits out of the wave's 16 ballots.
 __device__ __forceinline__ uint32_t obs_bits(const BandDesc& bd, int64_t p0, int64_t N) {
   static_assert(ORD_PT == 16, "two 16-byte loads of uint16 DNs");
-  const bool fast = bd.obs == OBS_DN16 && bd.unc_floor > 0.f && bd.unc_floor < 1e18f &&
-                    fabsf(bd.rel_unc * bd.scale) < 1e13f;
-  if (fast && p0 + ORD_PT <= N && (((uintptr_t)(bd.dn + p0)) & 15) == 0) {
+  const float ru = bd.rel_unc * bd.scale;
+  const bool fast = bd.obs == OBS_DN16 && !(bd.unc_floor >= 1e18f) && fabsf(ru) < 1e13f &&
+                    (bd.unc_floor > 0.f || (bd.rel_unc > 0.f && bd.scale > 0.f && ru > 1e-30f));
+  const bool vec = fast && p0 + ORD_PT <= N && (((uintptr_t)(bd.dn + p0)) & 15) == 0;
+  if (__all(vec)) {
     const uint4* v = reinterpret_cast<const uint4*>(bd.dn + p0);
     const uint4 lo = v[0], hi = v[1];
     const uint32_t u[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -150,12 +156,17 @@ __device__ __forceinline__ uint32_t obs_bits(const BandDesc& bd, int64_t p0, int
       m |= ((u[i] & 0xffffu) ? 1u : 0u) << (2 * i) | ((u[i] >> 16) ? 1u : 0u) << (2 * i + 1);
     return m;
   }
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = p0 - (int64_t)lane * ORD_PT;   // the wave's first pixel
   uint32_t m = 0;
+#pragma unroll
   for (int i = 0; i < ORD_PT; ++i) {
-    if (p0 + i >= N) break;
-    float y, w;
-    decode_obs<0>(bd, p0 + i, y, w);
-    if (w > 0.f) m |= 1u << i;
+    const int64_t q = w0 + (int64_t)i * 64 + lane;
+    float y = 0.f, w = 0.f;
+    if (q < N) decode_obs<0>(bd, q, y, w);
+    const uint64_t bal = __ballot(w > 0.f);
+    // lane L owns pixels 16 L .. 16 L + 15 of the wave: ballot L / 4, bits 16 (L % 4) ..
+    if ((lane >> 2) == i) m = (uint32_t)(bal >> (16 * (lane & 3))) & 0xffffu;
   }
   return m;
 }
@@ -169,7 +180,8 @@ __device__ __forceinline__ uint64_t obs_classes(const BandDesc* bands, const int
   for (int b = 0; b < nb; ++b) {
     const int g = (G > 1 && grp) ? grp[b] : 0;
     const uint32_t have = g == 0 ? g0 : (g == 1 ? g1 : g2);
-    if (have == 0xffffu) continue;   // every pixel of the tile already observed in g
+    if (__all(have == 0xffffu)) continue;   // every pixel of the wave already observed in g (wave-uniform:
+                                             // obs_bits' fallback is wave-cooperative)
     const uint32_t bits = obs_bits(bands[b], p0, N);
     if (g == 0) g0 |= bits;
     else if (g == 1) g1 |= bits;
@@ -205,7 +217,7 @@ __global__ __launch_bounds__(BLOCK) void obs_count_kernel(const BandDesc* bands,
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t p0 = (int64_t)blockIdx.x * ORD_CHUNK + (int64_t)threadIdx.x * ORD_PT;
   const int nv = ord_valid(p0, N);
-  const uint64_t cls = nv ? obs_classes<G>(bands, grp, nb, p0, N) : 0;
+  const uint64_t cls = obs_classes<G>(bands, grp, nb, p0, N);   // every lane: wave-cooperative
 #pragma unroll
   for (int c = 0; c < K; ++c) {
     int v = ord_count(cls, nv, c);
@@ -287,7 +299,7 @@ __global__ __launch_bounds__(BLOCK) void obs_scatter_kernel(const BandDesc* band
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t p0 = (int64_t)blockIdx.x * ORD_CHUNK + (int64_t)threadIdx.x * ORD_PT;
   const int nv = ord_valid(p0, N);
-  const uint64_t cls = nv ? obs_classes<G>(bands, grp, nb, p0, N) : 0;
+  const uint64_t cls = obs_classes<G>(bands, grp, nb, p0, N);   // every lane: wave-cooperative
   if (threadIdx.x < K && offs) {
     // the chunk's place in its class, after every pixel of the classes before it
     int g = offs[(int64_t)blockIdx.x * K + threadIdx.x];
