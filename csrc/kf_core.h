@@ -224,11 +224,25 @@ KF_HD int32_t geo_neighbour(const StripGeo& g, int64_t N, int64_t p, int k) {
 // hot path (TIP kernel: 89 -> 18 SGPR spill slots).
 constexpr int SPEC_ANY = 0, SPEC_PROP = 1, SPEC_PROP_REG = 2;
 
+// AnalysisArgs.variant: the production kernel (AV_DEFAULT) or an alternate
+// device path kept as a test oracle -- each is bit-identical to the default or
+// pinned against it by a GPU test (tests/test_gpu*.py, test_oracles.py); no
+// environment switch selects them in production runs.
+enum AnalysisVariant : int32_t {
+  AV_DEFAULT = 0,
+  AV_VALU_ORACLE = 4,        // GP sums on the f32 VALU record loop instead of the matrix cores
+  AV_GT_PREFETCH = 7,        // global tables: next chunk's fragments loaded under the current one
+  AV_RUNTIME_LAYOUT = 10,    // JRC-TIP bands through the runtime-layout kernel (BAND_LAYOUT_TIP's oracle)
+  AV_PER_BAND_OPERAND = 14,  // BAND_LAYOUT_SHARED_X: exponent operand rebuilt per band
+  AV_BLOCK_ORDER = 16,       // exponent MFMAs block by block (gpm_il_default's other order)
+  AV_GENERIC_SPEC = 18       // fused forecast through the generic launch instead of SPEC_PROP
+};
+
 struct AnalysisArgs {
   int64_t N, ld;
   int32_t n_bands, solve;
   int32_t fast_d, fast_obs;  // host hint: all bands GP with fast_d inputs, one encoding (0: generic)
-  int32_t variant;           // kernel variant selector (tuning; 0 = default)
+  int32_t variant;           // AnalysisVariant (AV_DEFAULT; the others are test oracles)
   int32_t gpm_frags;         // > 0: every band has an MFMA table; LDS fragments (16 B) of all bands + 1 zero
   int32_t gpm_global;        // 1: every band has an MFMA table, read from global memory (too large for LDS)
   const BandDesc* bands;

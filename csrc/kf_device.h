@@ -442,19 +442,9 @@ constexpr bool gpm_il_default() {
 template <int NP, int FD>
 static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
   // GP on the matrix cores when the host attached split-f16 tables to every band
-  // (variant 4 forces the VALU record loop, for A/B)
+  // (AV_VALU_ORACLE: the f32 VALU record loop, the tests' second device path)
   if constexpr (FD > 0 && FD <= GPM_MAX_D) {
-    if constexpr (NP == 7 && FD == 4) {
-      // variant 8 (A/B): the LDS-sized JRC-TIP tables read from global memory
-      // instead (no LDS: the waves per SIMD follow the VGPRs, not the table)
-      if (a.gpm_frags > 0 && a.variant == 8) {
-        if (a.fast_obs == OBS_DN16) {
-          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
-          return true;
-        }
-      }
-    }
-    if (a.gpm_frags > 0 && a.variant != 4 && a.n_bands <= GPM_MAX_BANDS) {
+    if (a.gpm_frags > 0 && a.variant != AV_VALU_ORACLE && a.n_bands <= GPM_MAX_BANDS) {
       const size_t lds = (size_t)a.gpm_frags * sizeof(kf_h8);
 #define KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_)                                                           \
   {                                                                                                              \
@@ -464,21 +454,23 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
   }
       // Both column blocks' exponent MFMAs issued before the first block's
       // exponentials (gpm_chunk IL) where that costs no occupancy
-      // (gpm_il_default); variant 16 (A/B): the other order
+      // (gpm_il_default); AV_BLOCK_ORDER: the other order
 #define KF_MFMA_GO(OBS_, BS_, MINW_, LAY_)                                   \
   {                                                                         \
-    if (gpm_il_default<NP, LAY_>() != (a.variant == 16)) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, true, SPEC_ANY) \
-    else KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, false, SPEC_ANY)                \
+    if (gpm_il_default<NP, LAY_>() != (a.variant == AV_BLOCK_ORDER))        \
+      KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, true, SPEC_ANY)                   \
+    else KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, false, SPEC_ANY)               \
   }
       // JRC-TIP layout with the forecast fused (every date after the first):
       // the launch's paths fixed at compile time (SPEC_PROP / SPEC_PROP_REG,
-      // kf_core.h); variant 18 (A/B): the generic kernel
-#define KF_MFMA_GO_SPEC(OBS_, BS_, MINW_, LAY_)                                                  \
-  {                                                                                             \
-    constexpr bool IL_ = gpm_il_default<NP, LAY_>();                                            \
-    if (!a.prop || a.variant == 16 || a.variant == 18) KF_MFMA_GO(OBS_, BS_, MINW_, LAY_)       \
-    else if (a.reg_v) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP_REG)                  \
-    else KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP)                                    \
+      // kf_core.h); AV_GENERIC_SPEC: the generic kernel
+#define KF_MFMA_GO_SPEC(OBS_, BS_, MINW_, LAY_)                                                      \
+  {                                                                                                 \
+    constexpr bool IL_ = gpm_il_default<NP, LAY_>();                                                \
+    if (!a.prop || a.variant == AV_BLOCK_ORDER || a.variant == AV_GENERIC_SPEC)                     \
+      KF_MFMA_GO(OBS_, BS_, MINW_, LAY_)                                                            \
+    else if (a.reg_v) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP_REG)                      \
+    else KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP)                                        \
   }
       // Launch bound of 3 workgroups per CU (MINW = 3, as the LDS tables
       // allow) up to 7 parameters: the compiler holds the kernel to <= 168
@@ -486,10 +478,11 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
       // profiles/r3_v13_*); 10 parameters would spill, so no bound there.
       constexpr int MW = NP <= 7 ? 3 : 1;
       // JRC-TIP band layout (AnalysisArgs.band_layout, checked on the host):
-      // band loop unrolled over the two compile-time maps (variant 10: the
-      // runtime-layout kernel, for A/B)
+      // band loop unrolled over the two compile-time maps (AV_RUNTIME_LAYOUT:
+      // the runtime-layout kernel, its oracle)
       bool tip = false;
-      if constexpr (NP == 7 && FD == 4) tip = a.band_layout == BAND_LAYOUT_TIP && a.n_bands == 2 && a.variant != 10;
+      if constexpr (NP == 7 && FD == 4)
+        tip = a.band_layout == BAND_LAYOUT_TIP && a.n_bands == 2 && a.variant != AV_RUNTIME_LAYOUT;
       if (a.fast_obs == OBS_DN16) {
         if constexpr (NP == 7 && FD == 4) {
           if (tip) {
@@ -515,41 +508,31 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
       return true;
     }
     if constexpr (FD == NP && NP >= 7) {
-      if (a.gpm_global && a.variant != 4) {
-        // variant 7 (A/B): register double buffer (next chunk's fragments
+      if (a.gpm_global && a.variant != AV_VALU_ORACLE) {
+        // AV_GT_PREFETCH: register double buffer (next chunk's fragments
         // loaded under the current one): 191.7 vs 191.6 ms/step without, so
         // the default leaves the latency to the other wave
-        if (a.fast_obs == OBS_DN16 && a.variant == 7)
+        constexpr bool IL = gpm_il_default<NP, BAND_LAYOUT_RUNTIME>();
+        if (a.fast_obs == OBS_DN16 && a.variant == AV_GT_PREFETCH)
           hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, true>), dim3(grid), dim3(BLOCK), 0, s, a);
-        else if (a.fast_obs == OBS_DN16 && a.prop && !a.reg_v && a.variant == 0 &&
-                 gpm_il_default<NP, BAND_LAYOUT_RUNTIME>())
+        else if (a.fast_obs == OBS_DN16 && a.prop && !a.reg_v && a.variant == AV_DEFAULT && IL)
           // fused forecast, no regulariser: the launch's paths fixed at compile time (SPEC_PROP)
-          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, false, true, SPEC_PROP>), dim3(grid), dim3(BLOCK),
-                             0, s, a);
-        else if (a.fast_obs == OBS_DN16 && (a.variant == 16) != gpm_il_default<NP, BAND_LAYOUT_RUNTIME>())
+          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, false, true, SPEC_PROP>), dim3(grid),
+                             dim3(BLOCK), 0, s, a);
+        else if (a.fast_obs == OBS_DN16 && (a.variant == AV_BLOCK_ORDER) != IL)
           hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, false, true>), dim3(grid), dim3(BLOCK), 0, s, a);
         else if (a.fast_obs == OBS_DN16)
           hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
         else if (a.fast_obs == OBS_F32)
-          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_F32, false, gpm_il_default<NP, BAND_LAYOUT_RUNTIME>()>),
-                             dim3(grid), dim3(BLOCK), 0, s, a);
+          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_F32, false, IL>), dim3(grid), dim3(BLOCK), 0, s, a);
         else
           return false;
         return true;
       }
     }
   }
-  // variant (A/B tuning, scripts/bench_kernels.py): 0 unroll-4 pairs (default),
-  // 1 unroll-4 + folded exponent, 2 unroll-8, 3 unroll-3 (GP fast paths only)
   if (a.fast_obs == OBS_DN16) {
-    if (FD > 0 && a.variant == 1)
-      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 4, true>), dim3(grid), dim3(BLOCK), 0, s, a);
-    else if (FD > 0 && a.variant == 2)
-      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 8>), dim3(grid), dim3(BLOCK), 0, s, a);
-    else if (FD > 0 && a.variant == 3)
-      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16, 3>), dim3(grid), dim3(BLOCK), 0, s, a);
-    else
-      hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
+    hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
   } else if (a.fast_obs == OBS_F32) {
     hipLaunchKernelGGL((analysis_kernel<NP, FD, OBS_F32>), dim3(grid), dim3(BLOCK), 0, s, a);
   } else if constexpr (FD <= 0) {

@@ -586,12 +586,12 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   int off = 0;
   // BAND_LAYOUT_SHARED_X (global tables, full-state GPs around one centre):
   // the exponent operand of the centred inputs once per iteration, each band
-  // patches its constant in (gpm_patch_c).  Variant 14: per band (A/B).
+  // patches its constant in (gpm_patch_c).  AV_PER_BAND_OPERAND: per band (oracle).
   constexpr bool SXC = GT && D == NP && D % 2 == 0;
   bool sx = false;
   kf_h8 sxb[2][gpm_k_steps(D)];
   if constexpr (SXC) {
-    sx = a.band_layout == BAND_LAYOUT_SHARED_X && a.variant != 14 && a.n_bands > 0;
+    sx = a.band_layout == BAND_LAYOUT_SHARED_X && a.variant != AV_PER_BAND_OPERAND && a.n_bands > 0;
     if (sx) {
       const KF_CONST_AS BandDesc* b0 = cptr(a.bands);
       float xi0[D], c0;

@@ -160,6 +160,10 @@ class HostRing {
       memcpy(reinterpret_cast<void*>(dst), slots_[s] + slot_off, nbytes);
       return;
     }
+    // an h2d_async of this slot still queued on the submitter would record the
+    // slot event after this copy's, so stream_wait / host_wait would track the
+    // older copy: let it be issued first (slot events in submission order)
+    wait_submitted(s);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (hipMemcpyAsync(reinterpret_cast<void*>(dst), slots_[s] + slot_off, nbytes, hipMemcpyHostToDevice, st) !=
         hipSuccess)

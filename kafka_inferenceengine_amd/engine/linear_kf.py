@@ -728,7 +728,9 @@ class LinearKalman:
         if bp and (gain or cfg.spatial_gamma > 0 or cfg.hessian_correction):
             raise ValueError("band_parallel runs the information form without regulariser / Hessian correction")
         if bp and not getattr(self, "_bp_checked", False):
-            self._band_parallel_check(specs)
+            nb_all = getattr(self.observations, "bands_per_observation", {}).get(timestep) \
+                if hasattr(self.observations, "bands_per_observation") else None
+            self._band_parallel_check(specs, nb_all)
         split = None if (precomp or gain or bp or cfg.spatial_gamma > 0) else self._split_plan(specs, dbs, h0_outs)
         if precomp or split:
             table = None
@@ -790,8 +792,6 @@ class LinearKalman:
             order, scratch = K.obs_order(table, N, self.device, buf, scratch, groups=groups,
                                          local=cfg.observed_first_local)
             self._order_bufs = (order if buf is None or buf.numel() < N else buf, scratch)
-            if os.environ.get("KAFKA_ORDER_DEBUG") == "identity":   # A/B: the gather without the partition
-                order = torch.arange(N, dtype=torch.int32, device=order.device)
         self._visit = order
         # spatial prior: a plain first iteration (config.spatial_first_plain; it
         # cannot end the loop), fused with the regularised prepare of the second
@@ -974,7 +974,7 @@ class LinearKalman:
         if cfg.gp_split == "auto" and d < cfg.gp_split_min_d and len(specs) < cfg.gp_split_min_bands:
             return None
         if (cfg.gp_split == "auto" and on_dev and d == self.n_params and d in K.GPM_GLOBAL_D
-                and K.DEFAULT_VARIANT != 4 and all(self._cache.get_mfma(s, self.device) is not None for s in specs)):
+                and K.DEFAULT_VARIANT != K.Variant.VALU_ORACLE and all(self._cache.get_mfma(s, self.device) is not None for s in specs)):
             # many full-state GP bands: the fused matrix-core kernel with the
             # tables in global memory beats the split path (34 bands: 631 vs
             # 1064 ms/step, profiles/r2_v10_prosail_mfma_g_ab.log)
@@ -1349,17 +1349,25 @@ class LinearKalman:
             K.analysis(n, self._bp_solve_tab, x_prev, fc.x, fc.P, x_out, A_out, None, self._bp_status,
                        self._partials, N=N, a_in=A_part, b_in=b_part)
 
-    def _band_parallel_check(self, specs):
+    def _band_parallel_check(self, specs, n_bands=None):
         """Refuse band-parallel where its C5 all-reduce dwarfs the analysis it
-        splits (parallel/policy.py; rank-uniform: every rank of a group sees the
-        same band count and emulators).  ``specs``: this rank's bands."""
+        splits (parallel/policy.py).  ``specs``: this rank's bands; ``n_bands``:
+        the date's full band count.  Rank-uniform by construction: bands are
+        dealt round-robin, so the ranks of a group can hold different band
+        counts and emulators (34 bands over 4 ranks: 9/9/8/8) -- the decision
+        uses the full band count and the group-wide largest training set (one
+        max all-reduce over the band group), so every rank raises or none does
+        (a split decision would leave the others waiting in the band
+        all-reduce)."""
         from ..parallel.policy import band_parallel_decision
 
         self._bp_checked = True
         B = self.band_comm.world
-        n_bands = len(specs) * B
-        n_train = max([int(getattr(s.emulator, "n_train", 0) or 0) for s in specs] or [0])
-        B_eff, why = band_parallel_decision(self.n_params, n_bands, n_train, B, self.device.type,
+        if n_bands is None:
+            n_bands = len(specs) * B
+        n_train_local = max([int(getattr(s.emulator, "n_train", 0) or 0) for s in specs] or [0])
+        n_train = int(self.band_comm.max_float(float(n_train_local)))
+        B_eff, why = band_parallel_decision(self.n_params, int(n_bands), n_train, B, self.device.type,
                                             force=self.config.band_parallel_force)
         if B_eff != B:
             raise ValueError(why + " (set band_parallel_force to run it anyway)")

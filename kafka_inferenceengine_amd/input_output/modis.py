@@ -24,7 +24,6 @@ from __future__ import annotations
 import datetime
 import glob
 import os
-from collections import namedtuple
 
 import numpy as np
 import scipy.sparse as sp
@@ -32,7 +31,7 @@ import scipy.sparse as sp
 from .observations import BHR_data
 from .sentinel import ross_li_kernels
 
-MOD09_data = namedtuple("MOD09_data", "reflectance mask uncertainty obs_op sza vza raa")
+from .records import MOD09_data  # noqa: F401  (re-export)
 
 # observations.py:100-103
 MOD09_QA_OK = np.array([8, 72, 136, 200, 1032, 1288, 2056, 2120, 2184, 2248])

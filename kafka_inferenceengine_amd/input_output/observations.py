@@ -11,13 +11,11 @@ from __future__ import annotations
 
 import datetime
 import os
-from collections import namedtuple
 
 import numpy as np
 import scipy.sparse as sp
 
-BHR_data = namedtuple("BHR_data", "observations mask uncertainty metadata emulator")
-ObsData = namedtuple("ObsData", "observations uncertainty mask metadata emulator")
+from .records import BHR_data, ObsData  # noqa: F401  (re-exports)
 
 
 def get_modis_dates(fnames):

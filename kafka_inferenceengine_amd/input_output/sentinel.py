@@ -24,7 +24,6 @@ import datetime
 import glob
 import os
 import xml.etree.ElementTree as ET
-from collections import namedtuple
 
 import numpy as np
 import scipy.sparse as sp
@@ -32,10 +31,7 @@ import scipy.sparse as sp
 from ..models.gp import GaussianProcessEmulator, pack_emulator_set, unpack_emulator_set
 from .tiff import read_tiff, write_tiff
 
-S2MSIdata = namedtuple("S2MSIdata", "observations uncertainty mask metadata emulator")
-SARdata = namedtuple("SARdata", "observations uncertainty mask metadata emulator")
-BHR_data = namedtuple("BHR_data", "observations mask uncertainty metadata emulator")
-MOD09_data = namedtuple("MOD09_data", "reflectance mask uncertainty obs_op sza vza raa")
+from .records import BHR_data, MOD09_data, S2MSIdata, SARdata  # noqa: F401  (re-exports)
 
 S2_BAND_MAP = ["02", "03", "04", "05", "06", "07", "08", "8A", "09", "12"]
 S2_EMULATOR_BANDS = [2, 3, 4, 5, 6, 7, 8, 9, 12, 13]

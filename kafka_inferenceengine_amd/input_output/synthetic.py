@@ -24,7 +24,6 @@ from __future__ import annotations
 import datetime as dt
 import math
 import os
-from collections import namedtuple
 
 import numpy as np
 import scipy.sparse as sp
@@ -36,7 +35,7 @@ from ..models.operators import OP_GP, OperatorSpec, gp_spec
 from ..ops import kernels as K
 from .streaming import DateStreamer
 
-S2MSIdata = namedtuple("S2MSIdata", "observations uncertainty mask metadata emulator")
+from .records import S2MSIdata
 
 M32 = 0xFFFFFFFF
 

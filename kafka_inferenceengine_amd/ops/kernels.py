@@ -9,8 +9,7 @@ the identical per-pixel source through the OpenMP host runner.
 from __future__ import annotations
 
 from dataclasses import dataclass
-
-import os
+from enum import IntEnum
 
 import numpy as np
 import torch
@@ -114,8 +113,24 @@ BAND_LAYOUT_TIP = 1
 BAND_LAYOUT_SHARED_X = 2
 FD_PRECOMP = -1   # kf_core.h: fast analysis kernel for all-precomputed operators
 FD_LINEAR = -2    # kf_core.h: fast analysis kernel for all-linear (identity/selection) operators
-# analysis fast-kernel variant (kf_kernels.hip:l_analysis_fast); env override for A/B runs
-DEFAULT_VARIANT = int(os.environ.get("KAFKA_ANALYSIS_VARIANT", "0"))
+
+
+class Variant(IntEnum):
+    """``AnalysisArgs.variant`` (kf_core.h ``AnalysisVariant``): the production
+    analysis kernel or an alternate device path kept as a test oracle (each is
+    bit-identical to the default or pinned against it by a GPU test)."""
+    DEFAULT = 0
+    VALU_ORACLE = 4          # GP sums on the f32 VALU record loop instead of the matrix cores
+    GT_PREFETCH = 7          # global tables: next chunk's fragments loaded under the current one
+    RUNTIME_LAYOUT = 10      # JRC-TIP bands through the runtime-layout kernel
+    PER_BAND_OPERAND = 14    # BAND_LAYOUT_SHARED_X: exponent operand rebuilt per band
+    BLOCK_ORDER = 16         # exponent MFMAs block by block
+    GENERIC_SPEC = 18        # fused forecast through the generic launch instead of SPEC_PROP
+
+
+# analysis variant of launches that pass none (tests switch it to an oracle path;
+# no environment variable reaches it)
+DEFAULT_VARIANT = Variant.DEFAULT
 
 
 class _PinnedRing:
@@ -292,7 +307,8 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     a.partials_first = _ptr(partials_first) if gn_fused == 2 else 0
     a.fast_d, a.fast_obs = (bands.fast_d, bands.fast_obs) if fast else (0, 0)
     a.band_layout = int(bands.layout) if (fast and (bands.layout != BAND_LAYOUT_TIP or n_params == 7)) else 0
-    a.variant = DEFAULT_VARIANT if variant is None else int(variant)
+    v = DEFAULT_VARIANT if variant is None else variant
+    a.variant = int(Variant(int(v)))     # unknown numbers raise
     a.gpm_frags = bands.gpm_frags if fast else 0
     a.gpm_global = int(bool(bands.gpm_global) and fast and bands.fast_d == n_params)
     a.bands = bands.ptr
@@ -428,7 +444,7 @@ def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status
     if a.fast_d < 0:     # precomputed / linear fast paths exist for K1 only
         a.fast_d, a.fast_obs = 0, 0
     # GP on the matrix cores with LDS tables (kf_device.h:gain_mfma_kernel, JRC-TIP)
-    a.gpm_frags = bands.gpm_frags if (fast and DEFAULT_VARIANT != 4) else 0
+    a.gpm_frags = bands.gpm_frags if (fast and DEFAULT_VARIANT != Variant.VALU_ORACLE) else 0
     a.bands = bands.ptr
     a.x_prev, a.x_f, a.p_f, a.x_out, a.p_out = map(_ptr, (x_prev, x_f, p_f, x_out, p_out))
     a.status, a.partials = _ptr(status), _ptr(partials)

@@ -453,3 +453,14 @@ def test_native_reader_rejects_bad_inputs(tmp_path):
     (tmp_path / "nocount.tif").write_bytes(bytes(bad))
     with pytest.raises(RuntimeError, match="no value"):
         tiff_info(tmp_path / "nocount.tif")
+
+
+def test_record_types_defined_once():
+    """each reference record type is one class, whichever
+    reader module it is imported from (isinstance / pickling agree)."""
+    from kafka_inferenceengine_amd.input_output import modis, observations, records, sentinel, synthetic
+
+    assert sentinel.S2MSIdata is synthetic.S2MSIdata is records.S2MSIdata
+    assert sentinel.BHR_data is observations.BHR_data is records.BHR_data
+    assert sentinel.MOD09_data is modis.MOD09_data is records.MOD09_data
+    assert sentinel.SARdata is records.SARdata
