@@ -118,6 +118,9 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(AnalysisArgs, partials, double*)
       .PTR_FIELD(AnalysisArgs, partials_first, double*)
       .PTR_FIELD(AnalysisArgs, order, const int32_t*)
+      .def_readwrite("n_visit", &AnalysisArgs::n_visit)
+      .PTR_FIELD(AnalysisArgs, dn_out, float*)
+      .def_readwrite("a_rows", &AnalysisArgs::a_rows)
       .def_readwrite("gn_fused", &AnalysisArgs::gn_fused)
       .def_readwrite("band_layout", &AnalysisArgs::band_layout)
       .PTR_FIELD(AnalysisArgs, prop, const PropArgs*)
@@ -295,6 +298,65 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
                                         P<int32_t>(order), local, (hipStream_t)stream), "obs_order");
     else if (host_obs_order(P<const BandDesc>(bands), P<const int32_t>(grp), nb, G, N, P<int32_t>(order), local) != 0)
       throw std::runtime_error("obs_order failed");
+  });
+  // per-chunk Gauss-Newton convergence (kf_core.h ChunkPartialArgs ...)
+  m.def("chunk_partials", [](uintptr_t dn, uintptr_t seg_start, uintptr_t seg_len, uintptr_t lc_ptr, uintptr_t lc_gid,
+                             int n_local, uintptr_t active, uintptr_t part, bool device, uintptr_t stream) {
+    ChunkPartialArgs a{};
+    a.dn = P<const float>(dn);
+    a.seg_start = P<const int32_t>(seg_start);
+    a.seg_len = P<const int32_t>(seg_len);
+    a.lc_ptr = P<const int32_t>(lc_ptr);
+    a.lc_gid = P<const int32_t>(lc_gid);
+    a.n_local = n_local;
+    a.active = P<const uint8_t>(active);
+    a.part = P<double>(part);
+    if (device) check_hip(dev_chunk_partials(a, (hipStream_t)stream), "chunk_partials");
+    else host_chunk_partials(a);
+  });
+  m.def("chunk_decide", [](uintptr_t part_all, int world, int nc, uintptr_t len_x, uintptr_t local_count, double tol,
+                           int n_iter, int min_iter, int max_iter, uintptr_t active, uintptr_t newly, uintptr_t iters,
+                           uintptr_t info, bool device, uintptr_t stream) {
+    ChunkDecideArgs a{};
+    a.part_all = P<const double>(part_all);
+    a.world = world;
+    a.nc = nc;
+    a.len_x = P<const double>(len_x);
+    a.local_count = P<const int32_t>(local_count);
+    a.tol = tol;
+    a.n_iter = n_iter;
+    a.min_iter = min_iter;
+    a.max_iter = max_iter;
+    a.active = P<uint8_t>(active);
+    a.newly = P<uint8_t>(newly);
+    a.iters = P<int32_t>(iters);
+    a.info = P<double>(info);
+    if (device) check_hip(dev_chunk_decide(a, (hipStream_t)stream), "chunk_decide");
+    else host_chunk_decide(a);
+  });
+  m.def("chunk_compact_blocks", &chunk_compact_blocks);
+  // -> kept slots on the host runner, -1 on the device (the count is known from chunk_decide's info)
+  m.def("chunk_compact", [](uintptr_t order_in, int64_t n_in, uintptr_t chunk_of, uintptr_t active, uintptr_t newly,
+                            uintptr_t counts, uintptr_t order_out, uintptr_t x_src, uintptr_t x_dst, int np, int64_t ld,
+                            bool device, uintptr_t stream) -> int64_t {
+    if (n_in > (int64_t)INT32_MAX) throw std::runtime_error("chunk_compact: more than 2^31 slots");
+    ChunkCompactArgs a{};
+    a.order_in = P<const int32_t>(order_in);
+    a.n_in = n_in;
+    a.chunk_of = P<const int32_t>(chunk_of);
+    a.active = P<const uint8_t>(active);
+    a.newly = P<const uint8_t>(newly);
+    a.counts = P<int32_t>(counts);
+    a.order_out = P<int32_t>(order_out);
+    a.x_src = P<const float>(x_src);
+    a.x_dst = P<float>(x_dst);
+    a.np = np;
+    a.ld = ld;
+    if (device) {
+      check_hip(dev_chunk_compact(a, (hipStream_t)stream), "chunk_compact");
+      return -1;
+    }
+    return host_chunk_compact(a);
   });
   m.def("lut_nearest", [](uintptr_t lut, int M, int D, uintptr_t x, int64_t N, int64_t ld, uintptr_t out,
                           bool device, uintptr_t stream) {

@@ -284,7 +284,23 @@ struct AnalysisArgs {
   // emulator runs on observed pixels only, as in the reference's operator
   // (utils.py:130-170, run_emulator on x0[mask])
   const int32_t* order;
+  // visiting slots of this launch (0: N): the per-chunk Gauss-Newton loop
+  // (EngineConfig.convergence_chunk) visits only the pixels of the chunks that
+  // have not converged, order[0 .. n_visit)
+  int64_t n_visit;
+  // per-pixel |x - x0|^2 of the launch's last iteration (the per-chunk norms,
+  // chunk_partials_kernel), stored at the pixel index; may be null
+  float* dn_out;
+  // packed precision rows stored to a_out (bit t: row t); 0 = every row.  The
+  // engine's store_precision="auto" keeps only what the next forecast reads
+  // (the LAI propagator: the TLAI diagonal entry, kf_tools.py:292-314)
+  uint64_t a_rows;
 };
+
+// slots visited by an analysis launch
+KF_HD int64_t visit_count(const AnalysisArgs& a) { return a.n_visit > 0 ? a.n_visit : a.N; }
+// packed precision row t stored under AnalysisArgs.a_rows
+KF_HD bool a_row_on(uint64_t rows, int t) { return rows == 0 || ((rows >> t) & 1u); }
 
 
 // ---------------------------------------------------------------------------
@@ -984,7 +1000,8 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
       if ((a->reg_mask >> j) & 1u) A[tri(NP, j, j)] += gd;
     if (store && a->a_out) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = A[t];
+      for (int t = 0; t < NT; ++t)
+          if (a_row_on(a->a_rows, t)) KF_PXS(a->a_out, t * ld, p) = A[t];
     }
     float dA[NP];   // output uncertainty: 1/sqrt(diag) of the regularised precision
 #pragma unroll
@@ -1012,7 +1029,8 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
       }
       if (store && a->a_out) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = Af[t];
+        for (int t = 0; t < NT; ++t)
+          if (a_row_on(a->a_rows, t)) KF_PXS(a->a_out, t * ld, p) = Af[t];
       }
 #pragma unroll
       for (int j = 0; j < NP; ++j) dA[j] = Af[tri(NP, j, j)];
@@ -1047,7 +1065,8 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
   }
   if (store && a->a_out) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = A[t];
+    for (int t = 0; t < NT; ++t)
+          if (a_row_on(a->a_rows, t)) KF_PXS(a->a_out, t * ld, p) = A[t];
   }
   if (store && a->b_out) {
 #pragma unroll
@@ -1082,7 +1101,8 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
       for (int j = 0; j < NP; ++j) dA[j] = A[tri(NP, j, j)];
       if (store && a->a_out) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) KF_PXS(a->a_out, t * ld, p) = A[t];
+        for (int t = 0; t < NT; ++t)
+          if (a_row_on(a->a_rows, t)) KF_PXS(a->a_out, t * ld, p) = A[t];
       }
     }
     if (store) {
@@ -2087,6 +2107,65 @@ KF_HD float pixel_jacobi_classic(const JacobiArgs& a, int64_t p) {
   }
   return dn;
 }
+
+// ---------------------------------------------------------------------------
+// Per-chunk Gauss-Newton convergence (EngineConfig.convergence_chunk).  The
+// reference never runs a whole tile as one filter: its drivers cut the raster
+// into get_chunks tiles (kafka_test_Py36.py:241, 256^2) and each chunk's own
+// LinearKalman tests ||x_a - x_prev||_2 / len(x_a) over that chunk alone
+// (linear_kf.py:293-304).  The engine keeps one filter per rank and evaluates
+// that test per chunk: the analysis writes each pixel's |x - x0|^2 (dn_out),
+// chunk_partials sums a chunk's pixels in a fixed order (bit-reproducible,
+// independent of the visiting order), the ranks' per-chunk partials are
+// all-gathered and summed in rank order (chunk_decide, identical on every
+// rank), and converged chunks leave the visiting order (chunk_compact).
+
+// this rank's pixels of a chunk: runs of consecutive local indices, one per
+// (chunk, raster row) -- the active pixels of a row inside a chunk's column
+// range are contiguous in the strip's row-major numbering
+struct ChunkPartialArgs {
+  const float* dn;           // [N] |x - x0|^2 per pixel (AnalysisArgs.dn_out)
+  const int32_t* seg_start;  // [S] first local pixel of each run
+  const int32_t* seg_len;    // [S] run length
+  const int32_t* lc_ptr;     // [n_local + 1]: runs of local chunk c are [lc_ptr[c], lc_ptr[c + 1]), row order
+  const int32_t* lc_gid;     // [n_local] global chunk id (get_chunks order, 0-based)
+  int32_t n_local;
+  const uint8_t* active;     // [nc] chunks still iterating (frozen ones are skipped)
+  double* part;              // [nc] this rank's sum per global chunk
+};
+
+struct ChunkDecideArgs {
+  const double* part_all;    // [world][nc] all ranks' partials (all-gathered)
+  int32_t world, nc;
+  const double* len_x;       // [nc] n_params x active pixels of the chunk (all ranks)
+  const int32_t* local_count;  // [nc] this rank's pixels of the chunk
+  double tol;
+  int32_t n_iter, min_iter, max_iter;
+  uint8_t* active;           // [nc] in/out
+  uint8_t* newly;            // [nc] out: converged (or bailed out) at this iteration
+  int32_t* iters;            // [nc] out: Gauss-Newton iterations of the chunk (set when it stops)
+  double* info;              // [4] chunks still active (all ranks), largest norm tested, this rank's active
+                             // pixels, chunks stopped at this iteration
+};
+
+// the reference's exit test (linear_kf.py:297-304) for one chunk
+KF_HD bool chunk_stops(double norm, int n_iter, int min_iter, int max_iter, double tol) {
+  return (norm < tol && n_iter >= min_iter) || n_iter > max_iter;
+}
+
+struct ChunkCompactArgs {
+  const int32_t* order_in;   // visiting order of the last launch (null: 0..n_in-1)
+  int64_t n_in;
+  const int32_t* chunk_of;   // [N] global chunk of each local pixel
+  const uint8_t* active;
+  const uint8_t* newly;
+  int32_t* counts;           // [blocks + 1] scratch (device)
+  int32_t* order_out;        // the active chunks' pixels, in order_in's order (stable)
+  const float* x_src;        // frozen copy: x of the newly stopped chunks' pixels from x_src ...
+  float* x_dst;              // ... into x_dst (the next launch's output buffer keeps their final x)
+  int32_t np;
+  int64_t ld;
+};
 
 // ---------------------------------------------------------------------------
 // K6: second-order (Hessian) correction for GP bands (kf_tools.py:26-72):

@@ -76,9 +76,13 @@ template <int NP, int FD = 0, int FOBS = 0, int UNR = 4, bool FOLD = false>
 __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
   double acc = 0.0, acc1 = 0.0;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
-  for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < a.N; q += stride) {
+  const int64_t nv = visit_count(a);
+  for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < nv; q += stride) {
     float dn1;
-    acc += (double)pixel_analysis<NP, FD, FOBS, UNR, FOLD>(a, visit_px(a.order, q), dn1);
+    const int64_t p = visit_px(a.order, q);
+    const float dn = pixel_analysis<NP, FD, FOBS, UNR, FOLD>(a, p, dn1);
+    if (a.dn_out) a.dn_out[p] = dn;
+    acc += (double)dn;
     acc1 += (double)dn1;
   }
   analysis_partials(a, acc, acc1);
@@ -112,13 +116,19 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
   double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BS;
-  for (int64_t base = (int64_t)blockIdx.x * BS + (threadIdx.x - lane); base < a.N; base += stride) {
+  const int64_t nv = visit_count(a);
+  for (int64_t base = (int64_t)blockIdx.x * BS + (threadIdx.x - lane); base < nv; base += stride) {
     const int64_t q = base + lane;
-    const bool act = q < a.N;
-    const int64_t p = visit_px(a.order, act ? q : a.N - 1);
+    const bool act = q < nv;
+    const int64_t p = visit_px(a.order, act ? q : nv - 1);
     float dn1;
     const float dn = pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT, IL, SPEC>(a, p, act, gpm_lds,
                                                                                      dn1 KF_PHASE_ARG);
+    {
+      // re-read through the opaque kernarg pointer: not pinned in SGPRs across the GP loop
+      float* dno = opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr())->dn_out;
+      if (act && dno) KF_PX(dno, 0, p) = dn;
+    }
     acc += act ? (double)dn : 0.0;
     acc1 += act ? (double)dn1 : 0.0;
   }
@@ -139,13 +149,19 @@ __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs 
   double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
-  for (int64_t base = (int64_t)blockIdx.x * BLOCK + (threadIdx.x - lane); base < a.N; base += stride) {
+  const int64_t nv = visit_count(a);
+  for (int64_t base = (int64_t)blockIdx.x * BLOCK + (threadIdx.x - lane); base < nv; base += stride) {
     const int64_t q = base + lane;
-    const bool act = q < a.N;
-    const int64_t p = visit_px(a.order, act ? q : a.N - 1);
+    const bool act = q < nv;
+    const int64_t p = visit_px(a.order, act ? q : nv - 1);
     float dn1;
     const float dn = pixel_analysis_mfma<NP, D, FOBS, true, PF, BAND_LAYOUT_RUNTIME, IL, SPEC>(
         a, p, act, nullptr, dn1 KF_PHASE_ARG);
+    {
+      // re-read through the opaque kernarg pointer: not pinned in SGPRs across the GP loop
+      float* dno = opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr())->dn_out;
+      if (act && dno) KF_PX(dno, 0, p) = dn;
+    }
     acc += act ? (double)dn : 0.0;
     acc1 += act ? (double)dn1 : 0.0;
   }

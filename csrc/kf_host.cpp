@@ -2,6 +2,7 @@
 // Compiled by g++ (-fopenmp); the math is byte-for-byte the source the
 // gfx950 kernels run, so CPU CI exercises the kernel code paths.
 #include <omp.h>
+#include <math.h>
 #include <string.h>
 #include "kf_launch.h"
 #include <algorithm>
@@ -40,13 +41,17 @@ static void grid_stride(int64_t N, int grid, double* partials, F&& f) {
 template <int NP>
 static int h_analysis(const AnalysisArgs& a, int grid) {
   const int64_t stride = (int64_t)grid * HBLOCK;
+  const int64_t nv = visit_count(a);
 #pragma omp parallel for schedule(dynamic, 4)
   for (int b = 0; b < grid; ++b) {
     double acc = 0.0, acc1 = 0.0;
     for (int t = 0; t < HBLOCK; ++t)
-      for (int64_t q = (int64_t)b * HBLOCK + t; q < a.N; q += stride) {
+      for (int64_t q = (int64_t)b * HBLOCK + t; q < nv; q += stride) {
         float dn1;
-        acc += (double)pixel_analysis<NP>(a, visit_px(a.order, q), dn1);
+        const int64_t p = visit_px(a.order, q);
+        const float dn = pixel_analysis<NP>(a, p, dn1);
+        if (a.dn_out) a.dn_out[p] = dn;
+        acc += (double)dn;
         acc1 += (double)dn1;
       }
     if (a.partials) a.partials[b] = acc;
@@ -190,6 +195,82 @@ int host_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int G, int
   }
   return 0;
 }
+// Per-chunk Gauss-Newton convergence: the device kernels' arithmetic in the
+// same order (thread-strided f64 sums, the xor shuffle tree of wave_sum, the
+// wave sums in order), so a chunk's sum is bit-identical on both paths.
+int host_chunk_partials(const ChunkPartialArgs& a) {
+  constexpr int T = HBLOCK;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int c = 0; c < a.n_local; ++c) {
+    const int g = a.lc_gid[c];
+    if (!a.active[g]) continue;
+    double acc[T];
+    for (int t = 0; t < T; ++t) acc[t] = 0.0;
+    for (int sg = a.lc_ptr[c]; sg < a.lc_ptr[c + 1]; ++sg) {
+      const int st = a.seg_start[sg], len = a.seg_len[sg];
+      for (int t = 0; t < T; ++t)
+        for (int i = t; i < len; i += T) acc[t] += (double)a.dn[st + i];
+    }
+    double tot = 0.0;
+    for (int w = 0; w < T / 64; ++w) {
+      double v[64];
+      for (int l = 0; l < 64; ++l) v[l] = acc[64 * w + l];
+      for (int off = 32; off > 0; off >>= 1) {
+        double nv[64];
+        for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+        for (int l = 0; l < 64; ++l) v[l] = nv[l];
+      }
+      tot += v[0];
+    }
+    a.part[g] = tot;
+  }
+  return 0;
+}
+
+int host_chunk_decide(const ChunkDecideArgs& a) {
+  double mx = 0.0;
+  int n_act = 0, px = 0, n_new = 0;
+  for (int g = 0; g < a.nc; ++g) {
+    const bool was = a.active[g] != 0;
+    bool stop = false;
+    if (was) {
+      double tot = 0.0;
+      for (int r = 0; r < a.world; ++r) tot += a.part_all[(int64_t)r * a.nc + g];
+      const double norm = sqrt(tot > 0.0 ? tot : 0.0) / a.len_x[g];
+      mx = std::max(mx, norm);
+      stop = chunk_stops(norm, a.n_iter, a.min_iter, a.max_iter, a.tol);
+    }
+    a.newly[g] = stop ? 1 : 0;
+    if (stop) {
+      a.active[g] = 0;
+      a.iters[g] = a.n_iter;
+      ++n_new;
+    } else if (was) {
+      ++n_act;
+      px += a.local_count[g];
+    }
+  }
+  a.info[0] = (double)n_act;
+  a.info[1] = mx;
+  a.info[2] = (double)px;
+  a.info[3] = (double)n_new;
+  return 0;
+}
+
+int64_t host_chunk_compact(const ChunkCompactArgs& a) {
+  int64_t k = 0;
+  for (int64_t q = 0; q < a.n_in; ++q) {
+    const int p = a.order_in ? a.order_in[q] : (int)q;
+    const int g = a.chunk_of[p];
+    if (a.active[g]) {
+      a.order_out[k++] = p;
+    } else if (a.newly[g] && a.x_dst) {
+      for (int j = 0; j < a.np; ++j) a.x_dst[(int64_t)j * a.ld + p] = a.x_src[(int64_t)j * a.ld + p];
+    }
+  }
+  return k;
+}
+
 int host_lut_nearest(const float* lut, int M, int D, const float* x, int64_t N, int64_t ld, int32_t* out) {
 #pragma omp parallel for schedule(static)
   for (int64_t p = 0; p < N; ++p) {

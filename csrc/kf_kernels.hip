@@ -377,6 +377,176 @@ hipError_t dev_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int 
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Per-chunk Gauss-Newton convergence (kf_core.h ChunkPartialArgs ...).
+
+// One workgroup per local chunk: thread t sums column offsets t, t + 256, ..
+// of the chunk's runs in row order, then a fixed shuffle tree per wave and the
+// wave sums in wave order (block_partial) -- the host runner repeats exactly
+// this order (kf_host.cpp), so a chunk's sum does not depend on the device or
+// on the order the analysis visited its pixels in.
+__global__ __launch_bounds__(BLOCK) void chunk_partials_kernel(ChunkPartialArgs a) {
+  const int c = blockIdx.x;
+  const int g = a.lc_gid[c];
+  if (!a.active[g]) return;   // frozen: its sum is no longer read (workgroup-uniform)
+  double acc = 0.0;
+  for (int sg = a.lc_ptr[c]; sg < a.lc_ptr[c + 1]; ++sg) {
+    const int st = a.seg_start[sg], len = a.seg_len[sg];
+    for (int i = threadIdx.x; i < len; i += BLOCK) acc += (double)a.dn[st + i];
+  }
+  __shared__ double red[BLOCK / 64];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < BLOCK / 64; ++w) t += red[w];
+    a.part[g] = t;
+  }
+}
+
+constexpr int DEC_BLOCK = 1024;
+__global__ __launch_bounds__(DEC_BLOCK) void chunk_decide_kernel(ChunkDecideArgs a) {
+  __shared__ double smax[DEC_BLOCK / 64];
+  __shared__ int sact[DEC_BLOCK / 64], spx[DEC_BLOCK / 64], snew[DEC_BLOCK / 64];
+  double mx = 0.0;
+  int n_act = 0, px = 0, n_new = 0;
+  for (int g = threadIdx.x; g < a.nc; g += DEC_BLOCK) {
+    const bool was = a.active[g] != 0;
+    bool stop = false;
+    if (was) {
+      double tot = 0.0;
+      for (int r = 0; r < a.world; ++r) tot += a.part_all[(int64_t)r * a.nc + g];   // rank order
+      const double norm = sqrt(tot > 0.0 ? tot : 0.0) / a.len_x[g];
+      mx = norm > mx ? norm : mx;
+      stop = chunk_stops(norm, a.n_iter, a.min_iter, a.max_iter, a.tol);
+    }
+    a.newly[g] = stop ? 1 : 0;
+    if (stop) {
+      a.active[g] = 0;
+      a.iters[g] = a.n_iter;
+      ++n_new;
+    } else if (was) {
+      ++n_act;
+      px += a.local_count[g];
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const double om = __shfl_xor(mx, off, 64);
+    mx = om > mx ? om : mx;
+    n_act += __shfl_xor(n_act, off, 64);
+    px += __shfl_xor(px, off, 64);
+    n_new += __shfl_xor(n_new, off, 64);
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    smax[wv] = mx;
+    sact[wv] = n_act;
+    spx[wv] = px;
+    snew[wv] = n_new;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = 0.0;
+    int na = 0, np_ = 0, nn = 0;
+    for (int w = 0; w < DEC_BLOCK / 64; ++w) {
+      m = smax[w] > m ? smax[w] : m;
+      na += sact[w];
+      np_ += spx[w];
+      nn += snew[w];
+    }
+    a.info[0] = (double)na;
+    a.info[1] = m;
+    a.info[2] = (double)np_;
+    a.info[3] = (double)nn;
+  }
+}
+
+// Stable compaction of the visiting order to the active chunks' pixels, the
+// x of pixels whose chunk stopped at this iteration copied into the next
+// launch's output buffer on the way (16 consecutive slots per thread): counts
+// per 4096-slot block, a scan (obs_scan_kernel), a scatter.
+constexpr int CMP_PT = 16;
+static_assert(BLOCK * CMP_PT == KF_CMP_CHUNK, "compaction block");
+
+__device__ __forceinline__ int cmp_slot_px(const ChunkCompactArgs& a, int64_t q) {
+  return a.order_in ? a.order_in[q] : (int)q;
+}
+
+__global__ __launch_bounds__(BLOCK) void chunk_count_kernel(ChunkCompactArgs a) {
+  __shared__ int red[BLOCK / 64];
+  const int64_t q0 = (int64_t)blockIdx.x * KF_CMP_CHUNK + (int64_t)threadIdx.x * CMP_PT;
+  int n = 0;
+  for (int i = 0; i < CMP_PT; ++i) {
+    const int64_t q = q0 + i;
+    if (q >= a.n_in) break;
+    const int p = cmp_slot_px(a, q);
+    const int g = a.chunk_of[p];
+    if (a.active[g]) {
+      ++n;
+    } else if (a.newly[g] && a.x_dst) {
+      for (int j = 0; j < a.np; ++j) a.x_dst[(int64_t)j * a.ld + p] = a.x_src[(int64_t)j * a.ld + p];
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) n += __shfl_xor(n, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < BLOCK / 64; ++w) t += red[w];
+    a.counts[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void chunk_scatter_kernel(ChunkCompactArgs a) {
+  __shared__ int wtot[BLOCK / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t q0 = (int64_t)blockIdx.x * KF_CMP_CHUNK + (int64_t)threadIdx.x * CMP_PT;
+  uint32_t keep = 0;
+  int px[CMP_PT];
+  for (int i = 0; i < CMP_PT; ++i) {
+    const int64_t q = q0 + i;
+    px[i] = 0;
+    if (q < a.n_in) {
+      px[i] = cmp_slot_px(a, q);
+      if (a.active[a.chunk_of[px[i]]]) keep |= 1u << i;
+    }
+  }
+  const int n = __popc(keep);
+  int v = n;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  if (lane == 63) wtot[wv] = v;
+  __syncthreads();
+  int base = a.counts[blockIdx.x] + v - n;
+  for (int w = 0; w < wv; ++w) base += wtot[w];
+  for (int i = 0; i < CMP_PT; ++i)
+    if ((keep >> i) & 1u) a.order_out[base++] = px[i];
+}
+
+int chunk_compact_blocks(int64_t n) { return (int)((n + KF_CMP_CHUNK - 1) / KF_CMP_CHUNK); }
+
+hipError_t dev_chunk_partials(const ChunkPartialArgs& a, hipStream_t s) {
+  if (a.n_local > 0) hipLaunchKernelGGL(chunk_partials_kernel, dim3(a.n_local), dim3(BLOCK), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t dev_chunk_decide(const ChunkDecideArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(chunk_decide_kernel, dim3(1), dim3(DEC_BLOCK), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t dev_chunk_compact(const ChunkCompactArgs& a, hipStream_t s) {
+  const int nb = chunk_compact_blocks(a.n_in);
+  if (nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(chunk_count_kernel, dim3(nb), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(obs_scan_kernel<1>, dim3(1), dim3(1024), 0, s, a.counts, nb);
+  hipLaunchKernelGGL(chunk_scatter_kernel, dim3(nb), dim3(BLOCK), 0, s, a);
+  return hipGetLastError();
+}
+
 bool gp_operator_supported(int np, int d) {
   return (np == 10 && (d == 10 || d == 4)) || (np == 7 && (d == 7 || d == 4)) || (np == d && np >= 2 && np <= 4);
 }

@@ -53,6 +53,16 @@ int reg_rho_blocks(int64_t N);
 hipError_t dev_reg_rho(const float* vrow, const StripGeo& g, int64_t N, const RegScheduleArgs& a, hipStream_t s);
 hipError_t dev_reg_schedule(const RegScheduleArgs& a, hipStream_t s);
 
+// per-chunk Gauss-Newton convergence (kf_core.h ChunkPartialArgs ...)
+constexpr int KF_CMP_CHUNK = 4096;   // visiting slots per compaction workgroup
+int chunk_compact_blocks(int64_t n);
+hipError_t dev_chunk_partials(const ChunkPartialArgs& a, hipStream_t s);
+hipError_t dev_chunk_decide(const ChunkDecideArgs& a, hipStream_t s);
+hipError_t dev_chunk_compact(const ChunkCompactArgs& a, hipStream_t s);
+int host_chunk_partials(const ChunkPartialArgs& a);
+int host_chunk_decide(const ChunkDecideArgs& a);
+int64_t host_chunk_compact(const ChunkCompactArgs& a);
+
 // Host runner: the same per-pixel code over OpenMP; the block partition
 // mirrors the device grid-stride mapping so partials have the same meaning.
 bool host_supported(int np);

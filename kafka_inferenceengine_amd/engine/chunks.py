@@ -1,0 +1,144 @@
+"""Per-chunk Gauss-Newton convergence: the reference's driver semantics on one filter.
+
+The reference never runs a whole tile as one filter.  Its drivers cut the
+raster with ``get_chunks`` (256² in ``kafka_test_Py36.py:241``, 128² in
+``kafka_test_S2.py:202``) and give every chunk its own ``LinearKalman``
+(``kafka_test_Py36.py:147-187``), so the Gauss-Newton exit test
+``||x_a - x_prev||_2 / len(x_a) < tol`` (``linear_kf.py:293-304``) is taken over
+ONE chunk: each chunk runs its own number of iterations.  Over a whole tile
+the same test is vacuous (the norm scales like rms(dx) / sqrt(n_p N)).
+
+``ChunkConvergence`` keeps the engine's one device state per rank and applies
+the test per chunk (``EngineConfig.convergence_chunk``):
+
+* the analysis writes each pixel's |x - x0|^2 (``AnalysisArgs.dn_out``);
+* ``chunk_partials`` sums them per chunk over this rank's pixels in a fixed
+  order (runs of one raster row, row order: independent of the visiting order
+  and of the device);
+* the per-chunk partials of every rank are all-gathered (C1: one f64 per
+  chunk, ~15 KB for a 10980² granule in 256² chunks) and summed in rank order
+  by ``chunk_decide`` -- the same decision on every rank -- which marks the
+  chunks that stop now;
+* ``chunk_compact`` removes the stopped chunks' pixels from the visiting
+  order (stable, so the observed-first order of ``obs_order`` survives) and
+  copies their final x into the next launch's output buffer: later launches
+  visit only the chunks still iterating, and the loop ends when none is left.
+
+Chunk ids follow ``get_chunks`` (X-major; ``chunk_no`` - 1); chunks without
+active pixels are never tested (the reference's farm skips them,
+``kafka_test_Py36.py:154``).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..ops import kernels as K
+
+
+def chunk_grid(shape, block):
+    """(nxb, nyb) chunk counts of ``get_chunks(W, H, block)`` over a raster of
+    ``shape`` = (H, W); ``block`` = (x size, y size) as in get_chunks."""
+    H, W = shape
+    bx, by = int(block[0]), int(block[1])
+    if bx < 1 or by < 1:
+        raise ValueError(f"convergence_chunk {block}: sizes must be >= 1")
+    return -(-W // bx), -(-H // by)
+
+
+def chunk_counts(state_mask, block) -> np.ndarray:
+    """Active pixels per chunk, indexed by get_chunks order (chunk_no - 1)."""
+    m = np.asarray(state_mask).astype(bool)
+    H, W = m.shape
+    bx, by = int(block[0]), int(block[1])
+    nxb, nyb = chunk_grid(m.shape, block)
+    pad = np.zeros((nyb * by, nxb * bx), dtype=np.int64)
+    pad[:H, :W] = m
+    cnt = pad.reshape(nyb, by, nxb, bx).sum(axis=(1, 3))      # [Y, X]
+    return np.ascontiguousarray(cnt.T).reshape(-1)              # X-major: X * nyb + Y
+
+
+class ChunkConvergence:
+    """Device state of the per-chunk Gauss-Newton test for one rank's strip."""
+
+    def __init__(self, partition, block, n_params: int, device, comm):
+        self.block = (int(block[0]), int(block[1]))
+        self.comm = comm
+        self.device = torch.device(device)
+        self.n_params = int(n_params)
+        H, W = partition.shape
+        bx, by = self.block
+        self.nxb, self.nyb = chunk_grid((H, W), self.block)
+        self.nc = self.nxb * self.nyb
+        counts = chunk_counts(partition.state_mask, self.block)
+        N = partition.N
+        self.N = N
+        idx = np.asarray(partition.local_idx, dtype=np.int64)
+        r_loc = idx // W
+        col = idx % W
+        gid = (col // bx) * self.nyb + (r_loc + partition.r0) // by
+        # runs of consecutive local pixels within one (raster row, chunk column)
+        key = r_loc * self.nxb + col // bx
+        starts = np.flatnonzero(np.r_[True, np.diff(key) != 0]) if N else np.zeros(0, np.int64)
+        lens = np.diff(np.r_[starts, N]) if N else np.zeros(0, np.int64)
+        seg_g, seg_row = gid[starts], r_loc[starts]
+        o = np.lexsort((seg_row, seg_g))
+        seg_start, seg_len, sg = starts[o], lens[o], seg_g[o]
+        lc_gid, first = np.unique(sg, return_index=True)
+        lc_ptr = np.r_[first, sg.size]
+        local_count = np.bincount(gid, minlength=self.nc) if N else np.zeros(self.nc, np.int64)
+        i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(self.device)  # noqa: E731
+        self.seg_start, self.seg_len = i32(seg_start), i32(seg_len)
+        self.lc_ptr, self.lc_gid = i32(lc_ptr), i32(lc_gid)
+        self.chunk_of = i32(gid) if N else torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.local_count = i32(local_count)
+        self.counts = counts
+        self.len_x = torch.from_numpy(np.maximum(counts, 1) * float(self.n_params)).to(self.device)
+        self.active0 = torch.from_numpy((counts > 0).astype(np.uint8)).to(self.device)
+        self.active = self.active0.clone()
+        self.newly = torch.zeros(self.nc, dtype=torch.uint8, device=self.device)
+        self.iters = torch.zeros(self.nc, dtype=torch.int32, device=self.device)
+        self.part = torch.zeros(self.nc, dtype=torch.float64, device=self.device)
+        self.info = torch.zeros(4, dtype=torch.float64, device=self.device)
+        self.dn = torch.zeros(max(N, 1), dtype=torch.float32, device=self.device)
+        self.orders = [torch.empty(max(N, 1), dtype=torch.int32, device=self.device) for _ in range(2)]
+        self.scratch = K.chunk_compact_scratch(max(N, 1), self.device)
+        self.tested = int((counts > 0).sum())   # chunks with active pixels (all ranks)
+
+    def begin(self):
+        """A new date: every chunk with active pixels iterates."""
+        self.active.copy_(self.active0)
+        self.iters.zero_()
+
+    def decide(self, n_iter: int, tol: float, min_iter: int, max_iter: int):
+        """Per-chunk norms of the last launch's dn and the exit test; returns
+        a pending read-back of (active chunks, largest norm, this rank's
+        active pixels, chunks stopped now)."""
+        from ..parallel.comm import PendingSum
+
+        if self.N:
+            K.chunk_partials(self.dn, self.seg_start, self.seg_len, self.lc_ptr, self.lc_gid, self.active, self.part)
+        part_all = self.comm.all_gather_vec(self.part)
+        K.chunk_decide(part_all, self.comm.world, self.len_x, self.local_count, tol, n_iter, min_iter, max_iter,
+                       self.active, self.newly, self.iters, self.info)
+        return PendingSum(self.info, 1, 4)
+
+    def compact(self, order_in, n_in: int, n_out: int, x_src, x_dst):
+        """Visiting order of the next launch (the active chunks' pixels of
+        order_in[:n_in]); the stopped chunks' x copied x_src -> x_dst."""
+        out = self.orders[0]
+        if order_in is not None and order_in.data_ptr() == out.data_ptr():
+            out = self.orders[1]
+        if n_in:
+            got = K.chunk_compact(order_in, n_in, self.chunk_of, self.active, self.newly, self.scratch, out,
+                                  x_src, x_dst)
+            if got is not None and got != n_out:
+                raise RuntimeError(f"chunk_compact kept {got} pixels, chunk_decide counted {n_out}")
+        return out
+
+    def histogram(self) -> dict:
+        """{Gauss-Newton iterations: chunks} of the date (every rank's chunks)."""
+        it = self.iters.cpu().numpy()
+        it = it[self.counts > 0]
+        vals, cnt = np.unique(it, return_counts=True)
+        return {int(v): int(c) for v, c in zip(vals, cnt)}

@@ -20,6 +20,16 @@ class EngineConfig:
     convergence_tolerance: float = 1e-3
     min_iterations: int = 2
     max_iterations: int = 25
+    # per-chunk exit test (reference driver semantics, engine/chunks.py): [x size,
+    # y size] of get_chunks tiles (kafka_test_Py36.py:241: 256^2; kafka_test_S2.py:202:
+    # 128^2) whose ||dx|| / len(x) is tested on its own, converged chunks frozen;
+    # None: one test over the whole tile / strip set (the norm of one filter)
+    convergence_chunk: list | None = None
+    # analysis precision stored per date: "auto" keeps what the next forecast
+    # reads (LAI propagator: the TLAI diagonal; prior reset: nothing) unless a
+    # checkpoint is due, the date is the run's last, the output is not fused or
+    # another consumer needs it; "always": every packed row, every date
+    store_precision: str = "auto"
     # analysis
     analysis_form: str = "information"        # 'information' (K1) | 'gain' (K1g)
     joseph: bool = False                      # Joseph-form covariance update (gain form)
@@ -112,6 +122,23 @@ class EngineConfig:
             raise ValueError("band_parallel must be >= 1")
         if self.min_iterations < 1 or self.max_iterations < self.min_iterations:
             raise ValueError("bad iteration limits")
+        if self.store_precision not in ("auto", "always"):
+            raise ValueError("store_precision must be 'auto' or 'always'")
+        if self.convergence_chunk is not None:
+            cc = self.convergence_chunk
+            if isinstance(cc, (int, float)):
+                cc = [int(cc), int(cc)]
+            if isinstance(cc, str):
+                cc = [int(v) for v in cc.replace("x", ",").split(",")]
+            cc = [int(v) for v in cc]
+            if len(cc) == 1:
+                cc = cc * 2
+            if len(cc) != 2 or min(cc) < 1:
+                raise ValueError("convergence_chunk must be [x size, y size] >= 1 (or one size)")
+            self.convergence_chunk = cc
+            if self.spatial_gamma > 0 or self.analysis_form != "information" or self.band_parallel > 1:
+                raise ValueError("convergence_chunk runs the information form without the spatial prior or "
+                                 "band-parallel")
         return self
 
     # ------------------------------------------------------------- IO

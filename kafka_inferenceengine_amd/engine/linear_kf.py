@@ -151,6 +151,9 @@ class LinearKalman:
         self.reg_tiled_launches = 0       # K9 temporal-blocking launches (kf_reg_tiled.hip)
         self.reg_overlapped_sweeps = 0    # C2 sweeps whose halo exchange ran under the interior rows
         self._output_written = None
+        self._chunks = None               # per-chunk convergence state (config.convergence_chunk)
+        self.last_chunk_iters = None      # {GN iterations: chunks} of the last date (chunked test)
+        self._full_precision_step = False
         band = getattr(self.comm, "band", None)
         self.band_comm = band if (band is not None and band.world > 1) else None
         self._bp_buf = None
@@ -242,6 +245,7 @@ class LinearKalman:
         st = self._materialize(st)
         if st.kind == kind:
             return st
+        st.require_full("the precision / covariance conversion")
         out = torch.empty_like(st.P)
         K.invert(self.n_params, st.P, out, N=st.N)
         return KFState(st.x, out, kind, st.N)
@@ -274,7 +278,15 @@ class LinearKalman:
             if resume_t is not None and timestep <= resume_t:
                 continue
             advance = analysis is not None and (not is_first or resume_t is not None)
-            analysis = self.step(timestep, locate_times, analysis if advance else forecast, advance, all_dates)
+            # the precision policy (store_precision="auto") keeps the full analysis
+            # precision where it is read: the returned final state, checkpoints
+            self._full_precision_step = (step_i == len(steps) - 1 or (
+                ckpt is not None and bool(self.config.checkpoint_every)
+                and (step_i + 1) % self.config.checkpoint_every == 0))
+            try:
+                analysis = self.step(timestep, locate_times, analysis if advance else forecast, advance, all_dates)
+            finally:
+                self._full_precision_step = False
             if ckpt is not None and self.config.checkpoint_every and (step_i + 1) % self.config.checkpoint_every == 0:
                 with self.timer.phase("checkpoint"):
                     ckpt.save(timestep, analysis)
@@ -529,9 +541,11 @@ class LinearKalman:
                         self.observations.prefetch(d_ahead)
                 if nxt and self.config.lookahead:
                     self._lookahead_fn = lambda d=nxt[0]: self._prepare_date(d)
+                rows = self._precision_rows(last_of_step=i == len(locate_times) - 1, more_dates=bool(nxt))
                 try:
                     res = self.do_all_bands_state(step, bands, forecast,
-                                                  table=prep[2] if (prep is not None and prep[1] is bands) else None)
+                                                  table=prep[2] if (prep is not None and prep[1] is bands) else None,
+                                                  store_rows=rows)
                 finally:
                     self._lookahead_fn = None
             forecast = res.state
@@ -539,6 +553,9 @@ class LinearKalman:
             info["norms"].append(res.norms[-1] if res.norms else None)
             rec = {"event": "date", "date": step.isoformat(), "n_iter": res.n_iter, "norms": res.norms,
                    "wall_s": time.perf_counter() - t0, "phases_ms": self.timer.snapshot()}
+            if self.last_chunk_iters is not None:
+                rec["chunk_iters"] = self.last_chunk_iters
+                info.setdefault("chunk_iters", []).append(self.last_chunk_iters)
             if self._reg_log:
                 rec["spatial"] = self._spatial_record()
             if self.metrics.enabled:
@@ -712,11 +729,18 @@ class LinearKalman:
         return (x, None, P, inn) if res.state.kind == PRECISION else (x, P, None, inn)
 
     def do_all_bands_state(self, timestep, bands, forecast: KFState, innovations=None,
-                           table=None) -> AssimilationResult:
-        """Gauss-Newton loop on device (linear_kf.py:245-307)."""
+                           table=None, store_rows=None) -> AssimilationResult:
+        """Gauss-Newton loop on device (linear_kf.py:245-307).
+
+        ``store_rows``: the packed precision rows the caller needs of the
+        analysis (None: all; a set of row indices otherwise, see
+        :meth:`_precision_rows`); the returned state marks the others invalid.
+        With ``EngineConfig.convergence_chunk`` the exit test runs per chunk
+        (:meth:`_gn_chunked`)."""
         cfg = self.config
         n = self.n_params
         N = self.N
+        self.last_chunk_iters = None
         specs = [s for s, _ in bands]
         dbs = [d for _, d in bands]
         need_inn = cfg.return_innovations if innovations is None else innovations
@@ -731,7 +755,12 @@ class LinearKalman:
             nb_all = getattr(self.observations, "bands_per_observation", {}).get(timestep) \
                 if hasattr(self.observations, "bands_per_observation") else None
             self._band_parallel_check(specs, nb_all)
-        split = None if (precomp or gain or bp or cfg.spatial_gamma > 0) else self._split_plan(specs, dbs, h0_outs)
+        chunked = bool(cfg.convergence_chunk)
+        if chunked and (gain or bp or cfg.spatial_gamma > 0):
+            raise ValueError("convergence_chunk runs the information form without band-parallel or the spatial "
+                             "prior (the spatial prior couples the chunks)")
+        split = None if (precomp or gain or bp or cfg.spatial_gamma > 0 or chunked) else \
+            self._split_plan(specs, dbs, h0_outs)
         if precomp or split:
             table = None
         elif h0_outs is not None:
@@ -770,6 +799,18 @@ class LinearKalman:
         if ((plain or spatial or (gain and not precomp)) and N and cfg.fuse_output
                 and hasattr(self.output, "device_targets")):
             out_t = self.output.device_targets(self, self.device)
+        # analysis precision rows stored (EngineConfig.store_precision): a mask of
+        # the rows the caller reads (0: all); no row at all -> no precision store.
+        # Paths whose output is dumped from the state afterwards keep every row
+        a_rows, p_valid = 0, None
+        if (store_rows is not None and not (gain or cfg.hessian_correction or cfg.spatial_gamma > 0)
+                and (out_t is not None or self.output is None)):
+            p_valid = 0
+            for r in store_rows:
+                p_valid |= 1 << int(r)
+            a_rows = p_valid
+            if p_valid == 0:
+                P_out = None
         # GN iterations 1 and 2 in one launch (the first never ends the loop): rank-
         # independent test, so every rank queues the same collectives
         fuse2 = (plain and cfg.fuse_gn and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
@@ -797,109 +838,115 @@ class LinearKalman:
         # cannot end the loop), fused with the regularised prepare of the second
         first_plain = spatial and cfg.spatial_first_plain and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
         fuse_sp = first_plain and cfg.fuse_gn
-        while True:
-            # the analysis precision is only needed from the iteration that can
-            # end the loop on: skip its 4*ntri B/px store before min_iterations
-            A_keep = P_out if n_iter >= cfg.min_iterations else None
-            out_now = out_t if n_iter >= cfg.min_iterations else None
-            if precomp:
-                pre = self._precompute_host(specs, dbs, x_prev)
-                table = build_table(specs, dbs, n, self._cache, self.device, h0_outs, pre)
-            if fuse2 or fuse_sp:
-                # iterations 1 + 2 in one launch: outputs of iteration 2 (which can end the loop)
-                red2 = self._red_hist[1:3]
-                with self.timer.phase("analysis"):
-                    if N:
-                        if fuse_sp:
-                            self._regularised_iteration(table, x_prev, fc, x_new, P_out, status, prop, out_t,
-                                                        final=True, partials_first=self._partials1)
+        if chunked:
+            x_prev, n_iter, norms = self._gn_chunked(table, specs, dbs, precomp, prop, fc, x_prev, x_new, P_out,
+                                                     status, order, out_t, h0_outs, a_rows)
+        else:
+            while True:
+                # the analysis precision is only needed from the iteration that can
+                # end the loop on: skip its 4*ntri B/px store before min_iterations
+                A_keep = P_out if n_iter >= cfg.min_iterations else None
+                out_now = out_t if n_iter >= cfg.min_iterations else None
+                if precomp:
+                    pre = self._precompute_host(specs, dbs, x_prev)
+                    table = build_table(specs, dbs, n, self._cache, self.device, h0_outs, pre)
+                if fuse2 or fuse_sp:
+                    # iterations 1 + 2 in one launch: outputs of iteration 2 (which can end the loop)
+                    red2 = self._red_hist[1:3]
+                    with self.timer.phase("analysis"):
+                        if N:
+                            if fuse_sp:
+                                self._regularised_iteration(table, x_prev, fc, x_new, P_out, status, prop, out_t,
+                                                            final=True, partials_first=self._partials1)
+                            else:
+                                K.analysis(n, table, x_prev, None if prop is not None else fc.x,
+                                           None if prop is not None else fc.P, x_new, P_out, None, status,
+                                           self._partials, N=N, prop=prop, out=out_t, gn_fused=2,
+                                           partials_first=self._partials1, order=order, a_rows=a_rows)
+                            K.reduce_partials(self._partials1, red2[0:1])
+                            K.reduce_partials(self._partials, red2[1:2])
                         else:
-                            K.analysis(n, table, x_prev, None if prop is not None else fc.x,
-                                       None if prop is not None else fc.P, x_new, P_out, None, status,
-                                       self._partials, N=N, prop=prop, out=out_t, gn_fused=2,
-                                       partials_first=self._partials1, order=order)
-                        K.reduce_partials(self._partials1, red2[0:1])
-                        K.reduce_partials(self._partials, red2[1:2])
-                    else:
-                        red2.zero_()
-                with self.timer.phase("converge"):
-                    pend2 = self.comm.sum_f64_async(red2)
-                fuse2 = fuse_sp = False
-                deferred.append((1, pend2.column(0)))
-                pend = pend2.column(1)
-                n_iter = 2
-                x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
-                if static_conv and not self._norms_needed_now():
-                    # norm 2 is exactly 0: converged.  Norm 1 is read after the
-                    # next launch is queued (no host wait between the steps)
-                    if self._lookahead_fn is not None:
-                        self._lookahead_fn()
-                        self._lookahead_fn = None
-                    self._resolve_lazy_norms()
-                    norms = [None, 0.0]
-                    self._lazy_norms.append((norms, deferred[0][1], pend, len_x, len(bands)))
-                    deferred = []
+                            red2.zero_()
+                    with self.timer.phase("converge"):
+                        pend2 = self.comm.sum_f64_async(red2)
+                    fuse2 = fuse_sp = False
+                    deferred.append((1, pend2.column(0)))
+                    pend = pend2.column(1)
+                    n_iter = 2
+                    x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
+                    if static_conv and not self._norms_needed_now():
+                        # norm 2 is exactly 0: converged.  Norm 1 is read after the
+                        # next launch is queued (no host wait between the steps)
+                        if self._lookahead_fn is not None:
+                            self._lookahead_fn()
+                            self._lookahead_fn = None
+                        self._resolve_lazy_norms()
+                        norms = [None, 0.0]
+                        self._lazy_norms.append((norms, deferred[0][1], pend, len_x, len(bands)))
+                        deferred = []
+                        break
+                else:
+                    with self.timer.phase("analysis"):
+                        if N:
+                            if gain:
+                                K.gain(n, table, x_prev, None if prop else fc.x, None if prop else fc.P, x_new, A_keep,
+                                       status, self._partials, N=N, joseph=cfg.joseph, prop=prop, out=out_now)
+                            elif first_plain and n_iter == 1:
+                                # the unfused form of fuse_sp's first iteration (same kernel path)
+                                K.analysis(n, table, x_prev, None if prop is not None else fc.x,
+                                           None if prop is not None else fc.P, x_new, None, None, status,
+                                           self._partials, N=N, prop=prop, order=order)
+                                self._reg_log.append({"solver": "plain", "rho": 0.0, "sweeps": 0, "r2": None,
+                                                      "count": 0})
+                            elif cfg.spatial_gamma > 0:
+                                self._regularised_iteration(table, x_prev, fc, x_new, A_keep, status, prop, out_now,
+                                                            final=n_iter >= cfg.min_iterations)
+                            elif bp:
+                                self._band_parallel_iteration(table, x_prev, fc, x_new, A_keep, status)
+                            elif split is not None:
+                                self._split_iteration(split, x_prev, fc, x_new, A_keep, status)
+                            elif prop is not None:
+                                K.analysis(n, table, x_prev, None, None, x_new, A_keep, None, status, self._partials, N=N,
+                                           prop=prop, out=out_now, order=order, a_rows=a_rows)
+                            else:
+                                K.analysis(n, table, x_prev, fc.x, fc.P, x_new, A_keep, None, status, self._partials, N=N,
+                                           out=out_now, order=order, a_rows=a_rows)
+                    red = self._red_hist[min(n_iter, self._red_hist.numel() - 1):][:1]
+                    with self.timer.phase("analysis"):
+                        if N:
+                            K.reduce_partials(self._partials, red)
+                        else:
+                            red.zero_()
+                    with self.timer.phase("converge"):
+                        pend = self.comm.sum_f64_async(red)
+                    x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
+                if n_iter < cfg.min_iterations:
+                    # this iteration cannot end the loop (n_iter <= max_iterations too):
+                    # queue the next one without waiting for the norm
+                    deferred.append((n_iter, pend))
+                    n_iter += 1
+                    continue
+                if self._lookahead_fn is not None:
+                    # host preparation of the next date runs under this iteration's kernels
+                    self._lookahead_fn()
+                    self._lookahead_fn = None
+                self._resolve_lazy_norms()
+                for it, pd in deferred:
+                    norms.append(self._log_norm(pd.result(), len_x, len(bands), it))
+                deferred = []
+                convergence_norm = self._log_norm(pend.result(), len_x, len(bands), n_iter)
+                norms.append(convergence_norm)
+                if convergence_norm < cfg.convergence_tolerance and n_iter >= cfg.min_iterations:
                     break
-            else:
-                with self.timer.phase("analysis"):
-                    if N:
-                        if gain:
-                            K.gain(n, table, x_prev, None if prop else fc.x, None if prop else fc.P, x_new, A_keep,
-                                   status, self._partials, N=N, joseph=cfg.joseph, prop=prop, out=out_now)
-                        elif first_plain and n_iter == 1:
-                            # the unfused form of fuse_sp's first iteration (same kernel path)
-                            K.analysis(n, table, x_prev, None if prop is not None else fc.x,
-                                       None if prop is not None else fc.P, x_new, None, None, status,
-                                       self._partials, N=N, prop=prop, order=order)
-                            self._reg_log.append({"solver": "plain", "rho": 0.0, "sweeps": 0, "r2": None,
-                                                  "count": 0})
-                        elif cfg.spatial_gamma > 0:
-                            self._regularised_iteration(table, x_prev, fc, x_new, A_keep, status, prop, out_now,
-                                                        final=n_iter >= cfg.min_iterations)
-                        elif bp:
-                            self._band_parallel_iteration(table, x_prev, fc, x_new, A_keep, status)
-                        elif split is not None:
-                            self._split_iteration(split, x_prev, fc, x_new, A_keep, status)
-                        elif prop is not None:
-                            K.analysis(n, table, x_prev, None, None, x_new, A_keep, None, status, self._partials, N=N,
-                                       prop=prop, out=out_now, order=order)
-                        else:
-                            K.analysis(n, table, x_prev, fc.x, fc.P, x_new, A_keep, None, status, self._partials, N=N,
-                                       out=out_now, order=order)
-                red = self._red_hist[min(n_iter, self._red_hist.numel() - 1):][:1]
-                with self.timer.phase("analysis"):
-                    if N:
-                        K.reduce_partials(self._partials, red)
-                    else:
-                        red.zero_()
-                with self.timer.phase("converge"):
-                    pend = self.comm.sum_f64_async(red)
-                x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
-            if n_iter < cfg.min_iterations:
-                # this iteration cannot end the loop (n_iter <= max_iterations too):
-                # queue the next one without waiting for the norm
-                deferred.append((n_iter, pend))
+                if n_iter > cfg.max_iterations:
+                    LOG.warning("Bailing out after 25 iterations!!!!!!")
+                    break
                 n_iter += 1
-                continue
-            if self._lookahead_fn is not None:
-                # host preparation of the next date runs under this iteration's kernels
-                self._lookahead_fn()
-                self._lookahead_fn = None
-            self._resolve_lazy_norms()
-            for it, pd in deferred:
-                norms.append(self._log_norm(pd.result(), len_x, len(bands), it))
-            deferred = []
-            convergence_norm = self._log_norm(pend.result(), len_x, len(bands), n_iter)
-            norms.append(convergence_norm)
-            if convergence_norm < cfg.convergence_tolerance and n_iter >= cfg.min_iterations:
-                break
-            if n_iter > cfg.max_iterations:
-                LOG.warning("Bailing out after 25 iterations!!!!!!")
-                break
-            n_iter += 1
         if ld != x_prev.shape[1]:
             raise RuntimeError("leading dimension changed")
-        state = KFState(x_prev, P_out, COVARIANCE if gain else PRECISION, N)
+        if P_out is None:          # no precision row needed: the forecast's buffer shape, nothing valid
+            P_out = torch.empty((ntri(n), ld), dtype=torch.float32, device=self.device)
+        state = KFState(x_prev, P_out, COVARIANCE if gain else PRECISION, N, p_valid=p_valid)
         self._output_written = state if out_t is not None else None
         if cfg.hessian_correction and not gain and N:
             with self.timer.phase("hessian"):
@@ -914,6 +961,129 @@ class LinearKalman:
                 y, w = db.decode()
                 inn.append(torch.where(w > 0, y - h0[:N], torch.zeros_like(y)))
         return AssimilationResult(state, n_iter, norms, inn)
+
+    # --------------------------------------------- precision store policy
+    def _precision_rows(self, last_of_step: bool, more_dates: bool):
+        """Packed precision rows of this date's analysis that anything reads
+        (None: all).  Under ``store_precision="auto"`` the analysis of a date
+        whose state only feeds the next step's forecast stores what that
+        forecast reads -- the propagated parameters' diagonal entries for the
+        LAI propagator (kf_tools.py:292-314: [6, 6] only), nothing for a prior
+        reset (no_propagation / prior only, kf_tools.py:316-353, 165-166), the
+        diagonal for the approximate information filter -- instead of the full
+        4 ntri B/px.  Full where the state is read otherwise: the run's last
+        step or a checkpoint step, the last observation date, a date whose
+        analysis is the next date's forecast within one step, a non-fused
+        output, reference-protocol propagators, the gain form."""
+        cfg = self.config
+        if (cfg.store_precision == "always" or self._full_precision_step or not last_of_step or not more_dates
+                or cfg.analysis_form == "gain" or cfg.band_sequential or cfg.hessian_correction
+                or cfg.spatial_gamma > 0 or cfg.return_innovations):
+            return None
+        if not (cfg.fuse_output and hasattr(self.output, "device_targets")) and self.output is not None:
+            return None            # the dump reads the precision diagonal (observations.py:392-393)
+        return self._next_forecast_rows()
+
+    def _next_forecast_rows(self):
+        """Packed rows of the analysis precision the next forecast reads (None:
+        all), from the configured propagator / prior (advance_state)."""
+        from ..inference.kf_tools import PROP_PRIOR_PARTIAL, PROP_INFO_APPROX
+
+        n = self.n_params
+        prop = self._state_propagator
+        spec = getattr(prop, "device_spec", None) if prop is not None else None
+        if prop is not None and spec is None:
+            return None                       # host (reference-protocol) propagator
+        if self.prior is not None and not hasattr(self.prior, "device_prior"):
+            return None
+        if prop is None:
+            # no propagator: the prior alone resets the state (nothing read); neither: identity
+            return set() if self.prior is not None else None
+        if spec.mode == PROP_PRIOR:
+            return set()
+        if spec.mode == PROP_PRIOR_PARTIAL:
+            return {tri_pos(n, int(j), int(j)) for j in spec.propagated}
+        if spec.mode == PROP_INFO_APPROX:
+            return {tri_pos(n, j, j) for j in range(n)}
+        return None
+
+    # ------------------------------------------------ per-chunk convergence
+    def _chunk_state(self):
+        from .chunks import ChunkConvergence
+
+        cc = self._chunks
+        block = tuple(int(v) for v in self.config.convergence_chunk)
+        if cc is None or cc.block != block:
+            cc = self._chunks = ChunkConvergence(self.partition, block, self.n_params, self.device, self.comm)
+        return cc
+
+    def _gn_chunked(self, table, specs, dbs, precomp, prop, fc, x_prev, x_new, P_out, status, order, out_t,
+                    h0_outs, a_rows):
+        """Gauss-Newton loop with the exit test per chunk (engine/chunks.py;
+        reference: one LinearKalman per get_chunks tile, kafka_test_Py36.py:147-187,
+        each testing ||x_a - x_prev|| / len(x_a) < tol, linear_kf.py:293-304).
+
+        Every launch writes each visited pixel's |dx|^2; after each iteration
+        that can end the loop the chunks are tested (one C1 all-gather of the
+        per-chunk partials), and the next launch visits only the pixels of the
+        chunks still iterating (the stopped chunks' x, precision, outputs and
+        status stay as their last iteration wrote them).  Returns (x, the
+        largest chunk's iteration count, the largest tested norm per
+        iteration)."""
+        cfg = self.config
+        n, N = self.n_params, self.N
+        cc = self._chunk_state()
+        cc.begin()
+        fx, fP = (None, None) if prop is not None else (fc.x, fc.P)
+        fuse = (cfg.fuse_gn and not precomp and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
+                and not (prop is None and fc is None))
+        n_iter, n_visit, vis, full = 1, N, order, True
+        norms = []
+        while True:
+            A_keep = P_out if n_iter >= cfg.min_iterations else None
+            out_now = out_t if n_iter >= cfg.min_iterations else None
+            if precomp:
+                pre = self._precompute_host(specs, dbs, x_prev)
+                table = build_table(specs, dbs, n, self._cache, self.device, h0_outs, pre)
+            kw = dict(prop=prop, order=vis, dn_out=cc.dn, a_rows=a_rows)
+            if not full:
+                kw["n_visit"] = n_visit
+            with self.timer.phase("analysis"):
+                if N and n_visit:
+                    if fuse and n_iter == 1:
+                        K.analysis(n, table, x_prev, fx, fP, x_new, P_out, None, status, None, N=N, out=out_t,
+                                   gn_fused=2, **kw)
+                    else:
+                        K.analysis(n, table, x_prev, fx, fP, x_new, A_keep, None, status, None, N=N, out=out_now,
+                                   **kw)
+            if fuse and n_iter == 1:
+                n_iter = 2
+            x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
+            if n_iter < cfg.min_iterations:
+                n_iter += 1
+                continue
+            with self.timer.phase("converge"):
+                pend = cc.decide(n_iter, cfg.convergence_tolerance, cfg.min_iterations, cfg.max_iterations)
+            if self._lookahead_fn is not None:
+                self._lookahead_fn()
+                self._lookahead_fn = None
+            n_act, mx, px, n_new = (pend.result(j) for j in range(4))
+            n_act, px = int(n_act), int(px)
+            norms.append(float(mx))
+            LOG.info("Iteration # %d: %d of %d chunks converged, %d still iterating, largest chunk norm %g",
+                     n_iter, int(n_new), cc.tested, n_act, mx)
+            if n_act == 0:
+                break
+            if n_iter > cfg.max_iterations:      # chunk_decide bails every chunk out past max_iterations
+                raise RuntimeError("per-chunk loop past max_iterations with active chunks")
+            with self.timer.phase("converge"):
+                vis = cc.compact(vis, n_visit if N else 0, px, x_prev, x_new)
+            n_visit, full = px, False
+            n_iter += 1
+        self.last_chunk_iters = cc.histogram()
+        if max(self.last_chunk_iters or {0: 0}) > cfg.max_iterations:
+            LOG.warning("Bailing out after 25 iterations!!!!!!")
+        return x_prev, n_iter, norms
 
     def _spatial_record(self) -> list:
         """Per GN iteration of the date: solver, Jacobi bound rho, sweeps and --
@@ -1453,6 +1623,7 @@ class LinearKalman:
             # written by the analysis kernel: bookkeeping only (no device work to time)
             self.output.mark_written(timestep, state, self)
             return
+        state.require_full("the output dump")
         with self.timer.phase("output"):
             if hasattr(self.output, "dump_state"):
                 self.output.dump_state(timestep, state, self)
@@ -1468,5 +1639,6 @@ class LinearKalman:
     def unc(self, state: KFState) -> torch.Tensor:
         """1/sqrt(diag(P^-1)) per parameter, [n_p, N] (observations.py:392-393)."""
         prec = self._as_kind(state, PRECISION)
+        prec.require_full("unc")
         idx = [tri_pos(self.n_params, j, j) for j in range(self.n_params)]
         return 1.0 / torch.sqrt(prec.P[idx, :self.N])

@@ -26,6 +26,21 @@ class KFState:
     P: torch.Tensor          # [ntri, ld] float32 (packed upper triangle)
     kind: str                # PRECISION | COVARIANCE
     N: int                   # active pixels (<= ld)
+    # packed rows of P that hold values (bit t: row t); None = all.  An analysis
+    # under EngineConfig.store_precision="auto" stores only what the next
+    # forecast reads (the LAI propagator: one diagonal entry, kf_tools.py:292-314)
+    p_valid: int | None = None
+
+    @property
+    def full(self) -> bool:
+        return self.p_valid is None
+
+    def require_full(self, what: str = "this operation"):
+        if self.p_valid is not None:
+            rows = [t for t in range(self.P.shape[0]) if (self.p_valid >> t) & 1]
+            raise RuntimeError(f"{what} needs the full packed {self.kind}, but this analysis stored rows {rows} only "
+                               "(EngineConfig.store_precision='auto' keeps what the next forecast reads); set "
+                               "store_precision='always' or read the state of the run's last date")
 
     @property
     def n_params(self) -> int:
@@ -36,12 +51,13 @@ class KFState:
         return self.x.device
 
     def clone(self) -> "KFState":
-        return KFState(self.x.clone(), self.P.clone(), self.kind, self.N)
+        return KFState(self.x.clone(), self.P.clone(), self.kind, self.N, self.p_valid)
 
     def copy_(self, other: "KFState") -> "KFState":
         self.x.copy_(other.x)
         self.P.copy_(other.P)
         self.kind = other.kind
+        self.p_valid = other.p_valid
         return self
 
     @classmethod
@@ -91,11 +107,13 @@ class KFState:
 
     def to_reference(self):
         """(x_flat numpy, LazyBlockDiag of P) — the reference's (x, P / P^-1)."""
+        self.require_full("to_reference")
         x = self.x[:, :self.N].detach().cpu().numpy().astype(np.float64)
         P = self.P[:, :self.N].detach().cpu().numpy()
         return soa_to_interleaved(x), LazyBlockDiag(P, self.n_params)
 
     def numpy(self):
+        self.require_full("numpy")
         return (self.x[:, :self.N].detach().cpu().numpy(), self.P[:, :self.N].detach().cpu().numpy())
 
 

@@ -61,6 +61,8 @@ class CheckpointManager:
         barrier) by the next ``save`` or by :meth:`finish`; ``latest`` only sees
         committed checkpoints.  With band-parallel groups only band slot 0 of
         each strip writes (every member holds the same state)."""
+        if hasattr(state, "require_full"):
+            state.require_full("a checkpoint")
         import threading
         import time
 

@@ -491,9 +491,9 @@ class MultiSensorObservations:
 
     @property
     def max_prefetch(self) -> int:
-        """Dates the engine may prefetch ahead of the one being assimilated."""
-        self._ensure_pool()
-        return self._streamer.max_ahead if self._streamer is not None else 1
+        """Dates the engine may prefetch ahead of the one being assimilated
+        (the tightest source: every source prefetches each date)."""
+        return min(int(getattr(s, "max_prefetch", 1)) for s in self.sources)
 
     def ingest_bytes(self) -> int:
         return sum(s.ingest_bytes() for s in self.sources)

@@ -239,7 +239,8 @@ def gp_operator_supported(n_params, d) -> bool:
 
 def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=None, b_out=None, status=None,
              partials=None, N=None, solve=True, fast=True, variant=None, a_in=None, b_in=None, prop=None,
-             out=None, reg=None, x0_out=None, gn_fused=1, partials_first=None, order=None):
+             out=None, reg=None, x0_out=None, gn_fused=1, partials_first=None, order=None, n_visit=None,
+             dn_out=None, a_rows=None):
     """K1 fused Gauss-Newton analysis (information form).
 
     ``gn_fused=2`` runs two Gauss-Newton iterations in this launch: the first
@@ -267,7 +268,14 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     ``order`` (int32 [N], from :func:`obs_order`): the pixel visiting order --
     the observed pixels first, so cloudy pixels fill whole waves that skip the
     GP; each pixel's result is the same in any order (the per-workgroup norm
-    partials sum different pixel sets)."""
+    partials sum different pixel sets).  ``n_visit``: visit only
+    ``order[:n_visit]`` (the per-chunk Gauss-Newton loop's active pixels;
+    needs ``order``).
+
+    ``dn_out`` (float32 [N]): each visited pixel's |x - x0|^2 of the launch's
+    last iteration, at its pixel index (per-chunk convergence norms).
+    ``a_rows``: bit mask of the packed precision rows stored to ``a_out``
+    (None / 0: every row; EngineConfig.store_precision)."""
     check_np(n_params)
     ref = next(t for t in (x_prev, x_f, x_out, a_out) if t is not None)
     N = int(ref.shape[1] if N is None else N)
@@ -368,9 +376,65 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     if order is not None:
         _check_vec(order, N, "order", torch.int32, dev)
         a.order = _ptr(order)
-    grid = grid_for(N)
+    nv = N
+    if n_visit is not None:
+        nv = int(n_visit)
+        if order is None or not 0 < nv <= N:
+            raise ValueError(f"n_visit={n_visit} needs an order and 0 < n_visit <= N={N}")
+        if gn_fused != 1 or reg is not None:
+            raise ValueError("n_visit: single-iteration launches without the regulariser")
+        a.n_visit = nv
+    if dn_out is not None:
+        _check_vec(dn_out, N, "dn_out", torch.float32, dev)
+        a.dn_out = _ptr(dn_out)
+    if a_rows:
+        if int(a_rows) >> nt:
+            raise ValueError(f"a_rows has bits past the {nt} packed rows")
+        a.a_rows = int(a_rows)
+    grid = grid_for(nv)
     ext().analysis(n_params, a, grid, _dev(ref), _stream(ref))
     return partials
+
+
+# ------------------------------------------------ per-chunk convergence
+def chunk_partials(dn, seg_start, seg_len, lc_ptr, lc_gid, active, part):
+    """part[g] = sum of dn over this rank's pixels of each active chunk g
+    (fixed order, kf_kernels.hip:chunk_partials_kernel); other entries kept."""
+    n_local = int(lc_gid.numel())
+    ext().chunk_partials(_ptr(dn), _ptr(seg_start), _ptr(seg_len), _ptr(lc_ptr), _ptr(lc_gid), n_local,
+                         _ptr(active), _ptr(part), _dev(part), _stream(part))
+
+
+def chunk_decide(part_all, world, len_x, local_count, tol, n_iter, min_iter, max_iter, active, newly, iters, info):
+    """The reference's exit test per chunk (linear_kf.py:297-304) on the
+    all-gathered partials [world, nc]; info <- (active chunks, largest norm
+    tested, this rank's active pixels, chunks stopped now)."""
+    nc = int(active.numel())
+    if part_all.numel() != world * nc or len_x.numel() != nc or local_count.numel() != nc:
+        raise ValueError("chunk_decide: inconsistent chunk vectors")
+    ext().chunk_decide(_ptr(part_all), int(world), nc, _ptr(len_x), _ptr(local_count), float(tol), int(n_iter),
+                       int(min_iter), int(max_iter), _ptr(active), _ptr(newly), _ptr(iters), _ptr(info),
+                       _dev(active), _stream(active))
+
+
+def chunk_compact_scratch(n: int, device) -> torch.Tensor:
+    return torch.empty(int(ext().chunk_compact_blocks(max(int(n), 1))) + 1, dtype=torch.int32, device=device)
+
+
+def chunk_compact(order_in, n_in, chunk_of, active, newly, counts, order_out, x_src=None, x_dst=None):
+    """order_out <- the slots of order_in[:n_in] (None: 0..n_in-1) whose chunk
+    is active, stable; x of the pixels whose chunk stopped now copied x_src ->
+    x_dst ([n_p, ld]).  Returns the kept count on the host runner, None on the
+    device (chunk_decide's info holds it)."""
+    n_in = int(n_in)
+    if order_in is not None and order_in.data_ptr() == order_out.data_ptr():
+        raise ValueError("chunk_compact: order_out must not alias order_in")
+    np_, ld = (0, 0) if x_src is None else (int(x_src.shape[0]), int(x_src.shape[1]))
+    if x_src is not None and (x_dst is None or x_dst.shape != x_src.shape):
+        raise ValueError("chunk_compact: x_src / x_dst of one shape")
+    r = ext().chunk_compact(_ptr(order_in), n_in, _ptr(chunk_of), _ptr(active), _ptr(newly), _ptr(counts),
+                            _ptr(order_out), _ptr(x_src), _ptr(x_dst), np_, ld, _dev(chunk_of), _stream(chunk_of))
+    return None if r < 0 else int(r)
 
 
 _GROUP_IDS = {}   # (device, band groups) -> int32 device tensor of obs_order

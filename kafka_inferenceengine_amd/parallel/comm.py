@@ -203,6 +203,16 @@ class Comm:
         dist.all_gather(list(out.unbind(0)), local, group=self.group)
         return PendingSum(out.reshape(-1), self.world, k)
 
+    def all_gather_vec(self, t: torch.Tensor) -> torch.Tensor:
+        """C1 for vectors (per-chunk norm partials): every rank's ``t`` in rank
+        order, [world * k]; the local tensor itself on one rank."""
+        if not self.distributed:
+            return t
+        k = t.numel()
+        out = torch.empty((self.world, k), dtype=t.dtype, device=t.device)
+        dist.all_gather(list(out.unbind(0)), t.reshape(k).contiguous(), group=self.group)
+        return out.reshape(-1)
+
     def sum_int(self, v: int) -> int:
         if not self.distributed:
             return int(v)

@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU call = a list of named steps, each under its own time limit, stopping at
 # the first failure (gpurun rules: no retries, nothing after a fault/timeout).
-#   bash scripts/gpu_step.sh tests[:FILTER] mfma_ab bench[:ARGS] prof[:ARGS] pmc:COUNTERS ...
+#   bash scripts/gpu_step.sh tests[:FILTER] smoke bench[:ARGS] cfg:CONFIG[ ARGS] py:SCRIPT[ ARGS] \
+#        prof[:ARGS] pmc:V/COUNTERS ...
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && mkdir -p gpurun_out
@@ -29,6 +30,18 @@ for step in "$@"; do
     bench)
       timeout -k 10 600 python -u bench.py $arg > gpurun_out/bench.log 2>&1 || { rc=$?; tail -20 gpurun_out/bench.log; stop bench $rc; }
       tail -1 gpurun_out/bench.log ;;
+    cfg)
+      # cfg:CONFIG [bench args] -> gpurun_out/bench_CONFIG.log (one JSON line at its end)
+      c=${arg%% *}; rest=""; [ "$c" != "$arg" ] && rest=${arg#* }
+      timeout -k 10 900 python -u bench.py --config $c $rest > gpurun_out/bench_$c.log 2>&1 \
+        || { rc=$?; tail -20 gpurun_out/bench_$c.log; stop cfg_$c $rc; }
+      echo "$c $(tail -1 gpurun_out/bench_$c.log | cut -c1-300)" ;;
+    py)
+      # py:SCRIPT [args] -> gpurun_out/py_<script name>.log
+      sc=${arg%% *}; rest=""; [ "$sc" != "$arg" ] && rest=${arg#* }; tag=$(basename $sc .py)
+      timeout -k 10 900 python -u $sc $rest > gpurun_out/py_$tag.log 2>&1 \
+        || { rc=$?; tail -20 gpurun_out/py_$tag.log; stop py_$tag $rc; }
+      tail -5 gpurun_out/py_$tag.log ;;
     prof)
       ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run \
         --output-format csv -- python "$R/bench.py" --steps 4 --warmup 1 $arg > "$R/gpurun_out/prof.log" 2>&1 ) \

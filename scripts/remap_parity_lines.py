@@ -32,7 +32,8 @@ def line_map(rev: str, path: str):
         return None
     new = (ROOT / path).read_text().splitlines()
     m = {}
-    sm = difflib.SequenceMatcher(a=old, b=new, autojunk=False)
+    # compared without indentation: a block moved into (or out of) a branch keeps its lines
+    sm = difflib.SequenceMatcher(a=[ln.strip() for ln in old], b=[ln.strip() for ln in new], autojunk=False)
     for a, b, n in sm.get_matching_blocks():
         for k in range(n):
             m[a + k + 1] = b + k + 1

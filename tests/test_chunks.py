@@ -1,0 +1,207 @@
+"""Per-chunk Gauss-Newton convergence (EngineConfig.convergence_chunk, engine/chunks.py).
+
+The reference cuts the raster with get_chunks and runs one LinearKalman per
+chunk (kafka_test_Py36.py:147-187, 241; kafka_test_S2.py:202), so every chunk
+tests ||x_a - x_prev|| / len(x_a) on its own (linear_kf.py:293-304).  The
+engine applies that test per chunk on one filter; these tests pin it against
+a farm of one engine per chunk (parallel/farm.py, the reference's model) and
+across 1 / 4 / 8 gloo ranks."""
+import datetime as dt
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import kafka_inferenceengine_amd as k
+from kafka_inferenceengine_amd.engine.chunks import ChunkConvergence, chunk_counts
+from kafka_inferenceengine_amd.input_output.utils import get_chunks
+from kafka_inferenceengine_amd.parallel import Comm, StripPartition, run_chunks
+
+H, W = 80, 96
+BLOCK = 16
+TOL = 3e-4
+DATES = [dt.datetime(2017, 7, 3) + dt.timedelta(days=2 * i) for i in range(3)]
+GRID = [DATES[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in DATES]
+
+
+def _mask():
+    m = np.ones((H, W), bool)
+    m[10:20, 5:40] = False        # a masked block: ragged chunks, one chunk fully masked
+    m[64:80, 80:96] = False
+    return m
+
+
+def _engine(mask, cfg, emulators=None, comm=None, partition=None, device="cpu"):
+    """Hard PROSAIL problem (strongly non-linear emulators): chunks need
+    different iteration counts, some never meet the tolerance and bail out."""
+    obs = k.SyntheticS2Observations(mask, dates=DATES, n_bands=10, n_train=40, device=device, stream=False, n_pool=3,
+                                    hard=True, spread_scale=1.0, rel_unc=0.02, seed=1, emulators=emulators,
+                                    partition=partition)
+    prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
+    kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
+                        state_propagation=None, prior=prior, device=device, comm=comm, partition=partition,
+                        config=k.EngineConfig(convergence_tolerance=TOL, **cfg))
+    return kf, obs, prior
+
+
+def _farm(mask, emulators, device="cpu"):
+    """One LinearKalman per get_chunks tile over the chunk's window of the
+    mask (kafka_test_Py36.py:147-187): {chunk_no: (GN iterations per date,
+    global raster index, x)}."""
+    def one(chunk):
+        x0, y0, nx, ny, no = chunk
+        m = np.zeros_like(mask)
+        m[y0:y0 + ny, x0:x0 + nx] = mask[y0:y0 + ny, x0:x0 + nx]
+        kf, _, prior = _engine(m, {}, emulators, device=device)
+        st = kf.run(GRID, kf.state_from_prior(prior), None, None)
+        return ([h["gn_iterations"][0] for h in kf.history], kf.partition.global_index(),
+                st.x[:, :st.N].cpu().numpy())
+    res = run_chunks(W, H, [BLOCK, BLOCK], one, skip_empty_mask=mask)
+    return {no: r for no, r in res.items() if r is not None}   # empty chunks are skipped (None)
+
+
+def test_chunk_ids_follow_get_chunks():
+    mask = _mask()
+    cnt = chunk_counts(mask, [BLOCK, BLOCK])
+    ref = [int(mask[y0:y0 + ny, x0:x0 + nx].sum()) for x0, y0, nx, ny, _ in get_chunks(W, H, [BLOCK, BLOCK])]
+    assert cnt.tolist() == ref
+    # a strip's runs cover its pixels once, each run inside one chunk and one raster row
+    part = StripPartition(mask, 1, 3)
+    cc = ChunkConvergence(part, [BLOCK, BLOCK], 10, "cpu", Comm.single("cpu"))
+    starts, lens = cc.seg_start.numpy(), cc.seg_len.numpy()
+    cover = np.zeros(part.N, int)
+    for s, n in zip(starts, lens):
+        cover[s:s + n] += 1
+        g = cc.chunk_of.numpy()[s:s + n]
+        assert (g == g[0]).all()
+        assert len(set(part.local_idx[s:s + n] // W)) == 1
+    assert (cover == 1).all()
+    assert cc.local_count.numpy().sum() == part.N
+
+
+def test_chunked_equals_farm_of_engines():
+    """Every chunk runs the iterations its own engine runs, date by date, and
+    the state is bit-identical to the farm's (the per-pixel analysis does not
+    depend on the other chunks)."""
+    mask = _mask()
+    kf, obs, prior = _engine(mask, {"convergence_chunk": [BLOCK, BLOCK]})
+    st = kf.run(GRID, kf.state_from_prior(prior), None, None)
+    hist = [h["chunk_iters"][0] for h in kf.history]
+    farm = _farm(mask, obs.emulators)
+    for d in range(len(DATES)):
+        want = {}
+        for its, _, _ in farm.values():
+            want[its[d]] = want.get(its[d], 0) + 1
+        assert hist[d] == want, (d, hist[d], want)
+    assert len({its[0] for its, _, _ in farm.values()}) >= 3, "the problem should need several iteration counts"
+    # per chunk: the engine's recorded iteration count of each chunk
+    iters = kf._chunks.iters.numpy()
+    for no, (its, _, _) in farm.items():
+        assert iters[no - 1] == its[-1], (no, iters[no - 1], its)
+    # the state: bit-identical pixel by pixel
+    pos = {g: i for i, g in enumerate(kf.partition.global_index())}
+    x = st.x[:, :st.N].numpy()
+    for no, (_, gidx, xc) in farm.items():
+        cols = [pos[g] for g in gidx]
+        assert np.array_equal(x[:, cols], xc), no
+    # the tile-global test stops every chunk together
+    kf2, _, prior2 = _engine(mask, {})
+    kf2.run(GRID, kf2.state_from_prior(prior2), None, None)
+    assert all("chunk_iters" not in r for r in kf2.metrics.records)
+
+
+def test_chunked_fused_forecast_tip_equals_farm():
+    """JRC-TIP with the LAI propagator (forecast fused into the analysis
+    kernel, GN 1 + 2 in one launch): chunked run == one engine per chunk."""
+    mask = np.ones((48, 40), bool)
+    mask[30:40, 0:12] = False
+
+    def build(m, cfg):
+        obs = k.SyntheticBHRObservations(m, n_train=40, device="cpu", stream=False, n_pool=3, seed=5, field_cell=6)
+        kf = k.LinearKalman(obs, None, m, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device="cpu",
+                            config=k.EngineConfig(convergence_tolerance=2e-5, max_iterations=6, **cfg))
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        return kf
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(4)]
+    kf = build(mask, {"convergence_chunk": [12, 16]})
+    x0, Pinv = k.JRCPrior(k.TIP_PARAMETERS, mask).process_prior(None)
+    st = kf.run(grid, x0, None, Pinv)
+    pos = {g: i for i, g in enumerate(kf.partition.global_index())}
+    want = [{} for _ in kf.history]
+    for x_off, y_off, nx, ny, no in get_chunks(40, 48, [12, 16]):
+        m = np.zeros_like(mask)
+        m[y_off:y_off + ny, x_off:x_off + nx] = mask[y_off:y_off + ny, x_off:x_off + nx]
+        if not m.any():
+            continue
+        kc = build(m, {})
+        xc0, Pc = k.JRCPrior(k.TIP_PARAMETERS, m).process_prior(None)
+        sc = kc.run(grid, xc0, None, Pc)
+        for d, h in enumerate(kc.history):
+            it = h["gn_iterations"][0]
+            want[d][it] = want[d].get(it, 0) + 1
+        cols = [pos[g] for g in kc.partition.global_index()]
+        assert np.array_equal(st.x[:, :st.N].numpy()[:, cols], sc.x[:, :sc.N].numpy()), no
+    assert [h["chunk_iters"][0] for h in kf.history] == want
+    assert any(len(w) > 1 for w in want)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_run(rank, world, port, q):
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.set_num_threads(1)
+    try:
+        mask = _mask()
+        comm = Comm(rank, world, "cpu") if world > 1 else Comm.single("cpu")
+        part = StripPartition(mask, rank, world)
+        kf, _, prior = _engine(mask, {"convergence_chunk": [BLOCK, BLOCK]}, comm=comm, partition=part)
+        st = kf.run(GRID, kf.state_from_prior(prior), None, None)
+        q.put((rank, st.x[:, :st.N].numpy().copy(), [h["chunk_iters"] for h in kf.history],
+               kf._chunks.iters.numpy().copy()))
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def _gather(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    if world == 1:
+        _rank_run(0, 1, 0, q)
+        return [q.get()]
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_run, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in range(world)), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_chunked_ranks_equal_one_rank(world):
+    """Chunks straddle the strip boundaries (16-row chunks over 10- to 20-row
+    strips): the per-chunk partials of the ranks are all-gathered and summed in
+    rank order, so every rank takes every chunk's decision and the result
+    equals one rank's."""
+    one = _gather(1)[0]
+    res = _gather(world)
+    x = np.concatenate([r[1] for r in res], 1)
+    assert np.array_equal(x, one[1])
+    for r in res:
+        assert r[2] == one[2]
+        assert np.array_equal(r[3], one[3])
