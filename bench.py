@@ -162,6 +162,9 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
                     help="override an EngineConfig field (A/B runs), e.g. --set gp_split=never")
+    ap.add_argument("--kernel-variant", type=int, default=0,
+                    help="analysis kernel variant (ops/kernels.py Variant; A/B of a test-oracle path, e.g. 20 = "
+                         "the persistent tile queue)")
     ap.add_argument("--band-parallel", type=int, default=1,
                     help="ranks per band group (strips x band groups; multi-band configs)")
     ap.add_argument("--band-parallel-force", action="store_true",
@@ -186,6 +189,8 @@ def main():
     from kafka_inferenceengine_amd.parallel import Comm, StripPartition
 
     from kafka_inferenceengine_amd.engine.config import EngineConfig
+    from kafka_inferenceengine_amd.ops import kernels as K0
+    K0.DEFAULT_VARIANT = K0.Variant(a.kernel_variant)
 
     # band-parallel only where its C5 all-reduce pays (parallel/policy.py); else pure strips
     from kafka_inferenceengine_amd.parallel.policy import band_parallel_decision

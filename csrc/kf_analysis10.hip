@@ -5,8 +5,8 @@
 
 namespace kf {
 
-hipError_t dev_analysis_np10(const AnalysisArgs& a, int grid, hipStream_t s) {
-  l_analysis<10>(a, grid, s);
+hipError_t dev_analysis_np10(const AnalysisArgs& a, int grid, hipStream_t s, int* n_part) {
+  l_analysis<10>(a, grid, s, n_part);
   return hipGetLastError();
 }
 

@@ -120,6 +120,7 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(AnalysisArgs, order, const int32_t*)
       .def_readwrite("n_visit", &AnalysisArgs::n_visit)
       .PTR_FIELD(AnalysisArgs, dn_out, float*)
+      .PTR_FIELD(AnalysisArgs, tile_ctr, int32_t*)
       .def_readwrite("a_rows", &AnalysisArgs::a_rows)
       .def_readwrite("gn_fused", &AnalysisArgs::gn_fused)
       .def_readwrite("band_layout", &AnalysisArgs::band_layout)
@@ -226,9 +227,12 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
 #endif
   m.def("set_gp_unroll", [](int n) { set_gp_unroll(n); });
 
+  // -> norm partial entries written (device: workgroups or 64-slot tiles; host: workgroups)
   m.def("analysis", [](int np, const AnalysisArgs& a, int grid, bool device, uintptr_t stream) {
-    if (device) check_hip(dev_analysis(np, a, grid, (hipStream_t)stream), "analysis");
+    int n_part = grid;
+    if (device) check_hip(dev_analysis(np, a, grid, (hipStream_t)stream, &n_part), "analysis");
     else check_host(host_analysis(np, a, grid), "analysis");
+    return n_part;
   });
   m.def("gain", [](int np, const GainArgs& a, int grid, bool device, uintptr_t stream) {
     if (device) check_hip(dev_gain(np, a, grid, (hipStream_t)stream), "gain");

@@ -72,6 +72,73 @@ __device__ __forceinline__ void analysis_partials(const AnalysisArgs& a, double 
   else if (a.partials) block_partial<BS>(acc, a.partials);
 }
 
+// Dynamic tile scheduling of the matrix-core analysis kernels: a persistent
+// grid (occupancy-sized, launch_tiles) whose waves claim 64-slot tiles of the
+// visiting order one at a time from per-XCD counters.  Tile t belongs to
+// group t % 8; the waves of workgroup b claim from group b % 8 first (the
+// workgroups of a launch are dealt to the 8 XCDs round-robin), so the tiles
+// in flight at any moment are a contiguous window of the order -- as on the
+// static grid-stride mapping (round 5: contiguous per-wave runs of a guided
+// schedule scattered ~3000 streams over the whole raster and ran 7 % slower)
+// -- and each counter sees 1/8 of the claims (one counter for all: ~50 M
+// atomics/s device-wide was the bound, 25 % slower at 15 M px).  A wave whose
+// group is exhausted steals from the next groups, so the tail is one tile per
+// wave; the observed-first order puts the cloudy (cheap) tiles last.  The LDS
+// tables are staged once per workgroup.  The norm partials are per tile: the
+// reduction does not depend on which wave ran which tile (bit-reproducible).
+// Claims are vector atomics of lane 0 (the next claim in flight under the
+// current tile), broadcast with readfirstlane.
+constexpr int TILE_GROUPS = 8;        // XCDs of an MI355X
+constexpr int TILE_CTR_STRIDE = 32;   // int32 slots between counters (128 B: own cache lines)
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ int tile_claim_raw(int32_t* ctr) {
+  int v = 0;
+  if ((threadIdx.x & 63) == 0) v = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return v;
+}
+
+__device__ __forceinline__ const KF_CONST_AS AnalysisArgs* kargs() {
+  return opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
+}
+
+// PIX(p, act, dn1) -> dn: one visiting slot's analysis (every lane of the wave)
+template <typename PIX>
+__device__ __forceinline__ void analysis_tiles(const AnalysisArgs& a, PIX&& pix) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nv = visit_count(a);
+  const int ntile = (int)((nv + 63) >> 6);
+  const int home = (int)(blockIdx.x % TILE_GROUPS);
+  for (int s = 0; s < TILE_GROUPS; ++s) {
+    const int g = (home + s) % TILE_GROUPS;
+    const int ng = ntile > g ? (ntile - g + TILE_GROUPS - 1) / TILE_GROUPS : 0;   // tiles g, g + 8, ...
+    int j = __builtin_amdgcn_readfirstlane(tile_claim_raw(kargs()->tile_ctr + g * TILE_CTR_STRIDE));
+    while (j < ng) {
+      const int jn = tile_claim_raw(kargs()->tile_ctr + g * TILE_CTR_STRIDE);   // in flight under this tile
+      const int t = g + j * TILE_GROUPS;
+      const int64_t q = ((int64_t)t << 6) + lane;
+      const bool act = q < nv;
+      const int64_t p = visit_px(a.order, act ? q : nv - 1);
+      float dn1;
+      const float dn = pix(p, act, dn1);
+      const KF_CONST_AS AnalysisArgs* ka = kargs();
+      float* dno = ka->dn_out;
+      if (act && dno) KF_PX(dno, 0, p) = dn;
+      double* pt = ka->partials;
+      double* pf = ka->partials_first;
+      if (pt) {
+        const double v = wave_sum(act ? (double)dn : 0.0);
+        if (lane == 0) pt[t] = v;
+      }
+      if (pf) {
+        const double v1 = wave_sum(act ? (double)dn1 : 0.0);
+        if (lane == 0) pf[t] = v1;
+      }
+      j = __builtin_amdgcn_readfirstlane(jn);
+    }
+  }
+}
+#endif
+
 template <int NP, int FD = 0, int FOBS = 0, int UNR = 4, bool FOLD = false>
 __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
   double acc = 0.0, acc1 = 0.0;
@@ -113,6 +180,13 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
   }
   __syncthreads();
   KF_PHASE(KF_PH_PROLOGUE)
+  if (a.tile_ctr) {
+    analysis_tiles(a, [&](int64_t p, bool act, float& dn1) {
+      return pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT, IL, SPEC>(a, p, act, gpm_lds, dn1 KF_PHASE_ARG);
+    });
+    KF_PHASE_KERNEL_END
+    return;
+  }
   double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BS;
@@ -146,6 +220,14 @@ __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs 
   static_assert(BLOCK / 64 == GPM_G_WAVES, "per-wave LDS transpose buffers of gp_mfma_sums_g_xb");
 #if defined(__HIP_DEVICE_COMPILE__)
   KF_PHASE_KERNEL_BEGIN
+  if (a.tile_ctr) {
+    analysis_tiles(a, [&](int64_t p, bool act, float& dn1) {
+      return pixel_analysis_mfma<NP, D, FOBS, true, PF, BAND_LAYOUT_RUNTIME, IL, SPEC>(a, p, act, nullptr,
+                                                                                       dn1 KF_PHASE_ARG);
+    });
+    KF_PHASE_KERNEL_END
+    return;
+  }
   double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
@@ -455,18 +537,43 @@ constexpr bool gpm_il_default() {
   return (NP == 7 && LAYOUT == BAND_LAYOUT_TIP) || NP >= 10;
 }
 
+// Launch of a matrix-core analysis kernel: the static grid-stride mapping
+// (partials per workgroup; the hardware dispatcher hands a finished
+// workgroup's slot to the next one, which balances the cloud-skip load), or
+// with AV_TILE_QUEUE the persistent tile queue (partials per 64-slot tile).
+// Round 5 measured the two within 0.5 % of each other at 10980^2, 3882^2 and
+// for PROSAIL (BENCHMARKS.md), so the default stays static.  *n_part: the
+// partial entries written.
+template <typename KernT>
+static void launch_tiles(KernT kernel, int bs, size_t lds, const AnalysisArgs& a, int grid, hipStream_t s,
+                         int* n_part) {
+  int32_t* ctr = a.variant == AV_TILE_QUEUE ? tile_counter(s) : nullptr;
+  if (!ctr) {
+    *n_part = grid;
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(bs), lds, s, a);
+    return;
+  }
+  AnalysisArgs b = a;
+  b.tile_ctr = ctr;
+  const int64_t tiles = (visit_count(a) + 63) / 64;
+  const int64_t need = (tiles + bs / 64 - 1) / (bs / 64);
+  const int pg = tile_grid(reinterpret_cast<const void*>(kernel), bs, lds);
+  *n_part = (int)tiles;
+  hipLaunchKernelGGL(kernel, dim3((int)(need < pg ? need : pg)), dim3(bs), lds, s, b);
+}
+
 template <int NP, int FD>
-static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
+static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s, int* n_part) {
+  *n_part = grid;
   // GP on the matrix cores when the host attached split-f16 tables to every band
   // (AV_VALU_ORACLE: the f32 VALU record loop, the tests' second device path)
   if constexpr (FD > 0 && FD <= GPM_MAX_D) {
     if (a.gpm_frags > 0 && a.variant != AV_VALU_ORACLE && a.n_bands <= GPM_MAX_BANDS) {
       const size_t lds = (size_t)a.gpm_frags * sizeof(kf_h8);
-#define KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_)                                                           \
-  {                                                                                                              \
-    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_, IL_, SPEC_>, lds);                         \
-    hipLaunchKernelGGL((analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_, IL_, SPEC_>), dim3(grid), dim3(BS_),  \
-                       lds, s, a);                                                                               \
+#define KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_)                                                        \
+  {                                                                                                           \
+    gpm_lds_attr(analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_, IL_, SPEC_>, lds);                      \
+    launch_tiles(analysis_mfma_kernel<NP, FD, OBS_, BS_, MINW_, LAY_, IL_, SPEC_>, BS_, lds, a, grid, s, n_part); \
   }
       // Both column blocks' exponent MFMAs issued before the first block's
       // exponentials (gpm_chunk IL) where that costs no occupancy
@@ -530,17 +637,17 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
         // the default leaves the latency to the other wave
         constexpr bool IL = gpm_il_default<NP, BAND_LAYOUT_RUNTIME>();
         if (a.fast_obs == OBS_DN16 && a.variant == AV_GT_PREFETCH)
-          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, true>), dim3(grid), dim3(BLOCK), 0, s, a);
-        else if (a.fast_obs == OBS_DN16 && a.prop && !a.reg_v && a.variant == AV_DEFAULT && IL)
+          launch_tiles(analysis_mfma_g_kernel<NP, FD, OBS_DN16, true>, BLOCK, 0, a, grid, s, n_part);
+        else if (a.fast_obs == OBS_DN16 && a.prop && !a.reg_v && (a.variant == AV_DEFAULT ||
+                                                                  a.variant == AV_TILE_QUEUE) && IL)
           // fused forecast, no regulariser: the launch's paths fixed at compile time (SPEC_PROP)
-          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, false, true, SPEC_PROP>), dim3(grid),
-                             dim3(BLOCK), 0, s, a);
+          launch_tiles(analysis_mfma_g_kernel<NP, FD, OBS_DN16, false, true, SPEC_PROP>, BLOCK, 0, a, grid, s, n_part);
         else if (a.fast_obs == OBS_DN16 && (a.variant == AV_BLOCK_ORDER) != IL)
-          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16, false, true>), dim3(grid), dim3(BLOCK), 0, s, a);
+          launch_tiles(analysis_mfma_g_kernel<NP, FD, OBS_DN16, false, true>, BLOCK, 0, a, grid, s, n_part);
         else if (a.fast_obs == OBS_DN16)
-          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_DN16>), dim3(grid), dim3(BLOCK), 0, s, a);
+          launch_tiles(analysis_mfma_g_kernel<NP, FD, OBS_DN16>, BLOCK, 0, a, grid, s, n_part);
         else if (a.fast_obs == OBS_F32)
-          hipLaunchKernelGGL((analysis_mfma_g_kernel<NP, FD, OBS_F32, false, IL>), dim3(grid), dim3(BLOCK), 0, s, a);
+          launch_tiles(analysis_mfma_g_kernel<NP, FD, OBS_F32, false, IL>, BLOCK, 0, a, grid, s, n_part);
         else
           return false;
         return true;
@@ -568,23 +675,27 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s) {
 // Fast-path instantiations: JRC-TIP (7 params, 4-input band GPs), PROSAIL
 // (10 params, full-state GPs) and full-state GPs for small states.
 template <int NP>
-static void l_analysis(const AnalysisArgs& a, int grid, hipStream_t s) {
+static void l_analysis(const AnalysisArgs& a, int grid, hipStream_t s, int* n_part) {
   bool done = false;
+  *n_part = grid;
   if (a.fast_d > 0) {
     if constexpr (NP == 7) {
-      if (a.fast_d == 4) done = l_analysis_fast<7, 4>(a, grid, s);
-      else if (a.fast_d == 7) done = l_analysis_fast<7, 7>(a, grid, s);
+      if (a.fast_d == 4) done = l_analysis_fast<7, 4>(a, grid, s, n_part);
+      else if (a.fast_d == 7) done = l_analysis_fast<7, 7>(a, grid, s, n_part);
     } else if constexpr (NP == 10) {
-      if (a.fast_d == 10) done = l_analysis_fast<10, 10>(a, grid, s);
+      if (a.fast_d == 10) done = l_analysis_fast<10, 10>(a, grid, s, n_part);
     } else if constexpr (NP <= 4) {
-      if (a.fast_d == NP) done = l_analysis_fast<NP, NP>(a, grid, s);
+      if (a.fast_d == NP) done = l_analysis_fast<NP, NP>(a, grid, s, n_part);
     }
   }
   else if (a.fast_d == FD_PRECOMP) {
-    done = l_analysis_fast<NP, FD_PRECOMP>(a, grid, s);
+    done = l_analysis_fast<NP, FD_PRECOMP>(a, grid, s, n_part);
   } else if (a.fast_d == FD_LINEAR) {
-    done = l_analysis_fast<NP, FD_LINEAR>(a, grid, s);
+    done = l_analysis_fast<NP, FD_LINEAR>(a, grid, s, n_part);
   }
-  if (!done) hipLaunchKernelGGL(analysis_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
+  if (!done) {
+    *n_part = grid;
+    hipLaunchKernelGGL(analysis_kernel<NP>, dim3(grid), dim3(BLOCK), 0, s, a);
+  }
 }
 }  // namespace kf

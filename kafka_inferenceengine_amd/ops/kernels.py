@@ -72,7 +72,15 @@ def grid_for(N: int) -> int:
 
 
 def partials_buffer(N: int, device) -> torch.Tensor:
-    return torch.zeros(grid_for(N), dtype=torch.float64, device=device)
+    """Norm partials of one launch over N pixels: one f64 per workgroup of a
+    grid-stride kernel or per 64-slot tile of the tile-queue kernels."""
+    return torch.zeros(max(grid_for(N), -(-int(N) // 64)), dtype=torch.float64, device=device)
+
+
+def _set_valid(partials, n):
+    """Entries of ``partials`` the last producer wrote (read by reduce_partials)."""
+    if partials is not None:
+        partials._kf_n = int(n)
 
 
 @dataclass
@@ -126,6 +134,7 @@ class Variant(IntEnum):
     PER_BAND_OPERAND = 14    # BAND_LAYOUT_SHARED_X: exponent operand rebuilt per band
     BLOCK_ORDER = 16         # exponent MFMAs block by block
     GENERIC_SPEC = 18        # fused forecast through the generic launch instead of SPEC_PROP
+    TILE_QUEUE = 20          # matrix-core kernels on a persistent grid pulling tiles from per-XCD counters
 
 
 # analysis variant of launches that pass none (tests switch it to an oracle path;
@@ -392,7 +401,11 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
             raise ValueError(f"a_rows has bits past the {nt} packed rows")
         a.a_rows = int(a_rows)
     grid = grid_for(nv)
-    ext().analysis(n_params, a, grid, _dev(ref), _stream(ref))
+    if partials is not None and partials.numel() < -(-nv // 64):
+        raise ValueError("partials must hold one entry per 64 visited pixels (partials_buffer)")
+    n_part = ext().analysis(n_params, a, grid, _dev(ref), _stream(ref))
+    _set_valid(partials, n_part)
+    _set_valid(partials_first if gn_fused == 2 else None, n_part)
     return partials
 
 
@@ -527,6 +540,7 @@ def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status
             raise ValueError("identity output needs plane >= N")
         a.out_mean, a.out_unc, a.out_idx, a.out_plane = _ptr(mean), _ptr(unc), _ptr(idx), plane
     ext().gain(n_params, a, grid_for(N), _dev(ref), _stream(ref))
+    _set_valid(partials, grid_for(N))
     return partials
 
 
@@ -548,6 +562,7 @@ def jacobi(n_params, a_in, b_in, x_ext, nbr, x_ref, x_out, gamma, reg_mask, N, a
     a.a_in, a.b_in, a.x_ext, a.nbr, a.x_ref, a.x_out = map(_ptr, (a_in, b_in, x_ext, nbr, x_ref, x_out))
     a.a_out, a.partials = _ptr(a_out), _ptr(partials)
     ext().jacobi(n_params, a, grid_for(N), _dev(a_in), _stream(a_in))
+    _set_valid(partials, grid_for(N))
     return partials
 
 
@@ -828,6 +843,7 @@ def reg_finish(n_params, u, v, z_ext, nbr, x_ref, x_out, gamma, reg_mask, N, par
         a.a_in = _ptr(a_prec)
         a.out_mean, a.out_unc, a.out_idx, a.out_plane = _ptr(mean), _ptr(unc), _ptr(idx), plane
     ext().jacobi(n_params, a, grid_for(N), _dev(u), _stream(u))
+    _set_valid(partials, grid_for(N))
     return partials
 
 
@@ -970,13 +986,15 @@ def unpack(n_params, x, a, mean=None, unc=None, idx=None, N=None):
 
 
 def reduce_partials(partials: torch.Tensor, out: torch.Tensor | None = None):
-    """Fixed-order f64 sum of per-block partials (device: one-wave kernel)."""
+    """Fixed-order f64 sum of the partials the last producer wrote (device:
+    one workgroup, or two levels for per-tile vectors)."""
+    n = min(int(getattr(partials, "_kf_n", partials.numel())), int(partials.numel()))
     if _dev(partials):
         if out is None:
             out = torch.empty(1, dtype=torch.float64, device=partials.device)
-        ext().reduce_partials(_ptr(partials), int(partials.numel()), _ptr(out), _stream(partials))
+        ext().reduce_partials(_ptr(partials), n, _ptr(out), _stream(partials))
         return out
-    val = float(np.sum(partials.numpy()))
+    val = float(np.sum(partials.numpy()[:n]))
     if out is None:
         return torch.tensor([val], dtype=torch.float64)
     out.fill_(val)
