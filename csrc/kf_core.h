@@ -1119,15 +1119,18 @@ KF_HD float analysis_epilogue(AP a, int64_t p, float (&A)[ntri(NP)], float (&b)[
       const float d = b[j] - x0[j];
       dn = fmaf(d, d, dn);
     }
-    if (store && a->out_mean) {
-      // fused output dump: the unpack pass's work without re-reading x and A
+    if (store && a->out_unc) {
+      // fused output dump: the unpack pass's work without re-reading x and A.
+      // out_mean null: the state's x is the mean raster (dense strip, identity
+      // map: DeviceOutput aliases it), only the uncertainty is written
       const int64_t r = a->out_idx ? KF_PXS(a->out_idx, 0, p) : p;
       const int64_t pl = a->out_plane;
+      if (a->out_mean) {
 #pragma unroll
-      for (int j = 0; j < NP; ++j) {
-        KF_PXS(a->out_mean, j * pl, r) = b[j];
-        KF_PXS(a->out_unc, j * pl, r) = kf_rsqrt(dA[j]);
+        for (int j = 0; j < NP; ++j) KF_PXS(a->out_mean, j * pl, r) = b[j];
       }
+#pragma unroll
+      for (int j = 0; j < NP; ++j) KF_PXS(a->out_unc, j * pl, r) = kf_rsqrt(dA[j]);
     }
   }
   if (store && a->status) KF_PXS(a->status, 0, p) = st;

@@ -142,12 +142,13 @@ class KafkaOutput:
         self.write_s.append(time.perf_counter() - t0)
 
     # ------------------------------------------------------- device path
-    def device_targets(self, engine, dev):
+    def device_targets(self, engine, dev, alias: bool = True):
         if self._dev is None:
             self._dev = DeviceOutput(self.parameter_list)
-        return self._dev.device_targets(engine, dev)
+        return self._dev.device_targets(engine, dev, alias)
 
     def mark_written(self, timestep, state, engine):
+        self._dev.mark_written(timestep, state, engine)
         self._ship(timestep, engine)
 
     def dump_state(self, timestep, state, engine):
@@ -185,6 +186,11 @@ class KafkaOutput:
                 hu.copy_(unc_d, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self._stream)
+            # the planes' next writer waits for this copy (DeviceOutput.release); an
+            # aliased mean (the state's x) is not recycled by the allocator before it
+            mean_d.record_stream(self._stream)
+            if not self._gathering(engine):
+                self._dev.release(ev)
         else:
             hm.copy_(mean_d)
             hu.copy_(unc_d)
@@ -253,38 +259,88 @@ class KafkaOutputMemory:
 
 class DeviceOutput:
     """Keeps the latest analysis rasters on the device (mean and unc planes on
-    the strip grid) — the unpack kernel runs every timestep, nothing leaves
-    the GPU unless ``to_host`` is called."""
+    the strip grid) — the analysis kernel writes them in its final iteration
+    (fused output), nothing leaves the GPU unless ``to_host`` is called.
 
-    def __init__(self, parameter_list, keep_history: bool = False):
+    On a dense strip (every pixel active: the identity raster map) the mean
+    raster IS the analysis state's x ([n_p, N] with N = H W), so it is not
+    written twice: ``mean`` then references the state's x (``alias_state``;
+    a state's buffers are never rewritten -- each date allocates new ones).
+    The uncertainty planes alternate between two buffers, so a reader of one
+    date's planes (``KafkaOutput``'s device-to-host copy) runs under the next
+    date's analysis; ``device_targets`` makes the analysis wait only for a
+    reader of the buffer it is about to overwrite (``release``)."""
+
+    def __init__(self, parameter_list, keep_history: bool = False, alias_state: bool = True):
         self.parameter_list = list(parameter_list)
         self.keep_history = keep_history
+        self.alias_state = bool(alias_state)
         self.mean = None
         self.unc = None
         self.timestep = None
         self.history = {}
+        self._mean_buf = None
+        self._unc_bufs = None
+        self._readers = [None, None]   # event of the last reader of each uncertainty buffer
+        self._turn = 0
+        self._alias = False
 
     def _ensure(self, engine, dev):
         part = engine.partition
         n = engine.n_params
         H, W = part.strip_shape
-        if self.mean is None or self.mean.device != dev:
-            self.mean = torch.zeros((n, H * W), dtype=torch.float32, device=dev)
-            self.unc = torch.zeros((n, H * W), dtype=torch.float32, device=dev)
+        if self._unc_bufs is None or self._unc_bufs[0].device != dev or self._unc_bufs[0].shape != (n, H * W):
+            self._unc_bufs = [torch.zeros((n, H * W), dtype=torch.float32, device=dev) for _ in range(2)]
+            self._mean_buf = None
+            self._readers = [None, None]
             idx = np.asarray(part.local_idx, dtype=np.int64)
             if idx.size and (idx.min() < 0 or idx.max() >= H * W):
                 raise ValueError("partition raster index outside the strip")
             self._idx = torch.from_numpy(idx).to(dev)
             self._identity = part.N == H * W
+            self._plane = H * W
+        if self.unc is None:
+            self.unc = self._unc_bufs[0]
 
-    def device_targets(self, engine, dev):
+    def _own_mean(self):
+        if self._mean_buf is None:
+            self._mean_buf = torch.zeros_like(self._unc_bufs[0])
+        return self._mean_buf
+
+    def _next_unc(self, dev):
+        """The uncertainty buffer of the next date (the other one than the
+        latest), after its last reader."""
+        self._turn ^= 1
+        ev = self._readers[self._turn]
+        if ev is not None and dev.type == "cuda":
+            torch.cuda.current_stream(dev).wait_event(ev)
+            self._readers[self._turn] = None
+        return self._unc_bufs[self._turn]
+
+    def release(self, event):
+        """A reader of the latest planes (recorded after its copy): the
+        buffer is not overwritten before it (next-but-one date)."""
+        self._readers[self._turn] = event
+
+    def device_targets(self, engine, dev, alias: bool = True):
         """(mean, unc, idx) rasters the analysis kernel can write directly
-        (fused output, AnalysisArgs.out_*); followed by ``mark_written``."""
+        (fused output, AnalysisArgs.out_*); followed by ``mark_written``.
+        mean None: the state's x is the mean raster (dense strips; ``alias``:
+        the caller's kernel writes the final x as the state, the plain
+        information-form analysis)."""
         self._ensure(engine, dev)
-        return self.mean, self.unc, None if self._identity else self._idx
+        unc = self._next_unc(dev)
+        self._alias = self.alias_state and self._identity and alias
+        self._pending = unc
+        return (None if self._alias else self._own_mean()), unc, None if self._identity else self._idx
 
     def mark_written(self, timestep, state, engine):
         self.timestep = timestep
+        self.unc = getattr(self, "_pending", self.unc)
+        if self._alias:
+            self.mean = state.x[:, :self._plane]
+        else:
+            self.mean = self._own_mean()
         if self.keep_history:
             self.history[timestep] = (self.mean.clone(), self.unc.clone())
 
@@ -292,8 +348,11 @@ class DeviceOutput:
         n = engine.n_params
         self._ensure(engine, state.x.device)
         prec = engine._as_kind(state, "precision")
+        unc = self._next_unc(state.x.device)
+        mean = self._own_mean()
         if state.N:
-            K.unpack(n, prec.x, prec.P, self.mean, self.unc, idx=None if self._identity else self._idx, N=state.N)
+            K.unpack(n, prec.x, prec.P, mean, unc, idx=None if self._identity else self._idx, N=state.N)
+        self._pending, self._alias = unc, False
         self.mark_written(timestep, state, engine)
 
     def to_host(self, shape=None):

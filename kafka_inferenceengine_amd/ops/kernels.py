@@ -346,9 +346,12 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
         mean, unc, idx = out
         if not solve:
             raise ValueError("fused output needs solve=True")
-        if unc is None or (mean is None) != (reg is not None):
-            raise ValueError("out = (mean, unc, idx); mean is None exactly with reg")
+        if unc is None or (reg is not None and mean is not None):
+            raise ValueError("out = (mean, unc, idx); with reg the mean is None (reg_finish writes it)")
         plane = unc.shape[1]
+        if mean is None and reg is None and (idx is not None or x_out is None or x_out.shape[1] != plane):
+            # the state's x is the mean raster (DeviceOutput alias): identity map, x's layout
+            raise ValueError("out mean None needs the identity map and x_out of the raster's plane")
         for t, nm in ((mean, "out mean"), (unc, "out unc")):
             if t is None:
                 continue
