@@ -319,9 +319,13 @@ def main():
     if a.dump_state and (comm.band is None or comm.band.rank == 0):
         np.save(f"{a.dump_state}.strip{rank}.npy", state.x[:, :state.N].cpu().numpy())
     st_last = getattr(kf, "last_status", None)
-    n_fb = 0 if st_last is None or not state.N else int(((st_last[:state.N] & 16) > 0).sum().item())
+    n_fb = 0 if st_last is None or not state.N else int(((st_last[:state.N] & K.ST_FALLBACK) > 0).sum().item())
+    # GP inputs outside the emulators' training box (+10 % margin) at the last date
+    n_ood = 0 if st_last is None or not state.N else \
+        int(((st_last[:state.N] & K.ST_OUT_OF_DOMAIN) > 0).sum().item())
     ok = comm.max_float(0.0 if ok_local else 1.0) == 0.0
     fallback = comm.sum_int(n_fb) / max(1, part.N_total)
+    out_of_domain = comm.sum_int(n_ood) / max(1, part.N_total)
     # distinct GPUs behind the ranks (a one-GPU multi-rank rehearsal is not scaling)
     n_dev = n_ranks
     if n_ranks > 1:
@@ -350,7 +354,8 @@ def main():
                           "global_batch": part.N_total, "seq_len": 1,
                           "gp_train_points": a.n_train or c.get("n_train"), "parallelism": f"tile-dp{world}" + (f" x band-tp{B}" if B > 1 else ""),
                           "gn_iterations": gn, "ms_per_gn_iteration": round(1e3 * elapsed / max(1, n_gn), 3),
-                          "finite": ok, "fallback_frac": round(fallback, 6), "ingest_bytes_per_step": ingest,
+                          "finite": ok, "fallback_frac": round(fallback, 6),
+                          "out_of_domain_frac": round(out_of_domain, 6), "ingest_bytes_per_step": ingest,
                           "baseline_updates_per_s": c["baseline"]}}
         if chunk_hist:
             rec["config"]["convergence_chunk"] = kf.config.convergence_chunk

@@ -66,6 +66,9 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .ARR_FIELD(BandDesc, map, int32_t)
       .def_readwrite("map_identity", &BandDesc::map_identity)
       .def_readwrite("map_kind", &BandDesc::map_kind)
+      .def_readwrite("dom_check", &BandDesc::dom_check)
+      .ARR_FIELD(BandDesc, dom_lo, float)
+      .ARR_FIELD(BandDesc, dom_hi, float)
       .def_readwrite("scale", &BandDesc::scale)
       .def_readwrite("rel_unc", &BandDesc::rel_unc)
       .def_readwrite("unc_floor", &BandDesc::unc_floor)

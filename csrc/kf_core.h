@@ -137,7 +137,12 @@ enum PropMode : int32_t {
   PROP_IDENTITY = 5       // x_f = M x_a, P_f^-1 = P_a^-1 (no inflation)
 };
 enum StatusBits : uint8_t {
-  ST_OK = 0, ST_NONSPD = 1, ST_NONFINITE = 2, ST_BAD_OP = 4, ST_NO_OBS = 8, ST_FALLBACK = 16
+  ST_OK = 0, ST_NONSPD = 1, ST_NONFINITE = 2, ST_BAD_OP = 4, ST_NO_OBS = 8, ST_FALLBACK = 16,
+  // a GP band's input (at the final iteration's linearisation point) lies
+  // outside the emulator's training box widened by a margin (BandDesc.dom_*):
+  // the emulator extrapolates there -- the analytic operator of the reference
+  // refuses such states (sar_forward_model.py:68-71,102-105: ValueError)
+  ST_OUT_OF_DOMAIN = 32
 };
 
 // One observation band as seen by the fused analysis kernel.  Built on the
@@ -164,7 +169,21 @@ struct BandDesc {
   float gpm_scale;             // 2^sigma: undoes the f16-range shift folded into the table's L'
   int32_t map_identity;        // 1: map[d] == d for every input d (full-state GP: no gather / scatter)
   int32_t map_kind;            // GPM_MAP_*: a map known at compile time (JRC-TIP bands), 0: runtime map
+  int32_t dom_check;           // GP: 1 = flag inputs outside [dom_lo, dom_hi] (ST_OUT_OF_DOMAIN)
+  float dom_lo[MAX_D];         // GP: training box of the centred inputs, widened by a margin
+  float dom_hi[MAX_D];
 };
+
+// GP inputs (centred, as the kernels form them) outside a band's domain box;
+// NaN counts as outside.  BD: BandDesc in any address space.
+template <int D, typename BD>
+KF_HD bool gp_out_of_domain(BD* bd, const float (&xi)[D]) {
+  if (!bd->dom_check) return false;
+  bool o = false;
+#pragma unroll
+  for (int d = 0; d < D; ++d) o = o || !(xi[d] >= bd->dom_lo[d] && xi[d] <= bd->dom_hi[d]);
+  return o;
+}
 
 // JRC-TIP band mappers (kafka/inference/kf_tools.py:19-23, band_selecta): the
 // matrix-core kernel gathers the GP inputs and updates only the 4 x 4 touched
@@ -1256,6 +1275,19 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
     if constexpr (FD > 0) h0o = opaque(cptr(a.bands + bi))->h0_out;   // not live across the GP loop
 #endif
     if (h0o) KF_PX(h0o, 0, p) = H0;
+    if constexpr (FD > 0) {
+      float xi[FD];
+#pragma unroll
+      for (int d = 0; d < FD; ++d) xi[d] = gather_state<NP>(x0, bd.map[d]) - bd.center[d];
+      if (gp_out_of_domain<FD>(&bd, xi)) st |= ST_OUT_OF_DOMAIN;
+    } else if constexpr (FD == 0) {
+      if (bd.op == OP_GP) {
+        float xi[NP];
+#pragma unroll
+        for (int d = 0; d < NP; ++d) xi[d] = d < bd.d ? gather_state<NP>(x0, bd.map[d]) - bd.center[d] : 0.f;
+        if (gp_out_of_domain<NP>(&bd, xi)) st |= ST_OUT_OF_DOMAIN;
+      }
+    }
     if (!ok) { st |= ST_BAD_OP; continue; }
     ++nobs;
     float yp;

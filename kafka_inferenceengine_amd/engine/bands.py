@@ -164,6 +164,9 @@ def band_desc(spec: OperatorSpec, obs: DeviceBand | None, n_params: int, cache: 
         d.map_kind = {(0, 1, 6, 2): 2, (3, 4, 6, 5): 3}.get(tuple(smap[:4]), 0)
     d.coef = [float(c) for c in spec.coef]
     d.center = [float(c) for c in spec.center]
+    if spec.kind == OP_GP and getattr(spec, "domain_lo", None) is not None:
+        d.dom_lo, d.dom_hi = [float(v) for v in spec.domain_lo], [float(v) for v in spec.domain_hi]
+        d.dom_check = 1
     if obs is None:
         d.obs = K.OBS_NONE
     elif obs.kind == K.OBS_DN16:

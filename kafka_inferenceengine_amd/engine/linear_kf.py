@@ -588,8 +588,9 @@ class LinearKalman:
         if st is not None and self.N:
             s = st[:self.N]
             bits = torch.stack([(s & b) > 0 for b in (K.ST_NO_OBS, K.ST_FALLBACK, K.ST_NONSPD, K.ST_NONFINITE,
-                                                      K.ST_BAD_OP)]).sum(1).cpu().tolist()
-            out["status"] = dict(zip(("no_obs", "fallback", "non_spd", "non_finite", "bad_operator"), bits))
+                                                      K.ST_BAD_OP, K.ST_OUT_OF_DOMAIN)]).sum(1).cpu().tolist()
+            out["status"] = dict(zip(("no_obs", "fallback", "non_spd", "non_finite", "bad_operator",
+                                      "out_of_domain"), bits))
             out["masked_fraction"] = bits[0] / self.N
         if hasattr(self.observations, "ingest_bytes"):
             total = int(self.observations.ingest_bytes())

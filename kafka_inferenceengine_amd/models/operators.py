@@ -50,6 +50,10 @@ class OperatorSpec:
     aux: np.ndarray | None = None         # per active pixel auxiliary (SAR theta)
     emulator: object = None
     gp_pos_pairs: int = 0                 # leading record pairs with alpha > 0
+    # GP: the training box of the centred inputs widened by GP_DOMAIN_MARGIN of its
+    # range per side (the kernels flag inputs outside it: ST_OUT_OF_DOMAIN)
+    domain_lo: list | None = None
+    domain_hi: list | None = None
 
     @property
     def d(self) -> int:
@@ -69,6 +73,11 @@ class LinearOperator:
         return cls(c, 0.0)
 
 
+# margin of a GP band's domain box beyond its training inputs, per side, as a
+# fraction of the input's training range (ST_OUT_OF_DOMAIN)
+GP_DOMAIN_MARGIN = 0.1
+
+
 def gp_spec(emulator: GaussianProcessEmulator, state_map) -> OperatorSpec:
     """Device operator description of a GP band (memoised per emulator and state
     map: the engine asks for it on every observation date)."""
@@ -83,8 +92,16 @@ def gp_spec(emulator: GaussianProcessEmulator, state_map) -> OperatorSpec:
 def _gp_spec(emulator: GaussianProcessEmulator, state_map) -> OperatorSpec:
     if emulator.n_inputs != len(state_map):
         raise ValueError(f"emulator has {emulator.n_inputs} inputs but state map has {len(state_map)}")
+    lo = hi = None
+    X = getattr(emulator, "inputs", None)
+    if X is not None and np.asarray(X).ndim == 2 and np.asarray(X).shape[0] > 0:
+        X = np.asarray(X, dtype=np.float64)
+        c = np.asarray(emulator.center(), dtype=np.float64)
+        tlo, thi = X.min(0), X.max(0)
+        pad = GP_DOMAIN_MARGIN * (thi - tlo)
+        lo, hi = list(map(float, tlo - pad - c)), list(map(float, thi + pad - c))
     return OperatorSpec(OP_GP, state_map, list(map(float, emulator.lam)), list(map(float, emulator.center())),
-                        float(emulator.mean), emulator.records(), None, emulator, emulator.n_pos_pairs)
+                        float(emulator.mean), emulator.records(), None, emulator, emulator.n_pos_pairs, lo, hi)
 
 
 # ---------------------------------------------------------------- helpers

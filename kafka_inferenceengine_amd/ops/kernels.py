@@ -19,7 +19,7 @@ from ..utils.blocks import ntri
 from . import _ext
 
 OBS_NONE, OBS_F32, OBS_DN16, OBS_BF16, OBS_BF16Y = 0, 1, 2, 3, 4
-ST_NONSPD, ST_NONFINITE, ST_BAD_OP, ST_NO_OBS, ST_FALLBACK = 1, 2, 4, 8, 16
+ST_NONSPD, ST_NONFINITE, ST_BAD_OP, ST_NO_OBS, ST_FALLBACK, ST_OUT_OF_DOMAIN = 1, 2, 4, 8, 16, 32
 SUPPORTED_NP = (1, 2, 3, 4, 7, 10)
 
 

@@ -154,3 +154,93 @@ def oracle_run_blocks(obs, state_mask, maps, time_grid, prior_mean, prior_cinv, 
         if on_step is not None:
             on_step(timestep, x_a, A_a)
     return x_a, A_a, iters
+
+
+def gp_predict64_torch(em, X, chunk=65536):
+    """gp_predict64 in float64 torch on X's device (the 1024^2 slice: ~10^9
+    kernel evaluations per band and iteration, minutes in NumPy)."""
+    import torch
+
+    dev = X.device
+    T = torch.as_tensor(np.asarray(em.inputs, dtype=np.float64), device=dev)
+    c = T.mean(0)
+    Tc = T - c
+    lam = torch.as_tensor(np.asarray(em.lam, dtype=np.float64), device=dev)
+    alpha = torch.as_tensor(np.asarray(em.alpha, dtype=np.float64), device=dev)
+    tt = (Tc * Tc * lam).sum(1)
+    B = torch.cat([alpha[:, None], alpha[:, None] * Tc], 1)
+    H = torch.empty(X.shape[0], dtype=torch.float64, device=dev)
+    dH = torch.empty_like(X)
+    for s in range(0, X.shape[0], chunk):
+        Xc = X[s:s + chunk] - c
+        xx = (Xc * Xc * lam).sum(1)
+        d2 = xx[:, None] + tt[None, :] - 2.0 * (Xc * lam) @ Tc.T
+        k = em.signal * torch.exp(-0.5 * torch.clamp(d2, min=0.0))
+        S = k @ B
+        H[s:s + chunk] = em.mean + S[:, 0]
+        dH[s:s + chunk] = -lam * (Xc * S[:, :1] - S[:, 1:])
+    return H, dH
+
+
+def oracle_run_blocks_torch(obs, state_mask, maps, time_grid, prior_mean, prior_cinv, propagated=(6,), q=None,
+                            tol=1e-3, min_iterations=2, max_iterations=25, x0=None, A0=None, device="cuda"):
+    """:func:`oracle_run_blocks` in float64 torch on ``device`` (same loop, same
+    per-pixel normal equations, solved by batched float64 Cholesky): the
+    oracle of the 1024^2 slice.  Returns (x [N, n], A [N, n, n], iters) on the
+    host."""
+    import torch
+
+    dev = torch.device(device)
+    sm = np.asarray(state_mask).astype(bool)
+    N = int(sm.sum())
+    f64 = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=dev)  # noqa: E731
+    mu, ci = f64(prior_mean), f64(prior_cinv)
+    n = mu.numel()
+    qv = torch.zeros(n, dtype=torch.float64, device=dev) if q is None else f64(q)
+    x_f = (mu if x0 is None else f64(x0)).expand(N, n).clone()
+    A_f = (ci if A0 is None else f64(A0)).expand(N, n, n).clone()
+    x_a = A_a = None
+    iters = []
+    for timestep, locate, is_first in iterate_time_grid(time_grid, obs.dates):
+        if not is_first:
+            x_f = mu.expand(N, n).clone()
+            A_f = ci.expand(N, n, n).clone()
+            for kk in propagated:
+                x_f[:, kk] = x_a[:, kk]
+                A_f[:, kk, kk] = 1.0 / (1.0 / A_a[:, kk, kk] + qv[kk])
+        if len(locate) == 0:
+            x_a, A_a = x_f, A_f
+            continue
+        for date in locate:
+            raw = []
+            for b in range(obs.bands_per_observation[date]):
+                d = obs.get_band_data(date, b)
+                m = np.asarray(d.mask)[sm]
+                w = np.asarray(d.uncertainty.diagonal())[sm.ravel()] if sp.issparse(d.uncertainty) else \
+                    np.asarray(d.uncertainty)[sm]
+                w = np.where(m & np.isfinite(w) & (w > 0), w, 0.0)
+                raw.append((f64(np.where(m, np.asarray(d.observations)[sm], 0.0)), f64(w), d.emulator))
+            x_prev = x_f.clone()
+            n_iter = 1
+            while True:
+                A = A_f.clone()
+                rhs = torch.einsum("nij,nj->ni", A_f, x_f)
+                for b, (y, w, em) in enumerate(raw):
+                    H0, dH = gp_predict64_torch(em, x_prev[:, list(maps[b])].contiguous())
+                    h = torch.zeros((N, n), dtype=torch.float64, device=dev)
+                    h[:, list(maps[b])] = dH
+                    yp = y + (h * x_prev).sum(1) - H0
+                    A += w[:, None, None] * h[:, :, None] * h[:, None, :]
+                    rhs += (w * yp)[:, None] * h
+                xa = torch.cholesky_solve(rhs[..., None], torch.linalg.cholesky(A))[..., 0]
+                norm = float(torch.linalg.norm((xa - x_prev).reshape(-1))) / float(N * n)
+                x_prev = xa
+                if norm < tol and n_iter >= min_iterations:
+                    break
+                if n_iter > max_iterations:
+                    break
+                n_iter += 1
+            iters.append(n_iter)
+            x_f, A_f = xa, A
+        x_a, A_a = x_f, A_f
+    return x_a.cpu().numpy(), A_a.cpu().numpy(), iters

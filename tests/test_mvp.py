@@ -34,9 +34,10 @@ def _rel(a, b):
     return np.abs(a - b).max(1) / (np.abs(b).max(1) + 1e-12)
 
 
-def mvp(device, size, n_dates=10, n_train=500, progress=False):
-    """Run the engine and the float64 block oracle; returns the per-date drift
-    records and the final (x, packed P) errors."""
+def mvp(device, size, n_dates=10, n_train=500, progress=False, torch_oracle=False):
+    """Run the engine and the float64 block oracle (``torch_oracle``: the
+    float64 torch twin on the engine's device, for 1024^2); returns the
+    per-date drift records and the final (x, packed P) errors."""
     mask = np.ones((size, size), bool)
     dates, grid = _grid(n_dates)
     jp = k.JRCPrior(k.TIP_PARAMETERS, mask)
@@ -56,11 +57,16 @@ def mvp(device, size, n_dates=10, n_train=500, progress=False):
     # step flipped is 1e-4 of reflectance)
     mu, _, ci = k.tip_prior()
     steps = []
-    xo, Ao, iters = oracle_run_blocks(obs, mask, k.TIP_BAND_MAPPER, grid, mu, ci, q=[0, 0, 0, 0, 0, 0, Q6],
-                                      x0=jp.mean, A0=jp.inv_covar,
-                                      on_step=lambda t, x, A: (steps.append((t, x.copy(), A.copy())),
-                                                               progress and print(f"oracle {t.date()} done",
-                                                                                  flush=True)))
+    if torch_oracle:
+        from oracle import oracle_run_blocks_torch
+        xo, Ao, iters = oracle_run_blocks_torch(obs, mask, k.TIP_BAND_MAPPER, grid, mu, ci,
+                                                q=[0, 0, 0, 0, 0, 0, Q6], x0=jp.mean, A0=jp.inv_covar, device=device)
+    else:
+        xo, Ao, iters = oracle_run_blocks(obs, mask, k.TIP_BAND_MAPPER, grid, mu, ci, q=[0, 0, 0, 0, 0, 0, Q6],
+                                          x0=jp.mean, A0=jp.inv_covar,
+                                          on_step=lambda t, x, A: (steps.append((t, x.copy(), A.copy())),
+                                                                   progress and print(f"oracle {t.date()} done",
+                                                                                      flush=True)))
     drift = []
     for t, x, A in steps:
         mean, unc = out.history[t]
@@ -88,8 +94,21 @@ def mvp(device, size, n_dates=10, n_train=500, progress=False):
             "worst": [{"pixel": int(i), "rel": float(pix[i]), "status": None if status is None else int(status[i]),
                        "x": [round(float(v), 5) for v in xs[:, i]], "x_oracle": [round(float(v), 5) for v in xo[i]]}
                       for i in worst]}
+    # in-domain pins: the parameters' scales over the tile,
+    # the error over the pixels whose GP inputs stayed inside the emulators'
+    # domain boxes (ST_OUT_OF_DOMAIN clear)
+    ood = np.zeros(N, bool) if status is None else (status & k.ops.kernels.ST_OUT_OF_DOMAIN) > 0
+    keep = ~ood
+    xs_scale = np.abs(xo.T).max(1) + 1e-12
+    ps_scale = np.abs(Po).max(1) + 1e-12
+    x_in = float((np.abs(xs - xo.T)[:, keep].max(1) / xs_scale).max()) if keep.any() else 0.0
+    p_in = float((np.abs(Ps - Po)[:, keep].max(1) / ps_scale).max()) if keep.any() else 0.0
+    pix_p = (np.abs(Ps - Po) / ps_scale[:, None]).max(0)
+    over = (pix > X_TOL) | (pix_p > P_TOL)
     return {"size": size, "n_dates": n_dates, "n_train": n_train, "gn": gn, "gn_oracle": iters,
-            "x_rel": x_err, "P_rel": p_err, "pixel_tail": tail, "drift": drift}
+            "x_rel": x_err, "P_rel": p_err, "pixel_tail": tail, "drift": drift,
+            "in_domain": {"x_rel": x_in, "P_rel": p_in, "n_flagged": int(ood.sum()), "frac_flagged": float(ood.mean()),
+                          "n_over_pin": int(over.sum()), "n_over_pin_unflagged": int((over & keep).sum())}}
 
 
 def test_block_oracle_equals_reference_api_oracle():
@@ -133,3 +152,25 @@ def test_mvp_slice_on_device(cuda):
     assert r["gn"] == r["gn_oracle"]
     assert r["x_rel"] < X_TOL, r
     assert r["P_rel"] < P_TOL, r
+
+
+@pytest.mark.gpu
+def test_mvp_slice_1024_in_domain(cuda):
+    """the slice at its specified 1024^2 (1,048,576 px, 10
+    dates, T = 500) against the float64 oracle (its torch twin on the device):
+    equal GN counts; x within 5e-4 and P^-1 within 1e-3 on every pixel whose GP
+    inputs stayed in the emulators' domain boxes; the pixels flagged
+    ST_OUT_OF_DOMAIN are <= 0.01 % of the tile and every pixel over a pin is
+    one of them (the weakly observed pixels whose TLAI left the training range,
+    docs/PARITY.md)."""
+    import time
+
+    t0 = time.perf_counter()
+    r = mvp(cuda, 1024, torch_oracle=True)
+    print("MVP1024 " + json.dumps({kk: v for kk, v in r.items() if kk != "drift"}), flush=True)
+    assert r["gn"] == r["gn_oracle"]
+    d = r["in_domain"]
+    assert d["x_rel"] < X_TOL and d["P_rel"] < P_TOL, d
+    assert d["frac_flagged"] <= 1e-4, d
+    assert d["n_over_pin_unflagged"] == 0, d
+    assert time.perf_counter() - t0 < 60
