@@ -320,7 +320,7 @@ def main():
         np.save(f"{a.dump_state}.strip{rank}.npy", state.x[:, :state.N].cpu().numpy())
     st_last = getattr(kf, "last_status", None)
     n_fb = 0 if st_last is None or not state.N else int(((st_last[:state.N] & K.ST_FALLBACK) > 0).sum().item())
-    # GP inputs outside the emulators' training box (+10 % margin) at the last date
+    # GP inputs outside the emulators' training box (models/operators.py GP_DOMAIN_MARGIN) at the last date
     n_ood = 0 if st_last is None or not state.N else \
         int(((st_last[:state.N] & K.ST_OUT_OF_DOMAIN) > 0).sum().item())
     ok = comm.max_float(0.0 if ok_local else 1.0) == 0.0

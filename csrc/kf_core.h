@@ -139,7 +139,7 @@ enum PropMode : int32_t {
 enum StatusBits : uint8_t {
   ST_OK = 0, ST_NONSPD = 1, ST_NONFINITE = 2, ST_BAD_OP = 4, ST_NO_OBS = 8, ST_FALLBACK = 16,
   // a GP band's input (at the final iteration's linearisation point) lies
-  // outside the emulator's training box widened by a margin (BandDesc.dom_*):
+  // outside the emulator's training box (widened by models/operators.py GP_DOMAIN_MARGIN, BandDesc.dom_*):
   // the emulator extrapolates there -- the analytic operator of the reference
   // refuses such states (sar_forward_model.py:68-71,102-105: ValueError)
   ST_OUT_OF_DOMAIN = 32
@@ -170,7 +170,7 @@ struct BandDesc {
   int32_t map_identity;        // 1: map[d] == d for every input d (full-state GP: no gather / scatter)
   int32_t map_kind;            // GPM_MAP_*: a map known at compile time (JRC-TIP bands), 0: runtime map
   int32_t dom_check;           // GP: 1 = flag inputs outside [dom_lo, dom_hi] (ST_OUT_OF_DOMAIN)
-  float dom_lo[MAX_D];         // GP: training box of the centred inputs, widened by a margin
+  float dom_lo[MAX_D];         // GP: training box of the centred inputs (+ GP_DOMAIN_MARGIN)
   float dom_hi[MAX_D];
 };
 

@@ -30,6 +30,10 @@ class EngineConfig:
     # checkpoint is due, the date is the run's last, the output is not fused or
     # another consumer needs it; "always": every packed row, every date
     store_precision: str = "auto"
+    # keep a per-pixel record of every date's ST_OUT_OF_DOMAIN (LinearKalman.
+    # ood_history): a state that left an emulator's domain carries the
+    # extrapolation forward through the propagated parameters (one uint8 OR per date)
+    domain_history: bool = False
     # analysis
     analysis_form: str = "information"        # 'information' (K1) | 'gain' (K1g)
     joseph: bool = False                      # Joseph-form covariance update (gain form)

@@ -18,8 +18,6 @@ from __future__ import annotations
 
 import bisect
 import logging
-import math
-import os
 import time
 from collections import namedtuple
 
@@ -39,6 +37,8 @@ from ..utils.blocks import ntri, pack_matrix, soa_to_interleaved, tri_pos
 from ..utils.metrics import MetricsLogger, PhaseTimer
 from .bands import DeviceBand, RecordCache, TableCache, build_table
 from .config import EngineConfig
+from .gn import GaussNewtonMixin, _GNRun
+from .spatial import SpatialPriorMixin
 from .state import COVARIANCE, PRECISION, KFState, LazyForecast
 
 LOG = logging.getLogger(__name__ + ".linear_kf")
@@ -46,6 +46,7 @@ LOG = logging.getLogger(__name__ + ".linear_kf")
 Metadata = namedtuple("Metadata", "mask uncertainty")
 Previous_State = namedtuple("Previous_State", "timestamp x_vect cov_m icov_mv")
 AssimilationResult = namedtuple("AssimilationResult", "state n_iter norms innovations")
+
 
 
 def _resolve_device(device):
@@ -84,7 +85,7 @@ def _jacobian_blocks(Hm, N: int, n: int) -> np.ndarray:
     return h
 
 
-class LinearKalman:
+class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
     """Iterated (Gauss-Newton) information-form Kalman filter over rasters."""
 
     def __init__(self, observations, output, state_mask, create_observation_operator, parameters_list,
@@ -153,6 +154,7 @@ class LinearKalman:
         self._output_written = None
         self._chunks = None               # per-chunk convergence state (config.convergence_chunk)
         self.last_chunk_iters = None      # {GN iterations: chunks} of the last date (chunked test)
+        self.ood_history = None           # config.domain_history: ST_OUT_OF_DOMAIN on any date so far
         self._full_precision_step = False
         band = getattr(self.comm, "band", None)
         self.band_comm = band if (band is not None and band.world > 1) else None
@@ -549,6 +551,10 @@ class LinearKalman:
                 finally:
                     self._lookahead_fn = None
             forecast = res.state
+            if self.config.domain_history and getattr(self, "last_status", None) is not None and self.N:
+                # pixels whose GP inputs left an emulator's domain on any date of the run
+                ood = self.last_status[:self.N] & K.ST_OUT_OF_DOMAIN
+                self.ood_history = ood if self.ood_history is None else (self.ood_history | ood)
             info["gn_iterations"].append(res.n_iter)
             info["norms"].append(res.norms[-1] if res.norms else None)
             rec = {"event": "date", "date": step.isoformat(), "n_iter": res.n_iter, "norms": res.norms,
@@ -788,9 +794,6 @@ class LinearKalman:
             P_out = torch.empty_like(fc.P)
         # every analysis / gain kernel writes the status of each of its N pixels
         status = torch.empty(max(N, 1), dtype=torch.uint8, device=self.device)
-        norms = []
-        deferred = []
-        n_iter = 1
         len_x = float(n * self.n_total)
         # fused output: an output with device rasters is written by the analysis
         # kernel itself in every iteration that can end the loop (the last one wins)
@@ -816,7 +819,7 @@ class LinearKalman:
         # GN iterations 1 and 2 in one launch (the first never ends the loop): rank-
         # independent test, so every rank queues the same collectives
         fuse2 = (plain and cfg.fuse_gn and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
-                 and n_iter == 1 and not (prop is None and fc is None))
+                 and not (prop is None and fc is None))
         # linear / identity operators: y' = y - offset does not depend on the
         # linearisation point (kf_core.h FD_LINEAR), so iteration 2 repeats
         # iteration 1 exactly and its norm is 0 -- converged without a read-back
@@ -840,110 +843,12 @@ class LinearKalman:
         # cannot end the loop), fused with the regularised prepare of the second
         first_plain = spatial and cfg.spatial_first_plain and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
         fuse_sp = first_plain and cfg.fuse_gn
-        if chunked:
-            x_prev, n_iter, norms = self._gn_chunked(table, specs, dbs, precomp, prop, fc, x_prev, x_new, P_out,
-                                                     status, order, out_t, h0_outs, a_rows)
-        else:
-            while True:
-                # the analysis precision is only needed from the iteration that can
-                # end the loop on: skip its 4*ntri B/px store before min_iterations
-                A_keep = P_out if n_iter >= cfg.min_iterations else None
-                out_now = out_t if n_iter >= cfg.min_iterations else None
-                if precomp:
-                    pre = self._precompute_host(specs, dbs, x_prev)
-                    table = build_table(specs, dbs, n, self._cache, self.device, h0_outs, pre)
-                if fuse2 or fuse_sp:
-                    # iterations 1 + 2 in one launch: outputs of iteration 2 (which can end the loop)
-                    red2 = self._red_hist[1:3]
-                    with self.timer.phase("analysis"):
-                        if N:
-                            if fuse_sp:
-                                self._regularised_iteration(table, x_prev, fc, x_new, P_out, status, prop, out_t,
-                                                            final=True, partials_first=self._partials1)
-                            else:
-                                K.analysis(n, table, x_prev, None if prop is not None else fc.x,
-                                           None if prop is not None else fc.P, x_new, P_out, None, status,
-                                           self._partials, N=N, prop=prop, out=out_t, gn_fused=2,
-                                           partials_first=self._partials1, order=order, a_rows=a_rows)
-                            K.reduce_partials(self._partials1, red2[0:1])
-                            K.reduce_partials(self._partials, red2[1:2])
-                        else:
-                            red2.zero_()
-                    with self.timer.phase("converge"):
-                        pend2 = self.comm.sum_f64_async(red2)
-                    fuse2 = fuse_sp = False
-                    deferred.append((1, pend2.column(0)))
-                    pend = pend2.column(1)
-                    n_iter = 2
-                    x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
-                    if static_conv and not self._norms_needed_now():
-                        # norm 2 is exactly 0: converged.  Norm 1 is read after the
-                        # next launch is queued (no host wait between the steps)
-                        if self._lookahead_fn is not None:
-                            self._lookahead_fn()
-                            self._lookahead_fn = None
-                        self._resolve_lazy_norms()
-                        norms = [None, 0.0]
-                        self._lazy_norms.append((norms, deferred[0][1], pend, len_x, len(bands)))
-                        deferred = []
-                        break
-                else:
-                    with self.timer.phase("analysis"):
-                        if N:
-                            if gain:
-                                K.gain(n, table, x_prev, None if prop else fc.x, None if prop else fc.P, x_new, A_keep,
-                                       status, self._partials, N=N, joseph=cfg.joseph, prop=prop, out=out_now)
-                            elif first_plain and n_iter == 1:
-                                # the unfused form of fuse_sp's first iteration (same kernel path)
-                                K.analysis(n, table, x_prev, None if prop is not None else fc.x,
-                                           None if prop is not None else fc.P, x_new, None, None, status,
-                                           self._partials, N=N, prop=prop, order=order)
-                                self._reg_log.append({"solver": "plain", "rho": 0.0, "sweeps": 0, "r2": None,
-                                                      "count": 0})
-                            elif cfg.spatial_gamma > 0:
-                                self._regularised_iteration(table, x_prev, fc, x_new, A_keep, status, prop, out_now,
-                                                            final=n_iter >= cfg.min_iterations)
-                            elif bp:
-                                self._band_parallel_iteration(table, x_prev, fc, x_new, A_keep, status)
-                            elif split is not None:
-                                self._split_iteration(split, x_prev, fc, x_new, A_keep, status)
-                            elif prop is not None:
-                                K.analysis(n, table, x_prev, None, None, x_new, A_keep, None, status, self._partials, N=N,
-                                           prop=prop, out=out_now, order=order, a_rows=a_rows)
-                            else:
-                                K.analysis(n, table, x_prev, fc.x, fc.P, x_new, A_keep, None, status, self._partials, N=N,
-                                           out=out_now, order=order, a_rows=a_rows)
-                    red = self._red_hist[min(n_iter, self._red_hist.numel() - 1):][:1]
-                    with self.timer.phase("analysis"):
-                        if N:
-                            K.reduce_partials(self._partials, red)
-                        else:
-                            red.zero_()
-                    with self.timer.phase("converge"):
-                        pend = self.comm.sum_f64_async(red)
-                    x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
-                if n_iter < cfg.min_iterations:
-                    # this iteration cannot end the loop (n_iter <= max_iterations too):
-                    # queue the next one without waiting for the norm
-                    deferred.append((n_iter, pend))
-                    n_iter += 1
-                    continue
-                if self._lookahead_fn is not None:
-                    # host preparation of the next date runs under this iteration's kernels
-                    self._lookahead_fn()
-                    self._lookahead_fn = None
-                self._resolve_lazy_norms()
-                for it, pd in deferred:
-                    norms.append(self._log_norm(pd.result(), len_x, len(bands), it))
-                deferred = []
-                convergence_norm = self._log_norm(pend.result(), len_x, len(bands), n_iter)
-                norms.append(convergence_norm)
-                if convergence_norm < cfg.convergence_tolerance and n_iter >= cfg.min_iterations:
-                    break
-                if n_iter > cfg.max_iterations:
-                    LOG.warning("Bailing out after 25 iterations!!!!!!")
-                    break
-                n_iter += 1
+        run = _GNRun(timestep=timestep, specs=specs, dbs=dbs, table=table, precomp=precomp, gain=gain, bp=bp,
+                     split=split, prop=prop, fc=fc, x_prev=x_prev, x_new=x_new, P_out=P_out, status=status,
+                     order=order, out_t=out_t, h0_outs=h0_outs, a_rows=a_rows, len_x=len_x, n_bands=len(bands),
+                     fuse2=fuse2, fuse_sp=fuse_sp, first_plain=first_plain, static_conv=static_conv)
+        # the iteration strategy: the reference's exit test per chunk or over the tile
+        x_prev, n_iter, norms = (self._gn_chunked if chunked else self._gn_global)(run)
         if ld != x_prev.shape[1]:
             raise RuntimeError("leading dimension changed")
         if P_out is None:          # no precision row needed: the forecast's buffer shape, nothing valid
@@ -952,7 +857,7 @@ class LinearKalman:
         self._output_written = state if out_t is not None else None
         if cfg.hessian_correction and not gain and N:
             with self.timer.phase("hessian"):
-                K.hessian(n, table, state.x, state.P, N=N)
+                K.hessian(n, run.table, state.x, state.P, N=N)
         if bp:
             status = self._band_parallel_status(status)
         self.last_status = status
@@ -1008,126 +913,6 @@ class LinearKalman:
         if spec.mode == PROP_INFO_APPROX:
             return {tri_pos(n, j, j) for j in range(n)}
         return None
-
-    # ------------------------------------------------ per-chunk convergence
-    def _chunk_state(self):
-        from .chunks import ChunkConvergence
-
-        cc = self._chunks
-        block = tuple(int(v) for v in self.config.convergence_chunk)
-        if cc is None or cc.block != block:
-            cc = self._chunks = ChunkConvergence(self.partition, block, self.n_params, self.device, self.comm)
-        return cc
-
-    def _gn_chunked(self, table, specs, dbs, precomp, prop, fc, x_prev, x_new, P_out, status, order, out_t,
-                    h0_outs, a_rows):
-        """Gauss-Newton loop with the exit test per chunk (engine/chunks.py;
-        reference: one LinearKalman per get_chunks tile, kafka_test_Py36.py:147-187,
-        each testing ||x_a - x_prev|| / len(x_a) < tol, linear_kf.py:293-304).
-
-        Every launch writes each visited pixel's |dx|^2; after each iteration
-        that can end the loop the chunks are tested (one C1 all-gather of the
-        per-chunk partials), and the next launch visits only the pixels of the
-        chunks still iterating (the stopped chunks' x, precision, outputs and
-        status stay as their last iteration wrote them).  Returns (x, the
-        largest chunk's iteration count, the largest tested norm per
-        iteration)."""
-        cfg = self.config
-        n, N = self.n_params, self.N
-        cc = self._chunk_state()
-        cc.begin()
-        fx, fP = (None, None) if prop is not None else (fc.x, fc.P)
-        fuse = (cfg.fuse_gn and not precomp and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
-                and not (prop is None and fc is None))
-        n_iter, n_visit, vis, full = 1, N, order, True
-        norms = []
-        while True:
-            A_keep = P_out if n_iter >= cfg.min_iterations else None
-            out_now = out_t if n_iter >= cfg.min_iterations else None
-            if precomp:
-                pre = self._precompute_host(specs, dbs, x_prev)
-                table = build_table(specs, dbs, n, self._cache, self.device, h0_outs, pre)
-            kw = dict(prop=prop, order=vis, dn_out=cc.dn, a_rows=a_rows)
-            if not full:
-                kw["n_visit"] = n_visit
-            with self.timer.phase("analysis"):
-                if N and n_visit:
-                    if fuse and n_iter == 1:
-                        K.analysis(n, table, x_prev, fx, fP, x_new, P_out, None, status, None, N=N, out=out_t,
-                                   gn_fused=2, **kw)
-                    else:
-                        K.analysis(n, table, x_prev, fx, fP, x_new, A_keep, None, status, None, N=N, out=out_now,
-                                   **kw)
-            if fuse and n_iter == 1:
-                n_iter = 2
-            x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
-            if n_iter < cfg.min_iterations:
-                n_iter += 1
-                continue
-            with self.timer.phase("converge"):
-                pend = cc.decide(n_iter, cfg.convergence_tolerance, cfg.min_iterations, cfg.max_iterations)
-            if self._lookahead_fn is not None:
-                self._lookahead_fn()
-                self._lookahead_fn = None
-            n_act, mx, px, n_new = (pend.result(j) for j in range(4))
-            n_act, px = int(n_act), int(px)
-            norms.append(float(mx))
-            LOG.info("Iteration # %d: %d of %d chunks converged, %d still iterating, largest chunk norm %g",
-                     n_iter, int(n_new), cc.tested, n_act, mx)
-            if n_act == 0:
-                break
-            if n_iter > cfg.max_iterations:      # chunk_decide bails every chunk out past max_iterations
-                raise RuntimeError("per-chunk loop past max_iterations with active chunks")
-            with self.timer.phase("converge"):
-                vis = cc.compact(vis, n_visit if N else 0, px, x_prev, x_new)
-            n_visit, full = px, False
-            n_iter += 1
-        self.last_chunk_iters = cc.histogram()
-        if max(self.last_chunk_iters or {0: 0}) > cfg.max_iterations:
-            LOG.warning("Bailing out after 25 iterations!!!!!!")
-        return x_prev, n_iter, norms
-
-    def _spatial_record(self) -> list:
-        """Per GN iteration of the date: solver, Jacobi bound rho, sweeps and --
-        with metrics on (one read-back + C1 sum) -- the RMS residual of the
-        coupled GMRF system after the sweeps."""
-        out = []
-        for r in self._reg_log:
-            e = {"solver": r["solver"], "rho": round(r["rho"], 6), "sweeps": r["sweeps"]}
-            if self.metrics.enabled and r["r2"] is not None:
-                tot = self.comm.sum_f64(r["r2"].reshape(1))
-                e["residual_rms"] = math.sqrt(max(tot, 0.0) / max(1, r["count"]))
-            out.append(e)
-        self._reg_log = []
-        return out
-
-    def _norms_needed_now(self) -> bool:
-        """Per-date metrics report the norms as they happen.  Rank-uniform on
-        purpose (the metrics path is part of the shared config): the answer
-        decides whether this rank queues another collective, so a per-process
-        setting such as the log level (INFO often on rank 0 only) must not
-        enter it -- INFO lines of statically converged dates are logged when
-        the deferred norms resolve."""
-        return bool(self.metrics.enabled)
-
-    def _resolve_lazy_norms(self):
-        """Fill in the deferred norms of statically converged dates (linear
-        operators): iteration 1's norm, and a check that iteration 2's is 0."""
-        while self._lazy_norms:
-            norms, p1, p2, len_x, nb = self._lazy_norms.pop(0)
-            norms[0] = self._log_norm(p1.result(), len_x, nb, 1)
-            n2 = p2.result()
-            if n2 != 0.0:
-                LOG.warning("linear operator: second Gauss-Newton norm %g is not 0", n2)
-                norms[1] = self._log_norm(n2, len_x, nb, 2)
-
-    @staticmethod
-    def _log_norm(total: float, len_x: float, n_bands: int, n_iter: int) -> float:
-        """convergence_norm = ||x_a - x_prev||_2 / len(x_a) (linear_kf.py:293-296)."""
-        convergence_norm = float(np.sqrt(max(total, 0.0)) / len_x)
-        LOG.info("Band {:d}, Iteration # {:d}, convergence norm: {:g}".format(n_bands - 1, n_iter,
-                                                                             convergence_norm))
-        return convergence_norm
 
     # ------------------------------------------------ split GP operator path
     def _split_plan_kind(self, specs):
@@ -1211,288 +996,6 @@ class LinearKalman:
                 K.analysis(n, an_tab, x_prev, fc.x, fc.P, None, A_c, b_c, status, None, N=N, solve=False,
                            a_in=a_in, b_in=b_in)
                 prev = (A_c, b_c)
-
-    def _regularised_iteration(self, table, x_prev, fc: KFState | None, x_out, A_out, status, prop=None, out=None,
-                               final=True, partials_first=None):
-        """GMRF spatial prior (K9 + C2), affine block-Jacobi form (kf_core.h):
-        the analysis kernel assembles (A, b) and, instead of solving, factors
-        A_reg = A + g deg E_R once and writes u = A_reg^-1 b and V = A_reg^-1 E_R;
-        each sweep then iterates only the k regularised fields z <- u_R + g V_RR
-        s(z) (s: neighbour sums, halo rows exchanged by C2), and the last one forms
-        x = u + g V s(z) with the convergence partials.  Identical to ``sweeps``
-        block-Jacobi sweeps of (A_reg) x = b + g E_R sum_q x_q.  The analysis
-        precision includes the smoother's diagonal.  With ``prop`` the forecast
-        is fused as in the plain path (first iteration: x0 = forecast, written
-        for the norm and the first sweep).  ``partials_first``: the launch runs
-        the plain first Gauss-Newton iteration in registers (its norm there)
-        and prepares the regularised second, linearised at x_1 (written to the
-        x0 buffer, the finish's reference for the norm)."""
-        from ..parallel.halo import HaloExchanger
-
-        if self._reg is None:
-            self._reg = HaloExchanger(self.partition, self.comm, self.n_params, self.device,
-                                      self.config.spatial_params)
-            self._reg_geo = self.partition.dense_geometry()
-        reg, geo = self._reg, self._reg_geo
-        n, N = self.n_params, self.N
-        gamma = self.config.spatial_gamma
-        sweeps = max(1, int(self.config.jacobi_sweeps))
-        rows = reg.reg_rows()
-        fx, fP = (fc.x, fc.P) if fc is not None else (None, None)
-        fused = partials_first is not None
-        if not rows:   # nothing regularised: plain analysis
-            K.analysis(n, table, x_prev, fx, fP, x_out, A_out, None, status, self._partials, N=N, prop=prop, out=out,
-                       gn_fused=2 if fused else 1, partials_first=partials_first, order=self._visit)
-            return
-        k = len(rows)
-        ld = x_out.shape[1]
-        if self._reg_uv is None or self._reg_uv[0].shape[1] != ld or self._reg_uv[1].shape[0] != k * n:
-            self._reg_uv = tuple(torch.empty((r, ld), dtype=torch.float32, device=self.device)
-                                 for r in (n, k * n, n))
-        u, v, x0_buf = self._reg_uv
-        x_ref = x_prev if (x_prev is not None and not fused) else x0_buf
-        # the final iteration's uncertainty raster comes from the prepare (diag of
-        # the regularised precision in registers), the mean from reg_finish
-        K.analysis(n, table, x_prev, fx, fP, u, A_out, None, status, None, N=N, prop=prop,
-                   reg=dict(gamma=gamma, mask=reg.reg_mask, v_out=v, nbr=None if geo else reg.nbr, geo=geo),
-                   x0_out=None if x_ref is x_prev else x0_buf,
-                   out=None if out is None else (None, out[1], out[2]),
-                   gn_fused=2 if fused else 1, partials_first=partials_first, order=self._visit)
-        if fused:
-            self._reg_log.append({"solver": "plain", "rho": 0.0, "sweeps": 0, "r2": None, "count": 0})
-        nbr = None if geo else reg.nbr
-        tol = self.config.spatial_tol if final else self.config.spatial_tol_first
-        depth = self._reg_tiled_depth(k)
-        if depth:
-            cur, rho, sweeps = self._reg_tiled_solve(reg, geo, u, v, x_ref, rows[0], gamma, tol, depth, sweeps)
-        else:
-            cur, rho, sweeps = self._reg_sweep_solve(reg, geo, nbr, u, v, x_ref, rows, gamma, tol, sweeps)
-        K.reg_finish(n, u, v, cur, nbr, x_ref, x_out, gamma, reg.reg_mask, N, partials=self._partials, geo=geo,
-                     out=None if out is None else (out[0], None, out[2]))
-        # residual of the coupled solve (metrics only): the finish applied one more
-        # Jacobi update to the last iterate, x_R - z = J z + f - z (device, read lazily)
-        r2 = None
-        if self.metrics.enabled:
-            r2 = sum(((x_out[r, :N] - cur[i, :N]).double().pow(2).sum() for i, r in enumerate(rows)),
-                     torch.zeros((), dtype=torch.float64, device=self.device))
-        self._reg_log.append({"solver": self.config.spatial_solver, "rho": rho, "sweeps": sweeps, "r2": r2,
-                              "count": k * self.n_total})
-
-    def _reg_tiled_depth(self, k: int) -> int:
-        """Sweeps per temporal-blocking pass of the coupled solve, 0 for the
-        per-sweep path.  Rank-uniform (every rank sees the whole state mask and
-        the strip bounds): one regularised field on a fully active raster, a
-        pass as deep as the shallowest strip (its deep halo comes from one
-        neighbour) and at most REG_TILE_MAX_SWEEPS."""
-        if not self.config.spatial_tiled or k != 1:
-            return 0
-        dense = getattr(self, "_mask_dense", None)
-        if dense is None:
-            dense = self._mask_dense = bool(self.state_mask.size) and bool(self.state_mask.all())
-        if not dense:
-            return 0
-        h_min = min(b - a for a, b in self.partition.bounds)
-        return int(min(K.REG_TILE_MAX_SWEEPS, h_min))
-
-    def _reg_rho_async(self, reg, v, rows, k, gamma):
-        """Chebyshev bound rho = max over pixels of g deg ||V_RR||_inf, a
-        Gershgorin bound of the Jacobi matrix's spectral radius (its spectrum is
-        real: J is similar to a symmetric matrix), max-reduced over the ranks
-        on the stream; returns a pending read-back (PendingSum, element 0)."""
-        from ..parallel.comm import PendingSum
-
-        n, N = self.n_params, self.N
-        if N and k == 1:
-            # V row (c * n + r_j): component r_j of column c (kf_core.h JacobiArgs); one
-            # field: V_RR >= 0 is the row itself (a view), one fused multiply + max
-            rho_t = (torch.amax(v[rows[0], :N] * reg.degrees) * gamma).reshape(1).double()
-        elif N:
-            blk = torch.stack([v[[c * n + r for c in range(k)], :N].abs().sum(0) for r in rows])   # [k, N]
-            rho_t = (gamma * blk.amax(0) * reg.degrees).amax().reshape(1).double()
-        else:
-            rho_t = torch.zeros(1, dtype=torch.float64, device=self.device)
-        return PendingSum(self.comm.all_reduce_(rho_t, op="max"), 1, 1)
-
-    def _reg_sweeps_for(self, rho: float, tol: float):
-        """(rho, sweeps) of the coupled solve: the sweeps (the finish included)
-        cut the error by ``tol`` at the Chebyshev rate sigma = rho / (1 + sqrt(1
-        - rho^2)); the same expressions as the device schedule
-        (kf_core.h:reg_cheb_schedule).  ``tol``: spatial_tol for an iteration
-        that can end the GN loop, spatial_tol_first before."""
-        cfg = self.config
-        if not rho < 1.0:
-            LOG.warning("spatial prior: Jacobi bound rho=%.4f >= 1, plain Jacobi sweeps", rho)
-            return 0.0, max(1, int(cfg.spatial_max_sweeps))
-        if rho <= 0.0:
-            return 0.0, 1
-        sigma = rho / (1.0 + math.sqrt(max(0.0, 1.0 - rho * rho)))
-        need = math.ceil(math.log(2.0 / tol) / math.log(1.0 / sigma))
-        return rho, int(min(max(1, need), int(cfg.spatial_max_sweeps)))
-
-    @staticmethod
-    def _cheb_weights(rho: float, n_sweeps: int):
-        """Chebyshev semi-iterative weights of the sweeps before the finish:
-        (omega, Chebyshev step?) -- the first step is plain Jacobi."""
-        sched, omega = [], 1.0
-        for it in range(n_sweeps):
-            if rho > 0 and it > 0:
-                omega = 1.0 / (1.0 - 0.5 * rho * rho) if it == 1 else 1.0 / (1.0 - 0.25 * rho * rho * omega)
-            sched.append((omega, rho > 0 and it > 0))
-        return sched
-
-    def _reg_sweep_solve(self, reg, geo, nbr, u, v, x_ref, rows, gamma, tol, sweeps):
-        """Coupled solve, one launch per sweep (masked strips, several fields).
-        The first sweep is plain Jacobi whatever rho is, so it is queued before
-        rho is read back: the host waits while the GPU runs it.  (With rho <= 0
-        the schedule has no sweep before the finish; V_RR deg = 0 everywhere
-        then, so that extra sweep leaves z = u and the finish unchanged.)  C2
-        overlap on distributed strips: each sweep's boundary rows, their
-        exchange posted, the interior rows under it."""
-        cfg = self.config
-        n, N = self.n_params, self.N
-        k = len(rows)
-        cheb = cfg.spatial_solver == "chebyshev"
-        pend = self._reg_rho_async(reg, v, rows, k, gamma) if cheb else None
-        rho = 0.0
-        z = reg.z_buffers(k)
-        for i, r in enumerate(rows):
-            z[0][i, :N].copy_(x_ref[r, :N])
-        cur = reg.fill_halo(z[0])
-        prev = None
-        overlap = self.comm.distributed and reg.split is not None
-        sa, sb = reg.split if overlap else (0, 0)
-        sched = [(1.0, False)] if cheb else self._cheb_weights(0.0, sweeps - 1)
-        it = 0
-        while it < len(sched):
-            omega, use_prev = sched[it]
-            nxt = next(b for b in z if b is not cur and b is not prev)
-            zp = prev if use_prev else None
-            if overlap:
-                with self.timer.phase("reg_boundary"):
-                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(0, sa), z_prev=zp,
-                                omega=omega)
-                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(N - sb, sb),
-                                z_prev=zp, omega=omega)
-                with self.timer.phase("halo"):
-                    hp = reg.start_fill(nxt)
-                with self.timer.phase("reg_interior"):
-                    K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, rows=(sa, N - sa - sb),
-                                z_prev=zp, omega=omega)
-                with self.timer.phase("halo"):
-                    nxt = reg.finish_fill(hp, nxt)
-                self.reg_overlapped_sweeps += 1
-            else:
-                K.reg_sweep(n, u, v, cur, nbr, nxt, gamma, reg.reg_mask, N, geo=geo, z_prev=zp, omega=omega)
-                nxt = reg.fill_halo(nxt)
-            prev, cur = cur, nxt
-            it += 1
-            if pend is not None:
-                # the first sweep is queued: read rho while the GPU runs it
-                rho, sweeps = self._reg_sweeps_for(pend.result(0), tol)
-                pend = None
-                sched = self._cheb_weights(rho, max(sweeps - 1, 1))
-        return cur, rho, sweeps
-
-    def _reg_tiled_solve(self, reg, geo, u, v, x_ref, j0, gamma, tol, depth, sweeps):
-        """Coupled solve of one regularised field on dense strips, `depth`
-        sweeps per pass out of LDS (kf_reg_tiled.hip).
-
-        * The schedule lives on the device: rho (one max pass over V_RR deg),
-          its all-rank max, then the sweep count and Chebyshev weights
-          (RegSchedule).  The first pass is queued at once and reads them; the
-          host reads the sweep count back while the GPU runs that pass, then
-          queues the rest (no host wait between the prepare and the sweeps).
-        * Tile-DP (C2): once per GN iteration the neighbours' u, v and initial
-          iterate rows, then once per pass the last two iterates -- `depth`
-          rows each -- instead of one row per sweep.  A pass runs its boundary
-          tile rows, posts their exchange and runs the interior under it.  The
-          finish reads the neighbours' adjacent row of the final iterate from
-          the last pass's exchange (no extra exchange).
-        Bit-identical to one launch per sweep, at any rank count."""
-        from ..parallel.comm import PendingSum
-
-        cfg = self.config
-        n, N = self.n_params, self.N
-        dist_ = self.comm.distributed
-        z = reg.z_buffers(1)
-        if self._reg_z4 is None or self._reg_z4.shape != z[0].shape:
-            self._reg_z4 = torch.zeros_like(z[0])
-        bufs = [z[0], z[1], z[2], self._reg_z4]
-        cur, prev = bufs[0], bufs[1]
-        cur[0, :N].copy_(x_ref[j0, :N])
-        cheb = cfg.spatial_solver == "chebyshev"
-        pend, rs, rho = None, None, 0.0
-        if cheb:
-            rs = getattr(self, "_reg_sched", None)
-            if rs is None or rs.max_sweeps != int(cfg.spatial_max_sweeps):
-                rs = self._reg_sched = K.RegSchedule(N, cfg.spatial_max_sweeps, self.device)
-            with self.timer.phase("reg_schedule"):
-                rs.rho_pass(v[j0], geo, N, gamma)
-                self.comm.all_reduce_(rs.rho, op="max")
-                rs.schedule(tol)
-                pend = PendingSum(rs.info, 1, 2)
-            n_sched = None
-        else:
-            n_sched = max(1, int(sweeps)) - 1
-            if n_sched == 0:
-                return reg.fill_halo(cur), 0.0, 1
-        halo, rows_b = None, None
-        if dist_:
-            if getattr(reg, "depth", None) != depth:
-                reg.deep_setup(depth)
-            with self.timer.phase("halo"):
-                reg.deep_finish(reg.deep_start({0: u[j0], 1: v[j0], 2: cur[0]}))
-            halo = reg.deep_halo()
-            T = K.reg_tile_rows(geo["h"])
-            ta, tb = K.reg_boundary_tile_rows(geo["h"], depth, halo[0] > 0, halo[1] > 0)
-            rows_b = ((0, ta), (tb, T), (ta, tb))
-        s_base = 0
-        while True:
-            o_cur, o_prev = [b for b in bufs if b is not cur and b is not prev]
-            if cheb:
-                kw = dict(sched=(rs.sched, rs.omega), s_base=s_base, nsweep=depth)
-            else:
-                ns = min(depth, n_sched - s_base)
-                part = self._cheb_weights(0.0, n_sched)[s_base:s_base + ns]
-                kw = dict(omegas=[o for o, _ in part], chebyshev=[c for _, c in part])
-
-            def launch(tr):
-                K.reg_sweeps_tiled(n, u, v, cur, prev, o_cur, o_prev, gamma, reg.reg_mask, N, geo, halo=halo,
-                                   tile_rows=tr, **kw)
-            if dist_:
-                with self.timer.phase("reg_boundary"):
-                    launch(rows_b[0])
-                    launch(rows_b[1])
-                with self.timer.phase("halo"):
-                    hp = reg.deep_start({2: o_cur[0], 3: o_prev[0]})
-                with self.timer.phase("reg_interior"):
-                    launch(rows_b[2])
-                with self.timer.phase("halo"):
-                    reg.deep_finish(hp)
-                self.reg_overlapped_sweeps += 1
-            else:
-                launch(None)
-            self.reg_tiled_launches += 1
-            cur, prev = o_cur, o_prev
-            s_base += depth
-            if n_sched is None:
-                # the first pass is queued: read the schedule while the GPU runs it
-                rho = pend.result(0)
-                sweeps = int(pend.result(1))
-                n_sched = sweeps - 1
-                if not rho < 1.0:
-                    LOG.warning("spatial prior: Jacobi bound rho=%.4f >= 1, plain Jacobi sweeps", rho)
-            if s_base >= n_sched:
-                break
-        if dist_:
-            # the finish's one-row halo: the neighbours' adjacent rows of the final iterate
-            w = int(geo["w"])
-            if halo[2] is not None:
-                cur[0, N:N + w].copy_(halo[2][2, (depth - 1) * w:depth * w])
-            if halo[3] is not None:
-                off = N + reg.n_up
-                cur[0, off:off + w].copy_(halo[3][2, :w])
-        return cur, rho, sweeps
 
     # ------------------------------------------------ band-parallel (TP-like)
     def _band_parallel_iteration(self, table, x_prev, fc: KFState, x_out, A_out, status):

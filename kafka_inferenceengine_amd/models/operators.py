@@ -75,7 +75,7 @@ class LinearOperator:
 
 # margin of a GP band's domain box beyond its training inputs, per side, as a
 # fraction of the input's training range (ST_OUT_OF_DOMAIN)
-GP_DOMAIN_MARGIN = 0.1
+GP_DOMAIN_MARGIN = 0.0
 
 
 def gp_spec(emulator: GaussianProcessEmulator, state_map) -> OperatorSpec:
