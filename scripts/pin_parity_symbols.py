@@ -16,7 +16,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 PKG = "kafka_inferenceengine_amd"
-CITE = re.compile(r"`((?:csrc|engine|inference|input_output|models|ops|parallel|utils)/[\w./]+):(\d+)`")
+CITE = re.compile(r"`((?:csrc|engine|inference|input_output|models|ops|parallel|utils)/[\w./]+):(\d+(?:,\d+)*)`")
 IDENT = re.compile(r"`([A-Za-z_][\w.]*)(?:\(\))?`")
 
 
@@ -69,7 +69,8 @@ def main():
     for line in text.splitlines(keepends=True):
         pieces, last = [], 0
         for mo in CITE.finditer(line):
-            rel, old = mo.group(1), int(mo.group(2))
+            rel, olds = mo.group(1), [int(v) for v in mo.group(2).split(",")]
+            old = olds[0]
             cell_start = line.rfind("|", 0, mo.start()) + 1
             # the symbol: nearest backticked identifier in the citation's cell, else
             # in the row's first cell (the reference component the row maps)
@@ -80,6 +81,23 @@ def main():
                 names = [m.group(1) for m in IDENT.finditer(first) if "/" not in m.group(1)][:1]
             new = old
             path = repo_path(rel)
+            if len(olds) > 1:
+                # several lines: one symbol per line, from the row's first cell
+                first = line.split("|")[1] if line.lstrip().startswith("|") else ""
+                fnames = [m.group(1) for m in IDENT.finditer(first) if "/" not in m.group(1)]
+                if len(fnames) == len(olds) and path.is_file():
+                    news = []
+                    for nm, o in zip(fnames, olds):
+                        defs = definitions(path, nm)
+                        news.append(min(defs, key=lambda d: abs(d - o)) if defs else o)
+                    if news != olds:
+                        moved += 1
+                    pieces.append(line[last:mo.start()] + f"`{rel}:{','.join(map(str, news))}`")
+                else:
+                    kept.append(f"{rel}:{mo.group(2)} (several lines)")
+                    pieces.append(line[last:mo.end()])
+                last = mo.end()
+                continue
             if names and path.is_file():
                 defs = definitions(path, names[-1])
                 if defs:
