@@ -1234,6 +1234,21 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
   int nobs = 0;
   for (int bi = 0; bi < a.n_bands; ++bi) {
     const BandDesc bd = cptr(a.bands)[bi];
+    // the linearisation point outside a GP band's domain box, observed or not
+    // (as the matrix-core kernels test it)
+    if constexpr (FD > 0) {
+      float xi[FD];
+#pragma unroll
+      for (int d = 0; d < FD; ++d) xi[d] = gather_state<NP>(x0, bd.map[d]) - bd.center[d];
+      if (gp_out_of_domain<FD>(&bd, xi)) st |= ST_OUT_OF_DOMAIN;
+    } else if constexpr (FD == 0) {
+      if (bd.op == OP_GP) {
+        float xi[NP];
+#pragma unroll
+        for (int d = 0; d < NP; ++d) xi[d] = d < bd.d ? gather_state<NP>(x0, bd.map[d]) - bd.center[d] : 0.f;
+        if (gp_out_of_domain<NP>(&bd, xi)) st |= ST_OUT_OF_DOMAIN;
+      }
+    }
     float y, w;
     decode_obs<FOBS>(bd, p, y, w);
     if (!(w > 0.f)) {
@@ -1275,19 +1290,6 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
     if constexpr (FD > 0) h0o = opaque(cptr(a.bands + bi))->h0_out;   // not live across the GP loop
 #endif
     if (h0o) KF_PX(h0o, 0, p) = H0;
-    if constexpr (FD > 0) {
-      float xi[FD];
-#pragma unroll
-      for (int d = 0; d < FD; ++d) xi[d] = gather_state<NP>(x0, bd.map[d]) - bd.center[d];
-      if (gp_out_of_domain<FD>(&bd, xi)) st |= ST_OUT_OF_DOMAIN;
-    } else if constexpr (FD == 0) {
-      if (bd.op == OP_GP) {
-        float xi[NP];
-#pragma unroll
-        for (int d = 0; d < NP; ++d) xi[d] = d < bd.d ? gather_state<NP>(x0, bd.map[d]) - bd.center[d] : 0.f;
-        if (gp_out_of_domain<NP>(&bd, xi)) st |= ST_OUT_OF_DOMAIN;
-      }
-    }
     if (!ok) { st |= ST_BAD_OP; continue; }
     ++nobs;
     float yp;

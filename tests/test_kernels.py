@@ -36,7 +36,7 @@ def test_analysis_vs_oracle(dn16):
     assert np.max(np.abs(A - Ar)) / np.abs(Ar).max() < 1e-5
     assert abs(red.item() - ((xr - prob["x"]) ** 2).sum()) / red.item() < 1e-3
     nobs = np.array([(w > 0) for _, w in prob["bands"]]).sum(0)
-    assert np.all((st == K.ST_NO_OBS) == (nobs == 0))
+    assert np.all(((st & ~np.uint8(K.ST_OUT_OF_DOMAIN)) == K.ST_NO_OBS) == (nobs == 0))   # + the domain flag
 
 
 def test_analysis_vs_torch_fp32_reference():
