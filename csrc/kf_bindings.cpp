@@ -125,6 +125,9 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(AnalysisArgs, dn_out, float*)
       .PTR_FIELD(AnalysisArgs, tile_ctr, int32_t*)
       .def_readwrite("a_rows", &AnalysisArgs::a_rows)
+      .def_readwrite("dom_check", &AnalysisArgs::dom_check)
+      .ARR_FIELD(AnalysisArgs, dom_lo, float)
+      .ARR_FIELD(AnalysisArgs, dom_hi, float)
       .def_readwrite("gn_fused", &AnalysisArgs::gn_fused)
       .def_readwrite("band_layout", &AnalysisArgs::band_layout)
       .PTR_FIELD(AnalysisArgs, prop, const PropArgs*)

@@ -169,21 +169,11 @@ struct BandDesc {
   float gpm_scale;             // 2^sigma: undoes the f16-range shift folded into the table's L'
   int32_t map_identity;        // 1: map[d] == d for every input d (full-state GP: no gather / scatter)
   int32_t map_kind;            // GPM_MAP_*: a map known at compile time (JRC-TIP bands), 0: runtime map
-  int32_t dom_check;           // GP: 1 = flag inputs outside [dom_lo, dom_hi] (ST_OUT_OF_DOMAIN)
-  float dom_lo[MAX_D];         // GP: training box of the centred inputs (+ GP_DOMAIN_MARGIN)
+  int32_t dom_check;           // GP: the training box of the centred inputs (+ GP_DOMAIN_MARGIN) is set:
+  float dom_lo[MAX_D];         // the host folds the bands' boxes into AnalysisArgs.dom_* (state space)
   float dom_hi[MAX_D];
 };
 
-// GP inputs (centred, as the kernels form them) outside a band's domain box;
-// NaN counts as outside.  BD: BandDesc in any address space.
-template <int D, typename BD>
-KF_HD bool gp_out_of_domain(BD* bd, const float (&xi)[D]) {
-  if (!bd->dom_check) return false;
-  bool o = false;
-#pragma unroll
-  for (int d = 0; d < D; ++d) o = o || !(xi[d] >= bd->dom_lo[d] && xi[d] <= bd->dom_hi[d]);
-  return o;
-}
 
 // JRC-TIP band mappers (kafka/inference/kf_tools.py:19-23, band_selecta): the
 // matrix-core kernel gathers the GP inputs and updates only the 4 x 4 touched
@@ -319,10 +309,27 @@ struct AnalysisArgs {
   // zeroed device counter the waves of a persistent grid pull 64-slot tiles
   // from; the norm partials are then per tile (partials[tile])
   int32_t* tile_ctr;
+  // GP domain box in state space (ST_OUT_OF_DOMAIN): the intersection over the
+  // GP bands of their inputs' training boxes mapped to the state indices they
+  // read (ops/kernels.py make_band_table); +-inf where no band constrains j
+  int32_t dom_check;
+  float dom_lo[MAX_D];
+  float dom_hi[MAX_D];
 };
 
 // slots visited by an analysis launch
 KF_HD int64_t visit_count(const AnalysisArgs& a) { return a.n_visit > 0 ? a.n_visit : a.N; }
+
+// the linearisation point outside the launch's GP domain box (NaN counts as
+// outside); AP: the launch arguments in any address space
+template <int NP, typename AP>
+KF_HD bool state_out_of_domain(AP a, const float (&x)[NP]) {
+  if (!a->dom_check) return false;
+  bool o = false;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) o = o || !(x[j] >= a->dom_lo[j] && x[j] <= a->dom_hi[j]);
+  return o;
+}
 // packed precision row t stored under AnalysisArgs.a_rows
 KF_HD bool a_row_on(uint64_t rows, int t) { return rows == 0 || ((rows >> t) & 1u); }
 
@@ -1234,21 +1241,6 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
   int nobs = 0;
   for (int bi = 0; bi < a.n_bands; ++bi) {
     const BandDesc bd = cptr(a.bands)[bi];
-    // the linearisation point outside a GP band's domain box, observed or not
-    // (as the matrix-core kernels test it)
-    if constexpr (FD > 0) {
-      float xi[FD];
-#pragma unroll
-      for (int d = 0; d < FD; ++d) xi[d] = gather_state<NP>(x0, bd.map[d]) - bd.center[d];
-      if (gp_out_of_domain<FD>(&bd, xi)) st |= ST_OUT_OF_DOMAIN;
-    } else if constexpr (FD == 0) {
-      if (bd.op == OP_GP) {
-        float xi[NP];
-#pragma unroll
-        for (int d = 0; d < NP; ++d) xi[d] = d < bd.d ? gather_state<NP>(x0, bd.map[d]) - bd.center[d] : 0.f;
-        if (gp_out_of_domain<NP>(&bd, xi)) st |= ST_OUT_OF_DOMAIN;
-      }
-    }
     float y, w;
     decode_obs<FOBS>(bd, p, y, w);
     if (!(w > 0.f)) {
@@ -1315,6 +1307,7 @@ KF_HD float pixel_analysis(const AnalysisArgs& a, int64_t p, float& dn_first) {
     }
   }
   if (nobs == 0) st |= ST_NO_OBS;
+  if (state_out_of_domain<NP>(&a, x0)) st |= ST_OUT_OF_DOMAIN;
   float dn;
 #if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (FD != 0) {

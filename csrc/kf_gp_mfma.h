@@ -701,26 +701,11 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     for (int bi = 0; bi < a.n_bands; ++bi) band(bi, std::integral_constant<int, -1>{});
   }
   if (nobs == 0) st |= ST_NO_OBS;
-  // the linearisation point outside a band emulator's domain box (after the GP
-  // loops: the bounds and centred inputs are not held across them)
-  {
-    auto dom = [&](int bi, auto mkc) {
-      constexpr int MKC = decltype(mkc)::value;
-      const KF_CONST_AS BandDesc* q = opaque(cptr(a.bands) + bi);
-      float xi[D], c = 0.f;
-      if constexpr (MKC == GPM_MAP_TIP_VIS || MKC == GPM_MAP_TIP_NIR) gpm_inputs_const<NP, D, MKC>(q, x0, xi, c);
-      else gpm_inputs<NP, D>(q, x0, xi, c);
-      if (gp_out_of_domain<D>(q, xi)) st |= ST_OUT_OF_DOMAIN;
-    };
-    if constexpr (LAYOUT == BAND_LAYOUT_TIP) {
-      dom(0, std::integral_constant<int, GPM_MAP_TIP_VIS>{});
-      dom(1, std::integral_constant<int, GPM_MAP_TIP_NIR>{});
-    } else {
-      for (int bi = 0; bi < a.n_bands; ++bi) dom(bi, std::integral_constant<int, -1>{});
-    }
-  }
   const KF_CONST_AS AnalysisArgs* ka =
       opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
+  // the linearisation point outside the GP bands' domain box (state space, one
+  // test for every band: AnalysisArgs.dom_*)
+  if (state_out_of_domain<NP>(ka, x0)) st |= ST_OUT_OF_DOMAIN;
   // one epilogue call site for the fused intermediate and the final iteration
   // (bit-identical intermediate x, kf_core.h); tail lanes (act = false) solve
   // too but store nothing: their x0 only feeds the next iteration's MFMA

@@ -10,7 +10,7 @@ with ``w`` the inverse variance (the reference's ``uncertainty``).
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 
 import numpy as np
 import torch
@@ -224,8 +224,7 @@ class TableCache:
         tab = build_table(specs, obs_list, n_params, cache, device)
         # keep the GP record / MFMA tables (cache-owned) and the specs, not the observations
         obs_ids = {id(t) for ob in obs_list for t in (ob.dn, ob.y, ob.w, ob.mask, ob.aux) if t is not None}
-        tab = K.BandTable(tab.buf, tab.n, tuple(t for t in tab.keepalive if id(t) not in obs_ids), tab.fast_d,
-                          tab.fast_obs, tab.gpm_frags, tab.gpm_global, tab.layout)
+        tab = replace(tab, keepalive=tuple(t for t in tab.keepalive if id(t) not in obs_ids))
         self._d[k] = (tab, tuple(specs))
         while len(self._d) > self.size:
             self._d.popitem(last=False)

@@ -97,6 +97,7 @@ class BandTable:
     gpm_frags: int = 0      # > 0: GP on the matrix cores, LDS fragments of all bands (kf_gp_mfma.h)
     gpm_global: bool = False  # GP on the matrix cores, tables read from global memory (too large for LDS)
     layout: int = 0         # BAND_LAYOUT_*: a band layout the kernels know at compile time (0: runtime)
+    dom: tuple | None = None  # GP domain box in state space (lo, hi lists; ST_OUT_OF_DOMAIN)
 
     @property
     def ptr(self) -> int:
@@ -222,7 +223,26 @@ def make_band_table(descs: list, device, keepalive=()) -> BandTable:
     elif (gpm_global and fast_d % 2 == 0 and all(d.map_identity for d in descs)
           and len({tuple(d.center[:fast_d]) for d in descs}) == 1):
         layout = BAND_LAYOUT_SHARED_X
-    return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs, gpm_frags, gpm_global, layout)
+    return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs, gpm_frags, gpm_global, layout,
+                     _state_domain(descs))
+
+
+def _state_domain(descs):
+    """The GP bands' input training boxes (BandDesc.dom_*, centred) folded into
+    one box in state space: input i of a band reads state map[i], so
+    x[map[i]] in [dom_lo[i] + center[i], dom_hi[i] + center[i]]; the
+    intersection over bands and inputs (+-inf where nothing constrains)."""
+    lo, hi, any_ = [-np.inf] * 16, [np.inf] * 16, False
+    for d in descs:
+        if d.op != OP_GP or not d.dom_check:
+            continue
+        m, c, dl, dh = d.map, d.center, d.dom_lo, d.dom_hi
+        for i in range(int(d.d)):
+            j = int(m[i])
+            lo[j] = max(lo[j], float(dl[i]) + float(c[i]))
+            hi[j] = min(hi[j], float(dh[i]) + float(c[i]))
+            any_ = True
+    return (lo, hi) if any_ else None
 
 
 # ------------------------------------------------------------------ ops
@@ -399,6 +419,8 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     if dn_out is not None:
         _check_vec(dn_out, N, "dn_out", torch.float32, dev)
         a.dn_out = _ptr(dn_out)
+    if bands.dom is not None:
+        a.dom_check, a.dom_lo, a.dom_hi = 1, list(bands.dom[0]), list(bands.dom[1])
     if a_rows:
         if int(a_rows) >> nt:
             raise ValueError(f"a_rows has bits past the {nt} packed rows")

@@ -39,6 +39,39 @@ def test_analysis_vs_oracle(dn16):
     assert np.all(((st & ~np.uint8(K.ST_OUT_OF_DOMAIN)) == K.ST_NO_OBS) == (nobs == 0))   # + the domain flag
 
 
+def _expected_out_of_domain(prob, x):
+    """Per band, as the reference emulators see it: the centred inputs outside
+    the training box (OperatorSpec.domain_lo/hi), on any GP band."""
+    out = np.zeros(len(x), bool)
+    for sp in prob["specs"]:
+        xi = x[:, list(sp.state_map)[:len(sp.domain_lo)]] - np.asarray(sp.center)[:len(sp.domain_lo)]
+        out |= ((xi < np.asarray(sp.domain_lo)) | (xi > np.asarray(sp.domain_hi))).any(1)
+    return out
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_domain_flag_marks_exactly_the_out_of_box_pixels(device):
+    """ST_OUT_OF_DOMAIN: set on the pixels whose linearisation point lies
+    outside some GP band's training box, observed or not, and on no other."""
+    prob = C.tip_problem(N=2048, seed=4)
+    x = prob["x"].copy()
+    x[:100, 6] = -1.0           # TLAI below every band's box
+    x[100:200, 0] = 5.0         # band 0's first input above its box
+    x[200:260, 5] = -3.0        # band 1 only
+    prob["x"] = x
+    for bd in prob["raw"]:      # the flag does not depend on the band being observed
+        for key in ("w", "dn"):
+            if key in bd:
+                bd[key][:50] = 0
+    for y, w in prob["bands"]:
+        w[:50] = 0.0
+    _, _, st, _ = _run_analysis(prob, device)
+    want = _expected_out_of_domain(prob, x.astype(np.float32).astype(np.float64))
+    assert want[:260].all() and 0 < want.sum() < len(want)
+    got = (st & K.ST_OUT_OF_DOMAIN) > 0
+    assert np.array_equal(got, want)
+
+
 def test_analysis_vs_torch_fp32_reference():
     """Plain PyTorch fp32 reference of the same op (batched normal equations)."""
     prob = C.tip_problem(seed=1)
