@@ -93,6 +93,17 @@ def build(cfg_name, a, mask, part, dev, comm):
         else:
             over[key] = type(dflt)(val)
 
+    def mkout(params):
+        # --output DIR: the reference's GeoTIFF granule writer (KafkaOutput: fused
+        # device rasters -> pinned host -> writer thread -> tiled DEFLATE GeoTIFF);
+        # default: device-resident rasters only (DeviceOutput)
+        if not a.output:
+            return k.DeviceOutput(params)
+        return k.KafkaOutput(params, [0.0, 10.0, 0.0, 0.0, 0.0, -10.0], "EPSG:32630", a.output,
+                             prefix=f"r{comm.rank}" if comm.world > 1 else None, level=a.output_level,
+                             predictor=3, strategy="rle" if a.output_level else None,
+                             keep_timesteps=a.output_keep)
+
     def mkcfg(**kw):
         # phase_timing: hipEvent pairs around each phase on the compute stream
         # (device time, resolved after the timed region) for the per-rank record
@@ -105,7 +116,7 @@ def build(cfg_name, a, mask, part, dev, comm):
         cfg = mkcfg()
         if cfg_name == "spatial":
             cfg = mkcfg(spatial_gamma=c["gamma"], spatial_params=[6], spatial_tol=c["tol"])
-        kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_nonlinear_observation_operator,
+        kf = k.LinearKalman(obs, mkout(k.TIP_PARAMETERS), mask, k.create_nonlinear_observation_operator,
                             k.TIP_PARAMETERS, state_propagation=k.propagate_information_filter_LAI, config=cfg,
                             comm=comm, partition=part)
         kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
@@ -114,7 +125,7 @@ def build(cfg_name, a, mask, part, dev, comm):
         dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(n_dates)]
         obs = k.SyntheticIdentityObservations(mask, dates=dates, partition=part, device=dev, n_pool=a.pool,
                                               stream=stream, cloud_fraction=a.cloud, seed=seed)
-        kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_linear_observation_operator,
+        kf = k.LinearKalman(obs, mkout(k.TIP_PARAMETERS), mask, k.create_linear_observation_operator,
                             k.TIP_PARAMETERS, state_propagation=k.propagate_information_filter_LAI,
                             config=mkcfg(), comm=comm, partition=part)
         kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
@@ -138,7 +149,7 @@ def build(cfg_name, a, mask, part, dev, comm):
             obs = k.MultiSensorObservations([s2, olci])
         prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
         gn = {"convergence_chunk": [c["chunk"], c["chunk"]]} if "chunk" in c else {}
-        kf = k.LinearKalman(obs, k.DeviceOutput(k.SAIL_PARAMETERS), mask, k.create_prosail_observation_operator,
+        kf = k.LinearKalman(obs, mkout(k.SAIL_PARAMETERS), mask, k.create_prosail_observation_operator,
                             k.SAIL_PARAMETERS, state_propagation=None, prior=prior,
                             config=mkcfg(**gn), comm=comm, partition=part)
         state = kf.state_from_prior(prior)
@@ -177,6 +188,12 @@ def main():
     ap.add_argument("--dump-state", default=None, metavar="PREFIX",
                     help="after the timed region, write each strip's final state x [n_p, N] to "
                          "PREFIX.strip<r>.npy (band slot 0 only; rehearsal checks against one rank)")
+    ap.add_argument("--output", default=None, metavar="DIR",
+                    help="write every timestep's mean/unc GeoTIFFs here (KafkaOutput; the timed region ends "
+                         "after the writer has drained); default: device rasters only")
+    ap.add_argument("--output-level", type=int, default=1, help="DEFLATE level of --output (0: uncompressed)")
+    ap.add_argument("--output-keep", type=int, default=2,
+                    help="keep only the newest N timesteps' files of --output on disk")
     a = ap.parse_args()
     if a.watchdog > 0:
         import faulthandler
@@ -251,6 +268,9 @@ def main():
             comm.barrier()
             if dev.type == "cuda":
                 torch.cuda.synchronize()
+            if a.output:
+                kf.output.flush()         # the warm-up dates' files are out of the timed region
+                w0 = kf.output.writer_stats()
             ph0 = kf.timer.cumulative()   # phase totals of the warm-up steps (subtracted below)
             h2d0 = sum(s.ingest_bytes() for s in srcs)
             t_start = time.perf_counter()
@@ -269,6 +289,10 @@ def main():
             for m in msgs:
                 log(m)
             msgs = []
+    t_drain = time.perf_counter()
+    if a.output:
+        kf.output.flush()                 # every timed date's files are on disk
+    t_drain = time.perf_counter() - t_drain
     comm.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -290,6 +314,23 @@ def main():
             "ingest_ms": phases.get("ingest", 0.0), "phases_ms": phases,
             "h2d_bytes": int(sum(s.ingest_bytes() for s in srcs) - h2d0),
             "gn_iterations": [h.get("gn_iterations") for h in kf.history[a.warmup:]]}
+    if a.output:
+        # granule writer over the timed dates: encode+write time per date, how long
+        # the engine blocked on the writer (full queue / pinned slot), the drain
+        w1 = kf.output.writer_stats()
+        n_w = w1["timesteps_written"] - w0["timesteps_written"]
+        ws = kf.output.write_s[w0["timesteps_written"]:]
+        mine["output"] = {"dir": a.output, "deflate_level": a.output_level, "timesteps": n_w,
+                          "write_ms_mean": round(1e3 * sum(ws) / max(1, len(ws)), 3),
+                          "write_ms_max": round(1e3 * max(ws), 3) if ws else None,
+                          "raster_MB_per_date": round((w1["raster_bytes"] - w0["raster_bytes"]) / max(1, n_w) / 1e6, 1),
+                          "file_MB_per_date": round((w1["file_bytes"] - w0["file_bytes"]) / max(1, n_w) / 1e6, 1),
+                          "queue_depth_max": w1.get("queue_depth_max"),
+                          "queue_wait_ms": round(1e3 * (w1.get("queue_wait_s", 0) - w0.get("queue_wait_s", 0)), 3),
+                          "slot_wait_ms": round(1e3 * (w1["slot_wait_s"] - w0["slot_wait_s"]), 3),
+                          "d2h_wait_ms": round(1e3 * (w1["d2h_s"] - w0["d2h_s"]), 3),
+                          "prune_ms": round(1e3 * (w1["prune_s"] - w0["prune_s"]), 3),
+                          "drain_ms": round(1e3 * t_drain, 3)}
     # per-chunk convergence (config.convergence_chunk): {GN iterations: chunks},
     # summed over the timed dates (the chunk decisions are the same on every rank)
     chunk_hist = {}
@@ -363,6 +404,8 @@ def main():
             n_ch = sum(chunk_hist.values())
             rec["config"]["chunk_gn_mean"] = round(sum(i * n for i, n in chunk_hist.items()) / max(1, n_ch), 3)
         rec["per_rank"] = sorted(per_rank, key=lambda r: r["rank"])
+        if a.output:
+            rec["output"] = [r.get("output") for r in rec["per_rank"]]
         # what torch.distributed saw: the driver can confirm from the record alone
         # that the N-GPU line came from N RCCL ranks on N distinct devices
         import torch.distributed as dist

@@ -365,52 +365,61 @@ void write(const std::string& path, const void* data, int nb, uint64_t H, uint64
   if (predictor == 3 && fmt != 3) throw std::runtime_error("predictor 3 needs floating-point samples");
   if (level <= 0) predictor = 1;
   const int bps = bits / 8;
+  // uncompressed: strips of whole rows written straight from the caller's
+  // planes (zero copy, parallel pwrite); compressed: tiles deflated on the pool
+  const bool striped = level <= 0;
+  const uint64_t row_bytes = W * (uint64_t)bps;
+  const uint64_t rps = striped ? std::max<uint64_t>(1, std::min<uint64_t>(H, (4ull << 20) / std::max<uint64_t>(1, row_bytes))) : 0;
+  const uint64_t nstrip = striped ? (H + rps - 1) / rps : 0;
   const uint64_t across = (W + tile - 1) / tile, down = (H + tile - 1) / tile;
-  const uint64_t nchunk = across * down * (uint64_t)nb;
+  const uint64_t nchunk = striped ? nstrip * (uint64_t)nb : across * down * (uint64_t)nb;
   const uint64_t traw = (uint64_t)tile * tile * bps;
-  std::vector<std::vector<uint8_t>> enc(nchunk);
+  std::vector<std::vector<uint8_t>> enc(striped ? 0 : nchunk);
   const uint8_t* src = static_cast<const uint8_t*>(data);
-  parallel_for((int64_t)nchunk, nthreads, [&](int64_t i) {
-    const uint64_t b = (uint64_t)i / (across * down), id = (uint64_t)i % (across * down);
-    const uint64_t ty = id / across, tx = id % across;
-    std::vector<uint8_t> t(traw, 0);   // edge tiles are zero padded (TIFF 6.0 §15)
-    const uint64_t y0 = ty * tile, x0 = tx * tile;
-    const uint64_t rows = std::min<uint64_t>(tile, H - y0), cols = std::min<uint64_t>(tile, W - x0);
-    const uint8_t* plane = src + b * H * W * bps;
-    for (uint64_t r = 0; r < rows; ++r)
-      std::memcpy(&t[r * tile * bps], plane + ((y0 + r) * W + x0) * bps, cols * bps);
-    if (level <= 0) {
-      enc[i] = std::move(t);
-      return;
-    }
-    if (predictor > 1) {
-      std::vector<uint8_t> tmp;
-      for (uint64_t r = 0; r < tile; ++r) apply_predictor(&t[r * tile * bps], tile, bps, predictor, tmp);
-    }
-    // zlib stream (TIFF compression 8); strategy Z_RLE / Z_HUFFMAN_ONLY trade a
-    // little ratio for ~3x encode speed on float rasters
-    z_stream zs{};
-    if (deflateInit2(&zs, level, Z_DEFLATED, 15, 8, strategy) != Z_OK) throw std::runtime_error("deflateInit2 failed");
-    std::vector<uint8_t> c(deflateBound(&zs, (uLong)traw));
-    zs.next_in = t.data();
-    zs.avail_in = (uInt)traw;
-    zs.next_out = c.data();
-    zs.avail_out = (uInt)c.size();
-    const int rc = deflate(&zs, Z_FINISH);
-    deflateEnd(&zs);
-    if (rc != Z_STREAM_END) throw std::runtime_error("deflate failed");
-    c.resize(zs.total_out);
-    enc[i] = std::move(c);
-  });
+  auto strip_ptr = [&](uint64_t i) {
+    const uint64_t b = i / nstrip, st = i % nstrip;
+    return src + (b * H + st * rps) * row_bytes;
+  };
+  auto strip_bytes = [&](uint64_t i) { return std::min<uint64_t>(rps, H - (i % nstrip) * rps) * row_bytes; };
+  if (!striped) {
+    parallel_for((int64_t)nchunk, nthreads, [&](int64_t i) {
+      const uint64_t b = (uint64_t)i / (across * down), id = (uint64_t)i % (across * down);
+      const uint64_t ty = id / across, tx = id % across;
+      // per-thread scratch reused across tiles (no page faults per tile)
+      thread_local std::vector<uint8_t> t, c, tmp;
+      const uint64_t y0 = ty * tile, x0 = tx * tile;
+      const uint64_t rows = std::min<uint64_t>(tile, H - y0), cols = std::min<uint64_t>(tile, W - x0);
+      t.resize(traw);
+      if (rows < tile || cols < tile) std::fill(t.begin(), t.end(), 0);   // edge tiles zero padded (TIFF 6.0 §15)
+      const uint8_t* plane = src + b * H * W * bps;
+      for (uint64_t r = 0; r < rows; ++r)
+        std::memcpy(&t[r * tile * bps], plane + ((y0 + r) * W + x0) * bps, cols * bps);
+      if (predictor > 1)
+        for (uint64_t r = 0; r < tile; ++r) apply_predictor(&t[r * tile * bps], tile, bps, predictor, tmp);
+      // zlib stream (TIFF compression 8); strategy Z_RLE / Z_HUFFMAN_ONLY trade a
+      // little ratio for ~3x encode speed on float rasters
+      z_stream zs{};
+      if (deflateInit2(&zs, level, Z_DEFLATED, 15, 8, strategy) != Z_OK) throw std::runtime_error("deflateInit2 failed");
+      c.resize(deflateBound(&zs, (uLong)traw));
+      zs.next_in = t.data();
+      zs.avail_in = (uInt)traw;
+      zs.next_out = c.data();
+      zs.avail_out = (uInt)c.size();
+      const int rc = deflate(&zs, Z_FINISH);
+      deflateEnd(&zs);
+      if (rc != Z_STREAM_END) throw std::runtime_error("deflate failed");
+      enc[i].assign(c.begin(), c.begin() + zs.total_out);
+    });
+  }
+  std::vector<uint64_t> offs(nchunk), cnts(nchunk);
+  for (uint64_t i = 0; i < nchunk; ++i) cnts[i] = striped ? strip_bytes(i) : enc[i].size();
   uint64_t payload = 0;
-  for (auto& c : enc) payload += c.size() + (c.size() & 1);
+  for (auto c : cnts) payload += c + (c & 1);
   const bool big = force_big > 0 || (force_big < 0 && payload > 3500000000ull);
   const uint64_t hdr = big ? 16 : 8;
-  std::vector<uint64_t> offs(nchunk), cnts(nchunk);
   uint64_t pos = hdr;
   for (uint64_t i = 0; i < nchunk; ++i) {
     offs[i] = pos;
-    cnts[i] = enc[i].size();
     pos += cnts[i] + (cnts[i] & 1);
   }
   std::vector<Tag> tags;
@@ -423,15 +432,22 @@ void write(const std::string& path, const void* data, int nb, uint64_t H, uint64
   tags.push_back(mk<uint16_t>(277, 3, {(uint16_t)nb}));
   tags.push_back(mk<uint16_t>(284, 3, {(uint16_t)(nb > 1 ? 2 : 1)}));
   tags.push_back(mk<uint16_t>(317, 3, {(uint16_t)predictor}));
-  tags.push_back(mk<uint32_t>(322, 4, {tile}));
-  tags.push_back(mk<uint32_t>(323, 4, {tile}));
+  // tiles: TileWidth/Length + TileOffsets/ByteCounts; strips: RowsPerStrip +
+  // StripOffsets/ByteCounts
+  const uint16_t t_off = striped ? 273 : 324, t_cnt = striped ? 279 : 325;
+  if (striped) {
+    tags.push_back(mk<uint32_t>(278, 4, {(uint32_t)rps}));
+  } else {
+    tags.push_back(mk<uint32_t>(322, 4, {tile}));
+    tags.push_back(mk<uint32_t>(323, 4, {tile}));
+  }
   if (big) {
-    tags.push_back(mk<uint64_t>(324, L, offs));
-    tags.push_back(mk<uint64_t>(325, L, cnts));
+    tags.push_back(mk<uint64_t>(t_off, L, offs));
+    tags.push_back(mk<uint64_t>(t_cnt, L, cnts));
   } else {
     std::vector<uint32_t> o32(offs.begin(), offs.end()), c32(cnts.begin(), cnts.end());
-    tags.push_back(mk<uint32_t>(324, L, o32));
-    tags.push_back(mk<uint32_t>(325, L, c32));
+    tags.push_back(mk<uint32_t>(t_off, L, o32));
+    tags.push_back(mk<uint32_t>(t_cnt, L, c32));
   }
   tags.push_back(mk<uint16_t>(339, 3, std::vector<uint16_t>(nb, (uint16_t)fmt)));
   if (gt.size() == 6) {
@@ -512,7 +528,8 @@ void write(const std::string& path, const void* data, int nb, uint64_t H, uint64
   f.write_at(h, hdr, 0);
   // chunk payloads in parallel pwrite (disjoint ranges)
   parallel_for((int64_t)nchunk, std::max(1, std::min(nthreads, 8)), [&](int64_t i) {
-    if (!enc[i].empty()) f.write_at(enc[i].data(), enc[i].size(), offs[i]);
+    if (striped) f.write_at(strip_ptr((uint64_t)i), cnts[i], offs[i]);
+    else if (!enc[i].empty()) f.write_at(enc[i].data(), enc[i].size(), offs[i]);
   });
   f.write_at(ifdb.data(), ifdb.size(), ifd);
   if (!extra.empty()) f.write_at(extra.data(), extra.size(), ifd + ifd_bytes);

@@ -333,6 +333,8 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         self._dump(timestep, analysis)
         rec = {"event": "timestep", "timestep": timestep.isoformat(), "wall_s": time.perf_counter() - t0,
                "n_pixels": self.n_total, **info}
+        if hasattr(self.output, "writer_stats"):
+            rec["output"] = self.output.writer_stats()     # granule writer: queue depth / waits / encode time
         self.metrics.log(rec)
         self.history.append(rec)
         return analysis

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import os
 import threading
+import time
 from queue import Queue
 
 import numpy as np
@@ -31,9 +32,17 @@ def _fname(folder, param, timestep, prefix, suffix=""):
 
 
 class _Writer:
-    def __init__(self):
-        self.q = Queue(maxsize=4)
+    """One background thread draining a bounded job queue.  Telemetry:
+    ``depth`` (jobs queued or running, sampled at each submit), ``wait_s``
+    (seconds the producer -- the engine's host thread -- blocked on a full
+    queue) and ``busy_s`` (seconds the thread spent in jobs)."""
+
+    def __init__(self, maxsize: int = 4):
+        self.q = Queue(maxsize=maxsize)
         self.err = None
+        self.depth = []
+        self.wait_s = 0.0
+        self.busy_s = 0.0
         self.t = threading.Thread(target=self._run, daemon=True)
         self.t.start()
 
@@ -42,17 +51,22 @@ class _Writer:
             job = self.q.get()
             if job is None:
                 return
+            t0 = time.perf_counter()
             try:
                 job()
             except Exception as e:  # surfaced on flush()
                 self.err = e
             finally:
+                self.busy_s += time.perf_counter() - t0
                 self.q.task_done()
 
     def submit(self, job):
         if self.err:
             raise self.err
+        self.depth.append(self.q.unfinished_tasks)
+        t0 = time.perf_counter()
         self.q.put(job)
+        self.wait_s += time.perf_counter() - t0
 
     def flush(self):
         self.q.join()
@@ -94,7 +108,8 @@ class KafkaOutput:
 
     def __init__(self, parameter_list, geotransform, projection, folder, prefix=None, fmt="GTiff",
                  compress="deflate", asynchronous=True, level: int = 6, tile: int = 256, gather: bool = False,
-                 threads: int | None = None, predictor: int = 1, strategy: str | None = None):
+                 threads: int | None = None, predictor: int = 1, strategy: str | None = None,
+                 keep_timesteps: int | None = None):
         self.geotransform = geotransform
         self.projection = projection
         self.folder = folder
@@ -108,6 +123,10 @@ class KafkaOutput:
         self.threads = threads
         self.predictor = int(predictor)
         self.strategy = strategy
+        # rolling local buffer: keep only the newest ``keep_timesteps`` timesteps'
+        # files on disk (a node that ships granules elsewhere; benchmarks)
+        self.keep_timesteps = keep_timesteps
+        self._by_step = []
         os.makedirs(folder, exist_ok=True)
         self._w = _Writer() if asynchronous else None
         self._dev = None          # DeviceOutput: device planes the analysis kernel writes
@@ -115,6 +134,10 @@ class KafkaOutput:
         self._stream = None
         self.written = []
         self.write_s = []         # per timestep: encode + write wall seconds (writer thread)
+        self.bytes_in = self.bytes_out = 0
+        self.prune_s = 0.0        # keep_timesteps: removing the older timesteps' files
+        self.slot_wait_s = 0.0    # engine thread blocked on a pinned slot still being written
+        self.d2h_s = 0.0          # writer thread waiting for the planes' device->host copy
 
     def _geo(self, engine=None):
         gt = list(self.geotransform) if self.geotransform is not None else None
@@ -131,15 +154,45 @@ class KafkaOutput:
         return self.prefix
 
     def _write_all(self, timestep, mean, unc, gt, prefix):
-        import time
         t0 = time.perf_counter()
+        names = []
         for planes, suffix in ((mean, ""), (unc, "_unc")):
             for ii, param in enumerate(self.parameter_list):
                 fn = _fname(self.folder, param, timestep, prefix, suffix)
                 write_tiff(fn, planes[ii], gt, self.projection, self.compress, level=self.level, tile=self.tile,
                            threads=self.threads, predictor=self.predictor, strategy=self.strategy)
                 self.written.append(fn)
+                names.append(fn)
+                self.bytes_in += planes[ii].nbytes
+                self.bytes_out += os.path.getsize(fn)
         self.write_s.append(time.perf_counter() - t0)
+        if self.keep_timesteps is not None:
+            t1 = time.perf_counter()
+            self._by_step.append(names)
+            while len(self._by_step) > self.keep_timesteps:
+                for fn in self._by_step.pop(0):
+                    if os.path.exists(fn):
+                        os.remove(fn)
+            self.prune_s += time.perf_counter() - t1
+
+    def writer_stats(self) -> dict:
+        """Granule output telemetry (per-timestep and cumulative): encode+write
+        seconds per timestep, raster bytes in / file bytes out, the writer
+        queue's depth at each submit and the seconds the engine blocked on it
+        (a full queue, or a pinned host slot still held by its writer job)."""
+        w = self._w
+        ws = self.write_s
+        out = {"timesteps_written": len(ws), "write_s_last": ws[-1] if ws else None,
+               "write_s_mean": sum(ws) / len(ws) if ws else None, "write_s_max": max(ws) if ws else None,
+               "raster_bytes": self.bytes_in, "file_bytes": self.bytes_out,
+               "ratio": round(self.bytes_in / self.bytes_out, 3) if self.bytes_out else None,
+               "slot_wait_s": round(self.slot_wait_s, 6), "d2h_s": round(self.d2h_s, 6),
+               "prune_s": round(self.prune_s, 6)}
+        if w is not None:
+            out.update({"queue_depth_last": w.depth[-1] if w.depth else 0,
+                        "queue_depth_max": max(w.depth) if w.depth else 0,
+                        "queue_wait_s": round(w.wait_s, 6), "writer_busy_s": round(w.busy_s, 6)})
+        return out
 
     # ------------------------------------------------------- device path
     def device_targets(self, engine, dev, alias: bool = True):
@@ -198,7 +251,9 @@ class KafkaOutput:
         def job(hm=hm, hu=hu, ev=ev, done=done):
             try:
                 if ev is not None:
+                    t0 = time.perf_counter()
                     ev.synchronize()
+                    self.d2h_s += time.perf_counter() - t0
                 self._write_all(timestep, hm.numpy().reshape(n, H, W), hu.numpy().reshape(n, H, W), gt, pf)
             finally:
                 done.set()
@@ -209,7 +264,6 @@ class KafkaOutput:
             job()
 
     def _next_slot(self, n, cols, cuda):
-        import threading
         if not self._host or self._host[0][0].shape != (n, cols):
             pin = cuda and torch.cuda.is_available()
             self._host = []
@@ -221,7 +275,9 @@ class KafkaOutput:
             self._turn = 0
         slot = self._host[self._turn % 2]
         self._turn += 1
+        t0 = time.perf_counter()
         slot[2].wait()                      # its previous writer job has finished with it
+        self.slot_wait_s += time.perf_counter() - t0
         return slot
 
     def dump_data(self, timestep, x_analysis, P_analysis, P_analysis_inv, state_mask, n_params):

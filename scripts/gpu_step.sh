@@ -8,6 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && mkdir -p gpurun_out
 export PYTHONPATH="$R${PYTHONPATH:+:$PYTHONPATH}"
 stop() { echo "!! step $1 rc=$2"; exit "$2"; }
+declare -A seen
 for step in "$@"; do
   name=${step%%:*}; arg=""; [ "$name" != "$step" ] && arg=${step#*:}
   case $name in
@@ -32,10 +33,12 @@ for step in "$@"; do
       tail -1 gpurun_out/bench.log ;;
     cfg)
       # cfg:CONFIG [bench args] -> gpurun_out/bench_CONFIG.log (one JSON line at its end)
+      # (a repeated CONFIG logs to bench_CONFIG_2.log, _3, ...)
       c=${arg%% *}; rest=""; [ "$c" != "$arg" ] && rest=${arg#* }
-      timeout -k 10 900 python -u bench.py --config $c $rest > gpurun_out/bench_$c.log 2>&1 \
-        || { rc=$?; tail -20 gpurun_out/bench_$c.log; stop cfg_$c $rc; }
-      echo "$c $(tail -1 gpurun_out/bench_$c.log | cut -c1-300)" ;;
+      seen[$c]=$(( ${seen[$c]:-0} + 1 )); lg=bench_$c; [ ${seen[$c]} -gt 1 ] && lg=${lg}_${seen[$c]}
+      timeout -k 10 900 python -u bench.py --config $c $rest > gpurun_out/$lg.log 2>&1 \
+        || { rc=$?; tail -20 gpurun_out/$lg.log; stop cfg_$c $rc; }
+      echo "$lg $(tail -1 gpurun_out/$lg.log | cut -c1-300)" ;;
     py)
       # py:SCRIPT [args] -> gpurun_out/py_<script name>.log
       sc=${arg%% *}; rest=""; [ "$sc" != "$arg" ] && rest=${arg#* }; tag=$(basename $sc .py)

@@ -23,6 +23,18 @@ def test_tiff_roundtrip_dtypes(tmp_path):
             assert info["geotransform"] == [10.0, 2.0, 0.0, 20.0, 0.0, -2.0]
 
 
+def test_native_uncompressed_stack_is_striped_zero_copy(tmp_path):
+    """Uncompressed native output: whole-row strips written straight from the
+    planes (several strips per plane, a short last strip), read back exactly."""
+    rng = np.random.default_rng(1)
+    a = rng.random((3, 300, 5000)).astype(np.float32)       # 20 KB rows -> 209-row strips
+    p = tmp_path / "stack_raw.tif"
+    k.write_tiff(p, a, [0.0, 10.0, 0.0, 0.0, 0.0, -10.0], "EPSG:32630", None)
+    b, info = k.read_tiff(p)
+    assert np.array_equal(b, a)
+    assert not info.get("tiled", False) and info.get("compression", 1) == 1
+
+
 def test_reads_reference_mask_tiff():
     path = "/root/reference/Barrax_pivots.tif"
     if not os.path.exists(path):
