@@ -18,7 +18,13 @@
 //          ProjectedCSType / GeographicType (EPSG) and the WKT as citation;
 //          GDAL_NODATA; optional horizontal predictor 2 / 3 and zlib strategy
 //          (RLE / Huffman-only for fast float output).  Tiles are compressed in
-//          parallel and written with parallel pwrite.
+//          parallel and written with parallel pwrite; uncompressed rasters are
+//          written as whole-row strips straight from the caller's planes.
+//          The zlib streams come from libdeflate when the system has it
+//          (libdeflate.so.0, dlopen'ed: 3-4x zlib's speed for the same
+//          standard stream, so TIFF compression 8 and every reader are
+//          unchanged), else from zlib with the requested strategy.
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -244,6 +250,49 @@ static void apply_predictor(uint8_t* row, uint64_t w, int bps, int pred, std::ve
   }
 }
 
+// libdeflate's stable C API, resolved at run time (no headers in this image)
+struct FastDeflate {
+  void* (*alloc)(int) = nullptr;
+  size_t (*compress)(void*, const void*, size_t, void*, size_t) = nullptr;
+  size_t (*bound)(void*, size_t) = nullptr;
+  void (*release)(void*) = nullptr;
+  bool ok = false;
+  FastDeflate() {
+    if (getenv("KAFKA_TIFF_ZLIB")) return;          // force zlib (tests compare the two)
+    void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    alloc = reinterpret_cast<void* (*)(int)>(dlsym(h, "libdeflate_alloc_compressor"));
+    compress = reinterpret_cast<size_t (*)(void*, const void*, size_t, void*, size_t)>(
+        dlsym(h, "libdeflate_zlib_compress"));
+    bound = reinterpret_cast<size_t (*)(void*, size_t)>(dlsym(h, "libdeflate_zlib_compress_bound"));
+    release = reinterpret_cast<void (*)(void*)>(dlsym(h, "libdeflate_free_compressor"));
+    ok = alloc && compress && bound && release;
+  }
+  static const FastDeflate& get() {
+    static const FastDeflate f;
+    return f;
+  }
+};
+
+// one compressor per thread and level (libdeflate's are not thread safe)
+struct ThreadCompressor {
+  void* c = nullptr;
+  int level = -1;
+  ~ThreadCompressor() {
+    if (c) FastDeflate::get().release(c);
+  }
+  void* at(int lv) {
+    if (lv != level) {
+      if (c) FastDeflate::get().release(c);
+      c = FastDeflate::get().alloc(lv);
+      level = lv;
+    }
+    return c;
+  }
+};
+
+bool fast_deflate_available() { return FastDeflate::get().ok; }
+
 static void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t)>& fn) {
   nthreads = std::max(1, std::min<int>(nthreads, (int)std::max<int64_t>(1, n)));
   std::atomic<int64_t> next{0};
@@ -396,6 +445,17 @@ void write(const std::string& path, const void* data, int nb, uint64_t H, uint64
         std::memcpy(&t[r * tile * bps], plane + ((y0 + r) * W + x0) * bps, cols * bps);
       if (predictor > 1)
         for (uint64_t r = 0; r < tile; ++r) apply_predictor(&t[r * tile * bps], tile, bps, predictor, tmp);
+      const FastDeflate& fd = FastDeflate::get();
+      if (fd.ok) {
+        thread_local ThreadCompressor tc;
+        void* comp = tc.at(std::min(level, 12));
+        if (!comp) throw std::runtime_error("libdeflate_alloc_compressor failed");
+        c.resize(fd.bound(comp, traw));
+        const size_t n = fd.compress(comp, t.data(), traw, c.data(), c.size());
+        if (n == 0) throw std::runtime_error("libdeflate_zlib_compress failed");
+        enc[i].assign(c.begin(), c.begin() + n);
+        return;
+      }
       // zlib stream (TIFF compression 8); strategy Z_RLE / Z_HUFFMAN_ONLY trade a
       // little ratio for ~3x encode speed on float rasters
       z_stream zs{};
@@ -568,6 +628,8 @@ void bind_tiff(py::module_& m) {
     tiff::read_window(path, band, reinterpret_cast<void*>(dst), r0, r1, c0, c1, nthreads, elem_bytes);
   }, py::arg("path"), py::arg("band"), py::arg("dst"), py::arg("r0"), py::arg("r1"), py::arg("c0"), py::arg("c1"),
      py::arg("nthreads"), py::arg("elem_bytes") = 0);
+  m.def("tiff_fast_deflate", &tiff::fast_deflate_available,
+        "True when tile DEFLATE uses libdeflate (else zlib)");
   m.def("write_raw", [](const std::string& path, uintptr_t src, uint64_t n, int nthreads, bool sync) {
     py::gil_scoped_release nogil;
     tiff::write_raw(path, reinterpret_cast<const void*>(src), n, nthreads, sync);
