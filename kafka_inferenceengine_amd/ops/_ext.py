@@ -32,20 +32,6 @@ except ImportError as e:  # pragma: no cover - exercised only when unbuilt
     _err = e
 
 
-def _apply_env(m):
-    """Tuning / A-B knobs: KAFKA_MAX_BLOCKS (grid cap of the per-pixel kernels),
-    KAFKA_GP_UNROLL (record-stream unroll of the split GP operator kernel)."""
-    if m is None:
-        return
-    if os.environ.get("KAFKA_MAX_BLOCKS") and hasattr(m, "set_max_blocks"):
-        m.set_max_blocks(int(os.environ["KAFKA_MAX_BLOCKS"]))
-    if os.environ.get("KAFKA_GP_UNROLL") and hasattr(m, "set_gp_unroll"):
-        m.set_gp_unroll(int(os.environ["KAFKA_GP_UNROLL"]))
-
-
-_apply_env(ext)
-
-
 def require_ext():
     if ext is None:
         raise RuntimeError(
@@ -70,5 +56,4 @@ def ensure_built(verbose: bool = False):
 
     ext = importlib.import_module("kafka_inferenceengine_amd._kafka_hip" + ("_checked" if CHECKED else ""))
     _err = None
-    _apply_env(ext)
     return ext

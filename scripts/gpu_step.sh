@@ -1,8 +1,9 @@
 #!/bin/bash
 # One GPU call = a list of named steps, each under its own time limit, stopping at
 # the first failure (gpurun rules: no retries, nothing after a fault/timeout).
-#   bash scripts/gpu_step.sh tests[:FILTER] smoke bench[:ARGS] cfg:CONFIG[ ARGS] py:SCRIPT[ ARGS] \
-#        prof[:ARGS] pmc:V/COUNTERS ...
+#   bash scripts/gpu_step.sh tests[:FILTER] tests_nox[:FILTER] smoke ab[:ARGS] bench[:ARGS] \
+#        cfg:CONFIG[ ARGS] py:SCRIPT[ ARGS] prof[:TAG/ARGS] trace[:TAG/ARGS] phase:ARGS \
+#        pmc:V/COUNTERS pmcb:COUNTERS/BENCH_ARGS ...
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && mkdir -p gpurun_out
@@ -45,11 +46,22 @@ for step in "$@"; do
       timeout -k 10 900 python -u $sc $rest > gpurun_out/py_$tag.log 2>&1 \
         || { rc=$?; tail -20 gpurun_out/py_$tag.log; stop py_$tag $rc; }
       tail -5 gpurun_out/py_$tag.log ;;
-    prof)
-      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run \
-        --output-format csv -- python "$R/bench.py" --steps 4 --warmup 1 $arg > "$R/gpurun_out/prof.log" 2>&1 ) \
-        || { rc=$?; tail -20 gpurun_out/prof.log; stop prof $rc; }
-      echo prof-done ;;
+    prof|trace)
+      # prof[:TAG/BENCH ARGS]  kernel statistics of bench.py (default: tip7, 4 steps) -> gpurun_out/prof[_TAG]/
+      # trace[:TAG/BENCH ARGS] the same plus the memory-copy trace (inter-kernel gaps, H2D overlap)
+      tag=""; rest="--steps 4 --warmup 1"
+      if [ -n "$arg" ]; then tag=_${arg%%/*}; rest=${arg#*/}; fi
+      extra=""; [ "$name" = trace ] && extra="--memory-copy-trace"
+      out="$R/gpurun_out/$name$tag"
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace $extra --stats -d "$out" -o run \
+        --output-format csv -- python "$R/bench.py" $rest > "$out.log" 2>&1 ) \
+        || { rc=$?; tail -20 "$out.log"; stop $name $rc; }
+      echo "$name$tag $(tail -1 "$out.log" | cut -c1-200)" ;;
+    phase)
+      # phase:BENCH ARGS  phase clocks of the fused analysis kernel (_build.py --prof, KAFKA_PROF=1)
+      KAFKA_PROF=1 timeout -k 10 300 python -u bench.py $arg > gpurun_out/phase.log 2>&1 \
+        || { rc=$?; tail -20 gpurun_out/phase.log; stop phase $rc; }
+      grep phase_clocks gpurun_out/phase.log; tail -1 gpurun_out/phase.log | cut -c1-200 ;;
     pmc)
       # pmc:V/C1,C2,...  (V = analysis variant, one counter pass per step)
       v=${arg%%/*}; ctrs=${arg#*/}; tag=${PMC_TAG:-pmc}_v${v}_$(echo "$ctrs" | md5sum | cut -c1-6)
@@ -57,6 +69,16 @@ for step in "$@"; do
         --output-format csv -- python "$R/scripts/bench_kernels.py" --rounds 1 --variants $v > "$R/gpurun_out/pmc.log" 2>&1 ) \
         || { rc=$?; tail -20 gpurun_out/pmc.log; stop pmc $rc; }
       echo pmc-done ;;
+    pmcb)
+      # pmcb:C1,C2,.../BENCH ARGS  one counter pass over bench.py's fused analysis kernels
+      # -> gpurun_out/pmcb/<md5 of the step>/ (+ .log)
+      ctrs=${arg%%/*}; rest=${arg#*/}; tag=$(echo "$arg" | md5sum | cut -c1-8)
+      mkdir -p "$R/gpurun_out/pmcb"; echo "$arg" > "$R/gpurun_out/pmcb/$tag.args"
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 -s KILL 300 rocprofv3 --kernel-trace --pmc ${ctrs//,/ } \
+        --kernel-include-regex "analysis" -d "$R/gpurun_out/pmcb/$tag" -o run --output-format csv -- \
+        python "$R/bench.py" $rest > "$R/gpurun_out/pmcb/$tag.log" 2>&1 ) \
+        || { rc=$?; tail -20 "gpurun_out/pmcb/$tag.log"; stop pmcb $rc; }
+      echo "pmcb $tag $arg" ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
 done
