@@ -123,7 +123,8 @@ def _build(args, comm):
     if args.out:
         out = k.KafkaOutput(params, info.get("geotransform", [0, 1, 0, 0, 0, -1]), info.get("projection", ""),
                             args.out, prefix=args.prefix, level=args.out_level, gather=args.out_gather,
-                            predictor=3 if args.out_fast else 1, strategy="rle" if args.out_fast else None)
+                            predictor=3 if args.out_fast else 1, strategy="rle" if args.out_fast else None,
+                            keep_timesteps=args.out_keep)
     else:
         out = k.DeviceOutput(params)
     kf = k.LinearKalman(obs, out, mask, factory, params, state_propagation=prop,
@@ -150,6 +151,8 @@ def cmd_run(args):
         dev = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
         comm = Comm.single(dev if dev != "cuda" else torch.device("cuda", torch.cuda.current_device()))
     kf, prior, grid, out = _build(args, comm)
+    import time
+    t_run = time.perf_counter()
     start = None
     if args.resume:
         from .input_output.checkpoint import CheckpointManager
@@ -158,12 +161,17 @@ def cmd_run(args):
     else:
         start = kf.state_from_prior(prior)
         state = kf.run(grid, start, None, None)
+    t_flush = time.perf_counter()
     if hasattr(out, "flush"):
         out.flush()
+    t_end = time.perf_counter()
     if comm.rank == 0:
         rec = {"timesteps": len(kf.history), "pixels": kf.n_total,
                "gn_iterations": [h.get("gn_iterations") for h in kf.history],
-               "finite": bool(np.isfinite(state.x[:, :state.N].cpu().numpy()).all())}
+               "finite": bool(np.isfinite(state.x[:, :state.N].cpu().numpy()).all()),
+               # end to end (ingest, assimilation, output drained) and per timestep
+               "wall_s": round(t_end - t_run, 3), "output_drain_s": round(t_end - t_flush, 3),
+               "timestep_wall_ms": [round(1e3 * h["wall_s"], 1) for h in kf.history if "wall_s" in h]}
         if kf.timer.enabled:
             rec["phases_ms"] = kf.timer.cumulative()
             ing = getattr(kf.observations, "_ingest", None)
@@ -174,7 +182,9 @@ def cmd_run(args):
             rec["checkpoint"] = {k_: [round(v, 3) for v in vals] for k_, vals in ck.stats.items() if k_ != "bytes"}
             rec["checkpoint"]["GB"] = [round(b / 1e9, 2) for b in ck.stats["bytes"]]
         if getattr(out, "write_s", None):
-            rec["output"] = {"files": len(out.written), "write_ms": [round(1e3 * t, 1) for t in out.write_s]}
+            # writer telemetry: queue depth, engine waits on the writer, encode time, bytes
+            rec["output"] = {"files": len(out.written), "write_ms": [round(1e3 * t, 1) for t in out.write_s],
+                             **out.writer_stats()}
         print(json.dumps(rec))
     comm.destroy()
 
@@ -269,6 +279,8 @@ def main(argv=None):
     r.add_argument("--out-level", type=int, default=6, help="DEFLATE level of the output GeoTIFFs (1: fastest)")
     r.add_argument("--out-fast", action="store_true",
                    help="floating-point predictor + run-length DEFLATE (about 3x faster encoding)")
+    r.add_argument("--out-keep", type=int, default=None,
+                   help="keep only the newest N timesteps' output files on local disk")
     r.add_argument("--out-gather", action="store_true", help="gather strips to rank 0 and write one raster")
     r.add_argument("--resume", default=None, help="checkpoint directory (latest) or checkpoint path")
     r.add_argument("--log-level", default="WARNING")

@@ -220,6 +220,55 @@ def test_obs_order_device_equals_host(cuda, stream):
     assert all(torch.equal(res[i], res[i + 4]) for i in range(4))
 
 
+def _orders(mask, devs, make_obs, groups_list, locals_=(True, False)):
+    from kafka_inferenceengine_amd.engine.bands import build_table
+    from kafka_inferenceengine_amd.ops import kernels as K
+    res = []
+    for dev in devs:
+        obs = make_obs(dev)
+        kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator if obs.__class__.__name__.
+                            startswith("SyntheticBHR") else k.create_prosail_observation_operator,
+                            k.TIP_PARAMETERS if obs.__class__.__name__.startswith("SyntheticBHR") else
+                            k.SAIL_PARAMETERS, device=dev)
+        bands = kf._device_bands(obs.dates[0])
+        table = build_table([s for s, _ in bands], [d for _, d in bands], kf.n_params, kf._cache, kf.device)
+        out = []
+        for groups in groups_list:
+            for local in locals_:
+                out.append(K.obs_order(table, kf.N, kf.device, groups=groups, local=local)[0].cpu())
+        res.append(out)
+        del kf, table, bands, obs
+    return res
+
+
+def test_obs_order_cross_tile_scan_carry(cuda):
+    """The global partition past one scan tile (obs_scan_kernel: 1024 x 8
+    chunks of 4096 pixels per tile, the carry between tiles): 6000^2 pixels =
+    8790 chunks, two tiles (a 10980^2 production tile has 29.4k chunks, four),
+    device equal to the host runner."""
+    mask = np.ones((6000, 6000), bool)
+    mask[:37, :] = False
+    mk = lambda dev: k.SyntheticBHRObservations(mask, n_train=20, device=dev, stream=True, n_pool=1,  # noqa: E731
+                                                field_cell=8)
+    dev_res, host_res = _orders(mask, (cuda, torch.device("cpu")), mk, [None], locals_=(False,))
+    assert int(mask.sum()) > 8192 * 4096
+    assert torch.equal(dev_res[0], host_res[0])
+
+
+def test_obs_order_eight_classes_partial_chunk(cuda):
+    """Three band groups (G = 3: eight observation classes) on a tile whose
+    last 4096-pixel chunk is partial: device equal to the host runner, chunk-
+    local and global."""
+    mask = np.ones((700, 331), bool)
+    mask[100:180, :] = False
+    mk = lambda dev: k.SyntheticS2Observations(mask, n_bands=3, n_train=20, device=dev, stream=True,  # noqa: E731
+                                               n_pool=1, cloud_fraction=0.4)
+    dev_res, host_res = _orders(mask, (cuda, torch.device("cpu")), mk, [[0, 1, 2], None])
+    assert int(mask.sum()) % 4096 != 0
+    for a, b in zip(dev_res, host_res):
+        assert torch.equal(a, b)
+
+
 def test_streamer_async_copies_keep_stream_order(cuda):
     """DateStreamer copies issued by the HostRing submitter thread (h2d_async)
     under running kernels: every acquired buffer holds its own date's entry,
