@@ -590,14 +590,17 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   constexpr bool SXC = GT && D == NP && D % 2 == 0;
   bool sx = false;
   kf_h8 sxb[2][gpm_k_steps(D)];
+  // the centred inputs too: every band of the layout has the same centre and
+  // the identity map, so gpm_inputs would recompute exactly these values
+  float sxi[SXC ? D : 1];
   if constexpr (SXC) {
     sx = a.band_layout == BAND_LAYOUT_SHARED_X && a.variant != AV_PER_BAND_OPERAND && a.n_bands > 0;
     if (sx) {
       const KF_CONST_AS BandDesc* b0 = cptr(a.bands);
-      float xi0[D], c0;
+      float c0;
 #pragma unroll
-      for (int d = 0; d < D; ++d) xi0[d] = x0[d] - b0->center[d];
-      gpm_operands<D>(xi0, 0.f, sxb, c0);
+      for (int d = 0; d < D; ++d) sxi[d] = x0[d] - b0->center[d];
+      gpm_operands<D>(sxi, 0.f, sxb, c0);
     }
   }
   // one band: GP sums on the matrix cores, value and Jacobian, normal equations.
@@ -619,9 +622,18 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     const bool any = __any(use);
     if (any) {
       float xi[D], c = 0.f;
-      if (TIPK && mk == GPM_MAP_TIP_VIS) gpm_inputs_const<NP, D, GPM_MAP_TIP_VIS>(bdp, x0, xi, c);
-      else if (TIPK && mk == GPM_MAP_TIP_NIR) gpm_inputs_const<NP, D, GPM_MAP_TIP_NIR>(bdp, x0, xi, c);
-      else gpm_inputs<NP, D>(bdp, x0, xi, c);
+      if (TIPK && mk == GPM_MAP_TIP_VIS) {
+        gpm_inputs_const<NP, D, GPM_MAP_TIP_VIS>(bdp, x0, xi, c);
+      } else if (TIPK && mk == GPM_MAP_TIP_NIR) {
+        gpm_inputs_const<NP, D, GPM_MAP_TIP_NIR>(bdp, x0, xi, c);
+      } else if (SXC && sx) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) xi[d] = sxi[SXC ? d : 0];
+#pragma unroll
+        for (int d = 0; d < D; ++d) c = fmaf(bdp->coef[d] * xi[d], xi[d], c);
+      } else {
+        gpm_inputs<NP, D>(bdp, x0, xi, c);
+      }
       c *= -0.5f * LOG2E;
       float S[D + 1];
       KF_PHASE(KF_PH_BAND_IN)

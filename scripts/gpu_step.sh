@@ -3,7 +3,7 @@
 # the first failure (gpurun rules: no retries, nothing after a fault/timeout).
 #   bash scripts/gpu_step.sh tests[:FILTER] tests_nox[:FILTER] smoke ab[:ARGS] bench[:ARGS] \
 #        cfg:CONFIG[ ARGS] py:SCRIPT[ ARGS] prof[:TAG/ARGS] trace[:TAG/ARGS] phase:ARGS \
-#        pmc:V/COUNTERS pmcb:COUNTERS/BENCH_ARGS ...
+#        pmc:V/COUNTERS pmcb:COUNTERS/BENCH_ARGS dist:N/BENCH_ARGS ...
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && mkdir -p gpurun_out
@@ -36,7 +36,8 @@ for step in "$@"; do
       # cfg:CONFIG [bench args] -> gpurun_out/bench_CONFIG.log (one JSON line at its end)
       # (a repeated CONFIG logs to bench_CONFIG_2.log, _3, ...)
       c=${arg%% *}; rest=""; [ "$c" != "$arg" ] && rest=${arg#* }
-      seen[$c]=$(( ${seen[$c]:-0} + 1 )); lg=bench_$c; [ ${seen[$c]} -gt 1 ] && lg=${lg}_${seen[$c]}
+      # LOGTAG=x: bench_CONFIGx.log (A/B of modules in one call: KAFKA_EXT=name LOGTAG=_name)
+      seen[$c]=$(( ${seen[$c]:-0} + 1 )); lg=bench_$c${LOGTAG:-}; [ ${seen[$c]} -gt 1 ] && lg=${lg}_${seen[$c]}
       timeout -k 10 900 python -u bench.py --config $c $rest > gpurun_out/$lg.log 2>&1 \
         || { rc=$?; tail -20 gpurun_out/$lg.log; stop cfg_$c $rc; }
       echo "$lg $(tail -1 gpurun_out/$lg.log | cut -c1-300)" ;;
@@ -62,6 +63,14 @@ for step in "$@"; do
       KAFKA_PROF=1 timeout -k 10 300 python -u bench.py $arg > gpurun_out/phase.log 2>&1 \
         || { rc=$?; tail -20 gpurun_out/phase.log; stop phase $rc; }
       grep phase_clocks gpurun_out/phase.log; tail -1 gpurun_out/phase.log | cut -c1-200 ;;
+    dist)
+      # dist:N/BENCH ARGS  N ranks of bench.py on this box's one GPU over gloo (a logic /
+      # contention rehearsal, not a scaling point: the ranks share the GPU and the CPUs)
+      n=${arg%%/*}; rest=${arg#*/}; port=$((29700 + RANDOM % 200))
+      KAFKA_DIST_BACKEND=gloo timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node=$n \
+        --master-addr=127.0.0.1 --master-port=$port bench.py --gpus $n --device cuda:0 $rest \
+        > gpurun_out/dist$n.log 2>&1 || { rc=$?; tail -20 gpurun_out/dist$n.log; stop dist $rc; }
+      echo "dist$n $(tail -1 gpurun_out/dist$n.log | cut -c1-300)" ;;
     pmc)
       # pmc:V/C1,C2,...  (V = analysis variant, one counter pass per step)
       v=${arg%%/*}; ctrs=${arg#*/}; tag=${PMC_TAG:-pmc}_v${v}_$(echo "$ctrs" | md5sum | cut -c1-6)
