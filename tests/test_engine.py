@@ -189,6 +189,33 @@ def test_kafka_output_tiff_roundtrip(tmp_path):
     assert len(out.write_s) == len(grid) - 1 and len(out.written) == 14 * (len(grid) - 1)
 
 
+def test_kafka_output_writer_telemetry_and_rolling_files(tmp_path):
+    """The granule writer's telemetry (per timestep in the metrics record and
+    writer_stats): queue depth at each submit, waits of the time loop on the
+    writer, encode time, raster and file bytes; keep_timesteps leaves only the
+    newest timesteps' files on disk.  Uncompressed output is written as strips
+    straight from the planes and reads back exactly."""
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=5)
+    grid = _grid(4)
+    out = k.KafkaOutput(k.TIP_PARAMETERS, [500000., 10., 0., 4000000., 0., -10.], "EPSG:32630", str(tmp_path),
+                        level=0, keep_timesteps=1)
+    kf = _engine(mask, obs, Q, out=out)
+    st = kf.run(grid, x0, None, Pinv)
+    out.flush()
+    ws = out.writer_stats()
+    n_ts = len(grid) - 1
+    assert ws["timesteps_written"] == n_ts and ws["queue_depth_max"] >= 0
+    assert ws["raster_bytes"] == n_ts * 14 * mask.size * 4 and ws["file_bytes"] >= ws["raster_bytes"]
+    assert ws["queue_wait_s"] >= 0 and ws["slot_wait_s"] >= 0 and ws["write_s_max"] > 0
+    recs = [h for h in kf.history if "output" in h]
+    assert len(recs) == n_ts and all("queue_depth_last" in h["output"] for h in recs)
+    files = sorted(p.name for p in tmp_path.iterdir())
+    assert len(files) == 14 and all(grid[-1].strftime("A%Y%j") in f for f in files)
+    arr, _ = k.read_tiff(tmp_path / f"TeLAI_{grid[-1].strftime('A%Y%j')}.tif")
+    assert np.array_equal(arr[mask], st.x[6].numpy())
+    assert not k.tiff_info(tmp_path / f"TeLAI_{grid[-1].strftime('A%Y%j')}.tif")["tiled"]
+
+
 def test_memory_output_reference_signature():
     mask, obs, prior, x0, Pinv, Q = _setup(seed=6)
     out = k.KafkaOutputMemory(k.TIP_PARAMETERS)
