@@ -142,7 +142,8 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         self._prepared = None           # (date, bands, table) made by it
         self._lazy_norms = []           # (norms, pending 1, pending 2, len_x, n_bands) of static convergence
         self._reg_log = []              # per GN iteration of the spatial prior: rho, sweeps, residual
-        self._order_bufs = None         # (order, scratch) of obs_order, reused across dates
+        self._order_bufs = [None, None]  # (order, scratch) of obs_order: two sets, alternating dates
+        self._order_turn = 0
         self._visit = None              # this date's pixel visiting order (config.observed_first)
         self._split_chunk = {}          # split path: bands per chunk, per band count
         self._reg = None
@@ -547,9 +548,10 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
                     self._lookahead_fn = lambda d=nxt[0]: self._prepare_date(d)
                 rows = self._precision_rows(last_of_step=i == len(locate_times) - 1, more_dates=bool(nxt))
                 try:
-                    res = self.do_all_bands_state(step, bands, forecast,
-                                                  table=prep[2] if (prep is not None and prep[1] is bands) else None,
-                                                  store_rows=rows)
+                    ready = prep is not None and prep[1] is bands
+                    res = self.do_all_bands_state(step, bands, forecast, table=prep[2] if ready else None,
+                                                  store_rows=rows,
+                                                  order=prep[3] if ready and prep[3] is not None else False)
                 finally:
                     self._lookahead_fn = None
             forecast = res.state
@@ -580,11 +582,38 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         table = None
         specs = [sp for sp, _ in bands]
         cfg = self.config
+        order = None
         if not (cfg.return_innovations or cfg.spatial_gamma > 0 or
                 self.band_comm is not None or any(sp.kind == OP_PRECOMP for sp in specs)) and \
                 self._split_plan_kind(specs) is None:
             table = self._tables.get(specs, [d for _, d in bands], self.n_params, self._cache, self.device)
-        self._prepared = (date, bands, table)
+            # the next date's observed-first order too: its passes run on the
+            # device after this date's launches, under the host's norm wait and
+            # step bookkeeping, instead of between the two dates' analyses
+            if cfg.analysis_form != "gain":
+                order = self._visit_order(date, specs, table)
+        self._prepared = (date, bands, table, order)
+
+    def _visit_order(self, timestep, specs, table):
+        """Observed-first visiting order of one date (config.observed_first; GP
+        bands on the fused kernels), or None.  The two buffer sets alternate by
+        date: a date's order is computed ahead (lookahead) while the previous
+        date's launches may still read theirs."""
+        cfg = self.config
+        N = self.N
+        if not (cfg.observed_first and table is not None and N and any(s.kind == OP_GP for s in specs)):
+            return None
+        slot = self._order_turn % 2
+        self._order_turn += 1
+        buf, scratch = self._order_bufs[slot] if self._order_bufs[slot] is not None else (None, None)
+        # band groups: the bands of one sensor share its clouds (multi-sensor sources)
+        groups = self.observations.band_groups(timestep) if hasattr(self.observations, "band_groups") else None
+        if groups is not None and (len(groups) != len(specs) or max(groups) > 2):
+            groups = None
+        order, scratch = K.obs_order(table, N, self.device, buf, scratch, groups=groups,
+                                     local=cfg.observed_first_local)
+        self._order_bufs[slot] = (order if buf is None or buf.numel() < N else buf, scratch)
+        return order
 
     def _health_metrics(self, wall_s: float) -> dict:
         """Per-date structured metrics: rank-local pixel updates/s,
@@ -738,14 +767,15 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         return (x, None, P, inn) if res.state.kind == PRECISION else (x, P, None, inn)
 
     def do_all_bands_state(self, timestep, bands, forecast: KFState, innovations=None,
-                           table=None, store_rows=None) -> AssimilationResult:
+                           table=None, store_rows=None, order=False) -> AssimilationResult:
         """Gauss-Newton loop on device (linear_kf.py:245-307).
 
         ``store_rows``: the packed precision rows the caller needs of the
         analysis (None: all; a set of row indices otherwise, see
         :meth:`_precision_rows`); the returned state marks the others invalid.
         With ``EngineConfig.convergence_chunk`` the exit test runs per chunk
-        (:meth:`_gn_chunked`)."""
+        (:meth:`_gn_chunked`).  ``order``: the date's visiting order computed
+        ahead with ``table`` (:meth:`_prepare_date`; False: compute it here)."""
         cfg = self.config
         n = self.n_params
         N = self.N
@@ -829,17 +859,8 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
                        and all(s.kind == OP_LINEAR for s in specs))
         # observed pixels first (config.observed_first): one order per date for
         # every analysis launch of it (GP bands on the fused kernels only)
-        order = None
-        if (cfg.observed_first and table is not None and N and not (gain or precomp or split or bp)
-                and any(s.kind == OP_GP for s in specs)):
-            buf, scratch = self._order_bufs if self._order_bufs is not None else (None, None)
-            # band groups: the bands of one sensor share its clouds (multi-sensor sources)
-            groups = self.observations.band_groups(timestep) if hasattr(self.observations, "band_groups") else None
-            if groups is not None and (len(groups) != len(specs) or max(groups) > 2):
-                groups = None
-            order, scratch = K.obs_order(table, N, self.device, buf, scratch, groups=groups,
-                                         local=cfg.observed_first_local)
-            self._order_bufs = (order if buf is None or buf.numel() < N else buf, scratch)
+        if order is False or table is None or not N or gain or precomp or split or bp:
+            order = None if (gain or precomp or split or bp) else self._visit_order(timestep, specs, table)
         self._visit = order
         # spatial prior: a plain first iteration (config.spatial_first_plain; it
         # cannot end the loop), fused with the regularised prepare of the second
