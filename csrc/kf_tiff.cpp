@@ -258,7 +258,6 @@ struct FastDeflate {
   void (*release)(void*) = nullptr;
   bool ok = false;
   FastDeflate() {
-    if (getenv("KAFKA_TIFF_ZLIB")) return;          // force zlib (tests compare the two)
     void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
     if (!h) return;
     alloc = reinterpret_cast<void* (*)(int)>(dlsym(h, "libdeflate_alloc_compressor"));
@@ -291,7 +290,12 @@ struct ThreadCompressor {
   }
 };
 
-bool fast_deflate_available() { return FastDeflate::get().ok; }
+// zlib even where libdeflate is present (A/B of the two encoders: tiff_deflate_backend)
+static std::atomic<bool> g_force_zlib{false};
+
+static bool use_fast_deflate() { return FastDeflate::get().ok && !g_force_zlib.load(std::memory_order_relaxed); }
+
+bool fast_deflate_available() { return use_fast_deflate(); }
 
 static void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t)>& fn) {
   nthreads = std::max(1, std::min<int>(nthreads, (int)std::max<int64_t>(1, n)));
@@ -446,7 +450,7 @@ void write(const std::string& path, const void* data, int nb, uint64_t H, uint64
       if (predictor > 1)
         for (uint64_t r = 0; r < tile; ++r) apply_predictor(&t[r * tile * bps], tile, bps, predictor, tmp);
       const FastDeflate& fd = FastDeflate::get();
-      if (fd.ok) {
+      if (use_fast_deflate()) {
         thread_local ThreadCompressor tc;
         void* comp = tc.at(std::min(level, 12));
         if (!comp) throw std::runtime_error("libdeflate_alloc_compressor failed");
@@ -630,6 +634,11 @@ void bind_tiff(py::module_& m) {
      py::arg("nthreads"), py::arg("elem_bytes") = 0);
   m.def("tiff_fast_deflate", &tiff::fast_deflate_available,
         "True when tile DEFLATE uses libdeflate (else zlib)");
+  m.def("tiff_deflate_backend", [](const std::string& b) {
+    if (b != "auto" && b != "zlib") throw std::invalid_argument("deflate backend: 'auto' or 'zlib'");
+    tiff::g_force_zlib.store(b == "zlib");
+    return tiff::fast_deflate_available();
+  }, "DEFLATE encoder of the TIFF writer: 'auto' (libdeflate when present) or 'zlib'; returns tiff_fast_deflate()");
   m.def("write_raw", [](const std::string& path, uintptr_t src, uint64_t n, int nthreads, bool sync) {
     py::gil_scoped_release nogil;
     tiff::write_raw(path, reinterpret_cast<const void*>(src), n, nthreads, sync);

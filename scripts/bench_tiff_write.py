@@ -21,7 +21,12 @@ def main():
     ap.add_argument("--dir", default="/tmp")
     ap.add_argument("--threads", type=int, nargs="+", default=[8, 16, 32])
     ap.add_argument("--levels", type=int, nargs="+", default=[0, 1, 6])
+    ap.add_argument("--deflate-backend", default="auto", choices=["auto", "zlib"],
+                    help="DEFLATE encoder: libdeflate when present (auto) or zlib")
     a = ap.parse_args()
+    from kafka_inferenceengine_amd.ops import kernels as K
+    fast = K.ext().tiff_deflate_backend(a.deflate_backend)
+    print(json.dumps({"deflate_backend": "libdeflate" if fast else "zlib"}), flush=True)
     from kafka_inferenceengine_amd.input_output.tiff import write_tiff
 
     rng = np.random.default_rng(0)

@@ -35,6 +35,26 @@ def test_native_uncompressed_stack_is_striped_zero_copy(tmp_path):
     assert not info.get("tiled", False) and info.get("compression", 1) == 1
 
 
+def test_deflate_backends_write_the_same_rasters(tmp_path):
+    """Tile DEFLATE through libdeflate (when the system has it) and through
+    zlib: both standard zlib streams (TIFF compression 8), both read back exactly."""
+    from kafka_inferenceengine_amd.ops import kernels as K
+    rng = np.random.default_rng(2)
+    a = (rng.random((2, 300, 517)) + np.linspace(0, 1, 517)).astype(np.float32)
+    out = {}
+    try:
+        for backend in ("zlib", "auto"):
+            K.ext().tiff_deflate_backend(backend)
+            p = tmp_path / f"d_{backend}.tif"
+            k.write_tiff(p, a, level=1, predictor=3, tile=128)
+            b, info = k.read_tiff(p)
+            assert np.array_equal(a, b) and k.tiff_info(p)["compression"] == 8
+            out[backend] = p.stat().st_size
+    finally:
+        K.ext().tiff_deflate_backend("auto")
+    assert all(v < a.nbytes for v in out.values())
+
+
 def test_reads_reference_mask_tiff():
     path = "/root/reference/Barrax_pivots.tif"
     if not os.path.exists(path):
