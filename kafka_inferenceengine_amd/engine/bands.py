@@ -9,7 +9,6 @@ with ``w`` the inverse variance (the reference's ``uncertainty``).
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field, replace
 
 import numpy as np
@@ -85,9 +84,8 @@ class RecordCache:
 
     def get_mfma(self, spec: OperatorSpec, device):
         """(table tensor, n_chunks, scale) of the matrix-core GP path, or None
-        (disabled with KAFKA_GP_MFMA=0, D > 10, or values outside f16 range)."""
-        if os.environ.get("KAFKA_GP_MFMA", "1") == "0":
-            return None
+        (D > 10, or values outside f16 range; the VALU loop is the analysis
+        variant Variant.VALU_ORACLE)."""
         key = (id(spec.emulator) if spec.emulator is not None else id(spec.records), str(device))
         hit = self._m.get(key)
         if hit is None:

@@ -23,7 +23,6 @@ from __future__ import annotations
 
 import datetime as dt
 import math
-import os
 
 import numpy as np
 import scipy.sparse as sp
@@ -228,7 +227,7 @@ class SyntheticObservations:
         if self.stream_mode:
             dtype = torch.int16 if self.encoding in ("dn16", "bf16", "bf16y") else torch.float32
             self._streamer = DateStreamer(self.n_pool, self._entry_shape(), dtype, self.device,
-                                          n_bufs=int(os.environ.get("KAFKA_STREAM_BUFS", 3)) if self.n_pool >= 3 else 2)
+                                          n_bufs=3 if self.n_pool >= 3 else 2)
             for k in range(self.n_pool):
                 data = self._synthesize(k)
                 self._streamer.host_view(k).copy_(data.cpu())
