@@ -184,7 +184,7 @@ class GaussNewtonMixin:
         n, N, prop, fc = self.n_params, self.N, run.prop, run.fc
         if run.fuse_sp:
             self._regularised_iteration(run.table, x_prev, fc, x_new, run.P_out, run.status, prop, run.out_t,
-                                        final=True, partials_first=self._partials1)
+                                        final=True, partials_first=self._partials1, a_rows=run.a_rows)
         else:
             K.analysis(n, run.table, x_prev, None if prop is not None else fc.x, None if prop is not None else fc.P,
                        x_new, run.P_out, None, run.status, self._partials, N=N, prop=prop, out=run.out_t,
@@ -208,7 +208,7 @@ class GaussNewtonMixin:
             self._reg_log.append({"solver": "plain", "rho": 0.0, "sweeps": 0, "r2": None, "count": 0})
         elif cfg.spatial_gamma > 0:
             self._regularised_iteration(table, x_prev, fc, x_new, A_keep, run.status, prop, out_now,
-                                        final=n_iter >= cfg.min_iterations)
+                                        final=n_iter >= cfg.min_iterations, a_rows=run.a_rows)
         elif run.bp:
             self._band_parallel_iteration(table, x_prev, fc, x_new, A_keep, run.status)
         elif run.split is not None:

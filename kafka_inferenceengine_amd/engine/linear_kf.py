@@ -840,7 +840,7 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         # the rows the caller reads (0: all); no row at all -> no precision store.
         # Paths whose output is dumped from the state afterwards keep every row
         a_rows, p_valid = 0, None
-        if (store_rows is not None and not (gain or cfg.hessian_correction or cfg.spatial_gamma > 0)
+        if (store_rows is not None and not (gain or cfg.hessian_correction)
                 and (out_t is not None or self.output is None)):
             p_valid = 0
             for r in store_rows:
@@ -908,7 +908,7 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         cfg = self.config
         if (cfg.store_precision == "always" or self._full_precision_step or not last_of_step or not more_dates
                 or cfg.analysis_form == "gain" or cfg.band_sequential or cfg.hessian_correction
-                or cfg.spatial_gamma > 0 or cfg.return_innovations):
+                or cfg.return_innovations):
             return None
         if not (cfg.fuse_output and hasattr(self.output, "device_targets")) and self.output is not None:
             return None            # the dump reads the precision diagonal (observations.py:392-393)

@@ -38,7 +38,7 @@ class SpatialPriorMixin:
         return out
 
     def _regularised_iteration(self, table, x_prev, fc: KFState | None, x_out, A_out, status, prop=None, out=None,
-                               final=True, partials_first=None):
+                               final=True, partials_first=None, a_rows=0):
         """GMRF spatial prior (K9 + C2), affine block-Jacobi form (kf_core.h):
         the analysis kernel assembles (A, b) and, instead of solving, factors
         A_reg = A + g deg E_R once and writes u = A_reg^-1 b and V = A_reg^-1 E_R;
@@ -48,7 +48,8 @@ class SpatialPriorMixin:
         block-Jacobi sweeps of (A_reg) x = b + g E_R sum_q x_q.  The analysis
         precision includes the smoother's diagonal.  With ``prop`` the forecast
         is fused as in the plain path (first iteration: x0 = forecast, written
-        for the norm and the first sweep).  ``partials_first``: the launch runs
+        for the norm and the first sweep).  ``a_rows``: the precision rows
+        stored (0: all; EngineConfig.store_precision).  ``partials_first``: the launch runs
         the plain first Gauss-Newton iteration in registers (its norm there)
         and prepares the regularised second, linearised at x_1 (written to the
         x0 buffer, the finish's reference for the norm)."""
@@ -67,7 +68,7 @@ class SpatialPriorMixin:
         fused = partials_first is not None
         if not rows:   # nothing regularised: plain analysis
             K.analysis(n, table, x_prev, fx, fP, x_out, A_out, None, status, self._partials, N=N, prop=prop, out=out,
-                       gn_fused=2 if fused else 1, partials_first=partials_first, order=self._visit)
+                       gn_fused=2 if fused else 1, partials_first=partials_first, order=self._visit, a_rows=a_rows)
             return
         k = len(rows)
         ld = x_out.shape[1]
@@ -82,7 +83,7 @@ class SpatialPriorMixin:
                    reg=dict(gamma=gamma, mask=reg.reg_mask, v_out=v, nbr=None if geo else reg.nbr, geo=geo),
                    x0_out=None if x_ref is x_prev else x0_buf,
                    out=None if out is None else (None, out[1], out[2]),
-                   gn_fused=2 if fused else 1, partials_first=partials_first, order=self._visit)
+                   gn_fused=2 if fused else 1, partials_first=partials_first, order=self._visit, a_rows=a_rows)
         if fused:
             self._reg_log.append({"solver": "plain", "rho": 0.0, "sweeps": 0, "r2": None, "count": 0})
         nbr = None if geo else reg.nbr

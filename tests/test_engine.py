@@ -709,3 +709,58 @@ def test_spatial_tiled_sweeps_equal_per_sweep_launches():
     b, nb = _spatial_dense_run("cpu", False)
     assert na > 0 and nb == 0
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("mode", ["lai", "spatial", "prior_reset", "info_approx"])
+def test_store_precision_auto_equals_always(mode):
+    """EngineConfig.store_precision="auto": a date whose analysis only feeds
+    the next forecast stores the precision rows that forecast reads (LAI
+    propagator: A[6,6]; prior reset: none; approximate information filter: the
+    diagonal).  Nothing else reads them, so every date's state, GN iterations
+    and output rasters equal the full store's bit for bit, and the run's final
+    state carries the full precision."""
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=12)
+    grid = _grid(6)
+    kw, prop, pri = {}, None, None
+    if mode == "spatial":
+        kw = dict(spatial_gamma=5.0, spatial_params=[6])
+    elif mode == "prior_reset":
+        pri = prior
+    elif mode == "info_approx":
+        prop = k.propagate_information_filter_approx_SLOW
+    res = []
+    for store in ("always", "auto"):
+        out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
+        if pri is not None:   # no propagator: the prior resets every date's forecast
+            kf = k.LinearKalman(obs, out, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS,
+                                state_propagation=None, prior=pri, device="cpu",
+                                config=k.EngineConfig(store_precision=store))
+            st = kf.run(grid, kf.state_from_prior(pri), None, None)
+        else:
+            kf = _engine(mask, obs, Q, out=out, prop=prop, store_precision=store, **kw)
+            st = kf.run(grid, x0, None, Pinv)
+        assert st.full
+        res.append((st, out, [h["gn_iterations"] for h in kf.history]))
+    (a, oa, ia), (b, ob, ib) = res
+    assert ia == ib
+    assert torch.equal(a.x, b.x) and torch.equal(a.P, b.P)
+    for t in oa.history:
+        assert torch.equal(oa.history[t][0], ob.history[t][0]) and torch.equal(oa.history[t][1], ob.history[t][1])
+
+
+def test_partial_precision_refuses_full_readers():
+    """A state stored with only some precision rows (KFState.p_valid) refuses
+    every reader of the full precision instead of returning stale rows."""
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=13)
+    grid = _grid(4)
+    kf = _engine(mask, obs, Q, store_precision="auto")
+    from kafka_inferenceengine_amd.inference import iterate_time_grid
+    dates = list(obs.dates)
+    t, loc, _ = next(s_ for s_ in iterate_time_grid(grid, dates) if len(s_[1]))
+    st = kf.step(t, loc, kf.state_from_prior(prior), advance=False, all_dates=dates)
+    assert not st.full and st.p_valid is not None
+    with pytest.raises(RuntimeError):
+        st.to_reference()
+    with pytest.raises(RuntimeError):
+        st.numpy()
+    assert st.clone().p_valid == st.p_valid     # a copy keeps the marker
