@@ -834,8 +834,8 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         out_t = None
         if ((plain or spatial or (gain and not precomp)) and N and cfg.fuse_output
                 and hasattr(self.output, "device_targets")):
-            # plain path: the final state's x doubles as the mean raster (dense strips)
-            out_t = self.output.device_targets(self, self.device, alias=plain)
+            # plain and spatial paths: the final state's x doubles as the mean raster (dense strips)
+            out_t = self.output.device_targets(self, self.device, alias=plain or spatial)
         # analysis precision rows stored (EngineConfig.store_precision): a mask of
         # the rows the caller reads (0: all); no row at all -> no precision store.
         # Paths whose output is dumped from the state afterwards keep every row

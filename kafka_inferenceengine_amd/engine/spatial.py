@@ -93,8 +93,9 @@ class SpatialPriorMixin:
             cur, rho, sweeps = self._reg_tiled_solve(reg, geo, u, v, x_ref, rows[0], gamma, tol, depth, sweeps)
         else:
             cur, rho, sweeps = self._reg_sweep_solve(reg, geo, nbr, u, v, x_ref, rows, gamma, tol, sweeps)
+        # mean raster: written by the finish, or (DeviceOutput alias, out[0] None) x_out itself
         K.reg_finish(n, u, v, cur, nbr, x_ref, x_out, gamma, reg.reg_mask, N, partials=self._partials, geo=geo,
-                     out=None if out is None else (out[0], None, out[2]))
+                     out=None if (out is None or out[0] is None) else (out[0], None, out[2]))
         # residual of the coupled solve (metrics only): the finish applied one more
         # Jacobi update to the last iterate, x_R - z = J z + f - z (device, read lazily)
         r2 = None

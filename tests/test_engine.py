@@ -764,3 +764,29 @@ def test_partial_precision_refuses_full_readers():
     with pytest.raises(RuntimeError):
         st.numpy()
     assert st.clone().p_valid == st.p_valid     # a copy keeps the marker
+
+
+@pytest.mark.parametrize("spatial", [False, True])
+def test_aliased_mean_raster_equals_written_one(spatial):
+    """DeviceOutput(alias_state=True): on dense strips the state's x is the
+    mean raster (the kernels write only the uncertainty); the rasters and the
+    states equal those of an output that has the mean written, bit for bit."""
+    mask = np.ones((24, 20), bool)
+    obs = k.SyntheticBHRObservations(mask, n_train=80, n_pool=5, device="cpu", seed=14, field_cell=8)
+    prior = k.JRCPrior(k.TIP_PARAMETERS, mask)
+    x0, Pinv = prior.process_prior(None)
+    Q = np.zeros_like(x0)
+    Q[6::7] = 0.04
+    grid = _grid(5)
+    kw = dict(spatial_gamma=5.0, spatial_params=[6]) if spatial else {}
+    res = []
+    for alias in (False, True):
+        out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True, alias_state=alias)
+        kf = _engine(mask, obs, Q, out=out, **kw)
+        st = kf.run(grid, x0, None, Pinv)
+        res.append((st, out))
+    (a, oa), (b, ob) = res
+    assert torch.equal(a.x, b.x) and torch.equal(a.P, b.P)
+    assert list(oa.history) == list(ob.history)
+    for t in oa.history:
+        assert torch.equal(oa.history[t][0], ob.history[t][0]) and torch.equal(oa.history[t][1], ob.history[t][1])
