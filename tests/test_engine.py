@@ -135,6 +135,21 @@ def test_checkpoint_resume_bit_identical(tmp_path):
     assert torch.equal(st.x, full.x) and torch.equal(st.P, full.P)
 
 
+def test_checkpoint_every_other_step_with_partial_precision_dates(tmp_path):
+    """store_precision="auto" keeps only the forecast's rows on dates that are
+    not checkpointed; a checkpoint step stores the full precision, so resuming
+    from it gives the uninterrupted run bit for bit."""
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=4)
+    grid = _grid(7)
+    full = _engine(mask, obs, Q).run(grid, x0, None, Pinv)
+    kf = _engine(mask, obs, Q, checkpoint_dir=str(tmp_path), checkpoint_every=2)
+    kf.run(grid[:6], x0, None, Pinv)
+    latest = k.CheckpointManager.latest(tmp_path)
+    assert latest is not None
+    st = _engine(mask, obs, Q).run(grid, None, None, None, resume_from=latest)
+    assert torch.equal(st.x, full.x) and torch.equal(st.P, full.P)
+
+
 def test_checkpoint_retention_keeps_newest(tmp_path):
     mask, obs, prior, x0, Pinv, Q = _setup(seed=4)
     grid = _grid(5)
