@@ -34,6 +34,21 @@ def test_cli_run_bhr_and_resume(tmp_path):
         assert json.loads(out.strip().splitlines()[-1])["timesteps"] == 2
 
 
+def test_cli_run_per_chunk_convergence_with_output_telemetry(tmp_path):
+    """cli run with the reference drivers' per-chunk exit test and GeoTIFF
+    output: the record carries the end-to-end wall, per-timestep wall and the
+    writer's telemetry (queue depth, waits, encode time)."""
+    out = _run("run", "--sensor", "s2", "--size", "40", "36", "--steps", "2", "--n-train", "30", "--device", "cpu",
+               "--convergence-chunk", "16", "--domain-history", "--out", str(tmp_path / "tif"), "--out-level", "1",
+               "--out-keep", "1")
+    rec = json.loads(out.strip().splitlines()[-1])
+    assert rec["timesteps"] == 2 and rec["finite"] and rec["wall_s"] > 0
+    assert len(rec["timestep_wall_ms"]) == 2
+    o = rec["output"]
+    assert o["timesteps_written"] == 2 and o["queue_depth_max"] >= 0 and o["raster_bytes"] > 0
+    assert len(os.listdir(tmp_path / "tif")) == 2 * 10        # newest timestep only: 10 params x (mean, unc)
+
+
 def test_cli_resume_without_checkpoint_fails_clearly(tmp_path):
     (tmp_path / "empty").mkdir()
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
