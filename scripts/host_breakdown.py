@@ -9,7 +9,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import numpy as np, torch
 from kafka_inferenceengine_amd.ops import kernels as K
 E = K.ext()
-NOOP = {"analysis", "reduce_partials", "gain", "propagate", "unpack", "gather"}
+NOOP = {"analysis", "reduce_partials", "gain", "propagate", "unpack", "gather", "obs_order"}
 class Fake:
     def __getattr__(self, nm):
         if nm in NOOP:
