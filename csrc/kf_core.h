@@ -232,6 +232,9 @@ KF_HD int32_t geo_neighbour(const StripGeo& g, int64_t N, int64_t p, int k) {
 // regulariser its prepare; the cold code no longer holds SGPRs across the
 // hot path (TIP kernel: 89 -> 18 SGPR spill slots).
 constexpr int SPEC_ANY = 0, SPEC_PROP = 1, SPEC_PROP_REG = 2;
+// SPEC_PROP_PF: SPEC_PROP whose grid loop also loads the next pixel group's
+// forecast inputs ahead (small emulators, kf_device.h:analysis_mfma_kernel)
+constexpr int SPEC_PROP_PF = 3;
 
 // AnalysisArgs.variant: the production kernel (AV_DEFAULT) or an alternate
 // device path kept as a test oracle -- each is bit-identical to the default or
@@ -859,6 +862,29 @@ template <int NP>
 KF_HD void forecast_partial(const KF_CONST_AS PropArgs* a, int64_t p, float (&xf)[NP], float (&P)[ntri(NP)]) {
   forecast_partial_precision<NP>(a, p, P);
   forecast_partial_mean<NP>(a, p, xf);
+}
+
+// The propagated parameter when exactly one is (the LAI propagator: TLAI), else -1.
+KF_HD int prop_single(uint32_t mask) { return (mask && !(mask & (mask - 1u))) ? __builtin_ctz(mask) : -1; }
+
+// forecast_partial with that parameter's x_a and P_a,jj already loaded (the
+// SPEC_PROP_PF kernels load the next pixel group's ahead): the same arithmetic.
+template <int NP>
+KF_HD void forecast_partial_pre(const KF_CONST_AS PropArgs* a, int64_t p, int j1, float xa1, float pa1,
+                                float (&xf)[NP], float (&P)[ntri(NP)]) {
+  const int64_t ld = a->ld;
+#pragma unroll
+  for (int t = 0; t < ntri(NP); ++t) P[t] = a->reset_cinv[t];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    if (j == j1) {
+      const float q = a->q_pix ? KF_PX(a->q_pix, j * ld, p) : a->q[j];
+      P[tri(NP, j, j)] = kf_rcp(kf_rcp(pa1) + q);
+      xf[j] = a->m[j] * xa1;
+    } else {
+      xf[j] = a->reset_mean[j];
+    }
+  }
 }
 
 // forecast_pixel computes the forecast (xf, P) of pixel p without storing it;

@@ -191,20 +191,63 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BS;
   const int64_t nv = visit_count(a);
-  for (int64_t base = (int64_t)blockIdx.x * BS + (threadIdx.x - lane); base < nv; base += stride) {
-    const int64_t q = base + lane;
-    const bool act = q < nv;
-    const int64_t p = visit_px(a.order, act ? q : nv - 1);
-    float dn1;
-    const float dn = pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT, IL, SPEC>(a, p, act, gpm_lds,
-                                                                                     dn1 KF_PHASE_ARG);
-    {
-      // re-read through the opaque kernarg pointer: not pinned in SGPRs across the GP loop
-      float* dno = opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr())->dn_out;
-      if (act && dno) KF_PX(dno, 0, p) = dn;
+  if constexpr (SPEC == SPEC_PROP_PF) {
+    // small emulators (short GP loops): the next pixel group's index and its
+    // single propagated parameter's x_a / P_a,jj are loaded before this group's
+    // analysis, so the forecast starts from registers instead of a dependent
+    // order -> state load chain (pixel indices < 2^31: one VGPR carried)
+    const KF_CONST_AS PropArgs* pa = cptr(a.prop);
+    const int pj = prop_single(pa->prop_mask);
+    int64_t base = (int64_t)blockIdx.x * BS + (threadIdx.x - lane);
+    uint32_t p32 = base < nv ? (uint32_t)visit_px(a.order, base + lane < nv ? base + lane : nv - 1) : 0u;
+    float px = 0.f, pp = 0.f;
+    if (pj >= 0 && base < nv) {
+      px = KF_PX(pa->x_a, pj * pa->ld, (int64_t)p32);
+      pp = KF_PX(pa->p_a, tri(NP, pj, pj) * pa->ld, (int64_t)p32);
     }
-    acc += act ? (double)dn : 0.0;
-    acc1 += act ? (double)dn1 : 0.0;
+    for (; base < nv; base += stride) {
+      const int64_t q = base + lane;
+      const bool act = q < nv;
+      const int64_t p = (int64_t)p32;
+      const int64_t bn = base + stride;
+      uint32_t pn = 0u;
+      float pxn = 0.f, ppn = 0.f;
+      if (bn < nv) {
+        pn = (uint32_t)visit_px(a.order, bn + lane < nv ? bn + lane : nv - 1);
+        if (pj >= 0) {
+          pxn = KF_PX(pa->x_a, pj * pa->ld, (int64_t)pn);
+          ppn = KF_PX(pa->p_a, tri(NP, pj, pj) * pa->ld, (int64_t)pn);
+        }
+      }
+      float dn1;
+      const float dn = pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT, IL, SPEC>(
+          a, p, act, gpm_lds, dn1 KF_PHASE_ARG, pj, px, pp);
+      {
+        float* dno = opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr())->dn_out;
+        if (act && dno) KF_PX(dno, 0, p) = dn;
+      }
+      acc += act ? (double)dn : 0.0;
+      acc1 += act ? (double)dn1 : 0.0;
+      p32 = pn;
+      px = pxn;
+      pp = ppn;
+    }
+  } else {
+    for (int64_t base = (int64_t)blockIdx.x * BS + (threadIdx.x - lane); base < nv; base += stride) {
+      const int64_t q = base + lane;
+      const bool act = q < nv;
+      const int64_t p = visit_px(a.order, act ? q : nv - 1);
+      float dn1;
+      const float dn = pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT, IL, SPEC>(a, p, act, gpm_lds,
+                                                                                       dn1 KF_PHASE_ARG);
+      {
+        // re-read through the opaque kernarg pointer: not pinned in SGPRs across the GP loop
+        float* dno = opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr())->dn_out;
+        if (act && dno) KF_PX(dno, 0, p) = dn;
+      }
+      acc += act ? (double)dn : 0.0;
+      acc1 += act ? (double)dn1 : 0.0;
+    }
   }
   analysis_partials<BS>(a, acc, acc1);
   KF_PHASE_KERNEL_END
@@ -593,6 +636,7 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s, int*
     if (!a.prop || a.variant == AV_BLOCK_ORDER || a.variant == AV_GENERIC_SPEC)                     \
       KF_MFMA_GO(OBS_, BS_, MINW_, LAY_)                                                            \
     else if (a.reg_v) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP_REG)                      \
+    else if (small) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP_PF)                          \
     else KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP)                                        \
   }
       // Launch bound of 3 workgroups per CU (MINW = 3, as the LDS tables
@@ -604,6 +648,12 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s, int*
       // band loop unrolled over the two compile-time maps (AV_RUNTIME_LAYOUT:
       // the runtime-layout kernel, its oracle)
       bool tip = false;
+      // small emulators (<= 4 chunks of 32 training points per band): the GP
+      // loop is too short to hide the next group's forecast loads, so the
+      // SPEC_PROP_PF kernel loads them ahead (T = 32: -2.2 %; at T = 500 the
+      // extra registers cost +0.5 %, profiles/r5_forecast_prefetch_ab.jsonl)
+      const bool small = a.gpm_frags <= 4 * a.n_bands * gpm_frags_per_chunk(FD) + 1;
+      (void)small;
       if constexpr (NP == 7 && FD == 4)
         tip = a.band_layout == BAND_LAYOUT_TIP && a.n_bands == 2 && a.variant != AV_RUNTIME_LAYOUT;
       if (a.fast_obs == OBS_DN16) {

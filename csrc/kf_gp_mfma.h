@@ -533,7 +533,8 @@ __device__ __forceinline__ void gpm_epilogue(const KF_CONST_AS BandDesc* q, cons
 template <int NP, int D, int FOBS, bool GT = false, bool PF = false, int LAYOUT = BAND_LAYOUT_RUNTIME,
           bool IL = false, int SPEC = SPEC_ANY>
 __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int64_t p, bool act,
-                                                     const kf_h8* lds, float& dn_first KF_PHASE_PARAM) {
+                                                     const kf_h8* lds, float& dn_first KF_PHASE_PARAM,
+                                                     int pre_j = -1, float pre_x = 0.f, float pre_p = 0.f) {
   constexpr int NT = ntri(NP);
   // LAYOUT == BAND_LAYOUT_TIP: two bands with the JRC-TIP VIS / NIR maps, the
   // band loop unrolled with both maps compile-time (no runtime map branches
@@ -554,7 +555,12 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   // correction form throughout (kf_core.h analysis_epilogue, DELTA)
   if (SPEC != SPEC_ANY || a.prop) {
     float xf[NP];
-    forecast_partial<NP>(opaque(cptr(a.prop)), p, xf, A);
+    // SPEC_PROP_PF: the single propagated parameter's x_a / P_a,jj of the first
+    // iteration were loaded ahead by the kernel's loop (pre_j >= 0)
+    if (SPEC == SPEC_PROP_PF && pre_j >= 0 && it == 0)
+      forecast_partial_pre<NP>(opaque(cptr(a.prop)), p, pre_j, pre_x, pre_p, xf, A);
+    else
+      forecast_partial<NP>(opaque(cptr(a.prop)), p, xf, A);
     if (!a.x_prev && it == 0) {
       // linearised at the forecast: the prior part P_f^-1 (x_f - x0) is 0
 #pragma unroll

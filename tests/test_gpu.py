@@ -449,11 +449,13 @@ def test_specialised_prosail_kernel_equals_generic_gpu(cuda):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("spatial", [False, True])
-def test_specialised_tip_kernel_equals_generic_gpu(cuda, spatial):
+@pytest.mark.parametrize("spatial,n_train", [(False, 500), (True, 500), (False, 32)])
+def test_specialised_tip_kernel_equals_generic_gpu(cuda, spatial, n_train):
     """The JRC-TIP kernels specialised for the fused forecast (SPEC_PROP, and
     SPEC_PROP_REG with the spatial prior: explicit-forecast / regulariser code
-    compiled out) give the same bits as the generic kernel (variant 18)."""
+    compiled out; SPEC_PROP_PF for small emulators, T = 32: the next pixel
+    group's forecast inputs loaded ahead) give the same bits as the generic
+    kernel (variant 18)."""
     from kafka_inferenceengine_amd.ops import kernels as K
     mask = np.ones((96, 160), bool)
     mask[5:20, 30:70] = False
@@ -465,7 +467,8 @@ def test_specialised_tip_kernel_equals_generic_gpu(cuda, spatial):
         for variant in (0, 18):
             K.DEFAULT_VARIANT = variant
             out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
-            obs = k.SyntheticBHRObservations(mask, n_train=500, device=cuda, stream=False, n_pool=3, field_cell=8)
+            obs = k.SyntheticBHRObservations(mask, n_train=n_train, device=cuda, stream=False, n_pool=3,
+                                             field_cell=8)
             kf = k.LinearKalman(obs, out, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS,
                                 device=cuda, state_propagation=k.propagate_information_filter_LAI,
                                 config=k.EngineConfig(**reg))

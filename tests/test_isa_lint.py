@@ -48,6 +48,7 @@ def test_built_code_objects_have_no_mfma_operand_hazards():
 HOT = {   # kernel: (min waves per SIMD, max scratch bytes per lane)
     "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb1ELi1EEEvNS_12AnalysisArgsE": (3, 0),   # tip7 headline (TIP layout, fused forecast)
     "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb1ELi2EEEvNS_12AnalysisArgsE": (3, 0),   # spatial (+ regulariser prepare)
+    "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb1ELi3EEEvNS_12AnalysisArgsE": (3, 0),   # small emulators (next group's forecast inputs ahead)
     "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb1ELi0EEEvNS_12AnalysisArgsE": (3, 0),   # generic TIP layout (first date)
     "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi1ELb0ELi0EEEvNS_12AnalysisArgsE": (3, 0),   # block-by-block variant (A/B)
     "_ZN2kf20analysis_mfma_kernelILi7ELi4ELi2ELi256ELi3ELi0ELb0ELi0EEEvNS_12AnalysisArgsE": (3, 0),   # runtime band layout
