@@ -874,8 +874,13 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         x_prev, n_iter, norms = (self._gn_chunked if chunked else self._gn_global)(run)
         if ld != x_prev.shape[1]:
             raise RuntimeError("leading dimension changed")
-        if P_out is None:          # no precision row needed: the forecast's buffer shape, nothing valid
-            P_out = torch.empty((ntri(n), ld), dtype=torch.float32, device=self.device)
+        if P_out is None:
+            # no precision row needed: a buffer of the forecast's shape with nothing
+            # valid (p_valid = 0), never written -- one shared by every such date
+            pu = getattr(self, "_p_unused", None)
+            if pu is None or pu.shape != (ntri(n), ld) or pu.device != self.device:
+                pu = self._p_unused = torch.empty((ntri(n), ld), dtype=torch.float32, device=self.device)
+            P_out = pu
         state = KFState(x_prev, P_out, COVARIANCE if gain else PRECISION, N, p_valid=p_valid)
         self._output_written = state if out_t is not None else None
         if cfg.hessian_correction and not gain and N:
