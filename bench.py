@@ -398,6 +398,13 @@ def main():
                           "finite": ok, "fallback_frac": round(fallback, 6),
                           "out_of_domain_frac": round(out_of_domain, 6), "ingest_bytes_per_step": ingest,
                           "baseline_updates_per_s": c["baseline"]}}
+        # the engine settings that decide what a step computes (reference semantics)
+        ec = kf.config
+        rec["config"]["engine"] = {"convergence_tolerance": ec.convergence_tolerance,
+                                   "min_iterations": ec.min_iterations, "max_iterations": ec.max_iterations,
+                                   "convergence": "per chunk" if ec.convergence_chunk else "tile",
+                                   "store_precision": ec.store_precision, "observed_first": ec.observed_first,
+                                   "fuse_gn": ec.fuse_gn, "analysis_form": ec.analysis_form}
         if chunk_hist:
             rec["config"]["convergence_chunk"] = kf.config.convergence_chunk
             rec["config"]["chunk_gn_histogram"] = {str(i): chunk_hist[i] for i in sorted(chunk_hist)}
