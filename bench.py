@@ -170,6 +170,8 @@ def main():
     ap.add_argument("--device", default=None)
     ap.add_argument("--profile", default=None, help="write a torch.profiler chrome trace here (rank 0)")
     ap.add_argument("--watchdog", type=float, default=0, help="dump Python stacks every N s (hang triage)")
+    ap.add_argument("--host-profile", default=None, metavar="PATH",
+                    help="cProfile of the timed steps' host work (rank 0) written to PATH (pstats)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
                     help="override an EngineConfig field (A/B runs), e.g. --set gp_split=never")
@@ -278,6 +280,10 @@ def main():
                 prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
                                                           torch.profiler.ProfilerActivity.CUDA])
                 prof.__enter__()
+            if a.host_profile and g_rank == 0:
+                import cProfile
+                hprof = cProfile.Profile()
+                hprof.enable()
         t0 = time.perf_counter()
         state = kf.step(t, loc, state, advance=not first, all_dates=dates)
         first = False
@@ -289,6 +295,9 @@ def main():
             for m in msgs:
                 log(m)
             msgs = []
+    if a.host_profile and g_rank == 0 and a.steps:
+        hprof.disable()
+        hprof.dump_stats(a.host_profile)
     t_drain = time.perf_counter()
     if a.output:
         kf.output.flush()                 # every timed date's files are on disk
