@@ -35,8 +35,18 @@ def _dev(t: torch.Tensor) -> bool:
     return t.device.type == "cuda"
 
 
+# the current HIP stream of a device as a raw handle: torch's C accessor when it
+# has one (torch.cuda.current_stream builds a Stream object through several
+# Python layers: ~10 us of the per-date host path over a date's launches)
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream(t: torch.Tensor) -> int:
-    return int(torch.cuda.current_stream(t.device).cuda_stream) if _dev(t) else 0
+    if not _dev(t):
+        return 0
+    if _RAW_STREAM is not None:
+        return int(_RAW_STREAM(t.device.index))
+    return int(torch.cuda.current_stream(t.device).cuda_stream)
 
 
 def _check_soa(t, rows, N, name, dtype=torch.float32, device=None):
@@ -508,7 +518,7 @@ def obs_order(bands: BandTable, N: int, device, out=None, scratch=None, groups=N
     if dev.type == "cuda" and not local and (scratch is None or scratch.numel() < nc):
         scratch = torch.empty(max(nc, 9), dtype=torch.int32, device=dev)
     ext().obs_order(bands.ptr, _ptr(grp), bands.n, G, N, _ptr(scratch), _ptr(out), bool(local), dev.type == "cuda",
-                    int(torch.cuda.current_stream(dev).cuda_stream) if dev.type == "cuda" else 0)
+                    _stream(out))
     return out[:N], scratch
 
 

@@ -79,11 +79,14 @@ class PhaseTimer:
                 s, e = self._free.pop()
             else:
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
+            # one stream lookup per phase (Event.record() without a stream looks
+            # the current one up again)
+            cur = torch.cuda.current_stream(self.device)
+            s.record(cur)
             try:
                 yield
             finally:
-                e.record()
+                e.record(cur)
                 self._pending.append((name, s, e))
                 if self.sync:
                     e.synchronize()
