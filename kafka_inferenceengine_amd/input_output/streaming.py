@@ -12,6 +12,7 @@ from __future__ import annotations
 import torch
 
 from ..ops import _ext
+from ..ops.kernels import current_raw_stream
 
 
 class DateStreamer:
@@ -125,7 +126,7 @@ class DateStreamer:
             # compute stream; the copy itself is issued by the ring's submitter
             # thread (hipMemcpyAsync can stall its caller for milliseconds)
             self.ring.h2d_async(k, dst.data_ptr(), self.entry_bytes, 0, int(self.stream.cuda_stream),
-                                int(torch.cuda.current_stream(self.device).cuda_stream))
+                                current_raw_stream(self.device))
             self._inflight.append(k)
         else:
             self.ring.h2d(k, dst.data_ptr(), self.entry_bytes, 0, 0)
@@ -140,7 +141,7 @@ class DateStreamer:
         b = self.prefetch(k, key)
         self._stamp[b] = self._clock
         if self.cuda:
-            self.ring.stream_wait(k, int(torch.cuda.current_stream(self.device).cuda_stream))
+            self.ring.stream_wait(k, current_raw_stream(self.device))
         self._current = key
         return self.bufs[b]
 
@@ -218,6 +219,6 @@ class RasterIngest:
             self.buf_key[b] = key
             self.bytes_h2d += self.slot_bytes
         if self.cuda:
-            self.ring.stream_wait(s, int(torch.cuda.current_stream(self.device).cuda_stream))
+            self.ring.stream_wait(s, current_raw_stream(self.device))
         self._current = key
         return self.bufs[b]

@@ -41,12 +41,15 @@ def _dev(t: torch.Tensor) -> bool:
 _RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
-def _stream(t: torch.Tensor) -> int:
-    if not _dev(t):
-        return 0
+def current_raw_stream(device: torch.device) -> int:
+    """Raw handle of ``device``'s current HIP stream."""
     if _RAW_STREAM is not None:
-        return int(_RAW_STREAM(t.device.index))
-    return int(torch.cuda.current_stream(t.device).cuda_stream)
+        return int(_RAW_STREAM(device.index if device.index is not None else torch.cuda.current_device()))
+    return int(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _stream(t: torch.Tensor) -> int:
+    return current_raw_stream(t.device) if _dev(t) else 0
 
 
 def _check_soa(t, rows, N, name, dtype=torch.float32, device=None):
