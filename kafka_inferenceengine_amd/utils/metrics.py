@@ -114,8 +114,21 @@ class PhaseTimer:
         del cur
         return {k: round(v, 3) for k, v in self.run_totals.items()}
 
-    def snapshot(self, reset: bool = True) -> dict:
-        if self._pending:
+    def snapshot(self, reset: bool = True, block: bool = True) -> dict:
+        """Phase totals since the last snapshot.  ``block=False`` accounts only
+        the phases that have finished (no host wait: a per-date wait would
+        serialise the host's next date behind the device's work when nothing
+        else waits, e.g. statically converged linear operators); the rest are
+        counted by a later snapshot, so run totals stay exact."""
+        if self._pending and not block:
+            done = 0
+            while done < len(self._pending) and self._pending[done][2].query():
+                name, s, e = self._pending[done]
+                self.totals[name] += s.elapsed_time(e)
+                self._free.append((s, e))
+                done += 1
+            del self._pending[:done]
+        elif self._pending:
             self._pending[-1][2].synchronize()
             for name, s, e in self._pending:
                 self.totals[name] += s.elapsed_time(e)
