@@ -4,8 +4,8 @@
   convergence norms, per-phase ms, wall time, pixel updates/s, per-pixel status
   counts, ingest bytes), one file per rank, plus a rank-0 summary aggregated
   over the ranks (``LinearKalman.metrics_summary``).
-* ``PhaseTimer`` — hipEvent-based (``torch.cuda.Event``) per-phase timing on
-  the compute stream; host clock on CPU.  Non-synchronising by default: the
+* ``PhaseTimer`` — hipEvent-based per-phase timing on the compute stream
+  (native event pool); host clock on CPU.  Non-synchronising by default: the
   event pairs are resolved lazily in ``snapshot()``.
 """
 from __future__ import annotations
@@ -51,17 +51,26 @@ _NULL = contextlib.nullcontext()
 
 
 class PhaseTimer:
-    """``enabled=False`` makes ``phase()`` a shared null context: two hipEvent
-    records and two stream lookups per phase are ~25 % of the engine's host
-    time per step, and nothing reads the totals unless metrics are on."""
+    """``enabled=False`` makes ``phase()`` a shared null context: nothing reads
+    the totals unless metrics or phase timing are on.  On the GPU each phase
+    edge is one call into the native event pool (``PhaseEvents``,
+    ``csrc/kf_stream.cpp``): hipEvent pairs recorded on the current stream and
+    resolved in completion order."""
 
     def __init__(self, device, sync: bool = False, enabled: bool = True):
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.sync = sync
         self.enabled = bool(enabled or sync)
-        self._pending = []
-        self._free = []                        # resolved event pairs, re-recorded (no hipEventCreate per phase)
+        self._ids = {}                         # phase name -> id in the native pool
+        self._names = []
+        self._ev = None
+        if self.cuda and self.enabled:
+            from ..ops import _ext
+            from ..ops.kernels import current_raw_stream
+
+            self._ev = _ext.require_ext().PhaseEvents()
+            self._cur = current_raw_stream
         self.totals = defaultdict(float)
         self.run_totals = defaultdict(float)   # over the whole run (snapshots reset `totals`)
 
@@ -73,23 +82,20 @@ class PhaseTimer:
     @contextlib.contextmanager
     def _phase(self, name: str):
         if self.cuda:
-            if not self._free and len(self._pending) > 32:
-                self._reap()
-            if self._free:
-                s, e = self._free.pop()
-            else:
-                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            # one stream lookup per phase (Event.record() without a stream looks
-            # the current one up again)
-            cur = torch.cuda.current_stream(self.device)
-            s.record(cur)
+            pid = self._ids.get(name)
+            if pid is None:
+                pid = self._ids[name] = len(self._names)
+                self._names.append(name)
+            stream = self._cur(self.device)
+            token = self._ev.begin(pid, stream)
             try:
                 yield
             finally:
-                e.record(cur)
-                self._pending.append((name, s, e))
+                self._ev.end(token, stream)
                 if self.sync:
-                    e.synchronize()
+                    self._absorb(self._ev.collect(True))
+                elif self._ev.pending > 64:
+                    self._absorb(self._ev.collect(False))   # recycle finished pairs
         else:
             t0 = time.perf_counter()
             try:
@@ -97,16 +103,9 @@ class PhaseTimer:
             finally:
                 self.totals[name] += 1e3 * (time.perf_counter() - t0)
 
-    def _reap(self):
-        """Account the oldest pending phases whose end event has completed
-        (non-blocking query) and recycle their event pairs."""
-        done = 0
-        while done < len(self._pending) and done < 32 and self._pending[done][2].query():
-            name, s, e = self._pending[done]
-            self.totals[name] += s.elapsed_time(e)
-            self._free.append((s, e))
-            done += 1
-        del self._pending[:done]
+    def _absorb(self, done):
+        for pid, ms in done:
+            self.totals[self._names[pid]] += ms
 
     def cumulative(self) -> dict:
         """Per-phase ms over the whole run (pending events included)."""
@@ -120,20 +119,8 @@ class PhaseTimer:
         serialise the host's next date behind the device's work when nothing
         else waits, e.g. statically converged linear operators); the rest are
         counted by a later snapshot, so run totals stay exact."""
-        if self._pending and not block:
-            done = 0
-            while done < len(self._pending) and self._pending[done][2].query():
-                name, s, e = self._pending[done]
-                self.totals[name] += s.elapsed_time(e)
-                self._free.append((s, e))
-                done += 1
-            del self._pending[:done]
-        elif self._pending:
-            self._pending[-1][2].synchronize()
-            for name, s, e in self._pending:
-                self.totals[name] += s.elapsed_time(e)
-                self._free.append((s, e))
-            self._pending = []
+        if self._ev is not None and self._ev.pending:
+            self._absorb(self._ev.collect(bool(block)))
         out = {k: round(v, 3) for k, v in self.totals.items()}
         if reset:
             for k, v in self.totals.items():

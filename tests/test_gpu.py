@@ -701,3 +701,26 @@ def test_dense_finish_vectorised_equals_host(cuda, rank, out):
     assert abs(d[3] - h[3]) <= 1e-5 * abs(h[3])
     if out == "mean":
         assert torch.equal(d[1], d[0]) and not d[2].any()
+
+
+@pytest.mark.gpu
+def test_phase_timer_native_events_gpu():
+    """PhaseTimer on the native event pool: nested and repeated phases, more
+    phases in flight than the recycle threshold, non-blocking snapshots that
+    leave unfinished phases for later, exact run totals."""
+    from kafka_inferenceengine_amd.utils.metrics import PhaseTimer
+
+    dev = torch.device("cuda", 0)
+    x = torch.randn(2048, 2048, device=dev)
+    for sync in (False, True):
+        t = PhaseTimer(dev, sync=sync)
+        for _ in range(80):
+            with t.phase("outer"):
+                with t.phase("mm"):
+                    y = x @ x
+                y.add_(1.0)
+        t.snapshot(block=False)
+        total = t.cumulative()
+        assert t._ev.pending == 0
+        assert set(total) == {"outer", "mm"}
+        assert 0 < total["mm"] <= total["outer"]
