@@ -38,6 +38,7 @@ class _PinnedMailbox:
     def __init__(self, width: int):
         self.buf = torch.zeros((self.SLOTS, max(1, width)), dtype=torch.float64, pin_memory=True)
         self.events = [None] * self.SLOTS
+        self.pool = [None] * self.SLOTS      # one reusable event per slot (no hipEventCreate per read-back)
         self.i = 0
 
     def take(self, n: int):
@@ -70,9 +71,11 @@ class PendingSum:
                 box = _MAILBOXES[key] = _PinnedMailbox(vals.numel())
             j, self.vals = box.take(vals.numel())
             self.vals.copy_(vals.reshape(-1).to(torch.float64), non_blocking=True)
-            self.event = torch.cuda.Event()
-            self.event.record(torch.cuda.current_stream(vals.device))
-            box.events[j] = self.event
+            ev = box.pool[j]
+            if ev is None:
+                ev = box.pool[j] = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(vals.device))
+            self.event = box.events[j] = ev
         else:
             self.vals = vals
 
