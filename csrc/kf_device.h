@@ -541,9 +541,9 @@ __global__ __launch_bounds__(BLOCK) void gather_kernel(const T* src, const int64
                                                       int rows, int64_t src_ld, int64_t dst_ld) {
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < n; p += stride) {
-    const int64_t s = idx[p];
-    KF_DCHECK(s >= 0 && s < src_ld);
-    for (int r = 0; r < rows; ++r) dst[r * dst_ld + p] = src[r * src_ld + s];
+    const int64_t s = idx[p];  // s < 0: no source pixel (a warp's uncovered target) -> 0 = no data
+    KF_DCHECK(s < src_ld);
+    for (int r = 0; r < rows; ++r) dst[r * dst_ld + p] = s >= 0 ? src[r * src_ld + s] : T(0);
   }
 }
 

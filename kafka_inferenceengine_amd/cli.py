@@ -48,12 +48,14 @@ def _mask(args):
 
 
 def _file_reference_raster(args):
-    """First raster of a file-driven BHR / S1 run (defines the grid when no --mask)."""
+    """First raster of a file-driven BHR / S2 / S1 run (defines the grid when no --mask)."""
     import glob
     import os
 
     if getattr(args, "bhr_folder", None):
         f = sorted(glob.glob(os.path.join(args.bhr_folder, "*_kernels_b0_k0.tif")))
+    elif getattr(args, "s2_folder", None):
+        f = sorted(glob.glob(os.path.join(args.s2_folder, "**", "B02_sur.tif"), recursive=True))
     elif getattr(args, "s1_folder", None):
         f = sorted(glob.glob(os.path.join(args.s1_folder, "S1_*", "theta.tif")))
     else:
@@ -91,7 +93,10 @@ def _build(args, comm):
             from .input_output.sentinel import Sentinel2Observations
             if not args.emulator_folder:
                 raise SystemExit("--s2-folder needs --emulator-folder")
-            obs = Sentinel2Observations(args.s2_folder, args.emulator_folder, mask)
+            # a --mask GeoTIFF is the state grid every band is warped onto
+            # (kafka_test_S2.py:155-162); without one the granule grid (ROI-cropped)
+            obs = Sentinel2Observations(args.s2_folder, args.emulator_folder, args.mask or mask,
+                                        roi=None if args.mask else args.roi)
         elif args.sensor == "s2":
             obs = k.SyntheticS2Observations(mask, n_bands=10, n_train=args.n_train or 250, **syn)
         else:
@@ -105,7 +110,7 @@ def _build(args, comm):
     elif args.sensor == "s1":
         if args.s1_folder:       # sigma0_VV / sigma0_VH / theta GeoTIFFs per acquisition
             from .input_output.sentinel import S1Observations
-            obs = S1Observations(args.s1_folder, mask, roi=args.roi)
+            obs = S1Observations(args.s1_folder, args.mask or mask, roi=None if args.mask else args.roi)
         else:
             obs = k.SyntheticS1Observations(mask, **syn)
         params, factory = ["lai", "sm"], k.create_sar_observation_operator
@@ -120,8 +125,12 @@ def _build(args, comm):
         step = 5
     else:
         raise SystemExit(f"unknown sensor {args.sensor}")
+    if args.s2_folder or args.s1_folder or args.bhr_folder:   # file readers define the output grid (as the reference drivers)
+        projection, geotransform = obs.define_output()
+    else:
+        projection, geotransform = info.get("projection", ""), info.get("geotransform", [0, 1, 0, 0, 0, -1])
     if args.out:
-        out = k.KafkaOutput(params, info.get("geotransform", [0, 1, 0, 0, 0, -1]), info.get("projection", ""),
+        out = k.KafkaOutput(params, geotransform, projection,
                             args.out, prefix=args.prefix, level=args.out_level, gather=args.out_gather,
                             predictor=3 if args.out_fast else 1, strategy="rle" if args.out_fast else None,
                             keep_timesteps=args.out_keep)

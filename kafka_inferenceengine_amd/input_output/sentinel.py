@@ -118,6 +118,50 @@ def _crop(a, roi):
     return a[uly:lry, ulx:lrx]
 
 
+class _StateGrid:
+    """The state mask's raster grid, onto which every band is warped.
+
+    ``state_mask`` is a GeoTIFF path (the reference's form: a file or VRT
+    handed to ``gdal.Warp`` as the target, ``kafka_test_S2.py:155-160``) or an
+    array with ``geotransform`` / ``projection``.  A bare array carries no
+    geometry: the reader then keeps the granule grid (cropped to ``roi``)."""
+
+    def __init__(self, state_mask, geotransform=None, projection=None):
+        self.geo = False
+        if isinstance(state_mask, (str, os.PathLike)):
+            arr, info = read_tiff(state_mask)
+            self.mask = np.asarray(arr).astype(bool)
+            geotransform = info.get("geotransform")
+            projection = info.get("epsg") or info.get("projection")
+            self.projection = info.get("projection", "")
+        else:
+            self.mask = None if state_mask is None else np.asarray(state_mask).astype(bool)
+            self.projection = "" if projection is None else projection
+        self.crs = projection
+        if geotransform is not None:
+            self.geo = True
+            self.gt = [float(v) for v in geotransform]
+            self.shape = self.mask.shape
+        self._warps = {}
+
+    def warp_for(self, path):
+        """GridWarp from the raster at ``path`` onto this grid (cached per source grid)."""
+        from .tiff import tiff_info
+        from .utils import GridWarp
+
+        i = tiff_info(path)
+        key = (i["shape"], tuple(i.get("geotransform", ())), i.get("epsg") or i.get("projection"))
+        w = self._warps.get(key)
+        if w is None:
+            w = self._warps[key] = GridWarp(i["shape"], i.get("geotransform", [0, 1, 0, 0, 0, -1]), self.shape,
+                                            self.gt, key[2], self.crs)
+        return w
+
+    def read(self, path, band=0, nodata=0):
+        """A band warped onto the grid (host path); equals ``reproject_image``."""
+        return self.warp_for(path).read(path, band, nodata)
+
+
 # ------------------------------------------------------------- Sentinel-2
 class Sentinel2Observations:
     """Sentinel-2 L2 surface-reflectance granules (``Sentinel2_Observations.py``).
@@ -131,16 +175,31 @@ class Sentinel2Observations:
     1e-4, valid = DN > 0, sigma = rel_unc x reflectance, weight = 1 / sigma^2 —
     the reference's :163-179 without the N x N sparse weight matrix).
     ``prefetch(date)`` starts the next date's decode under the current
-    kernels."""
+    kernels.
+
+    Grids: with a georeferenced state mask (a GeoTIFF path, or an array plus
+    ``mask_geotransform`` / ``mask_projection``) every band is warped onto the
+    mask's grid, nearest neighbour, as the reference's ``reproject_image``
+    call does (:166), and ``define_output`` returns the mask's geometry
+    (:100-113).  The host path decodes the bounding source window and warps
+    it (``GridWarp.read``, bit-identical to ``reproject_image``).  The device
+    path computes once per (band grid, strip) the source pixel under every
+    active state pixel; the pinned slot receives only the bounding source
+    window and the warp is the one gather that compacts the strip anyway
+    (uncovered pixels read as DN 0 = no data).  A mask without geometry
+    keeps the granule grid, cropped to ``roi``."""
 
     def __init__(self, parent_folder, emulator_folder, state_mask, chunk=None, roi=None, rel_unc=0.05,
-                 device_ingest: bool = True):
+                 device_ingest: bool = True, mask_geotransform=None, mask_projection=None):
         if not os.path.exists(parent_folder):
             raise IOError("S2 data folder doesn't exist")
         self.device_ingest = device_ingest
         self.parent = parent_folder
         self.emulator_folder = emulator_folder
         self.state_mask = state_mask
+        self.grid = _StateGrid(state_mask, mask_geotransform, mask_projection)
+        if self.grid.geo and roi is not None:
+            raise ValueError("roi crops the granule grid; with a georeferenced state mask the mask defines the grid")
         self.roi = roi
         self.rel_unc = rel_unc
         self.band_map = list(S2_BAND_MAP)
@@ -164,9 +223,16 @@ class Sentinel2Observations:
         self.bands_per_observation = {d: len(self.band_map) for d in self.dates}
 
     def define_output(self):
+        if self.grid.geo:                  # the state mask's geometry (:100-113)
+            return self.grid.projection, list(self.grid.gt)
+        from .tiff import tiff_info
         ref = glob.glob(os.path.join(self.date_data[self.dates[0]], "B02_sur.tif"))
-        info = read_tiff(ref[0])[1] if ref else {}
-        return info.get("projection", ""), info.get("geotransform", [0, 1, 0, 0, 0, -1])
+        info = tiff_info(ref[0]) if ref else {}
+        gt = list(info.get("geotransform", [0, 1, 0, 0, 0, -1]))
+        if self.roi is not None:
+            gt[0] += self.roi[0] * gt[1]
+            gt[3] += self.roi[1] * gt[5]
+        return info.get("projection", ""), gt
 
     def _find_emulator(self, sza, saa, vza, vaa):
         raa = vaa - saa
@@ -212,8 +278,11 @@ class Sentinel2Observations:
     def get_band_data(self, timestep, band):
         folder = self.date_data[timestep]
         metadata, ems = self._date_meta(timestep)
-        rho, _ = read_tiff(os.path.join(folder, f"B{self.band_map[band]}_sur.tif"))
-        rho = _crop(rho.astype(np.float64), self.roi)
+        path = os.path.join(folder, f"B{self.band_map[band]}_sur.tif")
+        if self.grid.geo:                  # warp onto the state grid (:166)
+            rho = self.grid.read(path).astype(np.float64)
+        else:
+            rho = _crop(read_tiff(path)[0].astype(np.float64), self.roi)
         mask = rho > 0
         rho = np.where(mask, rho / 10000., 0.0)
         unc = _weights(rho * self.rel_unc, mask)
@@ -233,17 +302,70 @@ class Sentinel2Observations:
             return
         self.partition = part = engine.partition
         self._device = engine.device
+        self._K = K
         H, W = part.local_mask.shape
+        self._warp_plan = None
+        self._date_files = {}
+        if self.grid.geo:
+            if self.grid.shape != part.state_mask.shape:
+                raise ValueError(f"state mask {self.grid.shape} differs from the engine's {part.state_mask.shape}")
+            plan = self._plan_warp(self.dates[0])
+            if plan is not None:
+                self._warp_plan = plan
+                elems = max((w[1] - w[0]) * (w[3] - w[2]) for w in plan["windows"].values())
+                self._ingest = RasterIngest(len(self.band_map), (1, elems), torch.int16, self._device)
+                return
         ulx, uly = (self.roi[0], self.roi[1]) if self.roi is not None else (0, 0)
         self._window = (uly + part.r0, uly + part.r0 + H, ulx, ulx + W)
         self._ingest = RasterIngest(len(self.band_map), (H, W), torch.int16, self._device)
         self._identity = part.N == H * W
         self._idx = None if self._identity else torch.from_numpy(part.local_idx).to(self._device)
-        self._K = K
+
+    def _band_paths(self, timestep):
+        folder = self.date_data[timestep]
+        return [os.path.join(folder, f"B{b}_sur.tif") for b in self.band_map]
+
+    def _plan_warp(self, timestep):
+        """Per band grid: the strip's bounding source window and, for every
+        active state pixel of the strip, its index into that window (-1 = not
+        covered).  None when every band's grid is the state grid (the crop
+        path is then exact)."""
+        import torch
+
+        part = self.partition
+        warps = [self.grid.warp_for(p) for p in self._band_paths(timestep)]
+        if all(w.identity for w in warps):
+            return None
+        windows, idx, band_key = {}, {}, []
+        for w in warps:
+            k = w.key()
+            band_key.append(k)
+            if k in windows:
+                continue
+            flat = w.index_of_mask(part.local_mask, row0=part.r0)
+            win = w.window(flat)
+            windows[k] = win
+            idx[k] = torch.from_numpy(w.local(flat, win)).to(self._device)
+        return {"windows": windows, "idx": idx, "band_key": band_key}
 
     def _files(self, timestep):
-        folder = self.date_data[timestep]
-        return [(os.path.join(folder, f"B{b}_sur.tif"), 0, self._window) for b in self.band_map]
+        hit = self._date_files.get(timestep)
+        if hit is not None:
+            return hit
+        paths = self._band_paths(timestep)
+        if self._warp_plan is None:
+            files = [(p, 0, self._window) for p in paths]
+        else:
+            plan = self._warp_plan
+            keys = [self.grid.warp_for(p).key() for p in paths]
+            if keys != plan["band_key"]:
+                raise ValueError(f"{self.date_data[timestep]}: band grids differ from the first date's; "
+                                 "one reader covers one granule grid")
+            files = [(p, 0, plan["windows"][k]) for p, k in zip(paths, keys)]
+        if len(self._date_files) > 64:
+            self._date_files.clear()
+        self._date_files[timestep] = files
+        return files
 
     def prefetch(self, timestep):
         if self._ingest is not None and timestep in self.date_data:
@@ -263,7 +385,9 @@ class Sentinel2Observations:
         key = f"S2A_MSI_{S2_EMULATOR_BANDS[band]:02d}"
         planes = self._ingest.acquire(timestep, self._files(timestep))
         dn = planes[band].reshape(-1)
-        if not self._identity:
+        if self._warp_plan is not None:    # warp + compaction: one gather (-1 -> DN 0)
+            dn = self._K.gather(dn, self._warp_plan["idx"][self._warp_plan["band_key"][band]])
+        elif not self._identity:
             dn = self._K.gather(dn, self._idx)
         return DeviceBand(self._K.OBS_DN16, dn=dn, scale=1e-4, rel_unc=self.rel_unc, unc_floor=0.0,
                           metadata=metadata, emulator=ems.get(key))
@@ -294,10 +418,20 @@ def write_s2_archive(root, dn_by_date: dict, emulators: dict, geotransform=None,
 
 # ------------------------------------------------------------- Sentinel-1
 class S1Observations:
+    """Sentinel-1 sigma0 (``Sentinel1_Observations.py``).  With a georeferenced
+    state mask (GeoTIFF path, or array plus ``mask_geotransform`` /
+    ``mask_projection``) sigma0 and the incidence angle are warped onto the
+    mask's grid, nearest neighbour, like the reference's ``reproject_image``
+    calls (:178,194); uncovered pixels read -999 (no data)."""
+
     POLS = ("VV", "VH")
 
-    def __init__(self, data_folder, state_mask, emulators=None, roi=None, rel_unc=0.05):
+    def __init__(self, data_folder, state_mask, emulators=None, roi=None, rel_unc=0.05, mask_geotransform=None,
+                 mask_projection=None):
         self.state_mask = state_mask
+        self.grid = _StateGrid(state_mask, mask_geotransform, mask_projection)
+        if self.grid.geo and roi is not None:
+            raise ValueError("roi crops the acquisition grid; with a georeferenced state mask the mask defines it")
         self.roi = roi
         self.rel_unc = rel_unc
         self.dates, self.date_data = [], {}
@@ -309,15 +443,29 @@ class S1Observations:
         self.emulators = emulators or {"VV": None, "VH": None}
         self.bands_per_observation = {d: 2 for d in self.dates}
 
+    def define_output(self):
+        if self.grid.geo:
+            return self.grid.projection, list(self.grid.gt)
+        from .tiff import tiff_info
+        info = tiff_info(os.path.join(self.date_data[self.dates[0]], "theta.tif"))
+        gt = list(info.get("geotransform", [0, 1, 0, 0, 0, -1]))
+        if self.roi is not None:
+            gt[0] += self.roi[0] * gt[1]
+            gt[3] += self.roi[1] * gt[5]
+        return info.get("projection", ""), gt
+
+    def _read(self, path):
+        if self.grid.geo:                  # warp onto the state grid (:178,194)
+            return self.grid.read(path, nodata=WRONG_VALUE).astype(np.float64)
+        return _crop(read_tiff(path)[0].astype(np.float64), self.roi)
+
     def get_band_data(self, timestep, band):
         pol = self.POLS[band]
         folder = self.date_data[timestep]
-        s0, _ = read_tiff(os.path.join(folder, f"sigma0_{pol}.tif"))
-        s0 = _crop(s0.astype(np.float64), self.roi)
+        s0 = self._read(os.path.join(folder, f"sigma0_{pol}.tif"))
         mask = s0 != WRONG_VALUE
         unc = _weights(np.where(mask, s0 * self.rel_unc, 0.0), mask)
-        theta, _ = read_tiff(os.path.join(folder, "theta.tif"))
-        meta = {"incidence_angle": _crop(theta.astype(np.float64), self.roi)}
+        meta = {"incidence_angle": self._read(os.path.join(folder, "theta.tif"))}
         return SARdata(np.where(mask, s0, 0.0), unc, mask, meta, self.emulators.get(pol))
 
 

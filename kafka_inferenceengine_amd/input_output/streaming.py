@@ -155,8 +155,11 @@ class RasterIngest:
     under date t's Gauss-Newton kernels; replaces the per-band
     GDAL reads of Sentinel2_Observations.py:148-185.
 
-    ``files``: list of ``(path, band_index_in_file, (r0, r1, c0, c1))``, all
-    windows of the same shape ``plane`` and element type ``dtype``."""
+    ``files``: list of ``(path, band_index_in_file, (r0, r1, c0, c1))`` of
+    element type ``dtype``; each window is decoded row-major into the start of
+    its plane, so windows of the shape ``plane`` fill it and smaller ones (a
+    warp reader's per-grid windows, ``plane = (1, max elements)``) leave a
+    tail the gather never reads."""
 
     def __init__(self, n_planes: int, plane, dtype, device, n_slots: int = 2, io_threads: int | None = None):
         import os
@@ -194,8 +197,8 @@ class RasterIngest:
                  next(i for i in range(len(self.slot_key)) if i != cur))
         self.ring.host_wait(s)          # the slot's previous H2D has finished reading it
         for i, (path, band, (r0, r1, c0, c1)) in enumerate(files):
-            if (r1 - r0, c1 - c0) != self.plane:
-                raise ValueError(f"window {(r0, r1, c0, c1)} is not a {self.plane} plane")
+            if (r1 - r0, c1 - c0) != self.plane and (r1 - r0) * (c1 - c0) > self.plane[0] * self.plane[1]:
+                raise ValueError(f"window {(r0, r1, c0, c1)} does not fit a {self.plane} plane")
             self.ring.read_tiff_async(s, str(path), int(band), r0, r1, c0, c1, self.esize, i * self.plane_bytes,
                                       self.io_threads)
             self.bytes_read += self.plane_bytes

@@ -1040,7 +1040,8 @@ def reduce_partials(partials: torch.Tensor, out: torch.Tensor | None = None):
 
 
 def gather(src, idx, out=None, rows=None):
-    """out[r, p] = src[r, idx[p]] (compaction of raster rows onto active pixels)."""
+    """out[r, p] = src[r, idx[p]] (compaction of raster rows onto active pixels);
+    idx[p] < 0 gives 0 (a warped grid's pixels no source pixel covers)."""
     if src.dim() == 1:
         src2, squeeze = src.view(1, -1), True
     else:
@@ -1049,7 +1050,11 @@ def gather(src, idx, out=None, rows=None):
     if out is None:
         out = torch.empty((src2.shape[0], n), dtype=src.dtype, device=src.device)
     if not _dev(src):
-        out.view(src2.shape[0], -1)[:, :n] = src2[:, idx]
+        o = out.view(src2.shape[0], -1)
+        o[:, :n] = src2[:, idx.clamp(min=0)]
+        miss = idx < 0
+        if bool(miss.any()):
+            o[:, :n][:, miss] = 0
         return out.view(-1) if squeeze else out
     eb = src.element_size()
     ext().gather(eb, _ptr(src2), _ptr(idx), _ptr(out), n, src2.shape[0], src2.stride(0),
