@@ -322,10 +322,12 @@ class DeviceOutput:
     raster IS the analysis state's x ([n_p, N] with N = H W), so it is not
     written twice: ``mean`` then references the state's x (``alias_state``;
     a state's buffers are never rewritten -- each date allocates new ones).
-    The uncertainty planes alternate between two buffers, so a reader of one
-    date's planes (``KafkaOutput``'s device-to-host copy) runs under the next
-    date's analysis; ``device_targets`` makes the analysis wait only for a
-    reader of the buffer it is about to overwrite (``release``)."""
+    The planes the output owns (the uncertainty planes, and the mean planes of
+    a masked strip, the gain form or ``dump_state``) alternate between two
+    buffer pairs, so a reader of one date's planes (``KafkaOutput``'s
+    device-to-host copy) runs under the next date's analysis;
+    ``device_targets`` makes the analysis wait only for a reader of the pair it
+    is about to overwrite (``release``)."""
 
     def __init__(self, parameter_list, keep_history: bool = False, alias_state: bool = True):
         self.parameter_list = list(parameter_list)
@@ -335,9 +337,9 @@ class DeviceOutput:
         self.unc = None
         self.timestep = None
         self.history = {}
-        self._mean_buf = None
+        self._mean_bufs = [None, None]
         self._unc_bufs = None
-        self._readers = [None, None]   # event of the last reader of each uncertainty buffer
+        self._readers = [None, None]   # event of the last reader of each (mean, unc) buffer pair
         self._turn = 0
         self._alias = False
 
@@ -347,7 +349,7 @@ class DeviceOutput:
         H, W = part.strip_shape
         if self._unc_bufs is None or self._unc_bufs[0].device != dev or self._unc_bufs[0].shape != (n, H * W):
             self._unc_bufs = [torch.zeros((n, H * W), dtype=torch.float32, device=dev) for _ in range(2)]
-            self._mean_buf = None
+            self._mean_bufs = [None, None]
             self._readers = [None, None]
             idx = np.asarray(part.local_idx, dtype=np.int64)
             if idx.size and (idx.min() < 0 or idx.max() >= H * W):
@@ -359,13 +361,16 @@ class DeviceOutput:
             self.unc = self._unc_bufs[0]
 
     def _own_mean(self):
-        if self._mean_buf is None:
-            self._mean_buf = torch.zeros_like(self._unc_bufs[0])
-        return self._mean_buf
+        """The mean planes of the current buffer pair (``_turn``): guarded by
+        the same reader event as its uncertainty planes."""
+        b = self._mean_bufs[self._turn]
+        if b is None:
+            b = self._mean_bufs[self._turn] = torch.zeros_like(self._unc_bufs[0])
+        return b
 
     def _next_unc(self, dev):
-        """The uncertainty buffer of the next date (the other one than the
-        latest), after its last reader."""
+        """The uncertainty buffer of the next date (the other pair than the
+        latest), after the last reader of that pair."""
         self._turn ^= 1
         ev = self._readers[self._turn]
         if ev is not None and dev.type == "cuda":

@@ -71,7 +71,12 @@ def epsg_of(projection) -> int:
         return int(projection)
     s = str(projection)
     m = re.findall(r'AUTHORITY\["EPSG",\s*"?(\d+)"?\]', s) or re.findall(r"EPSG:(\d+)", s)
-    return int(m[-1]) if m else 0
+    if m:
+        return int(m[-1])
+    m = re.search(r"UTM zone (\d+)\s*([NS])", s, re.I)      # a citation such as "WGS 84 / UTM zone 30N"
+    if m and "WGS" in s.upper():
+        return (32600 if m.group(2).upper() == "N" else 32700) + int(m.group(1))
+    return 0
 
 
 def write_tiff(path, array, geotransform=None, projection: str | None = None, compress: str | None = "deflate",

@@ -505,6 +505,43 @@ def test_fused_output_gpu(cuda, spatial):
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-6)
 
 
+def test_masked_strip_geotiff_mean_not_overwritten_by_next_date(cuda, tmp_path):
+    """A masked strip's mean planes are owned by the output (not the state's
+    x): the next date's fused analysis must not overwrite them while this
+    date's side-stream device-to-host copy still reads them.  A 2048^2 x 7
+    plane pair takes milliseconds to copy against a sub-millisecond identity
+    analysis, so without the double-buffered mean the GeoTIFF of date t would
+    hold date t+1's mean."""
+    from kafka_inferenceengine_amd.input_output.tiff import read_tiff
+    mask = np.ones((2048, 2048), bool)
+    mask[::7] = False
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=5 * i) for i in range(6)]
+
+    def run(out):
+        obs = k.SyntheticIdentityObservations(mask, device=cuda, stream=False, n_pool=2, seed=3)
+        kf = k.LinearKalman(obs, out, mask, k.create_linear_observation_operator, k.TIP_PARAMETERS, device=cuda,
+                            state_propagation=k.propagate_information_filter_LAI)
+        kf.set_trajectory_model()
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
+        if torch.device(cuda).type == "cuda":
+            torch.cuda.synchronize()
+        return kf
+
+    ref = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
+    run(ref)
+    out = k.KafkaOutput(k.TIP_PARAMETERS, None, "", str(tmp_path), compress=None)
+    run(out)
+    out.flush()
+    assert len(ref.history) >= 4
+    for ts, (m, u) in ref.history.items():
+        for p in (0, 6):
+            got = read_tiff(tmp_path / f"{k.TIP_PARAMETERS[p]}_{ts.strftime('A%Y%j')}.tif")[0]
+            assert np.array_equal(got.reshape(-1), m[p].cpu().numpy()), (ts, p)
+            gu = read_tiff(tmp_path / f"{k.TIP_PARAMETERS[p]}_{ts.strftime('A%Y%j')}_unc.tif")[0]
+            assert np.array_equal(gu.reshape(-1), u[p].cpu().numpy()), (ts, p)
+
+
 @pytest.mark.parametrize("regmask", [0b1000000, 0b1000101])
 def test_affine_jacobi_equals_classic_gpu(cuda, regmask):
     from test_kernels import affine_vs_classic_jacobi

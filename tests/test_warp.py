@@ -18,8 +18,29 @@ from kafka_inferenceengine_amd.input_output import sentinel as S
 from kafka_inferenceengine_amd.input_output.tiff import read_tiff, tiff_info
 from kafka_inferenceengine_amd.input_output.utils import GridWarp, reproject_image
 
-MASK = "/root/reference/Barrax_pivots.tif"
+REF_MASK = "/root/reference/Barrax_pivots.tif"
 UTM30N = "WGS 84 / UTM zone 30N|WGS 84"
+BARRAX_GT = [576452.584549, 10.0, 0.0, 4324696.153353, 0.0, -10.0]
+
+
+def _mask_file():
+    """The reference's Barrax_pivots.tif where the reference tree exists (this
+    container); on a GPU box a stand-in on the same grid (235 x 204, 10 m,
+    EPSG:32630) with five disc-shaped pivots."""
+    if os.path.exists(REF_MASK):
+        return REF_MASK
+    import tempfile
+    p = os.path.join(tempfile.gettempdir(), "kafka_barrax_grid_mask.tif")
+    if not os.path.exists(p):
+        yy, xx = np.mgrid[0:204, 0:235]
+        m = np.zeros((204, 235), np.uint8)
+        for cy, cx in ((50, 60), (60, 170), (150, 50), (140, 150), (100, 110)):
+            m[(yy - cy) ** 2 + (xx - cx) ** 2 < 40 ** 2] = 1
+        k.write_tiff(p, m, BARRAX_GT, UTM30N)
+    return p
+
+
+MASK = _mask_file()
 
 
 def _granule_grid():
@@ -118,7 +139,7 @@ def test_cli_s2_run_on_reference_mask(tmp_path, capsys):
     main(["run", "--sensor", "s2", "--s2-folder", data, "--emulator-folder", emus, "--mask", MASK,
           "--out", str(out), "--steps", "2", "--device", "cpu"])
     rec = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
-    assert rec["timesteps"] == 2 and rec["finite"] and rec["pixels"] == 13027
+    assert rec["timesteps"] == 2 and rec["finite"] and rec["pixels"] == int(read_tiff(MASK)[0].astype(bool).sum())
     files = sorted(p for p in os.listdir(out) if p.endswith(".tif"))
     assert files
     arr, info = read_tiff(out / files[0])
