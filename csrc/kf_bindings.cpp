@@ -152,6 +152,12 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .def_readwrite("fast_obs", &GainArgs::fast_obs)
       .def_readwrite("out_plane", &GainArgs::out_plane)
       .def_readwrite("gpm_frags", &GainArgs::gpm_frags)
+      .def_readwrite("gn_fused", &GainArgs::gn_fused)
+      .def_readwrite("n_visit", &GainArgs::n_visit)
+      .def_readwrite("pdiag_rows", &GainArgs::pdiag_rows)
+      .PTR_FIELD(GainArgs, partials_first, double*)
+      .PTR_FIELD(GainArgs, order, const int32_t*)
+      .PTR_FIELD(GainArgs, dn_out, float*)
       .PTR_FIELD(GainArgs, prop, const PropArgs*)
       .PTR_FIELD(GainArgs, out_mean, float*)
       .PTR_FIELD(GainArgs, out_unc, float*)
@@ -216,7 +222,10 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .ARR_FIELD(PropArgs, blend_cinv, float)
       .PTR_FIELD(PropArgs, blend_mean_pix, const float*)
       .PTR_FIELD(PropArgs, blend_cinv_pix, const float*)
-      .PTR_FIELD(PropArgs, status, uint8_t*);
+      .PTR_FIELD(PropArgs, status, uint8_t*)
+      .def_readwrite("cov_fast", &PropArgs::cov_fast)
+      .def_readwrite("pa_pdiag", &PropArgs::pa_pdiag)
+      .ARR_FIELD(PropArgs, reset_cov, float);
 
   m.def("supported_np", [](int np) { return host_supported(np); });
   m.def("grid", [](int64_t N) { return dev_grid(N); });

@@ -204,6 +204,14 @@ struct PropArgs {
   const float* blend_mean_pix;   // optional per-pixel prior mean [NP][ld]
   const float* blend_cinv_pix;   // optional per-pixel prior precision [NT][ld]
   uint8_t* status;
+  // Covariance-form consumers of a fused forecast (K1g).  cov_fast: reset_cov
+  // holds reset_cinv^-1 (packed), so the forecast covariance is that constant
+  // with one Sherman-Morrison rank-1 update per propagated parameter
+  // (gain_forecast) instead of a Cholesky inverse per pixel.  pa_pdiag: the
+  // analysis rows tri(j, j) of the propagated j hold the analysis PRECISION
+  // diagonal (the gain form's stored rows), read as is instead of inverting p_a.
+  int32_t cov_fast, pa_pdiag;
+  float reset_cov[MAX_NT];
 };
 
 // Dense row-strip geometry (every pixel of the strip and of the halo rows
@@ -1379,8 +1387,11 @@ KF_HD bool pixel_invert(const float* src, float* dst, int64_t ld, int64_t p) {
 //   s = h^T P h + 1/w,  k = P h / s,  x += k (y' - h^T x),  P -= k (P h)^T
 // with y' = y - H0 + h . x0 (iterated EKF linearised about x0).  Same fast
 // paths as K1 (FD: all-GP bands with FD inputs, FOBS: one encoding), the
-// forecast fused from the previous analysis covariance (prop) and the output
-// rasters written by the last iteration (out_mean / out_unc).
+// forecast fused from the previous analysis (prop), the output rasters written
+// by the last iteration (out_mean / out_unc), and K1's launch features: GN
+// iterations 1 + 2 in one launch (gn_fused), the observed-first visiting order,
+// the per-chunk visiting subset and |dx|^2 per pixel (order / n_visit / dn_out)
+// and the stored-rows policy (pdiag_rows).
 struct GainArgs {
   int64_t N, ld;
   int32_t n_bands, joseph;
@@ -1395,18 +1406,30 @@ struct GainArgs {
   double* partials;
   const PropArgs* prop;  // fused forecast (device copy; p_a = analysis COVARIANCE); x_f / p_f unused
   float* out_mean;       // fused output: x and 1/sqrt(diag P^-1) into [NP][out_plane] rasters
-  float* out_unc;
+  float* out_unc;        //   (out_mean null with out_unc set: the state's x is the mean raster)
   const int64_t* out_idx;
   int64_t out_plane;
   int32_t gpm_frags;     // > 0: GP on the matrix cores (LDS tables, as AnalysisArgs); gain_mfma_kernel
+  int32_t gn_fused;      // 2: iterations 1 and 2 in one launch (as AnalysisArgs.gn_fused)
+  double* partials_first;  // per-block sum (x_1 - x_0)^2 of the first fused iteration
+  const int32_t* order;  // visiting order (null: 0..N-1)
+  int64_t n_visit;       // visiting slots (0: N)
+  float* dn_out;         // per-pixel |x - x0|^2 of the last iteration (per-chunk norms); may be null
+  // stored rows: bit j set -> p_out row tri(j, j) receives the analysis
+  // PRECISION diagonal entry (P^-1)_jj and no covariance row is stored (what a
+  // fused forecast with PropArgs.pa_pdiag reads: the propagated parameters'
+  // entries); 0: the full analysis covariance
+  uint32_t pdiag_rows;
   int32_t pad_;
 };
 
+KF_HD int64_t visit_count(const GainArgs& a) { return a.n_visit > 0 ? a.n_visit : a.N; }
+
 // The partial-prior-reset forecast (forecast_partial) of an analysis held as a
 // covariance, returned as a covariance: Pa^-1 = inv(P_a) supplies the
-// propagated diagonals, C = reset precision with those diagonals, P_f = C^-1.
-// PROP_PRIOR (mask 0) and PROP_INFO_APPROX (all propagated, C0 = 0) map onto
-// it as for K1 (ops/kernels.py:prop_args).
+// propagated diagonals (or p_a holds them, pa_pdiag), C = reset precision with
+// those diagonals, P_f = C^-1.  PROP_PRIOR (mask 0) and PROP_INFO_APPROX (all
+// propagated, C0 = 0) map onto it as for K1 (ops/kernels.py:prop_args).
 template <int NP>
 KF_HD uint8_t forecast_partial_cov(const KF_CONST_AS PropArgs* a, int64_t p, float (&xf)[NP],
                                    float (&P)[ntri(NP)]) {
@@ -1417,11 +1440,18 @@ KF_HD uint8_t forecast_partial_cov(const KF_CONST_AS PropArgs* a, int64_t p, flo
 #pragma unroll
   for (int t = 0; t < NT; ++t) C[t] = a->reset_cinv[t];
   if (a->prop_mask) {
-    float U[NT], Pi[NT];
+    float Pi[NT];
+    if (a->pa_pdiag) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) U[t] = KF_PX(a->p_a, t * ld, p);
-    if (!chol_packed<NP>(U)) st |= ST_NONSPD;
-    chol_inverse<NP>(U, Pi);
+      for (int j = 0; j < NP; ++j)
+        if ((a->prop_mask >> j) & 1u) Pi[tri(NP, j, j)] = KF_PX(a->p_a, tri(NP, j, j) * ld, p);
+    } else {
+      float U[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) U[t] = KF_PX(a->p_a, t * ld, p);
+      if (!chol_packed<NP>(U)) st |= ST_NONSPD;
+      chol_inverse<NP>(U, Pi);
+    }
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
       if ((a->prop_mask >> j) & 1u) {
@@ -1433,6 +1463,62 @@ KF_HD uint8_t forecast_partial_cov(const KF_CONST_AS PropArgs* a, int64_t p, flo
   forecast_partial_mean<NP>(a, p, xf);
   if (!chol_packed<NP>(C)) st |= ST_NONSPD;
   chol_inverse<NP>(C, P);
+  return st;
+}
+
+// The same forecast without a Cholesky per pixel (PropArgs.cov_fast): C
+// differs from the constant reset precision C0 only in the propagated
+// diagonals, so P_f = C^-1 is the constant C0^-1 (reset_cov) updated by one
+// Sherman-Morrison rank-1 term per propagated j,
+//   (M + d e_j e_j^T)^-1 = M^-1 - d u u^T / (1 + d u_j),  u = M^-1 e_j.
+// Also returns the forecast precision diagonal cd (the information identity
+// diag(P_a^-1) = cd + sum_b w_b h_b^2 then gives the uncertainty raster and
+// the stored rows without inverting P_a).
+template <int NP>
+KF_HD uint8_t gain_forecast(const KF_CONST_AS PropArgs* a, int64_t p, float (&xf)[NP], float (&P)[ntri(NP)],
+                            float (&cd)[NP]) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a->ld;
+  uint8_t st = 0;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) P[t] = a->reset_cov[t];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) cd[j] = a->reset_cinv[tri(NP, j, j)];
+  if (a->prop_mask) {
+    float d[NP];
+    if (a->pa_pdiag) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j)
+        d[j] = ((a->prop_mask >> j) & 1u) ? KF_PX(a->p_a, tri(NP, j, j) * ld, p) : 1.f;
+    } else {
+      float U[NT], Pi[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) U[t] = KF_PX(a->p_a, t * ld, p);
+      if (!chol_packed<NP>(U)) st |= ST_NONSPD;
+      chol_inverse<NP>(U, Pi);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) d[j] = Pi[tri(NP, j, j)];
+    }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      if (!((a->prop_mask >> j) & 1u)) continue;
+      const float q = a->q_pix ? KF_PX(a->q_pix, j * ld, p) : a->q[j];
+      const float c = kf_rcp(kf_rcp(d[j]) + q);
+      const float delta = c - cd[j];
+      cd[j] = c;
+      float u[NP];
+#pragma unroll
+      for (int i = 0; i < NP; ++i) u[i] = P[sym<NP>(i, j)];
+      const float den = fmaf(delta, u[j], 1.f);
+      if (!(den > 0.f)) st |= ST_NONSPD;
+      const float f = delta * kf_rcp(den);
+#pragma unroll
+      for (int i = 0; i < NP; ++i)
+#pragma unroll
+        for (int k = i; k < NP; ++k) P[tri(NP, i, k)] = fmaf(-f * u[i], u[k], P[tri(NP, i, k)]);
+    }
+  }
+  forecast_partial_mean<NP>(a, p, xf);
   return st;
 }
 
@@ -1467,39 +1553,104 @@ KF_HD void gain_band_update(float (&P)[ntri(NP)], float (&x)[NP], const float (&
   }
 }
 
+// The forecast (x_f, P_f) of pixel p: fused (fast or Cholesky form) or read.
+// Returns the status bits; cd_ok: cd holds the forecast precision diagonal.
 template <int NP, typename GA>
-KF_HD float gain_finish(const GA& a, int64_t p, float (&x)[NP], float (&P)[ntri(NP)], const float (&x0)[NP],
-                        uint8_t st, int nobs);
-
-template <int NP, int FD = 0, int FOBS = 0>
-KF_HD float pixel_gain(const GainArgs& a, int64_t p) {
+KF_HD uint8_t gain_load_forecast(const GA& a, int64_t p, float (&xf)[NP], float (&P)[ntri(NP)], float (&cd)[NP],
+                                 bool& cd_ok) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a.ld;
-  float x0[NP], x[NP], P[NT];
-  uint8_t st = 0;
+  cd_ok = false;
   if (a.prop) {
-    st |= forecast_partial_cov<NP>(opaque(cptr(a.prop)), p, x, P);
-  } else {
-#pragma unroll
-    for (int j = 0; j < NP; ++j) x[j] = KF_PX(a.x_f, j * ld, p);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) P[t] = KF_PX(a.p_f, t * ld, p);
+    const KF_CONST_AS PropArgs* pa = opaque(cptr(a.prop));
+    if (pa->cov_fast) {
+      cd_ok = true;
+      return gain_forecast<NP>(pa, p, xf, P, cd);
+    }
+    return forecast_partial_cov<NP>(pa, p, xf, P);
   }
+#pragma unroll
+  for (int j = 0; j < NP; ++j) xf[j] = KF_PX(a.x_f, j * ld, p);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) P[t] = KF_PX(a.p_f, t * ld, p);
+  return 0;
+}
+
+template <int NP, typename GA>
+KF_HD float gain_finish(const GA& a, int64_t p, float (&x)[NP], float (&P)[ntri(NP)], const float (&x0)[NP],
+                        uint8_t st, int nobs, const float* dA);
+
+// One pixel of K1g over a.gn_fused (1 or 2) Gauss-Newton iterations.
+// EVAL(bi, x0, y, w, H0, h, ok) -> bool use: decodes band bi and, where it is
+// used, evaluates its operator at x0 (the matrix-core evaluator runs for the
+// whole wave: every lane calls it, act = false lanes included).  Iteration 2
+// restarts from the forecast linearised at iteration 1's x; the returned
+// |x - x0|^2 is the last iteration's, dn1 the first's.
+template <int NP, typename GA, typename EVAL>
+KF_HD float gain_pixel(const GA& a, int64_t p, bool act, float& dn1, EVAL&& eval) {
+  constexpr int NT = ntri(NP);
+  const int64_t ld = a.ld;
+  float xf[NP], x0[NP], x[NP], P[NT], cd[NP];
+  bool cd_ok;
+  const uint8_t st_fc = gain_load_forecast<NP>(a, p, xf, P, cd, cd_ok);
   if (a.x_prev) {
 #pragma unroll
     for (int j = 0; j < NP; ++j) x0[j] = KF_PX(a.x_prev, j * ld, p);
   } else {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) x0[j] = x[j];
+    for (int j = 0; j < NP; ++j) x0[j] = xf[j];
   }
+  const int gn = a.gn_fused > 1 ? 2 : 1;
+  dn1 = 0.f;
+  uint8_t st = st_fc;
   int nobs = 0;
-  for (int bi = 0; bi < a.n_bands; ++bi) {
+  float dA[NP];
+  for (int it = 0; it < gn; ++it) {
+    if (it > 0) {
+      // iteration 2 linearises at iteration 1's analysis, from the forecast again
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        const float d = x[j] - x0[j];
+        dn1 = fmaf(d, d, dn1);
+        x0[j] = x[j];
+      }
+      gain_load_forecast<NP>(a, p, xf, P, cd, cd_ok);
+      st = st_fc;
+      nobs = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      x[j] = xf[j];
+      dA[j] = cd[j];
+    }
+    for (int bi = 0; bi < a.n_bands; ++bi) {
+      float y, w, H0, h[NP];
+      bool ok;
+      const bool use = eval(bi, x0, y, w, H0, h, ok);
+      if (use && !ok) st |= ST_BAD_OP;
+      if (use && ok) {
+        ++nobs;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) dA[j] = fmaf(w * h[j], h[j], dA[j]);
+        gain_band_update<NP>(P, x, x0, h, H0, y, w, a.joseph != 0);
+      }
+    }
+  }
+  if (!act) return 0.f;
+  return gain_finish<NP>(a, p, x, P, x0, st, nobs, cd_ok ? dA : nullptr);
+}
+
+template <int NP, int FD = 0, int FOBS = 0>
+KF_HD float pixel_gain(const GainArgs& a, int64_t p, float& dn1) {
+  const int64_t ld = a.ld;
+  return gain_pixel<NP>(a, p, true, dn1, [&](int bi, const float (&x0)[NP], float& y, float& w, float& H0,
+                                             float (&h)[NP], bool& ok) -> bool {
     const BandDesc bd = cptr(a.bands)[bi];
-    float y, w;
     decode_obs<FOBS>(bd, p, y, w);
-    if (!(w > 0.f)) { if (bd.h0_out) KF_PX(bd.h0_out, 0, p) = 0.f; continue; }
-    float H0, h[NP];
-    bool ok;
+    if (!(w > 0.f)) {
+      if (bd.h0_out) KF_PX(bd.h0_out, 0, p) = 0.f;
+      return false;
+    }
     if constexpr (FD > 0) {
 #if defined(__HIP_DEVICE_COMPILE__)
       gp_eval<NP, FD, 4, false, true>(bd, x0, H0, h, a.bands + bi);
@@ -1517,35 +1668,30 @@ KF_HD float pixel_gain(const GainArgs& a, int64_t p) {
     if constexpr (FD > 0) h0o = opaque(cptr(a.bands + bi))->h0_out;
 #endif
     if (h0o) KF_PX(h0o, 0, p) = H0;
-    if (!ok) { st |= ST_BAD_OP; continue; }
-    ++nobs;
-    gain_band_update<NP>(P, x, x0, h, H0, y, w, a.joseph != 0);
-  }
-  return gain_finish<NP>(a, p, x, P, x0, st, nobs);
+    return true;
+  });
 }
 
 // K1g tail (shared with the matrix-core gain kernel, kf_gp_mfma.h): health
-// fallback, state / covariance stores, fused output; returns |x - x0|^2.
+// fallback, state / covariance (or precision-diagonal) stores, fused output;
+// returns |x - x0|^2.  dA: the analysis precision diagonal by the information
+// identity (fast forecasts), else null (inverted from P where needed).
 template <int NP, typename GA>
 KF_HD float gain_finish(const GA& a, int64_t p, float (&x)[NP], float (&P)[ntri(NP)], const float (&x0)[NP],
-                        uint8_t st, int nobs) {
+                        uint8_t st, int nobs, const float* dA) {
   constexpr int NT = ntri(NP);
   const int64_t ld = a.ld;
   if (nobs == 0) st |= ST_NO_OBS;
   bool fin = true;
 #pragma unroll
   for (int j = 0; j < NP; ++j) fin = fin && finitef(x[j]);
+  float dfb[NP];
   if (!fin) {
     // health fallback: keep the forecast for this pixel
     st |= ST_NONFINITE | ST_FALLBACK;
-    if (a.prop) {
-      forecast_partial_cov<NP>(opaque(cptr(a.prop)), p, x, P);
-    } else {
-#pragma unroll
-      for (int j = 0; j < NP; ++j) x[j] = KF_PX(a.x_f, j * ld, p);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) P[t] = KF_PX(a.p_f, t * ld, p);
-    }
+    bool cd_ok;
+    gain_load_forecast<NP>(a, p, x, P, dfb, cd_ok);
+    dA = cd_ok ? dfb : nullptr;
   }
   float dn = 0.f;
 #pragma unroll
@@ -1554,26 +1700,44 @@ KF_HD float gain_finish(const GA& a, int64_t p, float (&x)[NP], float (&P)[ntri(
     const float d = x[j] - x0[j];
     dn = fmaf(d, d, dn);
   }
-  if (a.p_out) {
+  const bool need_pi = a.out_unc || (a.p_out && a.pdiag_rows);
+  float pid[NP];
+  if (need_pi) {
+    if (dA) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) KF_PX(a.p_out, t * ld, p) = P[t];
+      for (int j = 0; j < NP; ++j) pid[j] = dA[j];
+    } else {
+      float U[NT], Pi[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) U[t] = P[t];
+      if (!chol_packed<NP>(U)) st |= ST_NONSPD;
+      chol_inverse<NP>(U, Pi);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) pid[j] = Pi[tri(NP, j, j)];
+    }
   }
-  if (a.out_mean) {
-    // fused output: 1/sqrt(diag P^-1), the information form's uncertainty raster
-    float U[NT], Pi[NT];
+  if (a.p_out) {
+    if (a.pdiag_rows) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) U[t] = P[t];
-    if (!chol_packed<NP>(U)) st |= ST_NONSPD;
-    chol_inverse<NP>(U, Pi);
+      for (int j = 0; j < NP; ++j)
+        if ((a.pdiag_rows >> j) & 1u) KF_PX(a.p_out, tri(NP, j, j) * ld, p) = pid[j];
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) KF_PX(a.p_out, t * ld, p) = P[t];
+    }
+  }
+  if (a.out_unc) {
+    // fused output: 1/sqrt(diag P^-1), the information form's uncertainty raster
     const int64_t r = a.out_idx ? KF_PX(a.out_idx, 0, p) : p;
     const int64_t pl = a.out_plane;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      KF_PX(a.out_mean, j * pl, r) = x[j];
-      KF_PX(a.out_unc, j * pl, r) = kf_rsqrt(Pi[tri(NP, j, j)]);
+      if (a.out_mean) KF_PX(a.out_mean, j * pl, r) = x[j];
+      KF_PX(a.out_unc, j * pl, r) = kf_rsqrt(pid[j]);
     }
   }
   if (a.status) KF_PX(a.status, 0, p) = st;
+  if (a.dn_out) KF_PX(a.dn_out, 0, p) = dn;
   return dn;
 }
 

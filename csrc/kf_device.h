@@ -322,26 +322,36 @@ __global__ __launch_bounds__(BLOCK) void gain_mfma_kernel(GainArgs a) {
     if (threadIdx.x == 0) gpm_lds[a.gpm_frags - 1] = kf_h8{};   // shared zero fragment
   }
   __syncthreads();
-  double acc = 0.0;
+  double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
-  for (int64_t base = (int64_t)blockIdx.x * BLOCK + (threadIdx.x - lane); base < a.N; base += stride) {
-    const int64_t p = base + lane;
-    const bool act = p < a.N;
-    const float dn = pixel_gain_mfma<NP, D, FOBS>(a, act ? p : a.N - 1, act, gpm_lds);
+  const int64_t nv = visit_count(a);
+  for (int64_t base = (int64_t)blockIdx.x * BLOCK + (threadIdx.x - lane); base < nv; base += stride) {
+    const int64_t q = base + lane;
+    const bool act = q < nv;
+    const int64_t p = visit_px(a.order, act ? q : nv - 1);
+    float dn1;
+    const float dn = pixel_gain_mfma<NP, D, FOBS>(a, p, act, gpm_lds, dn1);
     acc += act ? (double)dn : 0.0;
+    acc1 += act ? (double)dn1 : 0.0;
   }
-  if (a.partials) block_partial(acc, a.partials);
+  if (a.partials_first) block_partials2<BLOCK>(acc, acc1, a.partials, a.partials_first);
+  else if (a.partials) block_partial(acc, a.partials);
 #endif
 }
 
 template <int NP, int FD = 0, int FOBS = 0>
 __global__ __launch_bounds__(BLOCK) void gain_kernel(GainArgs a) {
-  double acc = 0.0;
+  double acc = 0.0, acc1 = 0.0;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
-  for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < a.N; p += stride)
-    acc += (double)pixel_gain<NP, FD, FOBS>(a, p);
-  if (a.partials) block_partial(acc, a.partials);
+  const int64_t nv = visit_count(a);
+  for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < nv; q += stride) {
+    float dn1;
+    acc += (double)pixel_gain<NP, FD, FOBS>(a, visit_px(a.order, q), dn1);
+    acc1 += (double)dn1;
+  }
+  if (a.partials_first) block_partials2<BLOCK>(acc, acc1, a.partials, a.partials_first);
+  else if (a.partials) block_partial(acc, a.partials);
 }
 
 // K1g launch: the all-GP fast instantiations (as l_analysis) or the generic kernel.

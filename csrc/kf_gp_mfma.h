@@ -738,41 +738,24 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
   }
 }
 
-// K1g (gain / covariance form) with the GP on the matrix cores: pixel_gain
-// (kf_core.h) with lane = pixel, the band's GP sums wave-cooperative as in
-// pixel_analysis_mfma, then the same scalar-band update and tail.
+// K1g (gain / covariance form) with the GP on the matrix cores: gain_pixel
+// (kf_core.h) with lane = pixel, each band's GP sums wave-cooperative as in
+// pixel_analysis_mfma (every lane of the wave takes part, act = false lanes
+// included), then the same scalar-band update and tail.
 template <int NP, int D, int FOBS>
-__device__ __forceinline__ float pixel_gain_mfma(const GainArgs& a, int64_t p, bool act, const kf_h8* lds) {
-  constexpr int NT = ntri(NP);
-  const int64_t ld = a.ld;
-  float x0[NP], x[NP], P[NT];
-  uint8_t st = 0;
-  if (a.prop) {
-    st |= forecast_partial_cov<NP>(opaque(cptr(a.prop)), p, x, P);
-  } else {
-#pragma unroll
-    for (int j = 0; j < NP; ++j) x[j] = KF_PX(a.x_f, j * ld, p);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) P[t] = KF_PX(a.p_f, t * ld, p);
-  }
-  if (a.x_prev) {
-#pragma unroll
-    for (int j = 0; j < NP; ++j) x0[j] = KF_PX(a.x_prev, j * ld, p);
-  } else {
-#pragma unroll
-    for (int j = 0; j < NP; ++j) x0[j] = x[j];
-  }
-  int nobs = 0;
-  int off = 0;
-  for (int bi = 0; bi < a.n_bands; ++bi) {
+__device__ __forceinline__ float pixel_gain_mfma(const GainArgs& a, int64_t p, bool act, const kf_h8* lds,
+                                                 float& dn1) {
+  return gain_pixel<NP>(a, p, act, dn1, [&](int bi, const float (&x0)[NP], float& y, float& w, float& H0,
+                                            float (&h)[NP], bool& ok) -> bool {
+    int off = 0;
+    for (int bj = 0; bj < bi; ++bj) off += cptr(a.bands)[bj].gpm_nchunk * gpm_frags_per_chunk(D);
     const KF_CONST_AS BandDesc* bdp = cptr(a.bands) + bi;
-    float y, w;
     decode_obs<FOBS>(*bdp, p, y, w);
     const bool use = act && (w > 0.f);
-    float H0 = 0.f, h[NP];
+    H0 = 0.f;
 #pragma unroll
     for (int j = 0; j < NP; ++j) h[j] = 0.f;
-    bool ok = false;
+    ok = false;
     const int nch = bdp->gpm_nchunk;
     if (__any(use)) {
       float xi[D], c = 0.f;
@@ -790,17 +773,10 @@ __device__ __forceinline__ float pixel_gain_mfma(const GainArgs& a, int64_t p, b
 #pragma unroll
       for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);
     }
-    off += nch * gpm_frags_per_chunk(D);
     float* h0o = opaque(bdp)->h0_out;
     if (act && h0o) KF_PX(h0o, 0, p) = use ? H0 : 0.f;
-    if (use && !ok) st |= ST_BAD_OP;
-    if (use && ok) {
-      ++nobs;
-      gain_band_update<NP>(P, x, x0, h, H0, y, w, a.joseph != 0);
-    }
-  }
-  if (!act) return 0.f;
-  return gain_finish<NP>(a, p, x, P, x0, st, nobs);
+    return use;
+  });
 }
 #endif
 }  // namespace kf

@@ -61,7 +61,20 @@ static int h_analysis(const AnalysisArgs& a, int grid) {
 }
 template <int NP>
 static int h_gain(const GainArgs& a, int grid) {
-  grid_stride(a.N, grid, a.partials, [&](int64_t p) { return pixel_gain<NP>(a, p); });
+  const int64_t stride = (int64_t)grid * HBLOCK;
+  const int64_t nv = visit_count(a);
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int b = 0; b < grid; ++b) {
+    double acc = 0.0, acc1 = 0.0;
+    for (int t = 0; t < HBLOCK; ++t)
+      for (int64_t q = (int64_t)b * HBLOCK + t; q < nv; q += stride) {
+        float dn1;
+        acc += (double)pixel_gain<NP>(a, visit_px(a.order, q), dn1);
+        acc1 += (double)dn1;
+      }
+    if (a.partials) a.partials[b] = acc;
+    if (a.partials_first) a.partials_first[b] = acc1;
+  }
   return 0;
 }
 template <int NP>

@@ -56,6 +56,7 @@ class _GNRun:
     out_t: object
     h0_outs: object
     a_rows: int
+    pdiag_rows: int
     len_x: float
     n_bands: int
     fuse2: bool
@@ -182,7 +183,12 @@ class GaussNewtonMixin:
         """GN iterations 1 and 2 in one launch (the plain analysis, or the plain
         first iteration with the regularised prepare of the second)."""
         n, N, prop, fc = self.n_params, self.N, run.prop, run.fc
-        if run.fuse_sp:
+        if run.gain:
+            fx, fP = (None, None) if prop is not None else (fc.x, fc.P)
+            K.gain(n, run.table, x_prev, fx, fP, x_new, run.P_out, run.status, self._partials, N=N,
+                   joseph=self.config.joseph, prop=prop, out=run.out_t, gn_fused=2, partials_first=self._partials1,
+                   order=run.order, pdiag_rows=run.pdiag_rows)
+        elif run.fuse_sp:
             self._regularised_iteration(run.table, x_prev, fc, x_new, run.P_out, run.status, prop, run.out_t,
                                         final=True, partials_first=self._partials1, a_rows=run.a_rows)
         else:
@@ -200,7 +206,7 @@ class GaussNewtonMixin:
         fx, fP = (None, None) if prop is not None else (fc.x, fc.P)
         if run.gain:
             K.gain(n, table, x_prev, fx, fP, x_new, A_keep, run.status, self._partials, N=N, joseph=cfg.joseph,
-                   prop=prop, out=out_now)
+                   prop=prop, out=out_now, order=run.order, pdiag_rows=run.pdiag_rows if A_keep is not None else 0)
         elif run.first_plain and n_iter == 1:
             # the unfused form of fuse_sp's first iteration (same kernel path)
             K.analysis(n, table, x_prev, fx, fP, x_new, None, None, run.status, self._partials, N=N, prop=prop,
@@ -242,7 +248,7 @@ class GaussNewtonMixin:
         n, N = self.n_params, self.N
         table, specs, dbs, precomp, prop, fc = run.table, run.specs, run.dbs, run.precomp, run.prop, run.fc
         x_prev, x_new, P_out, status, order, out_t = run.x_prev, run.x_new, run.P_out, run.status, run.order, run.out_t
-        h0_outs, a_rows = run.h0_outs, run.a_rows
+        h0_outs, a_rows, gain = run.h0_outs, run.a_rows, run.gain
         cc = self._chunk_state()
         cc.begin()
         fx, fP = (None, None) if prop is not None else (fc.x, fc.P)
@@ -256,17 +262,22 @@ class GaussNewtonMixin:
             if precomp:
                 pre = self._precompute_host(specs, dbs, x_prev)
                 table = build_table(specs, dbs, n, self._cache, self.device, h0_outs, pre)
-            kw = dict(prop=prop, order=vis, dn_out=cc.dn, a_rows=a_rows)
+            kw = dict(prop=prop, order=vis, dn_out=cc.dn)
             if not full:
                 kw["n_visit"] = n_visit
             with self.timer.phase("analysis"):
                 if N and n_visit:
-                    if fuse and n_iter == 1:
+                    first2 = fuse and n_iter == 1
+                    if gain:        # K1g: the same visiting, subset and per-pixel norms
+                        K.gain(n, table, x_prev, fx, fP, x_new, P_out if first2 else A_keep, status, None, N=N,
+                               joseph=cfg.joseph, out=out_t if first2 else out_now, gn_fused=2 if first2 else 1,
+                               pdiag_rows=run.pdiag_rows if (first2 or A_keep is not None) else 0, **kw)
+                    elif first2:
                         K.analysis(n, table, x_prev, fx, fP, x_new, P_out, None, status, None, N=N, out=out_t,
-                                   gn_fused=2, **kw)
+                                   gn_fused=2, a_rows=a_rows, **kw)
                     else:
                         K.analysis(n, table, x_prev, fx, fP, x_new, A_keep, None, status, None, N=N, out=out_now,
-                                   **kw)
+                                   a_rows=a_rows, **kw)
             if fuse and n_iter == 1:
                 n_iter = 2
             x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))

@@ -592,8 +592,7 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
             # the next date's observed-first order too: its passes run on the
             # device after this date's launches, under the host's norm wait and
             # step bookkeeping, instead of between the two dates' analyses
-            if cfg.analysis_form != "gain":
-                order = self._visit_order(date, specs, table)
+            order = self._visit_order(date, specs, table)
         self._prepared = (date, bands, table, order)
 
     def _visit_order(self, timestep, specs, table):
@@ -797,9 +796,9 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
                 if hasattr(self.observations, "bands_per_observation") else None
             self._band_parallel_check(specs, nb_all)
         chunked = bool(cfg.convergence_chunk)
-        if chunked and (gain or bp or cfg.spatial_gamma > 0):
-            raise ValueError("convergence_chunk runs the information form without band-parallel or the spatial "
-                             "prior (the spatial prior couples the chunks)")
+        if chunked and (bp or cfg.spatial_gamma > 0 or (gain and precomp)):
+            raise ValueError("convergence_chunk runs the fused information or gain form without band-parallel or "
+                             "the spatial prior (the spatial prior couples the chunks)")
         split = None if (precomp or gain or bp or cfg.spatial_gamma > 0 or chunked) else \
             self._split_plan(specs, dbs, h0_outs)
         if precomp or split:
@@ -837,32 +836,36 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         if ((plain or spatial or (gain and not precomp)) and N and cfg.fuse_output
                 and hasattr(self.output, "device_targets")):
             # plain and spatial paths: the final state's x doubles as the mean raster (dense strips)
-            out_t = self.output.device_targets(self, self.device, alias=plain or spatial)
+            out_t = self.output.device_targets(self, self.device, alias=plain or spatial or gain)
         # analysis precision rows stored (EngineConfig.store_precision): a mask of
         # the rows the caller reads (0: all); no row at all -> no precision store.
         # Paths whose output is dumped from the state afterwards keep every row
-        a_rows, p_valid = 0, None
-        if (store_rows is not None and not (gain or cfg.hessian_correction)
-                and (out_t is not None or self.output is None)):
+        a_rows, p_valid, pdiag_rows = 0, None, 0
+        diag_pos = {tri_pos(n, j, j): j for j in range(n)}
+        if (store_rows is not None and not cfg.hessian_correction
+                and (out_t is not None or self.output is None)
+                and not (gain and (precomp or any(r not in diag_pos for r in store_rows)))):
             p_valid = 0
             for r in store_rows:
                 p_valid |= 1 << int(r)
-            a_rows = p_valid
+                if gain:            # the gain form stores those rows as precision diagonal entries
+                    pdiag_rows |= 1 << diag_pos[int(r)]
+            a_rows = 0 if gain else p_valid
             if p_valid == 0:
                 P_out = None
         # GN iterations 1 and 2 in one launch (the first never ends the loop): rank-
         # independent test, so every rank queues the same collectives
-        fuse2 = (plain and cfg.fuse_gn and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
-                 and not (prop is None and fc is None))
+        fuse2 = ((plain or (gain and not precomp)) and cfg.fuse_gn and cfg.min_iterations >= 2
+                 and cfg.max_iterations >= 1 and not (prop is None and fc is None))
         # linear / identity operators: y' = y - offset does not depend on the
         # linearisation point (kf_core.h FD_LINEAR), so iteration 2 repeats
         # iteration 1 exactly and its norm is 0 -- converged without a read-back
-        static_conv = (fuse2 and cfg.convergence_tolerance > 0 and bool(specs)
+        static_conv = (fuse2 and plain and cfg.convergence_tolerance > 0 and bool(specs)
                        and all(s.kind == OP_LINEAR for s in specs))
         # observed pixels first (config.observed_first): one order per date for
         # every analysis launch of it (GP bands on the fused kernels only)
-        if order is False or table is None or not N or gain or precomp or split or bp:
-            order = None if (gain or precomp or split or bp) else self._visit_order(timestep, specs, table)
+        if order is False or table is None or not N or precomp or split or bp:
+            order = None if (precomp or split or bp) else self._visit_order(timestep, specs, table)
         self._visit = order
         # spatial prior: a plain first iteration (config.spatial_first_plain; it
         # cannot end the loop), fused with the regularised prepare of the second
@@ -870,7 +873,8 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         fuse_sp = first_plain and cfg.fuse_gn
         run = _GNRun(timestep=timestep, specs=specs, dbs=dbs, table=table, precomp=precomp, gain=gain, bp=bp,
                      split=split, prop=prop, fc=fc, x_prev=x_prev, x_new=x_new, P_out=P_out, status=status,
-                     order=order, out_t=out_t, h0_outs=h0_outs, a_rows=a_rows, len_x=len_x, n_bands=len(bands),
+                     order=order, out_t=out_t, h0_outs=h0_outs, a_rows=a_rows, pdiag_rows=pdiag_rows, len_x=len_x,
+                     n_bands=len(bands),
                      fuse2=fuse2, fuse_sp=fuse_sp, first_plain=first_plain, static_conv=static_conv)
         # the iteration strategy: the reference's exit test per chunk or over the tile
         x_prev, n_iter, norms = (self._gn_chunked if chunked else self._gn_global)(run)
@@ -883,7 +887,8 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
             if pu is None or pu.shape != (ntri(n), ld) or pu.device != self.device:
                 pu = self._p_unused = torch.empty((ntri(n), ld), dtype=torch.float32, device=self.device)
             P_out = pu
-        state = KFState(x_prev, P_out, COVARIANCE if gain else PRECISION, N, p_valid=p_valid)
+        state = KFState(x_prev, P_out, COVARIANCE if gain else PRECISION, N, p_valid=p_valid,
+                        p_diag_precision=gain and p_valid is not None)
         self._output_written = state if out_t is not None else None
         if cfg.hessian_correction and not gain and N:
             with self.timer.phase("hessian"):
@@ -911,14 +916,23 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         4 ntri B/px.  Full where the state is read otherwise: the run's last
         step or a checkpoint step, the last observation date, a date whose
         analysis is the next date's forecast within one step, a non-fused
-        output, reference-protocol propagators, the gain form."""
+        output, reference-protocol propagators; the gain form keeps the rows as
+        precision diagonal entries when its next forecast is fused (a light
+        propagator, no prior blend), the full covariance otherwise."""
         cfg = self.config
         if (cfg.store_precision == "always" or self._full_precision_step or not last_of_step or not more_dates
-                or cfg.analysis_form == "gain" or cfg.band_sequential or cfg.hessian_correction
-                or cfg.return_innovations):
+                or cfg.band_sequential or cfg.hessian_correction or cfg.return_innovations):
             return None
         if not (cfg.fuse_output and hasattr(self.output, "device_targets")) and self.output is not None:
             return None            # the dump reads the precision diagonal (observations.py:392-393)
+        if cfg.analysis_form == "gain":
+            # the gain form stores the rows as precision diagonal entries, which only
+            # its fused forecast reads (a light propagator without a prior blend:
+            # advance_state's lazy_cov); other forecasts invert the full covariance
+            prop = self._state_propagator
+            spec = getattr(prop, "device_spec", None) if prop is not None else None
+            if self.prior is not None or spec is None or not K.prop_is_light(spec.mode):
+                return None
         return self._next_forecast_rows()
 
     def _next_forecast_rows(self):

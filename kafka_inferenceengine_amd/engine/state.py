@@ -30,6 +30,10 @@ class KFState:
     # under EngineConfig.store_precision="auto" stores only what the next
     # forecast reads (the LAI propagator: one diagonal entry, kf_tools.py:292-314)
     p_valid: int | None = None
+    # COVARIANCE states only: the p_valid rows tri(j, j) hold the analysis
+    # PRECISION diagonal (P^-1)_jj -- what the gain form's stored-rows policy
+    # keeps for the next fused forecast (GainArgs.pdiag_rows / PropArgs.pa_pdiag)
+    p_diag_precision: bool = False
 
     @property
     def full(self) -> bool:
@@ -51,13 +55,14 @@ class KFState:
         return self.x.device
 
     def clone(self) -> "KFState":
-        return KFState(self.x.clone(), self.P.clone(), self.kind, self.N, self.p_valid)
+        return KFState(self.x.clone(), self.P.clone(), self.kind, self.N, self.p_valid, self.p_diag_precision)
 
     def copy_(self, other: "KFState") -> "KFState":
         self.x.copy_(other.x)
         self.P.copy_(other.P)
         self.kind = other.kind
         self.p_valid = other.p_valid
+        self.p_diag_precision = other.p_diag_precision
         return self
 
     @classmethod
@@ -150,7 +155,7 @@ class LazyForecast:
             return np.asarray(x).tobytes() if not isinstance(x, (int, float, bool, str)) else x
         ptr = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
         head = (ptr(self.src.x), ptr(self.src.P), self.N, self.src.x.shape[1], ptr(self.q_pix), ptr(bm), ptr(bc),
-                str(self.src.x.device))
+                str(self.src.x.device), bool(self.src.p_diag_precision))
         if "_key" in self.spec:        # memoised argument dict (LinearKalman.advance_state)
             return head + (self.spec["_key"],)
         return head + tuple((k, v(x)) for k, x in sorted(self.spec.items()))
@@ -171,7 +176,7 @@ class LazyForecast:
                 h._buf = hit[1]
                 return h
         h = K.prop_args(self.n_params, self.spec, self.src.x, self.src.P, N=self.N, q_pix=self.q_pix,
-                        blend_mean_pix=bm, blend_cinv_pix=bc, fused=True)
+                        blend_mean_pix=bm, blend_cinv_pix=bc, fused=True, pa_pdiag=self.src.p_diag_precision)
         if key is not None:
             self._cache["_misses"] = self._cache.get("_misses", 0) + 1
             if len(self._cache) >= 256:

@@ -526,14 +526,25 @@ def obs_order(bands: BandTable, N: int, device, out=None, scratch=None, groups=N
 
 
 def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status=None, partials=None, N=None,
-         joseph=False, prop=None, out=None, fast=True):
+         joseph=False, prop=None, out=None, fast=True, gn_fused=1, partials_first=None, order=None, n_visit=None,
+         dn_out=None, pdiag_rows=0):
     """K1g covariance/gain-form analysis (sequential scalar band updates).
 
     ``prop`` (:func:`prop_args` with ``fused=True`` over the analysis
     COVARIANCE) fuses the forecast as for :func:`analysis` (x_f / p_f None;
     ``x_prev=None`` linearises at it); ``out = (mean, unc, idx)`` writes the
-    output rasters (x, 1/sqrt(diag P^-1)) from the kernel; ``p_out`` may be
-    None in iterations that cannot end the Gauss-Newton loop."""
+    output rasters (x, 1/sqrt(diag P^-1)) from the kernel (mean None: the
+    state's x is the mean raster -- identity map, x_out's plane); ``p_out`` may
+    be None in iterations that cannot end the Gauss-Newton loop.
+
+    K1's launch features (:func:`analysis`): ``gn_fused=2`` runs iterations 1
+    and 2 in this launch (the first iteration's norm partials to
+    ``partials_first``); ``order`` / ``n_visit`` the visiting order and the
+    per-chunk subset; ``dn_out`` every visited pixel's |x - x0|^2.
+    ``pdiag_rows`` (bit j): store only the analysis precision diagonal entries
+    (P^-1)_jj of these parameters, into ``p_out`` rows tri(j, j) -- the rows a
+    fused forecast with ``PropArgs.pa_pdiag`` reads (the stored-rows policy);
+    0 stores the full covariance."""
     check_np(n_params)
     ref = next(t for t in (x_prev, x_f, x_out) if t is not None)
     N = int(ref.shape[1] if N is None else N)
@@ -553,6 +564,10 @@ def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status
     if prop is not None and (prop.args.ld != ld or prop.args.N < N or prop.device != dev or not prop.fused):
         raise ValueError("fused propagation arguments do not match the gain layout/device")
     _check_vec(status, N, "status", torch.uint8, dev)
+    if gn_fused not in (1, 2):
+        raise ValueError("gn_fused must be 1 or 2")
+    if partials_first is not None and (partials_first.dtype != torch.float64 or partials_first.numel() < grid_for(N)):
+        raise ValueError("partials_first must be float64 with >= grid_for(N) entries")
     a = ext().GainArgs()
     a.N, a.ld, a.n_bands, a.joseph = N, ld, bands.n, int(bool(joseph))
     a.fast_d, a.fast_obs = (bands.fast_d, bands.fast_obs) if fast else (0, 0)
@@ -563,12 +578,20 @@ def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status
     a.bands = bands.ptr
     a.x_prev, a.x_f, a.p_f, a.x_out, a.p_out = map(_ptr, (x_prev, x_f, p_f, x_out, p_out))
     a.status, a.partials = _ptr(status), _ptr(partials)
+    a.gn_fused = int(gn_fused)
+    a.partials_first = _ptr(partials_first) if gn_fused == 2 else 0
     if prop is not None:
         a.prop = _ptr(prop.device_copy())
     if out is not None:
         mean, unc, idx = out
-        plane = mean.shape[1]
+        if unc is None:
+            raise ValueError("out = (mean, unc, idx) needs the uncertainty planes")
+        plane = unc.shape[1]
+        if mean is None and (idx is not None or x_out is None or x_out.shape[1] != plane):
+            raise ValueError("out mean None needs the identity map and x_out of the raster's plane")
         for t, nm in ((mean, "out mean"), (unc, "out unc")):
+            if t is None:
+                continue
             _check_soa(t, n_params, 0, nm, device=dev)
             if t.shape[1] != plane:
                 raise ValueError("out mean / unc planes differ")
@@ -577,8 +600,28 @@ def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status
         elif plane < N:
             raise ValueError("identity output needs plane >= N")
         a.out_mean, a.out_unc, a.out_idx, a.out_plane = _ptr(mean), _ptr(unc), _ptr(idx), plane
-    ext().gain(n_params, a, grid_for(N), _dev(ref), _stream(ref))
-    _set_valid(partials, grid_for(N))
+    if order is not None:
+        _check_vec(order, N, "order", torch.int32, dev)
+        a.order = _ptr(order)
+    nv = N
+    if n_visit is not None:
+        nv = int(n_visit)
+        if order is None or not 0 < nv <= N:
+            raise ValueError(f"n_visit={n_visit} needs an order and 0 < n_visit <= N={N}")
+        if gn_fused != 1:
+            raise ValueError("n_visit: single-iteration launches")
+        a.n_visit = nv
+    if dn_out is not None:
+        _check_vec(dn_out, N, "dn_out", torch.float32, dev)
+        a.dn_out = _ptr(dn_out)
+    if pdiag_rows:
+        if int(pdiag_rows) >> n_params:
+            raise ValueError(f"pdiag_rows has bits past the {n_params} parameters")
+        a.pdiag_rows = int(pdiag_rows)
+    grid = grid_for(nv)
+    ext().gain(n_params, a, grid, _dev(ref), _stream(ref))
+    _set_valid(partials, grid)
+    _set_valid(partials_first if gn_fused == 2 else None, grid)
     return partials
 
 
@@ -885,14 +928,34 @@ def reg_finish(n_params, u, v, z_ext, nbr, x_ref, x_out, gamma, reg_mask, N, par
     return partials
 
 
+def _reset_cov(n_params, reset_cinv):
+    """Packed inverse of the (packed) reset precision C0 when it is SPD, else
+    None (PROP_INFO_APPROX: C0 = 0) -- the constant the K1g fast forecast
+    updates (kf_core.h:gain_forecast)."""
+    if reset_cinv is None:
+        return None
+    from ..utils.blocks import pack_matrix, unpack_blocks
+    C0 = unpack_blocks(np.asarray(reset_cinv, dtype=np.float64).reshape(-1, 1), n_params)[0]
+    try:
+        L = np.linalg.cholesky(C0)
+    except np.linalg.LinAlgError:
+        return None
+    if not np.all(np.isfinite(L)) or np.min(np.diag(L)) <= 1e-12 * max(1.0, np.max(np.abs(C0))):
+        return None
+    return pack_matrix(np.linalg.inv(C0))
+
+
 def prop_args(n_params, spec: dict, x_a, p_a, x_f=None, p_f=None, N=None, status=None, q_pix=None,
-              blend_mean_pix=None, blend_cinv_pix=None, fused=False):
+              blend_mean_pix=None, blend_cinv_pix=None, fused=False, pa_pdiag=False):
     """Validated ``PropArgs`` for :func:`propagate` or, with ``fused=True``, for
     a fused :func:`analysis`.  ``spec`` keys: mode, m, q, prop_mask,
     reset_mean, reset_cinv (packed), blend, quirk_blend, blend_mean,
     blend_cinv (packed).  The fused kernel evaluates one formula (partial
     prior reset, kf_core.h:forecast_partial); PROP_PRIOR and PROP_INFO_APPROX
-    are mapped onto it here."""
+    are mapped onto it here.  Fused arguments also carry C0^-1 for the K1g
+    fast forecast (``cov_fast``) and ``pa_pdiag``: ``p_a``'s propagated
+    diagonal rows hold the analysis precision diagonal (a gain-form analysis
+    under the stored-rows policy)."""
     check_np(n_params)
     if fused:
         if not prop_is_light(spec["mode"], spec.get("blend", False)):
@@ -935,6 +998,11 @@ def prop_args(n_params, spec: dict, x_a, p_a, x_f=None, p_f=None, N=None, status
     a.x_a, a.p_a, a.x_f, a.p_f = map(_ptr, (x_a, p_a, x_f, p_f))
     a.q_pix, a.blend_mean_pix, a.blend_cinv_pix = map(_ptr, (q_pix, blend_mean_pix, blend_cinv_pix))
     a.status = _ptr(status)
+    if fused:
+        a.pa_pdiag = int(bool(pa_pdiag))
+        cov = _reset_cov(n_params, spec.get("reset_cinv"))
+        if cov is not None:      # K1g: the forecast covariance by rank-1 updates of C0^-1
+            a.cov_fast, a.reset_cov = 1, [float(v) for v in cov]
     return PropHandle(a, dev, (x_a, p_a, x_f, p_f, q_pix, blend_mean_pix, blend_cinv_pix, status), fused)
 
 

@@ -114,16 +114,19 @@ def test_chunked_equals_farm_of_engines():
     assert all("chunk_iters" not in r for r in kf2.metrics.records)
 
 
-def test_chunked_fused_forecast_tip_equals_farm():
+@pytest.mark.parametrize("form", ["information", "gain"])
+def test_chunked_fused_forecast_tip_equals_farm(form):
     """JRC-TIP with the LAI propagator (forecast fused into the analysis
-    kernel, GN 1 + 2 in one launch): chunked run == one engine per chunk."""
+    kernel, GN 1 + 2 in one launch): chunked run == one engine per chunk, in
+    the information form (K1) and the gain form (K1g)."""
     mask = np.ones((48, 40), bool)
     mask[30:40, 0:12] = False
 
     def build(m, cfg):
         obs = k.SyntheticBHRObservations(m, n_train=40, device="cpu", stream=False, n_pool=3, seed=5, field_cell=6)
         kf = k.LinearKalman(obs, None, m, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device="cpu",
-                            config=k.EngineConfig(convergence_tolerance=2e-5, max_iterations=6, **cfg))
+                            config=k.EngineConfig(convergence_tolerance=2e-5, max_iterations=6, analysis_form=form,
+                                                  **cfg))
         kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
         return kf
     grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(4)]

@@ -122,6 +122,36 @@ def test_gain_form_equals_information_form():
     assert torch.allclose(a.P, bp.P, rtol=5e-3, atol=1e-1)
 
 
+def test_gain_form_fused_gn_order_and_stored_rows():
+    """K1g with K1's launch features: GN 1 + 2 in one launch equals two
+    launches bit for bit, the observed-first order changes no pixel, and the
+    stored-rows policy (the LAI precision diagonal instead of the covariance,
+    read by the next fused forecast) equals storing the full covariance."""
+    mask, obs, prior, x0, Pinv, Q = _setup(seed=6)
+    grid = _grid(5)
+
+    def run(**cfg):
+        out = k.DeviceOutput(k.TIP_PARAMETERS, keep_history=True)
+        kf = _engine(mask, obs, Q, out=out, analysis_form="gain", **cfg)
+        st = kf.run(grid, x0, None, Pinv)
+        return st, out, [h.get("gn_iterations") for h in kf.history], kf
+
+    base, ob, gb, kfb = run()
+    assert kfb._visit is not None or not kfb.config.observed_first
+    sep, os_, gs, _ = run(fuse_gn=False)
+    assert gb == gs
+    assert torch.equal(base.x, sep.x)
+    for t in ob.history:
+        assert torch.equal(ob.history[t][0], os_.history[t][0]) and torch.equal(ob.history[t][1], os_.history[t][1])
+    nat, _, gn_, _ = run(observed_first=False)
+    assert gn_ == gb and torch.equal(base.x, nat.x)
+    full, of, gf, _ = run(store_precision="always")
+    assert gf == gb
+    assert torch.allclose(base.x, full.x, rtol=1e-5, atol=1e-6)
+    for t in ob.history:
+        assert torch.allclose(ob.history[t][1], of.history[t][1], rtol=1e-4)
+
+
 def test_checkpoint_resume_bit_identical(tmp_path):
     mask, obs, prior, x0, Pinv, Q = _setup(seed=4)
     grid = _grid(6)

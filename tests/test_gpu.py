@@ -505,6 +505,36 @@ def test_fused_output_gpu(cuda, spatial):
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-6)
 
 
+def test_gain_form_equals_information_form_gpu(cuda):
+    """K1g on the matrix cores with K1's launch features (GN 1 + 2 in one
+    launch, observed-first order, the stored precision diagonal read by the
+    Sherman-Morrison fast forecast, fused output) against the information form
+    on the device, and against the host runner of the same gain code."""
+    mask = np.ones((64, 60), bool)
+    mask[5:12, 3:30] = False
+    grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
+
+    def run(dev, **cfg):
+        obs = k.SyntheticBHRObservations(mask, n_train=100, device=dev, stream=False, n_pool=3, field_cell=8, seed=2)
+        out = k.DeviceOutput(k.TIP_PARAMETERS)
+        kf = k.LinearKalman(obs, out, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS, device=dev,
+                            state_propagation=k.propagate_information_filter_LAI, config=k.EngineConfig(**cfg))
+        kf.set_trajectory_model()
+        kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+        st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
+        return st, out, [h.get("gn_iterations") for h in kf.history]
+
+    si, oi, gi = run(cuda)
+    sg, og, gg = run(cuda, analysis_form="gain")
+    sh, oh, gh = run("cpu", analysis_form="gain")
+    assert gi == gg == gh
+    N = si.N
+    assert close(sg.x[:, :N].cpu(), si.x[:, :N].cpu(), 2e-3)
+    assert close(og.unc.cpu(), oi.unc.cpu(), 5e-3)
+    assert close(sg.x[:, :N].cpu(), sh.x[:, :N].cpu(), 1e-3)
+    assert close(og.unc.cpu(), oh.unc.cpu(), 1e-3)
+
+
 def test_masked_strip_geotiff_mean_not_overwritten_by_next_date(cuda, tmp_path):
     """A masked strip's mean planes are owned by the output (not the state's
     x): the next date's fused analysis must not overwrite them while this
