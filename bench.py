@@ -41,12 +41,18 @@ BASELINE_10P = 4600.0
 HEADLINE_METRIC = "pixel-state updates/sec (whole node), 10980^2 S2 tile, 7-param state"
 
 CONFIGS = {
-    "tip7": dict(size=10980, n_train=500, model="JRC-TIP 7-param, 2-band GP-emulator operator, LAI propagator",
-                 baseline=BASELINE_7P),
-    "identity7": dict(size=1024, model="7-param state, identity observation operator (7 bands), "
-                                       "bf16 observations, LAI propagator", baseline=BASELINE_7P),
-    "prosail10": dict(size=10980, n_train=250, model="PROSAIL 10-param, 10-band S2 GP emulators, SAIL prior reset",
-                      baseline=BASELINE_10P),
+    # chunk: the reference drivers' Gauss-Newton exit test per get_chunks tile
+    # (one LinearKalman per chunk: 256^2 in the MCD43/TIP driver, kafka_test_Py36.py:241;
+    # 128^2 in the S2 driver, kafka_test_S2.py:202); --set convergence_chunk=tile
+    # tests over the whole state instead
+    "tip7": dict(size=10980, n_train=500, chunk=256,
+                 model="JRC-TIP 7-param, 2-band GP-emulator operator, LAI propagator, GN to convergence per 256^2 "
+                       "chunk", baseline=BASELINE_7P),
+    "identity7": dict(size=1024, chunk=256, model="7-param state, identity observation operator (7 bands), "
+                                                  "bf16 observations, LAI propagator", baseline=BASELINE_7P),
+    "prosail10": dict(size=10980, n_train=250, chunk=128,
+                      model="PROSAIL 10-param, 10-band S2 GP emulators, SAIL prior reset, GN to convergence per "
+                            "128^2 chunk", baseline=BASELINE_10P),
     # harder 10p-10b problem: T=500, strongly non-linear
     # emulators (Beer-law gap fraction, saturating leaf optics), wider truth.
     # Convergence-driven with the reference driver's semantics: the exit test
@@ -61,8 +67,9 @@ CONFIGS = {
                     model="JRC-TIP 7-param + GMRF spatial prior on TLAI (coupled solve per GN iteration: "
                           "Chebyshev-accelerated block Jacobi to 1e-3, halo exchange)",
                     baseline=BASELINE_7P),
-    "multisensor": dict(size=10980, n_train=250, model="PROSAIL 10-param, S2 13-band + OLCI-like 21-band joint "
-                                                       "GP operator", baseline=BASELINE_10P),
+    "multisensor": dict(size=10980, n_train=250, chunk=128,
+                        model="PROSAIL 10-param, S2 13-band + OLCI-like 21-band joint GP operator, GN to convergence "
+                              "per 128^2 chunk", baseline=BASELINE_10P),
 }
 
 
@@ -107,6 +114,8 @@ def build(cfg_name, a, mask, part, dev, comm):
     def mkcfg(**kw):
         # phase_timing: hipEvent pairs around each phase on the compute stream
         # (device time, resolved after the timed region) for the per-rank record
+        if "chunk" in c and a.band_parallel <= 1:
+            kw.setdefault("convergence_chunk", [c["chunk"], c["chunk"]])
         return k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel,
                               phase_timing=not a.no_telemetry, **{**kw, **over})
     if cfg_name in ("tip7", "spatial"):
@@ -148,10 +157,9 @@ def build(cfg_name, a, mask, part, dev, comm):
                                                seed=seed + 21)
             obs = k.MultiSensorObservations([s2, olci])
         prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
-        gn = {"convergence_chunk": [c["chunk"], c["chunk"]]} if "chunk" in c else {}
         kf = k.LinearKalman(obs, mkout(k.SAIL_PARAMETERS), mask, k.create_prosail_observation_operator,
                             k.SAIL_PARAMETERS, state_propagation=None, prior=prior,
-                            config=mkcfg(**gn), comm=comm, partition=part)
+                            config=mkcfg(), comm=comm, partition=part)
         state = kf.state_from_prior(prior)
     return obs, kf, state, dates
 
@@ -185,6 +193,8 @@ def main():
     ap.add_argument("--resident", action="store_true",
                     help="keep the synthetic observation pool in HBM (compute-only: no per-step H2D; "
                          "the default re-uploads every date from pinned host memory)")
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="multi-rank rehearsal on one GPU: gloo for device tensors (RehearsalComm), not RCCL")
     ap.add_argument("--no-telemetry", action="store_true",
                     help="no per-phase hipEvent timers (the per_rank record then has no phase times)")
     ap.add_argument("--dump-state", default=None, metavar="PREFIX",
@@ -225,6 +235,8 @@ def main():
         log(bp_why)
     if a.band_parallel_force:
         a.set.append("band_parallel_force=true")
+    if a.rehearse_gloo:       # several ranks on one GPU: the gloo harness (parallel/rehearsal.py)
+        from kafka_inferenceengine_amd.parallel.rehearsal import RehearsalComm as Comm
     comm = Comm.from_env(device=a.device, band_parallel=a.band_parallel, timeout_s=EngineConfig().comm_timeout_s)
     if comm.distributed or comm.band is not None:
         dev = comm.device

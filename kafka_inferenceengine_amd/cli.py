@@ -65,6 +65,32 @@ def _file_reference_raster(args):
     return f[0]
 
 
+# The reference drivers' chunking: one LinearKalman per get_chunks tile, so the
+# Gauss-Newton exit test is taken per chunk -- 256^2 for the MCD43 / TIP driver
+# (kafka_test_Py36.py:241), 128^2 for the Sentinel-2 driver (kafka_test_S2.py:202)
+DRIVER_CHUNK = {"bhr": 256, "identity": 256, "s2": 128, "multisensor": 128}
+
+
+def _engine_config(args):
+    """EngineConfig of a run: the command line / YAML, with the reference
+    driver's per-chunk convergence as the default (``--convergence-chunk tile``
+    tests over the whole state instead)."""
+    from .engine.config import EngineConfig
+
+    cfg = EngineConfig.from_args(args)
+    explicit = getattr(args, "convergence_chunk", None) is not None
+    if not explicit and getattr(args, "config_file", None):
+        import yaml
+        with open(args.config_file) as f:
+            explicit = "convergence_chunk" in (yaml.safe_load(f) or {})
+    if (not explicit and cfg.convergence_chunk is None and args.sensor in DRIVER_CHUNK and cfg.spatial_gamma <= 0
+            and cfg.band_parallel <= 1 and (getattr(args, "band_parallel", None) or 1) <= 1):
+        b = DRIVER_CHUNK[args.sensor]
+        cfg.convergence_chunk = [b, b]
+        cfg.validate()
+    return cfg
+
+
 def _build(args, comm):
     import kafka_inferenceengine_amd as k
     from .parallel import StripPartition
@@ -72,7 +98,7 @@ def _build(args, comm):
     mask, info = _mask(args)
     part = StripPartition(mask, comm.rank, comm.world)
     dev = comm.device
-    cfg = k.EngineConfig.from_args(args)
+    cfg = _engine_config(args)
     syn = dict(partition=part, device=dev, stream=True, cloud_fraction=args.cloud, seed=args.seed)
     if args.sensor == "bhr":
         if args.bhr_folder:      # MCD43 kernel-weight rasters (kafka_test.py:156-217)
@@ -152,7 +178,7 @@ def cmd_run(args):
 
     import kafka_inferenceengine_amd as k
 
-    cfg = k.EngineConfig.from_args(args)
+    cfg = _engine_config(args)
     comm = Comm.from_env(device=args.device, band_parallel=getattr(args, "band_parallel", None) or 1,
                          timeout_s=cfg.comm_timeout_s)
     if not comm.distributed and comm.band is None:

@@ -128,6 +128,9 @@ class EngineConfig:
             raise ValueError("bad iteration limits")
         if self.store_precision not in ("auto", "always"):
             raise ValueError("store_precision must be 'auto' or 'always'")
+        if isinstance(self.convergence_chunk, str) and self.convergence_chunk.strip().lower() in ("", "0", "tile",
+                                                                                                 "none", "off"):
+            self.convergence_chunk = None      # the exit test over the engine's whole state
         if self.convergence_chunk is not None:
             cc = self.convergence_chunk
             if isinstance(cc, (int, float)):

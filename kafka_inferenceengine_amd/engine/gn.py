@@ -278,9 +278,17 @@ class GaussNewtonMixin:
                     else:
                         K.analysis(n, table, x_prev, fx, fP, x_new, A_keep, None, status, None, N=N, out=out_now,
                                    a_rows=a_rows, **kw)
+            static = fuse and n_iter == 1 and run.static_conv and not self._norms_needed_now()
             if fuse and n_iter == 1:
                 n_iter = 2
             x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
+            if static:
+                # linear operators: iteration 2 repeats iteration 1 exactly, so every
+                # chunk's norm is 0 and every chunk stops at iteration 2 -- the
+                # decision is known without the per-chunk norms' read-back
+                cc.iters.copy_(cc.active0.to(torch.int32) * 2)
+                self.last_chunk_iters = {2: cc.tested} if cc.tested else {}
+                return x_prev, n_iter, [0.0]
             if n_iter < cfg.min_iterations:
                 n_iter += 1
                 continue

@@ -151,9 +151,11 @@ class Comm:
                 device = torch.device("cpu")
         device = torch.device(device)
         if not dist.is_initialized():
-            # KAFKA_DIST_BACKEND: rehearsal override (e.g. gloo for several ranks on
-            # one GPU); production is RCCL ("nccl") for device tensors
-            backend = backend or os.environ.get("KAFKA_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
+            # RCCL ("nccl") for device tensors, gloo for host tensors; gloo with
+            # device tensors (several ranks rehearsed on one GPU) is the
+            # RehearsalComm subclass (parallel/rehearsal.py), never this class
+            backend = backend or cls.default_backend(device)
+            cls.check_backend(backend, device)
             kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
             if backend == "nccl":
                 kw["device_id"] = device
@@ -173,6 +175,17 @@ class Comm:
         s_idx, b_idx = rank // B, rank % B
         band = cls(b_idx, B, device, bg[s_idx], band_groups[s_idx])
         return cls(s_idx, S, device, sg[b_idx], strip_groups[b_idx], band=band)
+
+    @staticmethod
+    def default_backend(device) -> str:
+        return "nccl" if torch.device(device).type == "cuda" else "gloo"
+
+    @staticmethod
+    def check_backend(backend: str, device):
+        """Production: device tensors go over RCCL only."""
+        if torch.device(device).type == "cuda" and backend != "nccl":
+            raise ValueError(f"backend {backend!r} for device tensors: the production communicator runs RCCL; "
+                             "multi-rank rehearsals on one GPU use parallel.rehearsal.RehearsalComm")
 
     @property
     def distributed(self) -> bool:
@@ -297,20 +310,6 @@ class Comm:
         empty entries are skipped consistently on both sides."""
         if not self.distributed:
             return PendingP2P([])
-        every = [t for ts in (send_up, send_down, recv_up, recv_down) for t in ts if t is not None and t.numel()]
-        if every and every[0].is_cuda and dist.get_backend(self.group) != "nccl":
-            # gloo P2P has no device-stream ordering (one-GPU rehearsals): stage
-            # through host memory so the sends see the finished pack kernels and
-            # the device sees the received rows in stream order (no overlap).
-            h_up = [None if t is None else t.cpu() for t in send_up]
-            h_dn = [None if t is None else t.cpu() for t in send_down]
-            r_up = [None if t is None else torch.empty(t.shape, dtype=t.dtype) for t in recv_up]
-            r_dn = [None if t is None else torch.empty(t.shape, dtype=t.dtype) for t in recv_down]
-            self.exchange_fields_async(h_up, h_dn, r_up, r_dn).wait()
-            for dst, src in zip(list(recv_up) + list(recv_down), r_up + r_dn):
-                if dst is not None and dst.numel():
-                    dst.copy_(src)
-            return PendingP2P([])
         ops = []
         if self.rank > 0:
             peer = self.ranks[self.rank - 1]
@@ -341,9 +340,6 @@ class Comm:
         """C3: gather variable-length pixel blocks [rows, n_i] onto rank 0."""
         if not self.distributed:
             return t
-        if t.is_cuda and dist.get_backend(self.group) != "nccl":  # gloo gather is host-only
-            out = self.gather_to_root(t.cpu(), sizes)
-            return None if out is None else out.to(t.device)
         rows = t.shape[0]
         maxn = max(sizes)
         pad = torch.zeros((rows, maxn), dtype=t.dtype, device=t.device)

@@ -67,8 +67,8 @@ for step in "$@"; do
       # dist:N/BENCH ARGS  N ranks of bench.py on this box's one GPU over gloo (a logic /
       # contention rehearsal, not a scaling point: the ranks share the GPU and the CPUs)
       n=${arg%%/*}; rest=${arg#*/}; port=$((29700 + RANDOM % 200))
-      KAFKA_DIST_BACKEND=gloo timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node=$n \
-        --master-addr=127.0.0.1 --master-port=$port bench.py --gpus $n --device cuda:0 $rest \
+      timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node=$n \
+        --master-addr=127.0.0.1 --master-port=$port bench.py --gpus $n --device cuda:0 --rehearse-gloo $rest \
         > gpurun_out/dist$n.log 2>&1 || { rc=$?; tail -20 gpurun_out/dist$n.log; stop dist $rc; }
       echo "dist$n $(tail -1 gpurun_out/dist$n.log | cut -c1-300)" ;;
     pmc)

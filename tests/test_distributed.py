@@ -261,12 +261,27 @@ def test_comm_collectives_one_rank_process_group():
     assert out["backend"] == "gloo"
 
 
-SCALE_CASES = [("tip7", []), ("spatial", []), ("prosail10", []), ("identity7", []), ("multisensor", []),
-               ("multisensor", ["--band-parallel", "2"])]
+# (config, args of both runs, args of the 8-rank run only).  The defaults run the
+# reference drivers' per-chunk exit test (tip7 / identity7 256^2, prosail10 /
+# multisensor / prosail10_hard 128^2); "chunk64" cuts tip7's 256^2 rehearsal tile
+# into 16 chunks and "tile" runs the tile-global test
+SCALE_CASES = [("tip7", [], []), ("tip7", ["--set", "convergence_chunk=64"], []),
+               ("tip7", ["--set", "convergence_chunk=tile"], []), ("spatial", [], []), ("prosail10", [], []),
+               ("prosail10_hard", [], []), ("identity7", [], []), ("multisensor", [], []),
+               ("multisensor", ["--set", "convergence_chunk=tile"], ["--band-parallel", "2"])]
+
+
+def _case_id(c, both, eight):
+    tag = c
+    if both:
+        tag += "-" + both[-1].split("=")[-1]
+    if eight:
+        tag += "-bp2"
+    return tag
 
 
 def _bench(nproc, config, extra, prefix, size=256):
-    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", KAFKA_DIST_BACKEND="gloo")
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
     args = [os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--steps", "2", "--warmup", "1", "--size",
             str(size), "--n-train", "24", "--device", "cpu", "--config", config, "--dump-state", prefix] + extra
     if nproc > 1:
@@ -283,17 +298,16 @@ def _bench(nproc, config, extra, prefix, size=256):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("config,extra", SCALE_CASES,
-                         ids=[c + ("-bp2" if e else "") for c, e in SCALE_CASES])
-def test_bench_eight_rank_rehearsal(tmp_path, config, extra):
+@pytest.mark.parametrize("config,both,extra", SCALE_CASES, ids=[_case_id(*c) for c in SCALE_CASES])
+def test_bench_eight_rank_rehearsal(tmp_path, config, both, extra):
     """The driver's SCALE run, rehearsed on the CPU: bench.py under
     torch.distributed.run with 8 ranks (gloo) at 256^2 -- one JSON line with 8
     per-rank records, what torch.distributed saw (backend, world size, the
     devices), the same GN iterations on every rank, and a final state equal to
     a one-rank run (reference analogue: the dask farm of
     kafka_test_Py36.py:241-255)."""
-    one = _bench(1, config, [], str(tmp_path / "one"))
-    rec = _bench(8, config, extra, str(tmp_path / "eight"))
+    one = _bench(1, config, both, str(tmp_path / "one"))
+    rec = _bench(8, config, both + extra, str(tmp_path / "eight"))
     assert rec["n_gpus"] == 8 and rec["value"] > 0 and rec["config"]["finite"]
     assert rec["config"]["fallback_frac"] < 0.01
     d = rec["dist"]
@@ -303,6 +317,11 @@ def test_bench_eight_rank_rehearsal(tmp_path, config, extra):
     assert [r["rank"] for r in pr] == list(range(8))
     assert all(r["gn_iterations"] == pr[0]["gn_iterations"] for r in pr)
     assert pr[0]["gn_iterations"] == one["per_rank"][0]["gn_iterations"]
+    # per-chunk convergence: the same chunk decisions at 1 and 8 ranks
+    assert rec["config"]["engine"]["convergence"] == one["config"]["engine"]["convergence"]
+    assert rec["config"].get("chunk_gn_histogram") == one["config"].get("chunk_gn_histogram")
+    if "tile" not in both and not extra and config != "spatial":
+        assert rec["config"]["engine"]["convergence"] == "per chunk" and rec["config"]["chunk_gn_histogram"]
     assert sorted(r["local_rank"] for r in pr) == list(range(8))
     S = 4 if extra else 8
     x8 = np.concatenate([np.load(tmp_path / f"eight.strip{s}.npy") for s in range(S)], axis=1)
