@@ -184,8 +184,8 @@ def main():
     ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
                     help="override an EngineConfig field (A/B runs), e.g. --set gp_split=never")
     ap.add_argument("--kernel-variant", type=int, default=0,
-                    help="analysis kernel variant (ops/kernels.py Variant; A/B of a test-oracle path, e.g. 20 = "
-                         "the persistent tile queue)")
+                    help="analysis kernel variant (ops/kernels.py Variant; A/B of a test-oracle path, e.g. 4 = "
+                         "the f32 VALU record loop)")
     ap.add_argument("--band-parallel", type=int, default=1,
                     help="ranks per band group (strips x band groups; multi-band configs)")
     ap.add_argument("--band-parallel-force", action="store_true",

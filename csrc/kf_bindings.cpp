@@ -123,7 +123,6 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(AnalysisArgs, order, const int32_t*)
       .def_readwrite("n_visit", &AnalysisArgs::n_visit)
       .PTR_FIELD(AnalysisArgs, dn_out, float*)
-      .PTR_FIELD(AnalysisArgs, tile_ctr, int32_t*)
       .def_readwrite("a_rows", &AnalysisArgs::a_rows)
       .def_readwrite("dom_check", &AnalysisArgs::dom_check)
       .ARR_FIELD(AnalysisArgs, dom_lo, float)

@@ -255,8 +255,7 @@ enum AnalysisVariant : int32_t {
   AV_RUNTIME_LAYOUT = 10,    // JRC-TIP bands through the runtime-layout kernel (BAND_LAYOUT_TIP's oracle)
   AV_PER_BAND_OPERAND = 14,  // BAND_LAYOUT_SHARED_X: exponent operand rebuilt per band
   AV_BLOCK_ORDER = 16,       // exponent MFMAs block by block (gpm_il_default's other order)
-  AV_GENERIC_SPEC = 18,      // fused forecast through the generic launch instead of SPEC_PROP
-  AV_TILE_QUEUE = 20         // matrix-core kernels on a persistent grid pulling tiles from per-XCD counters
+  AV_GENERIC_SPEC = 18       // fused forecast through the generic launch instead of SPEC_PROP
 };
 
 struct AnalysisArgs {
@@ -316,10 +315,6 @@ struct AnalysisArgs {
   // engine's store_precision="auto" keeps only what the next forecast reads
   // (the LAI propagator: the TLAI diagonal entry, kf_tools.py:292-314)
   uint64_t a_rows;
-  // dynamic tile scheduling (set by the launcher, kf_device.h analysis_tiles): a
-  // zeroed device counter the waves of a persistent grid pull 64-slot tiles
-  // from; the norm partials are then per tile (partials[tile])
-  int32_t* tile_ctr;
   // GP domain box in state space (ST_OUT_OF_DOMAIN): the intersection over the
   // GP bands of their inputs' training boxes mapped to the state indices they
   // read (ops/kernels.py make_band_table); +-inf where no band constrains j

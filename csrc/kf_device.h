@@ -72,73 +72,6 @@ __device__ __forceinline__ void analysis_partials(const AnalysisArgs& a, double 
   else if (a.partials) block_partial<BS>(acc, a.partials);
 }
 
-// Dynamic tile scheduling of the matrix-core analysis kernels: a persistent
-// grid (occupancy-sized, launch_tiles) whose waves claim 64-slot tiles of the
-// visiting order one at a time from per-XCD counters.  Tile t belongs to
-// group t % 8; the waves of workgroup b claim from group b % 8 first (the
-// workgroups of a launch are dealt to the 8 XCDs round-robin), so the tiles
-// in flight at any moment are a contiguous window of the order -- as on the
-// static grid-stride mapping (round 5: contiguous per-wave runs of a guided
-// schedule scattered ~3000 streams over the whole raster and ran 7 % slower)
-// -- and each counter sees 1/8 of the claims (one counter for all: ~50 M
-// atomics/s device-wide was the bound, 25 % slower at 15 M px).  A wave whose
-// group is exhausted steals from the next groups, so the tail is one tile per
-// wave; the observed-first order puts the cloudy (cheap) tiles last.  The LDS
-// tables are staged once per workgroup.  The norm partials are per tile: the
-// reduction does not depend on which wave ran which tile (bit-reproducible).
-// Claims are vector atomics of lane 0 (the next claim in flight under the
-// current tile), broadcast with readfirstlane.
-constexpr int TILE_GROUPS = 8;        // XCDs of an MI355X
-constexpr int TILE_CTR_STRIDE = 32;   // int32 slots between counters (128 B: own cache lines)
-#if defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__ int tile_claim_raw(int32_t* ctr) {
-  int v = 0;
-  if ((threadIdx.x & 63) == 0) v = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return v;
-}
-
-__device__ __forceinline__ const KF_CONST_AS AnalysisArgs* kargs() {
-  return opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
-}
-
-// PIX(p, act, dn1) -> dn: one visiting slot's analysis (every lane of the wave)
-template <typename PIX>
-__device__ __forceinline__ void analysis_tiles(const AnalysisArgs& a, PIX&& pix) {
-  const int lane = threadIdx.x & 63;
-  const int64_t nv = visit_count(a);
-  const int ntile = (int)((nv + 63) >> 6);
-  const int home = (int)(blockIdx.x % TILE_GROUPS);
-  for (int s = 0; s < TILE_GROUPS; ++s) {
-    const int g = (home + s) % TILE_GROUPS;
-    const int ng = ntile > g ? (ntile - g + TILE_GROUPS - 1) / TILE_GROUPS : 0;   // tiles g, g + 8, ...
-    int j = __builtin_amdgcn_readfirstlane(tile_claim_raw(kargs()->tile_ctr + g * TILE_CTR_STRIDE));
-    while (j < ng) {
-      const int jn = tile_claim_raw(kargs()->tile_ctr + g * TILE_CTR_STRIDE);   // in flight under this tile
-      const int t = g + j * TILE_GROUPS;
-      const int64_t q = ((int64_t)t << 6) + lane;
-      const bool act = q < nv;
-      const int64_t p = visit_px(a.order, act ? q : nv - 1);
-      float dn1;
-      const float dn = pix(p, act, dn1);
-      const KF_CONST_AS AnalysisArgs* ka = kargs();
-      float* dno = ka->dn_out;
-      if (act && dno) KF_PX(dno, 0, p) = dn;
-      double* pt = ka->partials;
-      double* pf = ka->partials_first;
-      if (pt) {
-        const double v = wave_sum(act ? (double)dn : 0.0);
-        if (lane == 0) pt[t] = v;
-      }
-      if (pf) {
-        const double v1 = wave_sum(act ? (double)dn1 : 0.0);
-        if (lane == 0) pf[t] = v1;
-      }
-      j = __builtin_amdgcn_readfirstlane(jn);
-    }
-  }
-}
-#endif
-
 template <int NP, int FD = 0, int FOBS = 0, int UNR = 4, bool FOLD = false>
 __global__ __launch_bounds__(BLOCK) void analysis_kernel(AnalysisArgs a) {
   double acc = 0.0, acc1 = 0.0;
@@ -180,13 +113,6 @@ __global__ __launch_bounds__(BS, MINW) void analysis_mfma_kernel(AnalysisArgs a)
   }
   __syncthreads();
   KF_PHASE(KF_PH_PROLOGUE)
-  if (a.tile_ctr) {
-    analysis_tiles(a, [&](int64_t p, bool act, float& dn1) {
-      return pixel_analysis_mfma<NP, D, FOBS, false, false, LAYOUT, IL, SPEC>(a, p, act, gpm_lds, dn1 KF_PHASE_ARG);
-    });
-    KF_PHASE_KERNEL_END
-    return;
-  }
   double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BS;
@@ -263,14 +189,6 @@ __global__ __launch_bounds__(BLOCK, 2) void analysis_mfma_g_kernel(AnalysisArgs 
   static_assert(BLOCK / 64 == GPM_G_WAVES, "per-wave LDS transpose buffers of gp_mfma_sums_g_xb");
 #if defined(__HIP_DEVICE_COMPILE__)
   KF_PHASE_KERNEL_BEGIN
-  if (a.tile_ctr) {
-    analysis_tiles(a, [&](int64_t p, bool act, float& dn1) {
-      return pixel_analysis_mfma<NP, D, FOBS, true, PF, BAND_LAYOUT_RUNTIME, IL, SPEC>(a, p, act, nullptr,
-                                                                                       dn1 KF_PHASE_ARG);
-    });
-    KF_PHASE_KERNEL_END
-    return;
-  }
   double acc = 0.0, acc1 = 0.0;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
@@ -590,29 +508,17 @@ constexpr bool gpm_il_default() {
   return (NP == 7 && LAYOUT == BAND_LAYOUT_TIP) || NP >= 10;
 }
 
-// Launch of a matrix-core analysis kernel: the static grid-stride mapping
+// Launch of a matrix-core analysis kernel on the static grid-stride mapping
 // (partials per workgroup; the hardware dispatcher hands a finished
-// workgroup's slot to the next one, which balances the cloud-skip load), or
-// with AV_TILE_QUEUE the persistent tile queue (partials per 64-slot tile).
-// Round 5 measured the two within 0.5 % of each other at 10980^2, 3882^2 and
-// for PROSAIL (BENCHMARKS.md), so the default stays static.  *n_part: the
-// partial entries written.
+// workgroup's slot to the next one, which balances the cloud-skip load).
+// Round 5's persistent tile queue with per-XCD counters measured within
+// 0.5 % of it at 10980^2, 3882^2 and for PROSAIL and was removed in round 6.
+// *n_part: the partial entries written.
 template <typename KernT>
 static void launch_tiles(KernT kernel, int bs, size_t lds, const AnalysisArgs& a, int grid, hipStream_t s,
                          int* n_part) {
-  int32_t* ctr = a.variant == AV_TILE_QUEUE ? tile_counter(s) : nullptr;
-  if (!ctr) {
-    *n_part = grid;
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(bs), lds, s, a);
-    return;
-  }
-  AnalysisArgs b = a;
-  b.tile_ctr = ctr;
-  const int64_t tiles = (visit_count(a) + 63) / 64;
-  const int64_t need = (tiles + bs / 64 - 1) / (bs / 64);
-  const int pg = tile_grid(reinterpret_cast<const void*>(kernel), bs, lds);
-  *n_part = (int)tiles;
-  hipLaunchKernelGGL(kernel, dim3((int)(need < pg ? need : pg)), dim3(bs), lds, s, b);
+  *n_part = grid;
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(bs), lds, s, a);
 }
 
 template <int NP, int FD>
@@ -698,8 +604,7 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s, int*
         constexpr bool IL = gpm_il_default<NP, BAND_LAYOUT_RUNTIME>();
         if (a.fast_obs == OBS_DN16 && a.variant == AV_GT_PREFETCH)
           launch_tiles(analysis_mfma_g_kernel<NP, FD, OBS_DN16, true>, BLOCK, 0, a, grid, s, n_part);
-        else if (a.fast_obs == OBS_DN16 && a.prop && !a.reg_v && (a.variant == AV_DEFAULT ||
-                                                                  a.variant == AV_TILE_QUEUE) && IL)
+        else if (a.fast_obs == OBS_DN16 && a.prop && !a.reg_v && a.variant == AV_DEFAULT && IL)
           // fused forecast, no regulariser: the launch's paths fixed at compile time (SPEC_PROP)
           launch_tiles(analysis_mfma_g_kernel<NP, FD, OBS_DN16, false, true, SPEC_PROP>, BLOCK, 0, a, grid, s, n_part);
         else if (a.fast_obs == OBS_DN16 && (a.variant == AV_BLOCK_ORDER) != IL)

@@ -567,40 +567,6 @@ hipError_t dev_analysis(int np, const AnalysisArgs& a, int grid, hipStream_t s, 
   return hipGetLastError();
 }
 
-int32_t* tile_counter(hipStream_t s) {
-  static std::mutex mu;
-  static int32_t* ctr[64] = {};
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  int32_t* c;
-  {
-    std::lock_guard<std::mutex> g(mu);
-    if (dev < 0 || dev >= 64) return nullptr;
-    if (!ctr[dev] && hipMalloc(&ctr[dev], sizeof(int32_t) * TILE_GROUPS * TILE_CTR_STRIDE) != hipSuccess)
-      ctr[dev] = nullptr;
-    c = ctr[dev];
-  }
-  if (c) (void)hipMemsetAsync(c, 0, sizeof(int32_t) * TILE_GROUPS * TILE_CTR_STRIDE, s);
-  return c;
-}
-
-int tile_grid(const void* kernel, int block, size_t lds) {
-  static std::mutex mu;
-  static std::map<std::tuple<int, const void*, int, size_t>, int> cache;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  const auto key = std::make_tuple(dev, kernel, block, lds);
-  std::lock_guard<std::mutex> g(mu);
-  auto it = cache.find(key);
-  if (it != cache.end()) return it->second;
-  int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu < 1)
-    per_cu = 1;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-  const int n = per_cu * cus;
-  cache[key] = n;
-  return n;
-}
 hipError_t dev_gain(int np, const GainArgs& a, int grid, hipStream_t s) {
   KF_NP_SWITCH(np, l_gain, a, grid, s);
   return hipGetLastError();
@@ -651,55 +617,11 @@ hipError_t dev_unpack(int np, const float* x, const float* a, int64_t N, int64_t
   KF_NP_SWITCH(np, l_unpack, x, a, N, ld, idx, mean, unc, plane, grid_for(N, KF_MAX_BLOCKS), s);
   return hipGetLastError();
 }
-// Large partial vectors (one per 64-slot tile: 1.9 M at 120 M px) in two
-// fixed-order levels: contiguous slices of RED_SLICE entries per workgroup
-// (reduce_partials_kernel over each), then one workgroup over the slice sums.
-constexpr int RED_SLICE = RED_BLOCK * 16;
-__global__ __launch_bounds__(RED_BLOCK) void reduce_slices_kernel(const double* partials, int n, double* out) {
-  const int64_t b0 = (int64_t)blockIdx.x * RED_SLICE;
-  const int m = (int)(n - b0 < RED_SLICE ? n - b0 : RED_SLICE);
-  __shared__ double red[RED_BLOCK / 64];
-  double s = 0.0;
-  for (int i = threadIdx.x; i < m; i += RED_BLOCK) s += partials[b0 + i];
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int w = 0; w < RED_BLOCK / 64; ++w) t += red[w];
-    out[blockIdx.x] = t;
-  }
-}
-
+// Fixed-order f64 sum of a launch's norm partials: one workgroup (at most
+// KF_MAX_BLOCKS = 65536 entries, 512 KiB: a few microseconds).  No scratch
+// buffer, so reductions on different streams never share state.
 hipError_t dev_reduce(const double* partials, int n, double* out, hipStream_t s) {
-  if (n <= RED_SLICE) {
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(RED_BLOCK), 0, s, partials, n, out);
-    return hipGetLastError();
-  }
-  static std::mutex mu;
-  static double* tmp[64] = {};
-  static int cap[64] = {};
-  const int nb = (n + RED_SLICE - 1) / RED_SLICE;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (dev < 0 || dev >= 64) return hipErrorInvalidValue;
-  double* t;
-  {
-    std::lock_guard<std::mutex> g(mu);
-    if (cap[dev] < nb) {
-      if (tmp[dev]) (void)hipFree(tmp[dev]);   // a larger vector than any before: once per size class
-      const int c = nb < 4096 ? 4096 : nb;
-      if (hipMalloc(&tmp[dev], sizeof(double) * (size_t)c) != hipSuccess) {
-        tmp[dev] = nullptr;
-        cap[dev] = 0;
-        return hipErrorOutOfMemory;
-      }
-      cap[dev] = c;
-    }
-    t = tmp[dev];
-  }
-  hipLaunchKernelGGL(reduce_slices_kernel, dim3(nb), dim3(RED_BLOCK), 0, s, partials, n, t);
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(RED_BLOCK), 0, s, t, nb, out);
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(RED_BLOCK), 0, s, partials, n, out);
   return hipGetLastError();
 }
 hipError_t dev_gather(int elem_bytes, const void* src, const int64_t* idx, void* dst, int64_t n, int rows,

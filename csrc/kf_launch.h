@@ -23,15 +23,10 @@ int dev_grid(int64_t N);
 void set_max_blocks(int n);
 void set_gp_unroll(int n);
 int get_max_blocks();
-// *n_part: norm partial entries written (workgroups of a grid-stride launch,
-// 64-slot tiles of a tile-queue launch)
+// *n_part: norm partial entries written (workgroups of the grid-stride launch)
 hipError_t dev_analysis(int np, const AnalysisArgs& a, int grid, hipStream_t s, int* n_part);
 hipError_t dev_analysis_np7(const AnalysisArgs& a, int grid, hipStream_t s, int* n_part);
 hipError_t dev_analysis_np10(const AnalysisArgs& a, int grid, hipStream_t s, int* n_part);
-// tile queue of the matrix-core analysis kernels: this device's counter, zeroed
-// on stream s; the persistent grid of a kernel (occupancy x CUs, cached)
-int32_t* tile_counter(hipStream_t s);
-int tile_grid(const void* kernel, int block, size_t lds);
 #ifdef KF_PHASE_CLOCKS
 hipError_t phase_clocks_np7(unsigned long long* out, bool reset);
 hipError_t phase_clocks_np10(unsigned long long* out, bool reset);

@@ -338,9 +338,13 @@ class PhaseEvents {
     }
   }
 
-  // record the start of ``phase`` on ``stream``; returns the token for end()
+  // record the start of ``phase`` on ``stream``; returns the token for end().
+  // The pool belongs to the device current at its first begin(): its events
+  // are created there, and later begins switch to it (hipEventRecord needs the
+  // event's device) and restore the caller's device.
   int begin(int phase, int64_t stream) {
     if (phase < 0) throw std::runtime_error("PhaseEvents: negative phase id");
+    DeviceGuard g(device_);
     int t;
     if (!free_.empty()) {
       t = free_.back();
@@ -362,6 +366,7 @@ class PhaseEvents {
   void end(int token, int64_t stream) {
     if (token < 0 || token >= static_cast<int>(slots_.size()))
       throw std::runtime_error("PhaseEvents: bad token");
+    DeviceGuard g(device_);
     if (hipEventRecord(slots_[token].stop, reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
       throw std::runtime_error("PhaseEvents: hipEventRecord failed");
     done_.push_back(token);
@@ -380,7 +385,16 @@ class PhaseEvents {
       Slot& sl = slots_[done_.front()];
       if (!block && hipEventQuery(sl.stop) != hipSuccess) break;
       float ms = 0.f;
-      if (hipEventElapsedTime(&ms, sl.start, sl.stop) != hipSuccess) ms = 0.f;
+      hipError_t e = hipEventElapsedTime(&ms, sl.start, sl.stop);
+      if (e == hipErrorNotReady) {
+        // a phase recorded on another stream than the newest one need not have
+        // finished when that one has: wait for its own events, then read it
+        py::gil_scoped_release nogil;
+        if (hipEventSynchronize(sl.start) != hipSuccess || hipEventSynchronize(sl.stop) != hipSuccess)
+          throw std::runtime_error("PhaseEvents: hipEventSynchronize failed");
+        e = hipEventElapsedTime(&ms, sl.start, sl.stop);
+      }
+      if (e != hipSuccess) throw std::runtime_error("PhaseEvents: hipEventElapsedTime failed");
       out.emplace_back(sl.phase, ms);
       free_.push_back(done_.front());
       done_.pop_front();
@@ -395,9 +409,24 @@ class PhaseEvents {
     hipEvent_t start = nullptr, stop = nullptr;
     int phase = 0;
   };
+  // switches to the pool's device (fixed by the first use) for one call
+  struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int& dev) {
+      if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+      if (dev < 0) dev = prev;
+      else if (prev != dev && hipSetDevice(dev) != hipSuccess)
+        throw std::runtime_error("PhaseEvents: hipSetDevice failed");
+    }
+    ~DeviceGuard() {
+      int cur = -1;
+      if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+  };
   std::vector<Slot> slots_;
   std::vector<int> free_;
   std::deque<int> done_;
+  int device_ = -1;
 };
 
 }  // namespace

@@ -450,7 +450,10 @@ void write(const std::string& path, const void* data, int nb, uint64_t H, uint64
       if (predictor > 1)
         for (uint64_t r = 0; r < tile; ++r) apply_predictor(&t[r * tile * bps], tile, bps, predictor, tmp);
       const FastDeflate& fd = FastDeflate::get();
-      if (use_fast_deflate()) {
+      // libdeflate has no zlib strategies: a requested Z_RLE / Z_HUFFMAN_ONLY
+      // (--out-fast) always runs zlib, so its speed and ratio do not depend on
+      // which libraries the host has
+      if (use_fast_deflate() && strategy == Z_DEFAULT_STRATEGY) {
         thread_local ThreadCompressor tc;
         void* comp = tc.at(std::min(level, 12));
         if (!comp) throw std::runtime_error("libdeflate_alloc_compressor failed");

@@ -313,7 +313,9 @@ def main(argv=None):
     r.add_argument("--prefix", default=None)
     r.add_argument("--out-level", type=int, default=6, help="DEFLATE level of the output GeoTIFFs (1: fastest)")
     r.add_argument("--out-fast", action="store_true",
-                   help="floating-point predictor + run-length DEFLATE (about 3x faster encoding)")
+                   help="floating-point predictor + run-length DEFLATE (zlib's Z_RLE: about 3x faster encoding "
+                        "than zlib level 6; always zlib, also where libdeflate is present -- writer_stats reports "
+                        "the encoder)")
     r.add_argument("--out-keep", type=int, default=None,
                    help="keep only the newest N timesteps' output files on local disk")
     r.add_argument("--out-gather", action="store_true", help="gather strips to rank 0 and write one raster")

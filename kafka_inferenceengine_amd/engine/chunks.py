@@ -113,7 +113,15 @@ class ChunkConvergence:
     def decide(self, n_iter: int, tol: float, min_iter: int, max_iter: int):
         """Per-chunk norms of the last launch's dn and the exit test; returns
         a pending read-back of (active chunks, largest norm, this rank's
-        active pixels, chunks stopped now)."""
+        active pixels, chunks stopped now).
+
+        The decision is rank-uniform (every rank sums the same gathered
+        partials in rank order) but not rank-count invariant by construction:
+        a chunk cut by a strip boundary sums its pixels in per-rank groups, so
+        its f64 norm can differ in the last bits between 1, 4 and 8 ranks, and a
+        chunk whose norm sits within that rounding of ``tol`` could stop one
+        iteration apart.  The 1 / 4 / 8-rank equality tests
+        (tests/test_chunks.py, the 8-rank bench rehearsal) pin the cases run."""
         from ..parallel.comm import PendingSum
 
         if self.N:

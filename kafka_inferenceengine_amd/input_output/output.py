@@ -187,12 +187,24 @@ class KafkaOutput:
                "raster_bytes": self.bytes_in, "file_bytes": self.bytes_out,
                "ratio": round(self.bytes_in / self.bytes_out, 3) if self.bytes_out else None,
                "slot_wait_s": round(self.slot_wait_s, 6), "d2h_s": round(self.d2h_s, 6),
-               "prune_s": round(self.prune_s, 6)}
+               "prune_s": round(self.prune_s, 6), "deflate_backend": self.deflate_backend()}
         if w is not None:
             out.update({"queue_depth_last": w.depth[-1] if w.depth else 0,
                         "queue_depth_max": max(w.depth) if w.depth else 0,
                         "queue_wait_s": round(w.wait_s, 6), "writer_busy_s": round(w.busy_s, 6)})
         return out
+
+    def deflate_backend(self) -> str | None:
+        """Encoder of the DEFLATE tiles: libdeflate (default strategy, when the
+        host has it) or zlib (always for the rle / huffman strategies)."""
+        if self.compress != "deflate":
+            return None
+        from .tiff import _native
+        E = _native()
+        if E is None or not self.tile:
+            return "zlib (python)"
+        fast = hasattr(E, "tiff_fast_deflate") and bool(E.tiff_fast_deflate())
+        return "libdeflate" if fast and self.strategy in (None, "default") else "zlib"
 
     # ------------------------------------------------------- device path
     def device_targets(self, engine, dev, alias: bool = True):

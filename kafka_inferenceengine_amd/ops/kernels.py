@@ -85,9 +85,9 @@ def grid_for(N: int) -> int:
 
 
 def partials_buffer(N: int, device) -> torch.Tensor:
-    """Norm partials of one launch over N pixels: one f64 per workgroup of a
-    grid-stride kernel or per 64-slot tile of the tile-queue kernels."""
-    return torch.zeros(max(grid_for(N), -(-int(N) // 64)), dtype=torch.float64, device=device)
+    """Norm partials of one launch over N pixels: one f64 per workgroup of the
+    grid-stride kernels."""
+    return torch.zeros(grid_for(N), dtype=torch.float64, device=device)
 
 
 def _set_valid(partials, n):
@@ -148,7 +148,6 @@ class Variant(IntEnum):
     PER_BAND_OPERAND = 14    # BAND_LAYOUT_SHARED_X: exponent operand rebuilt per band
     BLOCK_ORDER = 16         # exponent MFMAs block by block
     GENERIC_SPEC = 18        # fused forecast through the generic launch instead of SPEC_PROP
-    TILE_QUEUE = 20          # matrix-core kernels on a persistent grid pulling tiles from per-XCD counters
 
 
 # analysis variant of launches that pass none (tests switch it to an oracle path;
@@ -439,8 +438,8 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
             raise ValueError(f"a_rows has bits past the {nt} packed rows")
         a.a_rows = int(a_rows)
     grid = grid_for(nv)
-    if partials is not None and partials.numel() < -(-nv // 64):
-        raise ValueError("partials must hold one entry per 64 visited pixels (partials_buffer)")
+    if partials is not None and partials.numel() < grid:
+        raise ValueError("partials must hold one entry per workgroup (partials_buffer)")
     n_part = ext().analysis(n_params, a, grid, _dev(ref), _stream(ref))
     _set_valid(partials, n_part)
     _set_valid(partials_first if gn_fused == 2 else None, n_part)
@@ -1093,7 +1092,7 @@ def unpack(n_params, x, a, mean=None, unc=None, idx=None, N=None):
 
 def reduce_partials(partials: torch.Tensor, out: torch.Tensor | None = None):
     """Fixed-order f64 sum of the partials the last producer wrote (device:
-    one workgroup, or two levels for per-tile vectors)."""
+    one workgroup)."""
     n = min(int(getattr(partials, "_kf_n", partials.numel())), int(partials.numel()))
     if _dev(partials):
         if out is None:

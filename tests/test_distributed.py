@@ -320,7 +320,7 @@ def test_bench_eight_rank_rehearsal(tmp_path, config, both, extra):
     # per-chunk convergence: the same chunk decisions at 1 and 8 ranks
     assert rec["config"]["engine"]["convergence"] == one["config"]["engine"]["convergence"]
     assert rec["config"].get("chunk_gn_histogram") == one["config"].get("chunk_gn_histogram")
-    if "tile" not in both and not extra and config != "spatial":
+    if not any("=tile" in b for b in both) and not extra and config != "spatial":
         assert rec["config"]["engine"]["convergence"] == "per chunk" and rec["config"]["chunk_gn_histogram"]
     assert sorted(r["local_rank"] for r in pr) == list(range(8))
     S = 4 if extra else 8
