@@ -109,7 +109,7 @@ def build(cfg_name, a, mask, part, dev, comm):
         return k.KafkaOutput(params, [0.0, 10.0, 0.0, 0.0, 0.0, -10.0], "EPSG:32630", a.output,
                              prefix=f"r{comm.rank}" if comm.world > 1 else None, level=a.output_level,
                              predictor=3, strategy="rle" if a.output_level else None,
-                             keep_timesteps=a.output_keep)
+                             keep_timesteps=a.output_keep, encoder=a.output_encoder)
 
     def mkcfg(**kw):
         # phase_timing: hipEvent pairs around each phase on the compute stream
@@ -204,6 +204,8 @@ def main():
                     help="write every timestep's mean/unc GeoTIFFs here (KafkaOutput; the timed region ends "
                          "after the writer has drained); default: device rasters only")
     ap.add_argument("--output-level", type=int, default=1, help="DEFLATE level of --output (0: uncompressed)")
+    ap.add_argument("--output-encoder", default="auto", choices=["auto", "device", "host"],
+                    help="DEFLATE tiles of --output encoded on the GPU (auto / device) or on the host thread pool")
     ap.add_argument("--output-keep", type=int, default=2,
                     help="keep only the newest N timesteps' files of --output on disk")
     a = ap.parse_args()
@@ -342,6 +344,7 @@ def main():
         n_w = w1["timesteps_written"] - w0["timesteps_written"]
         ws = kf.output.write_s[w0["timesteps_written"]:]
         mine["output"] = {"dir": a.output, "deflate_level": a.output_level, "timesteps": n_w,
+                          "encoder": w1.get("deflate_backend"),
                           "write_ms_mean": round(1e3 * sum(ws) / max(1, len(ws)), 3),
                           "write_ms_max": round(1e3 * max(ws), 3) if ws else None,
                           "raster_MB_per_date": round((w1["raster_bytes"] - w0["raster_bytes"]) / max(1, n_w) / 1e6, 1),

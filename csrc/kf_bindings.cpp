@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 #include "kf_launch.h"
+#include "kf_deflate.h"
 #include "kf_stream.h"
 
 namespace py = pybind11;
@@ -294,6 +295,33 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
                                      P<float>(mean), P<float>(unc), plane, (hipStream_t)stream), "unpack");
     else check_host(host_unpack(np, P<const float>(x), P<const float>(a), N, ld, P<const int64_t>(idx),
                                 P<float>(mean), P<float>(unc), plane), "unpack");
+  });
+  // GeoTIFF tile encoder (predictor 3 + fixed-Huffman zlib per 256^2 tile)
+  m.attr("DFL_TILE") = DFL_TILE;
+  m.attr("DFL_BOUND") = DFL_BOUND;
+  m.def("deflate_tiles", [](uintptr_t src, int64_t plane_ld, int H, int W, int nplanes, uintptr_t out,
+                            uintptr_t sizes, bool device, uintptr_t stream) {
+    DflArgs a{};
+    a.src = P<const float>(src);
+    a.plane_ld = plane_ld;
+    a.H = H;
+    a.W = W;
+    a.nplanes = nplanes;
+    a.tiles_x = (W + DFL_TILE - 1) / DFL_TILE;
+    a.tiles_y = (H + DFL_TILE - 1) / DFL_TILE;
+    a.out = P<uint8_t>(out);
+    a.sizes = P<uint32_t>(sizes);
+    if ((int64_t)H * W > plane_ld) throw std::runtime_error("deflate_tiles: plane_ld < H * W");
+    if (device) check_hip(dev_deflate_tiles(a, (hipStream_t)stream), "deflate_tiles");
+    else {
+      py::gil_scoped_release nogil;
+      check_host(host_deflate_tiles(a), "deflate_tiles");
+    }
+  });
+  m.def("deflate_pack", [](uintptr_t scratch, uintptr_t sizes, uintptr_t offs, uintptr_t packed, int ntiles,
+                           uintptr_t stream) {
+    check_hip(dev_deflate_pack(P<const uint8_t>(scratch), P<const uint32_t>(sizes), P<const int64_t>(offs),
+                               P<uint8_t>(packed), ntiles, (hipStream_t)stream), "deflate_pack");
   });
   m.def("reduce_partials", [](uintptr_t partials, int n, uintptr_t out, uintptr_t stream) {
     check_hip(dev_reduce(P<const double>(partials), n, P<double>(out), (hipStream_t)stream), "reduce_partials");

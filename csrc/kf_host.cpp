@@ -5,6 +5,7 @@
 #include <math.h>
 #include <string.h>
 #include "kf_launch.h"
+#include "kf_deflate.h"
 #include <algorithm>
 #include <vector>
 
@@ -166,6 +167,59 @@ static int h_unpack(const float* x, const float* a, int64_t N, int64_t ld, const
       if (mean) mean[j * plane + r] = x[j * ld + p];
       if (unc) unc[j * plane + r] = kf_rsqrt(a[tri(NP, j, j) * ld + p]);
     }
+  }
+  return 0;
+}
+
+// GeoTIFF tiles on the host: the same row encoder as dfl_tile_kernel, rows in
+// order into one byte stream per tile (bit-identical streams)
+int host_deflate_tiles(const DflArgs& a) {
+  const int per = a.tiles_x * a.tiles_y, n = a.nplanes * per;
+  if (n <= 0) return -1;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int tile = 0; tile < n; ++tile) {
+    const int plane = tile / per, tt = tile - plane * per;
+    const int ty = tt / a.tiles_x, tx = tt - ty * a.tiles_x;
+    const int x0 = tx * DFL_TILE;
+    const int ncol = a.W - x0 < DFL_TILE ? a.W - x0 : DFL_TILE;
+    uint8_t* o = a.out + (int64_t)tile * DFL_BOUND;
+    int64_t nb = 0;
+    uint64_t acc = 0;
+    int nacc = 0;
+    auto sink = [&](uint32_t bits, int len) {
+      acc |= (uint64_t)bits << nacc;
+      nacc += len;
+      while (nacc >= 8) {
+        o[nb++] = (uint8_t)(acc & 0xFFu);
+        acc >>= 8;
+        nacc -= 8;
+      }
+    };
+    sink(0x78u, 8);
+    sink(0x01u, 8);
+    sink(1u, 1);                 // BFINAL
+    sink(1u, 2);                 // BTYPE 01: fixed Huffman
+    uint64_t t1 = 0, t2 = 0;
+    for (int r = 0; r < DFL_TILE; ++r) {
+      const int64_t y = (int64_t)ty * DFL_TILE + r;
+      const bool rin = y < a.H;
+      const float* rowp = a.src + (int64_t)plane * a.plane_ld + (rin ? y : 0) * a.W + x0;
+      auto row = [&](int c) -> uint32_t {
+        if (!(rin && c < ncol)) return 0u;
+        uint32_t u;
+        memcpy(&u, rowp + c, 4);
+        return u;
+      };
+      uint64_t s1, s2;
+      dfl_encode_row(row, DFL_RAW - (int64_t)r * DFL_ROW, sink, s1, s2);
+      t1 += s1;
+      t2 += s2;
+    }
+    sink(0u, 7);                 // end of block
+    if (nacc) sink(0u, 8 - nacc);
+    const uint32_t adler = dfl_adler(t1, t2, DFL_RAW);
+    for (int k = 3; k >= 0; --k) sink((adler >> (8 * k)) & 0xFFu, 8);
+    a.sizes[tile] = (uint32_t)nb;
   }
   return 0;
 }

@@ -91,4 +91,20 @@ int host_reg_tiled(const RegTileArgs& a);
 int host_reg_rho(const float* vrow, const StripGeo& g, int64_t N, const RegScheduleArgs& a);
 int host_reg_schedule(const RegScheduleArgs& a);
 
+// GeoTIFF tile encoder (kf_deflate.h / kf_deflate.hip): planes [nplanes][plane_ld]
+// of H x W float32 rasters -> one zlib stream per 256 x 256 tile at
+// out + tile * DFL_BOUND, its byte count in sizes[tile] (tiles plane-major,
+// row-major within a plane)
+struct DflArgs {
+  const float* src;
+  int64_t plane_ld;
+  int32_t H, W, nplanes, tiles_x, tiles_y, pad_;
+  uint8_t* out;
+  uint32_t* sizes;
+};
+hipError_t dev_deflate_tiles(const DflArgs& a, hipStream_t s);
+hipError_t dev_deflate_pack(const uint8_t* scratch, const uint32_t* sizes, const int64_t* offs, uint8_t* packed,
+                            int ntiles, hipStream_t s);
+int host_deflate_tiles(const DflArgs& a);
+
 }  // namespace kf

@@ -412,6 +412,11 @@ void write_raw(const std::string& path, const void* data, uint64_t n, int nthrea
   if (sync && ::fsync(f.fd) != 0) throw std::runtime_error("fsync failed: " + path);
 }
 
+void write_chunks(const std::string& path, int nb, uint64_t H, uint64_t W, int bits, int fmt, uint32_t tile,
+                  uint64_t rps, int comp, int predictor, const std::vector<uint64_t>& cnts,
+                  const std::function<const uint8_t*(uint64_t)>& chunk, int nthreads, const std::vector<double>& gt,
+                  int epsg, const std::string& citation, const std::string& nodata, int force_big);
+
 void write(const std::string& path, const void* data, int nb, uint64_t H, uint64_t W, int bits, int fmt,
            uint32_t tile, int level, int nthreads, const std::vector<double>& gt, int epsg,
            const std::string& citation, const std::string& nodata, int force_big, int predictor, int strategy) {
@@ -478,8 +483,23 @@ void write(const std::string& path, const void* data, int nb, uint64_t H, uint64
       enc[i].assign(c.begin(), c.begin() + zs.total_out);
     });
   }
-  std::vector<uint64_t> offs(nchunk), cnts(nchunk);
+  std::vector<uint64_t> cnts(nchunk);
   for (uint64_t i = 0; i < nchunk; ++i) cnts[i] = striped ? strip_bytes(i) : enc[i].size();
+  write_chunks(path, nb, H, W, bits, fmt, striped ? 0u : tile, rps, level > 0 ? 8 : 1, predictor, cnts,
+               [&](uint64_t i) { return striped ? strip_ptr(i) : enc[i].data(); }, nthreads, gt, epsg, citation,
+               nodata, force_big);
+}
+
+// The file of a raster whose chunks (tiles, or strips when tile == 0) are
+// already encoded: header, chunk payloads (parallel pwrite), IFD with the
+// GeoTIFF tags.  comp: TIFF compression tag (1 / 8).
+void write_chunks(const std::string& path, int nb, uint64_t H, uint64_t W, int bits, int fmt, uint32_t tile,
+                  uint64_t rps, int comp, int predictor, const std::vector<uint64_t>& cnts,
+                  const std::function<const uint8_t*(uint64_t)>& chunk, int nthreads, const std::vector<double>& gt,
+                  int epsg, const std::string& citation, const std::string& nodata, int force_big) {
+  const bool striped = tile == 0;
+  const uint64_t nchunk = cnts.size();
+  std::vector<uint64_t> offs(nchunk);
   uint64_t payload = 0;
   for (auto c : cnts) payload += c + (c & 1);
   const bool big = force_big > 0 || (force_big < 0 && payload > 3500000000ull);
@@ -494,7 +514,7 @@ void write(const std::string& path, const void* data, int nb, uint64_t H, uint64
   tags.push_back(mk<uint32_t>(256, 4, {(uint32_t)W}));
   tags.push_back(mk<uint32_t>(257, 4, {(uint32_t)H}));
   tags.push_back(mk<uint16_t>(258, 3, std::vector<uint16_t>(nb, (uint16_t)bits)));
-  tags.push_back(mk<uint16_t>(259, 3, {(uint16_t)(level > 0 ? 8 : 1)}));
+  tags.push_back(mk<uint16_t>(259, 3, {(uint16_t)comp}));
   tags.push_back(mk<uint16_t>(262, 3, {1}));
   tags.push_back(mk<uint16_t>(277, 3, {(uint16_t)nb}));
   tags.push_back(mk<uint16_t>(284, 3, {(uint16_t)(nb > 1 ? 2 : 1)}));
@@ -595,8 +615,7 @@ void write(const std::string& path, const void* data, int nb, uint64_t H, uint64
   f.write_at(h, hdr, 0);
   // chunk payloads in parallel pwrite (disjoint ranges)
   parallel_for((int64_t)nchunk, std::max(1, std::min(nthreads, 8)), [&](int64_t i) {
-    if (striped) f.write_at(strip_ptr((uint64_t)i), cnts[i], offs[i]);
-    else if (!enc[i].empty()) f.write_at(enc[i].data(), enc[i].size(), offs[i]);
+    if (cnts[i]) f.write_at(chunk((uint64_t)i), cnts[i], offs[i]);
   });
   f.write_at(ifdb.data(), ifdb.size(), ifd);
   if (!extra.empty()) f.write_at(extra.data(), extra.size(), ifd + ifd_bytes);
@@ -656,6 +675,20 @@ void bind_tiff(py::module_& m) {
   }, py::arg("path"), py::arg("src"), py::arg("nb"), py::arg("H"), py::arg("W"), py::arg("bits"), py::arg("fmt"),
      py::arg("tile"), py::arg("level"), py::arg("nthreads"), py::arg("gt"), py::arg("epsg"), py::arg("citation"),
      py::arg("nodata"), py::arg("force_big"), py::arg("predictor") = 1, py::arg("strategy") = 0);
+  // tiles already encoded (the device encoder, kf_deflate.hip): data + offsets[i]
+  // holds sizes[i] bytes of tile i (row-major tiles of one band)
+  m.def("tiff_write_tiles", [](const std::string& path, uintptr_t data, uint64_t H, uint64_t W, int bits, int fmt,
+                               uint32_t tile, int comp, int predictor, const std::vector<uint64_t>& offsets,
+                               const std::vector<uint64_t>& sizes, int nthreads, const std::vector<double>& gt,
+                               int epsg, const std::string& citation, const std::string& nodata, int force_big) {
+    const uint64_t n = ((W + tile - 1) / tile) * ((H + tile - 1) / tile);
+    if (offsets.size() != n || sizes.size() != n) throw std::runtime_error("tiff_write_tiles: one offset and size per tile");
+    if (tile == 0 || tile % 16) throw std::runtime_error("tiff_write_tiles: tile edge must be a multiple of 16");
+    py::gil_scoped_release nogil;
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(data);
+    tiff::write_chunks(path, 1, H, W, bits, fmt, tile, 0, comp, predictor, sizes,
+                       [&](uint64_t i) { return base + offsets[i]; }, nthreads, gt, epsg, citation, nodata, force_big);
+  });
 }
 
 }  // namespace kf

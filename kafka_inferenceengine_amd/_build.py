@@ -34,10 +34,10 @@ EXT_PATH = PKG_DIR / f"_kafka_hip{EXT_SUFFIX}"
 CHECKED_EXT_PATH = PKG_DIR / f"_kafka_hip_checked{EXT_SUFFIX}"
 PROF_EXT_PATH = PKG_DIR / f"_kafka_hip_prof{EXT_SUFFIX}"
 
-HEADERS = ["kf_core.h", "kf_launch.h", "kf_stream.h", "kf_device.h", "kf_gp_mfma.h", "kf_tiff.h"]
+HEADERS = ["kf_core.h", "kf_launch.h", "kf_stream.h", "kf_device.h", "kf_gp_mfma.h", "kf_tiff.h", "kf_deflate.h"]
 # device translation units (compiled concurrently: the NP = 7 / 10 analysis
 # instantiations dominate the build)
-HIP_SOURCES = ["kf_kernels.hip", "kf_analysis7.hip", "kf_analysis10.hip", "kf_reg_tiled.hip"]
+HIP_SOURCES = ["kf_kernels.hip", "kf_analysis7.hip", "kf_analysis10.hip", "kf_reg_tiled.hip", "kf_deflate.hip"]
 
 
 def _pybind_includes() -> list[str]:

@@ -159,7 +159,7 @@ def _build(args, comm):
         out = k.KafkaOutput(params, geotransform, projection,
                             args.out, prefix=args.prefix, level=args.out_level, gather=args.out_gather,
                             predictor=3 if args.out_fast else 1, strategy="rle" if args.out_fast else None,
-                            keep_timesteps=args.out_keep)
+                            keep_timesteps=args.out_keep, encoder=args.out_encoder)
     else:
         out = k.DeviceOutput(params)
     kf = k.LinearKalman(obs, out, mask, factory, params, state_propagation=prop,
@@ -316,6 +316,9 @@ def main(argv=None):
                    help="floating-point predictor + run-length DEFLATE (zlib's Z_RLE: about 3x faster encoding "
                         "than zlib level 6; always zlib, also where libdeflate is present -- writer_stats reports "
                         "the encoder)")
+    r.add_argument("--out-encoder", default="auto", choices=["auto", "device", "host"],
+                   help="DEFLATE tiles encoded on the GPU (device: predictor 3 + fixed-Huffman run-length streams, "
+                        "only compressed tiles cross PCIe) or by the host thread pool; auto: device on a GPU")
     r.add_argument("--out-keep", type=int, default=None,
                    help="keep only the newest N timesteps' output files on local disk")
     r.add_argument("--out-gather", action="store_true", help="gather strips to rank 0 and write one raster")

@@ -104,12 +104,25 @@ class KafkaOutput:
     3x faster than level 6 at a similar ratio.
     With ``gather=True`` and several ranks, strips are gathered to rank 0
     (C3, ``Comm.gather_to_root``) and written as one raster; otherwise every
-    rank writes its strip with a per-rank prefix and a shifted geotransform."""
+    rank writes its strip with a per-rank prefix and a shifted geotransform.
+
+    ``encoder``: "device" encodes the DEFLATE tiles on the GPU
+    (``ops.kernels.TileEncoder``, csrc/kf_deflate.hip: predictor 3 and one
+    fixed-Huffman zlib stream per 256 x 256 tile) on the side stream, so only
+    the compressed tiles cross PCIe and the writer thread only writes files;
+    "host" sends the raw planes to the native CPU encoder (``level``,
+    ``strategy``, ``predictor``); "auto" (default): device for GPU planes with
+    DEFLATE output in 256-pixel tiles."""
 
     def __init__(self, parameter_list, geotransform, projection, folder, prefix=None, fmt="GTiff",
                  compress="deflate", asynchronous=True, level: int = 6, tile: int = 256, gather: bool = False,
                  threads: int | None = None, predictor: int = 1, strategy: str | None = None,
-                 keep_timesteps: int | None = None):
+                 keep_timesteps: int | None = None, encoder: str = "auto"):
+        if encoder not in ("auto", "device", "host"):
+            raise ValueError("encoder must be 'auto', 'device' or 'host'")
+        self.encoder = encoder
+        self._enc = None          # ops.kernels.TileEncoder (device encoder)
+        self._eslots = []         # device encoder: ring of 2 (packed device buffer, meta pinned, host pinned, done)
         self.geotransform = geotransform
         self.projection = projection
         self.folder = folder
@@ -166,6 +179,9 @@ class KafkaOutput:
                 self.bytes_in += planes[ii].nbytes
                 self.bytes_out += os.path.getsize(fn)
         self.write_s.append(time.perf_counter() - t0)
+        self._prune(names)
+
+    def _prune(self, names):
         if self.keep_timesteps is not None:
             t1 = time.perf_counter()
             self._by_step.append(names)
@@ -199,6 +215,8 @@ class KafkaOutput:
         host has it) or zlib (always for the rle / huffman strategies)."""
         if self.compress != "deflate":
             return None
+        if self._eslots:
+            return "device (fixed-Huffman run-length zlib streams, kf_deflate.hip)"
         from .tiff import _native
         E = _native()
         if E is None or not self.tile:
@@ -222,6 +240,14 @@ class KafkaOutput:
         self._dev.dump_state(timestep, state, engine)
         self._ship(timestep, engine)
 
+    def _device_encode(self, cuda: bool) -> bool:
+        if self.encoder == "host" or not cuda or self.compress != "deflate":
+            return False
+        ok = self.tile == 256
+        if self.encoder == "device" and not ok:
+            raise ValueError("the device encoder writes 256-pixel tiles")
+        return ok
+
     def _ship(self, timestep, engine):
         """Device planes -> pinned host (async, side stream) -> writer thread."""
         mean_d, unc_d = self._dev.mean, self._dev.unc
@@ -237,6 +263,9 @@ class KafkaOutput:
             mean_d, unc_d = full[:n], full[n:]
             H = sum(rows)
         cuda = mean_d.is_cuda
+        if self._device_encode(cuda):
+            self._ship_encoded(timestep, mean_d, unc_d, n, H, W, gt, pf, release=not self._gathering(engine))
+            return
         if cuda and self._stream is None:
             self._stream = torch.cuda.Stream(mean_d.device)
         # ring of two pinned buffer pairs; a pair is reused once its writer job is done
@@ -274,6 +303,93 @@ class KafkaOutput:
             self._w.submit(job)
         else:
             job()
+
+    def _ship_encoded(self, timestep, mean_d, unc_d, n, H, W, gt, pf, release: bool):
+        """Device encoder: both rasters' tiles encoded and packed into one device
+        buffer on the side stream, their sizes / offsets to pinned host memory;
+        the writer thread then copies exactly the compressed bytes and writes
+        the files (no encode on the host)."""
+        from ..ops.kernels import TileEncoder
+        from ..ops import _ext
+        dev = mean_d.device
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(dev)
+        if self._enc is None:
+            self._enc = TileEncoder()
+        tx, ty = TileEncoder.tiles(H, W)
+        per = tx * ty
+        nt = n * per
+        bound = int(_ext.require_ext().DFL_BOUND)
+        packed, meta_h, host_box, done = self._next_enc_slot(2 * nt * bound, 4 * nt, dev)
+        done.clear()
+        self._stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(self._stream):
+            _, sm, om = self._enc.encode(mean_d, H, W, packed=packed)
+            _, su, ou = self._enc.encode(unc_d, H, W, packed=packed, base=om[-1:] + sm[-1:])
+            meta_h.copy_(torch.cat([sm, om, su, ou]), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+        mean_d.record_stream(self._stream)
+        unc_d.record_stream(self._stream)
+        if release:
+            self._dev.release(ev)
+        wstream = self._wstream = getattr(self, "_wstream", None) or torch.cuda.Stream(dev)
+
+        def job(packed=packed, meta_h=meta_h, host_box=host_box, ev=ev, done=done):
+            try:
+                t0 = time.perf_counter()
+                ev.synchronize()
+                m = meta_h.numpy().reshape(4, nt)
+                total = int(m[3, -1] + m[2, -1])
+                host = host_box[0]
+                if host is None or host.numel() < total:
+                    host = host_box[0] = torch.empty(int(total * 1.25) + 4096, dtype=torch.uint8, pin_memory=True)
+                with torch.cuda.stream(wstream):
+                    host[:total].copy_(packed[:total], non_blocking=True)
+                wstream.synchronize()
+                self.d2h_s += time.perf_counter() - t0
+                self._write_encoded(timestep, host, m, n, per, H, W, gt, pf)
+            finally:
+                done.set()
+
+        if self._w is not None:
+            self._w.submit(job)
+        else:
+            job()
+
+    def _write_encoded(self, timestep, host, meta, n, per, H, W, gt, prefix):
+        from .tiff import write_tiff_tiles
+        t0 = time.perf_counter()
+        names = []
+        sm, om, su, ou = meta
+        for sizes, offs, suffix in ((sm, om, ""), (su, ou, "_unc")):
+            for ii, param in enumerate(self.parameter_list):
+                fn = _fname(self.folder, param, timestep, prefix, suffix)
+                sl = slice(ii * per, (ii + 1) * per)
+                write_tiff_tiles(fn, H, W, host, offs[sl], sizes[sl], gt, self.projection, predictor=3,
+                                 threads=self.threads)
+                self.written.append(fn)
+                names.append(fn)
+                self.bytes_in += H * W * 4
+                self.bytes_out += os.path.getsize(fn)
+        self.write_s.append(time.perf_counter() - t0)
+        self._prune(names)
+
+    def _next_enc_slot(self, packed_bytes, meta_n, dev):
+        if not self._eslots or self._eslots[0][0].numel() < packed_bytes or self._eslots[0][1].numel() != meta_n:
+            self._eslots = []
+            for _ in range(2):
+                ev = threading.Event()
+                ev.set()
+                self._eslots.append((torch.empty(packed_bytes, dtype=torch.uint8, device=dev),
+                                     torch.empty(meta_n, dtype=torch.int64, pin_memory=True), [None], ev))
+            self._eturn = 0
+        slot = self._eslots[self._eturn % 2]
+        self._eturn += 1
+        t0 = time.perf_counter()
+        slot[3].wait()                      # its previous writer job has copied its tiles out
+        self.slot_wait_s += time.perf_counter() - t0
+        return slot
 
     def _next_slot(self, n, cols, cuda):
         if not self._host or self._host[0][0].shape != (n, cols):

@@ -106,6 +106,24 @@ def write_tiff(path, array, geotransform=None, projection: str | None = None, co
     _write_tiff_py(path, a, geotransform, projection, compress, rows_per_strip, bigtiff, nodata)
 
 
+def write_tiff_tiles(path, H: int, W: int, data, offsets, sizes, geotransform=None, projection: str | None = None,
+                     nodata=None, predictor: int = 3, bigtiff: bool | None = None, threads: int | None = None,
+                     tile: int = 256):
+    """A float32 GeoTIFF from tiles already encoded as zlib streams
+    (``ops.kernels.TileEncoder``: tile i's ``sizes[i]`` bytes at ``data`` +
+    ``offsets[i]``, row-major tiles); only the file layout is written here."""
+    E = _native()
+    if E is None or not hasattr(E, "tiff_write_tiles"):
+        raise RuntimeError("write_tiff_tiles needs the native extension")
+    ptr = data.data_ptr() if hasattr(data, "data_ptr") else np.asarray(data).ctypes.data
+    gt = [float(v) for v in geotransform] if geotransform is not None else []
+    big = -1 if bigtiff is None else int(bool(bigtiff))
+    E.tiff_write_tiles(str(path), ptr, int(H), int(W), 32, 3, int(tile), 8, int(predictor),
+                       [int(v) for v in offsets], [int(v) for v in sizes], threads or _threads(), gt,
+                       epsg_of(projection), "" if projection is None else str(projection),
+                       "" if nodata is None else str(nodata), big)
+
+
 def _write_tiff_py(path, array, geotransform=None, projection: str | None = None, compress: str | None = "deflate",
                    rows_per_strip: int = 64, bigtiff: bool | None = None, nodata=None):
     a = np.ascontiguousarray(np.asarray(array))

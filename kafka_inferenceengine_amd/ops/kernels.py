@@ -1071,6 +1071,63 @@ def hessian(n_params, bands: BandTable, x, a, N=None):
     ext().hessian(n_params, bands.ptr, bands.n, _ptr(x), _ptr(a), N, x.shape[1], _dev(x), _stream(x))
 
 
+class TileEncoder:
+    """GeoTIFF tiles encoded on the device (csrc/kf_deflate.h): each 256 x 256
+    tile of each float32 plane becomes one zlib stream (TIFF predictor 3,
+    fixed-Huffman DEFLATE with run-length matches), packed back to back.
+    ``encode(planes, H, W)`` -> (packed uint8, sizes int64, offsets int64), all
+    on the planes' device and queued on the current stream; the scratch and
+    packed buffers are kept for the next call of the same shape.  On the CPU
+    the host runner of the same row encoder produces the same bytes."""
+
+    def __init__(self):
+        self._bufs = {}
+
+    @staticmethod
+    def tiles(H: int, W: int) -> tuple[int, int]:
+        t = int(ext().DFL_TILE)
+        return -(-int(W) // t), -(-int(H) // t)
+
+    def _buf(self, key, n, dtype, device):
+        b = self._bufs.get(key)
+        if b is None or b.numel() < n or b.device != device:
+            b = self._bufs[key] = torch.empty(n, dtype=dtype, device=device)
+        return b[:n]
+
+    def encode(self, planes: torch.Tensor, H: int, W: int, packed: torch.Tensor | None = None, base=None):
+        """``packed``: the output buffer (default: the encoder's own); ``base``:
+        an int64 scalar tensor added to the offsets (several rasters packed
+        into one buffer back to back, device-side: no host read-back)."""
+        if planes.dtype != torch.float32 or planes.dim() != 2 or planes.stride(1) != 1:
+            raise ValueError("planes: [n, ld] float32 with unit column stride")
+        n, ld = planes.shape
+        if H * W > ld:
+            raise ValueError(f"plane of {ld} values holds no {H} x {W} raster")
+        tx, ty = self.tiles(H, W)
+        nt = n * tx * ty
+        bound = int(ext().DFL_BOUND)
+        dev = planes.device
+        scratch = self._buf("scratch", nt * bound, torch.uint8, dev)
+        sizes = self._buf("sizes", nt, torch.int32, dev)        # uint32 byte counts (< 2^31)
+        ext().deflate_tiles(_ptr(planes), planes.stride(0), int(H), int(W), int(n), _ptr(scratch), _ptr(sizes),
+                            _dev(planes), _stream(planes))
+        s64 = sizes.to(torch.int64)
+        offs = torch.cumsum(s64, 0) - s64
+        if base is not None:
+            offs += base
+        if packed is None:
+            packed = self._buf("packed", nt * bound, torch.uint8, dev)
+        if not _dev(planes):
+            sz, of = s64.numpy(), offs.numpy()
+            src = scratch.numpy().reshape(nt, bound)
+            dst = packed.numpy()
+            for i in range(nt):
+                dst[of[i]:of[i] + sz[i]] = src[i, :sz[i]]
+            return packed, s64, offs
+        ext().deflate_pack(_ptr(scratch), _ptr(sizes), _ptr(offs), _ptr(packed), nt, _stream(planes))
+        return packed, s64, offs
+
+
 def unpack(n_params, x, a, mean=None, unc=None, idx=None, N=None):
     """Scatter mean and 1/sqrt(diag(P^-1)) onto raster planes [n_p, H*W]."""
     check_np(n_params)
