@@ -97,7 +97,8 @@ class ChunkConvergence:
         self.active0 = torch.from_numpy((counts > 0).astype(np.uint8)).to(self.device)
         self.active = self.active0.clone()
         self.newly = torch.zeros(self.nc, dtype=torch.uint8, device=self.device)
-        self.iters = torch.zeros(self.nc, dtype=torch.int32, device=self.device)
+        self._iters = torch.zeros(self.nc, dtype=torch.int32, device=self.device)
+        self._static = None   # set_static(): every tested chunk stopped at this iteration (filled lazily)
         self.part = torch.zeros(self.nc, dtype=torch.float64, device=self.device)
         self.info = torch.zeros(4, dtype=torch.float64, device=self.device)
         self.dn = torch.zeros(max(N, 1), dtype=torch.float32, device=self.device)
@@ -105,10 +106,26 @@ class ChunkConvergence:
         self.scratch = K.chunk_compact_scratch(max(N, 1), self.device)
         self.tested = int((counts > 0).sum())   # chunks with active pixels (all ranks)
 
+    @property
+    def iters(self) -> torch.Tensor:
+        """Gauss-Newton iterations of every chunk on the last date (0: untested)."""
+        if self._static is not None:
+            self._iters.copy_(self.active0.to(torch.int32) * self._static)
+            self._static = None
+        return self._iters
+
     def begin(self):
         """A new date: every chunk with active pixels iterates."""
+        self._static = None
         self.active.copy_(self.active0)
-        self.iters.zero_()
+        self._iters.zero_()
+
+    def set_static(self, n_iter: int) -> dict:
+        """A date whose every chunk stops at ``n_iter`` by construction (linear
+        operators: iteration 2 repeats iteration 1 exactly): no device work,
+        the per-chunk counts are filled in only if read.  Returns the histogram."""
+        self._static = int(n_iter)
+        return {int(n_iter): self.tested} if self.tested else {}
 
     def decide(self, n_iter: int, tol: float, min_iter: int, max_iter: int):
         """Per-chunk norms of the last launch's dn and the exit test; returns
@@ -128,7 +145,7 @@ class ChunkConvergence:
             K.chunk_partials(self.dn, self.seg_start, self.seg_len, self.lc_ptr, self.lc_gid, self.active, self.part)
         part_all = self.comm.all_gather_vec(self.part)
         K.chunk_decide(part_all, self.comm.world, self.len_x, self.local_count, tol, n_iter, min_iter, max_iter,
-                       self.active, self.newly, self.iters, self.info)
+                       self.active, self.newly, self._iters, self.info)
         return PendingSum(self.info, 1, 4)
 
     def compact(self, order_in, n_in: int, n_out: int, x_src, x_dst):

@@ -250,10 +250,15 @@ class GaussNewtonMixin:
         x_prev, x_new, P_out, status, order, out_t = run.x_prev, run.x_new, run.P_out, run.status, run.order, run.out_t
         h0_outs, a_rows, gain = run.h0_outs, run.a_rows, run.gain
         cc = self._chunk_state()
-        cc.begin()
         fx, fP = (None, None) if prop is not None else (fc.x, fc.P)
         fuse = (cfg.fuse_gn and not precomp and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
                 and not (prop is None and fc is None))
+        # linear operators: iteration 2 repeats iteration 1 exactly, so every
+        # chunk's norm is 0 and every chunk stops at iteration 2 -- the decision
+        # is known without the per-chunk norms' read-back
+        static = fuse and run.static_conv and not self._norms_needed_now()
+        if not static:
+            cc.begin()
         n_iter, n_visit, vis, full = 1, N, order, True
         norms = []
         while True:
@@ -262,7 +267,7 @@ class GaussNewtonMixin:
             if precomp:
                 pre = self._precompute_host(specs, dbs, x_prev)
                 table = build_table(specs, dbs, n, self._cache, self.device, h0_outs, pre)
-            kw = dict(prop=prop, order=vis, dn_out=cc.dn)
+            kw = dict(prop=prop, order=vis, dn_out=None if static else cc.dn)
             if not full:
                 kw["n_visit"] = n_visit
             with self.timer.phase("analysis"):
@@ -278,16 +283,11 @@ class GaussNewtonMixin:
                     else:
                         K.analysis(n, table, x_prev, fx, fP, x_new, A_keep, None, status, None, N=N, out=out_now,
                                    a_rows=a_rows, **kw)
-            static = fuse and n_iter == 1 and run.static_conv and not self._norms_needed_now()
             if fuse and n_iter == 1:
                 n_iter = 2
             x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
             if static:
-                # linear operators: iteration 2 repeats iteration 1 exactly, so every
-                # chunk's norm is 0 and every chunk stops at iteration 2 -- the
-                # decision is known without the per-chunk norms' read-back
-                cc.iters.copy_(cc.active0.to(torch.int32) * 2)
-                self.last_chunk_iters = {2: cc.tested} if cc.tested else {}
+                self.last_chunk_iters = cc.set_static(n_iter)
                 return x_prev, n_iter, [0.0]
             if n_iter < cfg.min_iterations:
                 n_iter += 1

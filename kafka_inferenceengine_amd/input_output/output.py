@@ -320,7 +320,11 @@ class KafkaOutput:
         per = tx * ty
         nt = n * per
         bound = int(_ext.require_ext().DFL_BOUND)
-        packed, meta_h, host_box, done = self._next_enc_slot(2 * nt * bound, 4 * nt, dev)
+        # pinned host bytes for the compressed tiles: allocated with the slot (a
+        # multi-GB pinned allocation in the writer thread would stall a timed
+        # date), sized for the raw planes plus the fixed-Huffman worst case
+        host_bytes = int(2 * n * H * W * 4 * 1.13) + 2 * nt * 64 + (1 << 20)
+        packed, meta_h, host_box, done = self._next_enc_slot(2 * nt * bound, 4 * nt, dev, host_bytes)
         done.clear()
         self._stream.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(self._stream):
@@ -375,14 +379,17 @@ class KafkaOutput:
         self.write_s.append(time.perf_counter() - t0)
         self._prune(names)
 
-    def _next_enc_slot(self, packed_bytes, meta_n, dev):
+    def _next_enc_slot(self, packed_bytes, meta_n, dev, host_bytes):
         if not self._eslots or self._eslots[0][0].numel() < packed_bytes or self._eslots[0][1].numel() != meta_n:
+            for sl in self._eslots:
+                sl[3].wait()                # a writer job still reading a slot being replaced
             self._eslots = []
             for _ in range(2):
                 ev = threading.Event()
                 ev.set()
                 self._eslots.append((torch.empty(packed_bytes, dtype=torch.uint8, device=dev),
-                                     torch.empty(meta_n, dtype=torch.int64, pin_memory=True), [None], ev))
+                                     torch.empty(meta_n, dtype=torch.int64, pin_memory=True),
+                                     [torch.empty(host_bytes, dtype=torch.uint8, pin_memory=True)], ev))
             self._eturn = 0
         slot = self._eslots[self._eturn % 2]
         self._eturn += 1

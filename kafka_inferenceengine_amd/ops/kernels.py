@@ -48,6 +48,25 @@ def current_raw_stream(device: torch.device) -> int:
     return int(torch.cuda.current_stream(device).cuda_stream)
 
 
+def _sig(t):
+    """Identity of an operand for the launch memos: address, shape, strides, dtype, device."""
+    return None if t is None else (t.data_ptr(), tuple(t.shape), t.stride(), t.dtype, t.device)
+
+
+# validated analysis argument blocks by operand identity (analysis(): launch memo)
+_ANALYSIS_MEMO: dict = {}
+
+
+def _table_key(bands) -> tuple:
+    """What an argument block takes from a band table (computed once per table)."""
+    k = bands.__dict__.get("_memo_key")
+    if k is None:
+        dom = None if bands.dom is None else (tuple(bands.dom[0]), tuple(bands.dom[1]))
+        k = bands.__dict__["_memo_key"] = (bands.ptr, bands.n, bands.fast_d, bands.fast_obs, bands.gpm_frags,
+                                           bool(bands.gpm_global), bands.layout, dom)
+    return k
+
+
 def _stream(t: torch.Tensor) -> int:
     return current_raw_stream(t.device) if _dev(t) else 0
 
@@ -316,9 +335,31 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     ``dn_out`` (float32 [N]): each visited pixel's |x - x0|^2 of the launch's
     last iteration, at its pixel index (per-chunk convergence norms).
     ``a_rows``: bit mask of the packed precision rows stored to ``a_out``
-    (None / 0: every row; EngineConfig.store_precision)."""
-    check_np(n_params)
+    (None / 0: every row; EngineConfig.store_precision).
+
+    Launch memo: the engine's steady state repeats the same operands date
+    after date (buffers alternate, arguments are memoised upstream), so a call
+    whose tensors (address, shape, stride, dtype) and options equal an earlier
+    validated one reuses its argument block: no re-validation and none of the
+    ~50 per-field writes into the native struct on the per-date host path."""
     ref = next(t for t in (x_prev, x_f, x_out, a_out) if t is not None)
+    key = None
+    if reg is None:
+        key = (n_params, _table_key(bands), N, bool(solve), bool(fast),
+               DEFAULT_VARIANT if variant is None else variant, gn_fused, n_visit, a_rows,
+               None if prop is None else (prop.device_copy().data_ptr(), prop.args.ld, prop.args.N, prop.fused,
+                                          prop.device),
+               _sig(x_prev), _sig(x_f), _sig(pf_inv), _sig(x_out), _sig(a_out), _sig(b_out), _sig(status),
+               _sig(partials), _sig(a_in), _sig(b_in), _sig(x0_out), _sig(partials_first), _sig(order), _sig(dn_out),
+               None if out is None else (_sig(out[0]), _sig(out[1]), _sig(out[2])))
+        hit = _ANALYSIS_MEMO.get(key)
+        if hit is not None:
+            a, grid = hit
+            n_part = ext().analysis(n_params, a, grid, _dev(ref), _stream(ref))
+            _set_valid(partials, n_part)
+            _set_valid(partials_first if gn_fused == 2 else None, n_part)
+            return partials
+    check_np(n_params)
     N = int(ref.shape[1] if N is None else N)
     dev = ref.device
     nt = ntri(n_params)
@@ -441,6 +482,10 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     if partials is not None and partials.numel() < grid:
         raise ValueError("partials must hold one entry per workgroup (partials_buffer)")
     n_part = ext().analysis(n_params, a, grid, _dev(ref), _stream(ref))
+    if key is not None:
+        if len(_ANALYSIS_MEMO) >= 64:
+            _ANALYSIS_MEMO.clear()
+        _ANALYSIS_MEMO[key] = (a, grid)
     _set_valid(partials, n_part)
     _set_valid(partials_first if gn_fused == 2 else None, n_part)
     return partials
