@@ -321,6 +321,7 @@ def main():
         torch.cuda.synchronize()
     t_local = time.perf_counter() - t_start
     elapsed = comm.max_float(t_local)
+    kf.resolve_pending()      # deferred read-backs (lazy norms, per-chunk histograms) of the timed dates
     for m in msgs:
         log(m)
     # per-rank telemetry of the timed steps (device time per phase from the

@@ -163,7 +163,42 @@ class ChunkConvergence:
 
     def histogram(self) -> dict:
         """{Gauss-Newton iterations: chunks} of the date (every rank's chunks)."""
-        it = self.iters.cpu().numpy()
-        it = it[self.counts > 0]
-        vals, cnt = np.unique(it, return_counts=True)
+        return self._hist(self.iters.cpu().numpy())
+
+    def _hist(self, it) -> dict:
+        vals, cnt = np.unique(it[self.counts > 0], return_counts=True)
         return {int(v): int(c) for v, c in zip(vals, cnt)}
+
+    def histogram_async(self, on_resolve=None) -> dict:
+        """The date's histogram without a host wait: the per-chunk counts go to
+        pinned memory in stream order and the returned dict is filled in place
+        by :meth:`resolve` (the next date, or the run's end), so the host does
+        not drain the stream between dates.  ``on_resolve(hist)`` runs then."""
+        if self._static is not None or self.device.type != "cuda":
+            h = self.set_static(self._static) if self._static is not None else self.histogram()
+            if on_resolve is not None:
+                on_resolve(h)
+            return h
+        if not hasattr(self, "_pinned"):
+            self._pinned = [torch.empty(self.nc, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+            self._pin_turn = 0
+            self._pending = []
+        if len(self._pending) >= 2:
+            self.resolve()
+        buf = self._pinned[self._pin_turn % 2]
+        self._pin_turn += 1
+        buf.copy_(self._iters, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        out = {}
+        self._pending.append((out, buf, ev, on_resolve))
+        return out
+
+    def resolve(self):
+        """Fill the histograms :meth:`histogram_async` handed out."""
+        for out, buf, ev, cb in getattr(self, "_pending", []):
+            ev.synchronize()
+            out.update(self._hist(buf.numpy()))
+            if cb is not None:
+                cb(out)
+        self._pending = []

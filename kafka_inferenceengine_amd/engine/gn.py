@@ -77,6 +77,13 @@ class GaussNewtonMixin:
         the deferred norms resolve."""
         return bool(self.metrics.enabled)
 
+    def resolve_pending(self):
+        """Every deferred read-back of the dates run so far: the norms of
+        statically converged dates and the per-chunk iteration histograms."""
+        self._resolve_lazy_norms()
+        if self._chunks is not None:
+            self._chunks.resolve()
+
     def _resolve_lazy_norms(self):
         """Fill in the deferred norms of statically converged dates (linear
         operators): iteration 1's norm, and a check that iteration 2's is 0."""
@@ -250,6 +257,7 @@ class GaussNewtonMixin:
         x_prev, x_new, P_out, status, order, out_t = run.x_prev, run.x_new, run.P_out, run.status, run.order, run.out_t
         h0_outs, a_rows, gain = run.h0_outs, run.a_rows, run.gain
         cc = self._chunk_state()
+        cc.resolve()            # the previous dates' histograms (their read-backs finished long ago)
         fx, fP = (None, None) if prop is not None else (fc.x, fc.P)
         fuse = (cfg.fuse_gn and not precomp and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
                 and not (prop is None and fc is None))
@@ -310,7 +318,12 @@ class GaussNewtonMixin:
                 vis = cc.compact(vis, n_visit if N else 0, px, x_prev, x_new)
             n_visit, full = px, False
             n_iter += 1
-        self.last_chunk_iters = cc.histogram()
-        if max(self.last_chunk_iters or {0: 0}) > cfg.max_iterations:
-            LOG.warning("Bailing out after 25 iterations!!!!!!")
+        def bail(hist, max_it=cfg.max_iterations):
+            if max(hist or {0: 0}) > max_it:
+                LOG.warning("Bailing out after 25 iterations!!!!!!")
+        # per-date metrics serialise the record now; otherwise the histogram is
+        # read back without draining the stream (filled in by the next date)
+        self.last_chunk_iters = cc.histogram() if self._norms_needed_now() else cc.histogram_async(bail)
+        if self._norms_needed_now():
+            bail(self.last_chunk_iters)
         return x_prev, n_iter, norms

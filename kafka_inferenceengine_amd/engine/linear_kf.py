@@ -296,7 +296,7 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         if ckpt is not None:
             with self.timer.phase("checkpoint"):
                 ckpt.finish()
-        self._resolve_lazy_norms()
+        self.resolve_pending()
         self.final_state = analysis
         if self.metrics.enabled:
             self.metrics_summary()

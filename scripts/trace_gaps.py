@@ -5,7 +5,7 @@ import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-ana = [r for r in rows if "analysis_kernel" in r["Kernel_Name"]][-K:]
+ana = [r for r in rows if "analysis" in r["Kernel_Name"] and "_kernel" in r["Kernel_Name"]][-K:]
 t0, t1 = int(ana[0]["Start_Timestamp"]), int(ana[-1]["End_Timestamp"])
 sel = [r for r in rows if t0 <= int(r["Start_Timestamp"]) <= t1]
 busy_end, idle = t0, 0
