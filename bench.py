@@ -197,6 +197,9 @@ def main():
                     help="multi-rank rehearsal on one GPU: gloo for device tensors (RehearsalComm), not RCCL")
     ap.add_argument("--no-telemetry", action="store_true",
                     help="no per-phase hipEvent timers (the per_rank record then has no phase times)")
+    ap.add_argument("--telemetry", default="auto", choices=["auto", "on", "off"],
+                    help="per-phase hipEvent timers in the timed steps: auto = on unless a warm-up step takes "
+                         "under 2 ms (their event records would then be a visible share of the step)")
     ap.add_argument("--dump-state", default=None, metavar="PREFIX",
                     help="after the timed region, write each strip's final state x [n_p, N] to "
                          "PREFIX.strip<r>.npy (band slot 0 only; rehearsal checks against one rank)")
@@ -278,9 +281,15 @@ def main():
     gc.freeze()
     prof = None
     first = True
+    warm_ms = None          # fastest warm-up step after the first (telemetry auto)
+    telemetry = "off" if a.no_telemetry else "on"
     msgs = []   # per-step lines of the timed steps are printed after the timed region
     for i, (t, loc, is_first) in enumerate(steps[:a.warmup + a.steps]):
         if i == a.warmup:
+            if a.telemetry == "off" or (a.telemetry == "auto" and warm_ms is not None
+                                        and comm.max_float(warm_ms) < 2.0):
+                kf.timer.enabled = False      # sub-2 ms steps: no per-phase event records
+                telemetry = "off"
             comm.barrier()
             if dev.type == "cuda":
                 torch.cuda.synchronize()
@@ -303,7 +312,10 @@ def main():
         first = False
         if dev.type == "cuda" and i == a.warmup - 1:
             torch.cuda.synchronize()
-        msgs.append(f"step {i}{' (warmup)' if i < a.warmup else ''} {(time.perf_counter() - t0) * 1e3:.1f} ms "
+        step_ms = (time.perf_counter() - t0) * 1e3
+        if i < a.warmup and i > 0:
+            warm_ms = step_ms if warm_ms is None else min(warm_ms, step_ms)
+        msgs.append(f"step {i}{' (warmup)' if i < a.warmup else ''} {step_ms:.1f} ms "
                     f"gn_iters={kf.history[-1].get('gn_iterations')}")
         if i < a.warmup:
             for m in msgs:
@@ -429,7 +441,8 @@ def main():
                                    "min_iterations": ec.min_iterations, "max_iterations": ec.max_iterations,
                                    "convergence": "per chunk" if ec.convergence_chunk else "tile",
                                    "store_precision": ec.store_precision, "observed_first": ec.observed_first,
-                                   "fuse_gn": ec.fuse_gn, "analysis_form": ec.analysis_form}
+                                   "fuse_gn": ec.fuse_gn, "analysis_form": ec.analysis_form,
+                                   "phase_telemetry": telemetry}
         if chunk_hist:
             rec["config"]["convergence_chunk"] = kf.config.convergence_chunk
             rec["config"]["chunk_gn_histogram"] = {str(i): chunk_hist[i] for i in sorted(chunk_hist)}
