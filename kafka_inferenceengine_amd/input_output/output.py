@@ -122,6 +122,7 @@ class KafkaOutput:
             raise ValueError("encoder must be 'auto', 'device' or 'host'")
         self.encoder = encoder
         self._enc = None          # ops.kernels.TileEncoder (device encoder)
+        self._copier = None       # device encoder: the thread bringing compressed tiles to pinned memory
         self._eslots = []         # device encoder: ring of 2 (packed device buffer, meta pinned, host pinned, done)
         self.geotransform = geotransform
         self.projection = projection
@@ -339,11 +340,21 @@ class KafkaOutput:
             self._dev.release(ev)
         wstream = self._wstream = getattr(self, "_wstream", None) or torch.cuda.Stream(dev)
 
-        def job(packed=packed, meta_h=meta_h, host_box=host_box, ev=ev, done=done):
+        # two stages on two threads: the copier brings date t + 1's compressed
+        # tiles to pinned memory while the writer writes date t's files (the
+        # slot -- device packed buffer and pinned bytes -- is released after the
+        # write; the ring of two keeps the stages one date apart)
+        def write(host, m, done=done):
+            try:
+                self._write_encoded(timestep, host, m, n, per, H, W, gt, pf)
+            finally:
+                done.set()
+
+        def copy(packed=packed, meta_h=meta_h, host_box=host_box, ev=ev, done=done):
             try:
                 t0 = time.perf_counter()
                 ev.synchronize()
-                m = meta_h.numpy().reshape(4, nt)
+                m = meta_h.numpy().reshape(4, nt).copy()
                 total = int(m[3, -1] + m[2, -1])
                 host = host_box[0]
                 if host is None or host.numel() < total:
@@ -352,14 +363,20 @@ class KafkaOutput:
                     host[:total].copy_(packed[:total], non_blocking=True)
                 wstream.synchronize()
                 self.d2h_s += time.perf_counter() - t0
-                self._write_encoded(timestep, host, m, n, per, H, W, gt, pf)
-            finally:
+            except BaseException:
                 done.set()
+                raise
+            if self._w is not None:
+                self._w.submit(lambda: write(host, m))
+            else:
+                write(host, m)
 
         if self._w is not None:
-            self._w.submit(job)
+            if self._copier is None:
+                self._copier = _Writer()
+            self._copier.submit(copy)
         else:
-            job()
+            copy()
 
     def _write_encoded(self, timestep, host, meta, n, per, H, W, gt, prefix):
         from .tiff import write_tiff_tiles
@@ -427,6 +444,8 @@ class KafkaOutput:
         self._write_all(timestep, mean, unc, self.geotransform, self.prefix)
 
     def flush(self):
+        if self._copier is not None:
+            self._copier.flush()       # its jobs hand their writes to the writer thread
         if self._w is not None:
             self._w.flush()
 
