@@ -114,17 +114,27 @@ class ChunkConvergence:
             self._static = None
         return self._iters
 
+    @property
+    def ready(self) -> bool:
+        """begin() was queued after the last date (the next date may start)."""
+        return getattr(self, "_ready", False)
+
     def begin(self):
-        """A new date: every chunk with active pixels iterates."""
-        self._static = None
+        """A new date: every chunk with active pixels iterates.  (The per-chunk
+        iteration counts need no reset: every chunk that iterates stops on some
+        iteration, bailing out past max_iterations at the latest, and chunk_decide
+        records it then; chunks without pixels keep 0.)"""
+        if self._static is not None:
+            self.iters        # a static date's counts (read before they would be overwritten)
         self.active.copy_(self.active0)
-        self._iters.zero_()
+        self._ready = True
 
     def set_static(self, n_iter: int) -> dict:
         """A date whose every chunk stops at ``n_iter`` by construction (linear
         operators: iteration 2 repeats iteration 1 exactly): no device work,
         the per-chunk counts are filled in only if read.  Returns the histogram."""
         self._static = int(n_iter)
+        self._ready = False
         return {int(n_iter): self.tested} if self.tested else {}
 
     def decide(self, n_iter: int, tol: float, min_iter: int, max_iter: int):
@@ -141,6 +151,7 @@ class ChunkConvergence:
         (tests/test_chunks.py, the 8-rank bench rehearsal) pin the cases run."""
         from ..parallel.comm import PendingSum
 
+        self._ready = False
         if self.N:
             K.chunk_partials(self.dn, self.seg_start, self.seg_len, self.lc_ptr, self.lc_gid, self.active, self.part)
         part_all = self.comm.all_gather_vec(self.part)

@@ -257,7 +257,6 @@ class GaussNewtonMixin:
         x_prev, x_new, P_out, status, order, out_t = run.x_prev, run.x_new, run.P_out, run.status, run.order, run.out_t
         h0_outs, a_rows, gain = run.h0_outs, run.a_rows, run.gain
         cc = self._chunk_state()
-        cc.resolve()            # the previous dates' histograms (their read-backs finished long ago)
         fx, fP = (None, None) if prop is not None else (fc.x, fc.P)
         fuse = (cfg.fuse_gn and not precomp and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
                 and not (prop is None and fc is None))
@@ -265,8 +264,8 @@ class GaussNewtonMixin:
         # chunk's norm is 0 and every chunk stops at iteration 2 -- the decision
         # is known without the per-chunk norms' read-back
         static = fuse and run.static_conv and not self._norms_needed_now()
-        if not static:
-            cc.begin()
+        if not static and not cc.ready:
+            cc.begin()          # (normally queued at the end of the previous date, off this date's host path)
         n_iter, n_visit, vis, full = 1, N, order, True
         norms = []
         while True:
@@ -291,6 +290,8 @@ class GaussNewtonMixin:
                     else:
                         K.analysis(n, table, x_prev, fx, fP, x_new, A_keep, None, status, None, N=N, out=out_now,
                                    a_rows=a_rows, **kw)
+            if n_iter == 1:
+                cc.resolve()    # the previous dates' histograms, under this launch (read-backs done long ago)
             if fuse and n_iter == 1:
                 n_iter = 2
             x_prev, x_new = x_new, (x_prev if x_prev is not None else torch.empty_like(x_new))
@@ -326,4 +327,5 @@ class GaussNewtonMixin:
         self.last_chunk_iters = cc.histogram() if self._norms_needed_now() else cc.histogram_async(bail)
         if self._norms_needed_now():
             bail(self.last_chunk_iters)
+        cc.begin()              # the next date's reset, queued behind this date's read-backs
         return x_prev, n_iter, norms
