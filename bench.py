@@ -114,7 +114,7 @@ def build(cfg_name, a, mask, part, dev, comm):
     def mkcfg(**kw):
         # phase_timing: hipEvent pairs around each phase on the compute stream
         # (device time, resolved after the timed region) for the per-rank record
-        if "chunk" in c and a.band_parallel <= 1:
+        if "chunk" in c:
             kw.setdefault("convergence_chunk", [c["chunk"], c["chunk"]])
         return k.EngineConfig(metrics_path=a.metrics, band_parallel=a.band_parallel,
                               phase_timing=not a.no_telemetry, **{**kw, **over})

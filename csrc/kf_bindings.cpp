@@ -299,8 +299,9 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
   // GeoTIFF tile encoder (predictor 3 + fixed-Huffman zlib per 256^2 tile)
   m.attr("DFL_TILE") = DFL_TILE;
   m.attr("DFL_BOUND") = DFL_BOUND;
+  m.attr("DFL_ROW_SCRATCH") = (int64_t)DFL_TILE * DFL_ROW_WORDS * 4;   // scratch bytes per tile (device)
   m.def("deflate_tiles", [](uintptr_t src, int64_t plane_ld, int H, int W, int nplanes, uintptr_t out,
-                            uintptr_t sizes, bool device, uintptr_t stream) {
+                            uintptr_t sizes, bool device, uintptr_t stream, uintptr_t scratch) {
     DflArgs a{};
     a.src = P<const float>(src);
     a.plane_ld = plane_ld;
@@ -311,6 +312,8 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
     a.tiles_y = (H + DFL_TILE - 1) / DFL_TILE;
     a.out = P<uint8_t>(out);
     a.sizes = P<uint32_t>(sizes);
+    a.scratch = P<uint8_t>(scratch);
+    if (device && !scratch) throw std::runtime_error("deflate_tiles: the device encoder needs its row scratch");
     if ((int64_t)H * W > plane_ld) throw std::runtime_error("deflate_tiles: plane_ld < H * W");
     if (device) check_hip(dev_deflate_tiles(a, (hipStream_t)stream), "deflate_tiles");
     else {

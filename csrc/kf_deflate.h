@@ -29,6 +29,8 @@ constexpr int64_t DFL_RAW = (int64_t)DFL_TILE * DFL_ROW;        // 262144 bytes 
 // worst case: header 2 + (19 + 9 bits per byte + 7 EOB + 7 pad) / 8 + Adler 4, rounded to 16
 constexpr int64_t DFL_BOUND = ((2 + (19 + 9 * DFL_RAW + 14) / 8 + 4) + 15) / 16 * 16;
 constexpr int DFL_HEAD_BITS = 19;   // zlib header (16) + BFINAL/BTYPE (3)
+// scratch words of one encoded row (9 bits per byte at most, plus a partial word)
+constexpr int DFL_ROW_WORDS = (9 * DFL_ROW + 31) / 32 + 1;
 constexpr uint32_t DFL_ADLER_MOD = 65521u;
 
 KF_HD uint32_t dfl_rev(uint32_t code, int len) {

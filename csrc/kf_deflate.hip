@@ -6,9 +6,10 @@
 //
 // Launch: one workgroup of 256 threads per tile (thread = tile row), grid =
 // planes x tiles (a 10980^2 x 7 date: 12,943 workgroups, 50 per CU).
-//   pass 1: each thread encodes its row into a bit counter and the Adler-32
-//           partials; a workgroup scan gives every row its bit offset;
-//   pass 2: each thread re-encodes its row into 32-bit words at that offset.
+//   pass 1: each thread encodes its row once, into a word-aligned scratch
+//           slot of its own, with the Adler-32 partials; a workgroup scan
+//           gives every row its bit offset in the stream;
+//   pass 2: each thread moves its row's words to that offset (a shift).
 //           Words wholly inside a row's range are stored directly; the one
 //           word a row shares with the next (its tail) goes through LDS and is
 //           OR-ed into the next row's head word, so no atomics and no zeroed
@@ -37,10 +38,26 @@ __global__ __launch_bounds__(DFL_TILE) void dfl_tile_kernel(DflArgs a) {
   auto row = [&](int c) -> uint32_t { return (rin && c < ncol) ? __float_as_uint(rowp[c]) : 0u; };
   const int64_t rest = DFL_RAW - (int64_t)r * DFL_ROW;
 
-  // pass 1: bits of this row, Adler partials
+  // pass 1: the row's bit string into its own word-aligned scratch slot (one
+  // encode of the row), its length and Adler partials
+  uint32_t* rs = reinterpret_cast<uint32_t*>(a.scratch) + ((int64_t)tile * DFL_TILE + r) * DFL_ROW_WORDS;
   uint64_t nbits = 0, s1 = 0, s2 = 0;
-  dfl_encode_row(row, rest, [&](uint32_t, int l) { nbits += (uint64_t)l; }, s1, s2);
-  KF_DCHECK(nbits >= 64);
+  {
+    uint64_t acc = 0;
+    int nacc = 0, wi = 0;
+    dfl_encode_row(row, rest, [&](uint32_t bits, int len) {
+      acc |= (uint64_t)bits << nacc;
+      nacc += len;
+      nbits += (uint64_t)len;
+      if (nacc >= 32) {
+        rs[wi++] = (uint32_t)acc;
+        acc >>= 32;
+        nacc -= 32;
+      }
+    }, s1, s2);
+    if (nacc > 0) rs[wi] = (uint32_t)acc;
+  }
+  KF_DCHECK(nbits >= 64 && nbits <= 32u * DFL_ROW_WORDS);
 
   __shared__ uint64_t scan[DFL_TILE];
   __shared__ uint64_t red1[DFL_TILE / 64], red2[DFL_TILE / 64];
@@ -72,7 +89,9 @@ __global__ __launch_bounds__(DFL_TILE) void dfl_tile_kernel(DflArgs a) {
   }
   const uint32_t adler = dfl_adler(t1, t2, DFL_RAW);
 
-  // pass 2: words
+  // pass 2: the row's words shifted to its bit offset in the stream.  Words
+  // wholly inside the row's range are stored; the word shared with the next
+  // row goes through LDS (every row emits >= 65 bits: no word spans 3 rows)
   uint32_t* out = reinterpret_cast<uint32_t*>(a.out + (int64_t)tile * DFL_BOUND);
   const bool shared_left = r > 0 && (start & 31u) != 0;
   uint64_t wi = start >> 5;
@@ -99,8 +118,9 @@ __global__ __launch_bounds__(DFL_TILE) void dfl_tile_kernel(DflArgs a) {
       nacc -= 32;
     }
   };
-  uint64_t d1, d2;
-  dfl_encode_row(row, rest, sink, d1, d2);
+  const int full = (int)(nbits >> 5), part = (int)(nbits & 31u);
+  for (int k = 0; k < full; ++k) sink(rs[k], 32);
+  if (part) sink(rs[full] & ((1u << part) - 1u), part);
   if (r == DFL_TILE - 1) {
     sink(0u, 7);                                       // end of block (code 256: 7 zero bits)
     const int pad = (8 - (int)(((wi << 5) + nacc) & 7u)) & 7;

@@ -101,6 +101,7 @@ struct DflArgs {
   int32_t H, W, nplanes, tiles_x, tiles_y, pad_;
   uint8_t* out;
   uint32_t* sizes;
+  uint8_t* scratch;   // device: DFL_TILE * DFL_ROW_WORDS words per tile (row bit strings before the shift)
 };
 hipError_t dev_deflate_tiles(const DflArgs& a, hipStream_t s);
 hipError_t dev_deflate_pack(const uint8_t* scratch, const uint32_t* sizes, const int64_t* offs, uint8_t* packed,

@@ -83,8 +83,7 @@ def _engine_config(args):
         import yaml
         with open(args.config_file) as f:
             explicit = "convergence_chunk" in (yaml.safe_load(f) or {})
-    if (not explicit and cfg.convergence_chunk is None and args.sensor in DRIVER_CHUNK and cfg.spatial_gamma <= 0
-            and cfg.band_parallel <= 1 and (getattr(args, "band_parallel", None) or 1) <= 1):
+    if not explicit and cfg.convergence_chunk is None and args.sensor in DRIVER_CHUNK and cfg.spatial_gamma <= 0:
         b = DRIVER_CHUNK[args.sensor]
         cfg.convergence_chunk = [b, b]
         cfg.validate()

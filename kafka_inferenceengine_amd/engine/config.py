@@ -143,9 +143,8 @@ class EngineConfig:
             if len(cc) != 2 or min(cc) < 1:
                 raise ValueError("convergence_chunk must be [x size, y size] >= 1 (or one size)")
             self.convergence_chunk = cc
-            if self.spatial_gamma > 0 or self.band_parallel > 1:
-                raise ValueError("convergence_chunk runs without the spatial prior (which couples the chunks) or "
-                                 "band-parallel")
+            if self.spatial_gamma > 0:
+                raise ValueError("convergence_chunk runs without the spatial prior (which couples the chunks)")
         return self
 
     # ------------------------------------------------------------- IO

@@ -258,7 +258,7 @@ class GaussNewtonMixin:
         h0_outs, a_rows, gain = run.h0_outs, run.a_rows, run.gain
         cc = self._chunk_state()
         fx, fP = (None, None) if prop is not None else (fc.x, fc.P)
-        fuse = (cfg.fuse_gn and not precomp and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
+        fuse = (cfg.fuse_gn and not precomp and not run.bp and cfg.min_iterations >= 2 and cfg.max_iterations >= 1
                 and not (prop is None and fc is None))
         # linear operators: iteration 2 repeats iteration 1 exactly, so every
         # chunk's norm is 0 and every chunk stops at iteration 2 -- the decision
@@ -280,7 +280,10 @@ class GaussNewtonMixin:
             with self.timer.phase("analysis"):
                 if N and n_visit:
                     first2 = fuse and n_iter == 1
-                    if gain:        # K1g: the same visiting, subset and per-pixel norms
+                    if run.bp:      # C5 band groups: the all-reduced normal equations, same subset and norms
+                        self._band_parallel_iteration(table, x_prev, fc, x_new, A_keep, status, order=vis,
+                                                      n_visit=kw.get("n_visit"), dn_out=cc.dn)
+                    elif gain:      # K1g: the same visiting, subset and per-pixel norms
                         K.gain(n, table, x_prev, fx, fP, x_new, P_out if first2 else A_keep, status, None, N=N,
                                joseph=cfg.joseph, out=out_t if first2 else out_now, gn_fused=2 if first2 else 1,
                                pdiag_rows=run.pdiag_rows if (first2 or A_keep is not None) else 0, **kw)

@@ -796,9 +796,8 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
                 if hasattr(self.observations, "bands_per_observation") else None
             self._band_parallel_check(specs, nb_all)
         chunked = bool(cfg.convergence_chunk)
-        if chunked and (bp or cfg.spatial_gamma > 0 or (gain and precomp)):
-            raise ValueError("convergence_chunk runs the fused information or gain form without band-parallel or "
-                             "the spatial prior (the spatial prior couples the chunks)")
+        if chunked and (cfg.spatial_gamma > 0 or (gain and precomp) or (bp and gain)):
+            raise ValueError("convergence_chunk runs without the spatial prior (which couples the chunks)")
         split = None if (precomp or gain or bp or cfg.spatial_gamma > 0 or chunked) else \
             self._split_plan(specs, dbs, h0_outs)
         if precomp or split:
@@ -1042,11 +1041,16 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
                 prev = (A_c, b_c)
 
     # ------------------------------------------------ band-parallel (TP-like)
-    def _band_parallel_iteration(self, table, x_prev, fc: KFState, x_out, A_out, status):
+    def _band_parallel_iteration(self, table, x_prev, fc: KFState, x_out, A_out, status, order=None, n_visit=None,
+                                 dn_out=None):
         """C5: this rank accumulates sum_b w h h^T and sum_b w h y' over its own
         bands (band slot 0 also adds the forecast precision), one RCCL
         all-reduce of the packed [A | b] per pixel within the band group, then
-        every member solves redundantly (identical x on the group)."""
+        every member solves redundantly (identical x on the group).  ``order`` /
+        ``n_visit`` / ``dn_out``: the per-chunk loop's visiting subset and
+        per-pixel norms (both launches visit the same pixels; the all-reduced
+        entries of the others are never read)."""
+        vis = dict(order=order, n_visit=n_visit)
         n, N = self.n_params, self.N
         nt = ntri(n)
         ld = fc.x.shape[1]
@@ -1057,16 +1061,17 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         A_part, b_part = self._bp_buf[:nt], self._bp_buf[nt:]
         if N:
             if self.band_comm.rank == 0:
-                K.analysis(n, table, x_prev, fc.x, fc.P, None, A_part, b_part, status, None, N=N, solve=False)
+                K.analysis(n, table, x_prev, fc.x, fc.P, None, A_part, b_part, status, None, N=N, solve=False, **vis)
             else:
                 self._bp_buf.zero_()
                 K.analysis(n, table, x_prev, fc.x, fc.P, None, A_part, b_part, status, None, N=N, solve=False,
-                           a_in=A_part, b_in=b_part)
+                           a_in=A_part, b_in=b_part, **vis)
         with self.timer.phase("band_allreduce"):
             self.band_comm.all_reduce_(self._bp_buf)
         if N:
             K.analysis(n, self._bp_solve_tab, x_prev, fc.x, fc.P, x_out, A_out, None, self._bp_status,
-                       self._partials, N=N, a_in=A_part, b_in=b_part)
+                       None if dn_out is not None else self._partials, N=N, a_in=A_part, b_in=b_part,
+                       dn_out=dn_out, **vis)
 
     def _band_parallel_check(self, specs, n_bands=None):
         """Refuse band-parallel where its C5 all-reduce dwarfs the analysis it

@@ -1154,8 +1154,9 @@ class TileEncoder:
         dev = planes.device
         scratch = self._buf("scratch", nt * bound, torch.uint8, dev)
         sizes = self._buf("sizes", nt, torch.int32, dev)        # uint32 byte counts (< 2^31)
+        rows = self._buf("rows", nt * int(ext().DFL_ROW_SCRATCH), torch.uint8, dev) if _dev(planes) else None
         ext().deflate_tiles(_ptr(planes), planes.stride(0), int(H), int(W), int(n), _ptr(scratch), _ptr(sizes),
-                            _dev(planes), _stream(planes))
+                            _dev(planes), _stream(planes), _ptr(rows))
         s64 = sizes.to(torch.int64)
         offs = torch.cumsum(s64, 0) - s64
         if base is not None:

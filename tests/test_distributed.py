@@ -332,7 +332,7 @@ def test_bench_eight_rank_rehearsal(tmp_path, config, both, extra):
         assert np.array_equal(x8, x1)   # deep-halo tiled passes: bit-identical at any rank count
 
 
-def _bp_worker(rank, world, port, B, q):
+def _bp_worker(rank, world, port, B, q, chunk=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     import kafka_inferenceengine_amd as k
@@ -341,12 +341,12 @@ def _bp_worker(rank, world, port, B, q):
     torch.set_num_threads(1)
     comm = Comm.from_env(device="cpu", band_parallel=B)
     try:
-        q.put(_bp_run(k, comm, StripPartition))
+        q.put(_bp_run(k, comm, StripPartition, chunk))
     finally:
         comm.destroy()
 
 
-def _bp_run(k, comm, StripPartition):
+def _bp_run(k, comm, StripPartition, chunk=None):
     mask = np.ones((20, 18), bool)
     mask[3:6, 2:9] = False
     part = StripPartition(mask, comm.rank, comm.world)
@@ -355,27 +355,28 @@ def _bp_run(k, comm, StripPartition):
     prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
     kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
                         state_propagation=None, prior=prior, device="cpu", comm=comm, partition=part,
-                        config=k.EngineConfig(gp_split="never"))
+                        config=k.EngineConfig(gp_split="never", convergence_chunk=chunk,
+                                              convergence_tolerance=2e-4 if chunk else 1e-3))
     grid = [obs.dates[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in obs.dates[:2]]
     st = kf.run(grid, kf.state_from_prior(prior), None, None)
     g = comm.ranks[comm.rank] if comm.band is None else comm.band.ranks[comm.band.rank]
-    return (g, part.offset, st.x.numpy().copy(), [h["gn_iterations"] for h in kf.history],
-            kf.last_status.numpy().copy())
+    its = [h["gn_iterations"] for h in kf.history] if chunk is None else [h["chunk_iters"] for h in kf.history]
+    return (g, part.offset, st.x.numpy().copy(), its, kf.last_status.numpy().copy())
 
 
 @pytest.mark.parametrize("world,B", [(2, 2), (4, 2), (8, 2)],
                          ids=["1strip-x-2bands", "2strips-x-2bands", "4strips-x-2bands"])
-def test_band_parallel_equals_single_rank(world, B):
+def test_band_parallel_equals_single_rank(world, B, chunk=None):
     """Band-parallel (TP-like) decomposition: bands split over the ranks of a
     strip, normal equations all-reduced (C5) — same result as one rank."""
     import kafka_inferenceengine_amd as k
     from kafka_inferenceengine_amd.parallel import Comm, StripPartition
 
-    ref = _bp_run(k, Comm.single("cpu"), StripPartition)
+    ref = _bp_run(k, Comm.single("cpu"), StripPartition, chunk)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bp_worker, args=(r, world, port, B, q)) for r in range(world)]
+    procs = [ctx.Process(target=_bp_worker, args=(r, world, port, B, q, chunk)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
@@ -392,6 +393,13 @@ def test_band_parallel_equals_single_rank(world, B):
     assert np.allclose(x, ref[2], rtol=1e-4, atol=1e-5)
     assert all(r[3] == ref[3] for r in res)
     assert np.array_equal(st, ref[4][:ref[2].shape[1]])
+
+
+def test_band_parallel_per_chunk_convergence():
+    """Band-parallel with the per-chunk exit test (6 x 6 chunks): the chunk
+    decisions are taken on the all-reduced solve's per-pixel norms, so every
+    band group stops the same chunks on the same iteration as one rank."""
+    test_band_parallel_equals_single_rank(4, 2, chunk=[6, 6])
 
 
 def test_metrics_summary_aggregates_ranks(tmp_path):
