@@ -388,14 +388,31 @@ hipError_t dev_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int 
 // wave sums in wave order (block_partial) -- the host runner repeats exactly
 // this order (kf_host.cpp), so a chunk's sum does not depend on the device or
 // on the order the analysis visited its pixels in.
+// The runs' (start, length) go through LDS first (one coalesced load per
+// CHUNK_SEG_LDS runs) and the run loop is unrolled, so a thread keeps several
+// dn loads in flight instead of one scalar-descriptor -> load -> add chain per
+// run (the same per-thread summation order as before: bit-identical).
+constexpr int CHUNK_SEG_LDS = 512;
 __global__ __launch_bounds__(BLOCK) void chunk_partials_kernel(ChunkPartialArgs a) {
   const int c = blockIdx.x;
   const int g = a.lc_gid[c];
   if (!a.active[g]) return;   // frozen: its sum is no longer read (workgroup-uniform)
+  __shared__ int sst[CHUNK_SEG_LDS], slen[CHUNK_SEG_LDS];
   double acc = 0.0;
-  for (int sg = a.lc_ptr[c]; sg < a.lc_ptr[c + 1]; ++sg) {
-    const int st = a.seg_start[sg], len = a.seg_len[sg];
-    for (int i = threadIdx.x; i < len; i += BLOCK) acc += (double)a.dn[st + i];
+  const int s0 = a.lc_ptr[c], s1 = a.lc_ptr[c + 1];
+  for (int b0 = s0; b0 < s1; b0 += CHUNK_SEG_LDS) {
+    const int nb = s1 - b0 < CHUNK_SEG_LDS ? s1 - b0 : CHUNK_SEG_LDS;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nb; i += BLOCK) {
+      sst[i] = a.seg_start[b0 + i];
+      slen[i] = a.seg_len[b0 + i];
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < nb; ++k) {
+      const int st = sst[k], len = slen[k];
+      for (int i = threadIdx.x; i < len; i += BLOCK) acc += (double)a.dn[st + i];
+    }
   }
   __shared__ double red[BLOCK / 64];
   acc = wave_sum(acc);
