@@ -35,7 +35,20 @@ __global__ __launch_bounds__(DFL_TILE) void dfl_tile_kernel(DflArgs a) {
   const bool rin = y < a.H;
   const int ncol = a.W - x0 < DFL_TILE ? a.W - x0 : DFL_TILE;
   const float* rowp = a.src + (int64_t)plane * a.plane_ld + (rin ? y : 0) * a.W + x0;
-  auto row = [&](int c) -> uint32_t { return (rin && c < ncol) ? __float_as_uint(rowp[c]) : 0u; };
+  // the row's samples in groups of 16: one burst of independent loads into this
+  // thread's LDS line per group (the encoder reads columns in order, 4 passes
+  // over the row, one per byte plane), instead of one dependent load per byte
+  __shared__ uint32_t line[DFL_TILE][17];
+  auto row = [&](int c) -> uint32_t {
+    if ((c & 15) == 0) {
+      uint32_t v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = (rin && c + j < ncol) ? __float_as_uint(rowp[c + j]) : 0u;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) line[r][j] = v[j];
+    }
+    return line[r][c & 15];
+  };
   const int64_t rest = DFL_RAW - (int64_t)r * DFL_ROW;
 
   // pass 1: the row's bit string into its own word-aligned scratch slot (one

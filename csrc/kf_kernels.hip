@@ -408,8 +408,23 @@ __global__ __launch_bounds__(BLOCK) void chunk_partials_kernel(ChunkPartialArgs 
       slen[i] = a.seg_len[b0 + i];
     }
     __syncthreads();
-#pragma unroll 8
-    for (int k = 0; k < nb; ++k) {
+    int k = 0;
+    // runs no longer than the workgroup (chunk widths <= 256, the drivers'
+    // 128^2 / 256^2): one element per thread and run, 8 runs' loads issued
+    // before their adds (in run order: the same sums)
+    for (; k + 8 <= nb; k += 8) {
+      bool short_runs = true;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) short_runs = short_runs && slen[k + u] <= BLOCK;
+      if (!short_runs) break;
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = (int)threadIdx.x < slen[k + u] ? a.dn[sst[k + u] + threadIdx.x] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if ((int)threadIdx.x < slen[k + u]) acc += (double)v[u];
+    }
+    for (; k < nb; ++k) {
       const int st = sst[k], len = slen[k];
       for (int i = threadIdx.x; i < len; i += BLOCK) acc += (double)a.dn[st + i];
     }
