@@ -192,3 +192,26 @@ def test_s2_warp_device_ingest_gpu(tmp_path):
             dn = db.dn.cpu().numpy().view(np.uint16)
             ref = reproject_image(os.path.join(folder, f"B{S.S2_BAND_MAP[b]}_sur.tif"), MASK)
             assert np.array_equal(dn, ref[part.r0:part.r1][part.local_mask])
+
+
+@pytest.mark.gpu
+def test_cli_s2_run_on_mask_gpu(cuda, tmp_path, capsys):
+    """The S2 driver workflow on the GPU: warped device ingest, per-128^2-chunk
+    convergence (the CLI default for S2), outputs on the mask's grid, and the
+    same states as the CPU run."""
+    from kafka_inferenceengine_amd.cli import main
+    data, emus, dates = _s2_archive(tmp_path / "arch")
+    recs = []
+    for dev in ("cpu", "cuda"):
+        out = tmp_path / f"out_{dev}"
+        main(["run", "--sensor", "s2", "--s2-folder", data, "--emulator-folder", emus, "--mask", MASK,
+              "--out", str(out), "--steps", "2", "--device", dev])
+        recs.append(json.loads(capsys.readouterr().out.strip().splitlines()[-1]))
+        name = sorted(p for p in os.listdir(out) if p.endswith(".tif") and "_unc" not in p)[0]
+        arr, info = read_tiff(out / name)
+        assert arr.shape == (204, 235) and info["geotransform"] == tiff_info(MASK)["geotransform"]
+        recs[-1]["first"] = arr
+    assert recs[0]["gn_iterations"] == recs[1]["gn_iterations"] and recs[1]["finite"]
+    m = read_tiff(MASK)[0].astype(bool)
+    a, b = recs[0]["first"][m], recs[1]["first"][m]
+    assert np.allclose(a, b, rtol=2e-3, atol=2e-3), float(np.abs(a - b).max())
