@@ -350,7 +350,8 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
   });
   // per-chunk Gauss-Newton convergence (kf_core.h ChunkPartialArgs ...)
   m.def("chunk_partials", [](uintptr_t dn, uintptr_t seg_start, uintptr_t seg_len, uintptr_t lc_ptr, uintptr_t lc_gid,
-                             int n_local, uintptr_t active, uintptr_t part, bool device, uintptr_t stream) {
+                             int n_local, uintptr_t active, uintptr_t part, uintptr_t gpart, int groups, bool device,
+                             uintptr_t stream) {
     ChunkPartialArgs a{};
     a.dn = P<const float>(dn);
     a.seg_start = P<const int32_t>(seg_start);
@@ -360,6 +361,8 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
     a.n_local = n_local;
     a.active = P<const uint8_t>(active);
     a.part = P<double>(part);
+    a.gpart = P<double>(gpart);
+    a.groups = groups;
     if (device) check_hip(dev_chunk_partials(a, (hipStream_t)stream), "chunk_partials");
     else host_chunk_partials(a);
   });

@@ -2342,7 +2342,11 @@ KF_HD float pixel_jacobi_classic(const JacobiArgs& a, int64_t p) {
 
 // this rank's pixels of a chunk: runs of consecutive local indices, one per
 // (chunk, raster row) -- the active pixels of a row inside a chunk's column
-// range are contiguous in the strip's row-major numbering
+// range are contiguous in the strip's row-major numbering.  The summation
+// order: runs in groups of CHUNK_GROUP_RUNS (row order); within a group, a
+// thread-strided f64 sum per column slot, the xor shuffle tree of wave_sum and
+// the wave sums in order; the group totals then in group order.
+constexpr int CHUNK_GROUP_RUNS = 16;
 struct ChunkPartialArgs {
   const float* dn;           // [N] |x - x0|^2 per pixel (AnalysisArgs.dn_out)
   const int32_t* seg_start;  // [S] first local pixel of each run
@@ -2352,6 +2356,8 @@ struct ChunkPartialArgs {
   int32_t n_local;
   const uint8_t* active;     // [nc] chunks still iterating (frozen ones are skipped)
   double* part;              // [nc] this rank's sum per global chunk
+  double* gpart;             // [n_local * groups] scratch: the group totals
+  int32_t groups;            // >= ceil(runs / CHUNK_GROUP_RUNS) of every local chunk
 };
 
 struct ChunkDecideArgs {

@@ -383,61 +383,63 @@ hipError_t dev_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int 
 // ---------------------------------------------------------------------------
 // Per-chunk Gauss-Newton convergence (kf_core.h ChunkPartialArgs ...).
 
-// One workgroup per local chunk: thread t sums column offsets t, t + 256, ..
-// of the chunk's runs in row order, then a fixed shuffle tree per wave and the
-// wave sums in wave order (block_partial) -- the host runner repeats exactly
-// this order (kf_host.cpp), so a chunk's sum does not depend on the device or
-// on the order the analysis visited its pixels in.
-// The runs' (start, length) go through LDS first (one coalesced load per
-// CHUNK_SEG_LDS runs) and the run loop is unrolled, so a thread keeps several
-// dn loads in flight instead of one scalar-descriptor -> load -> add chain per
-// run (the same per-thread summation order as before: bit-identical).
-constexpr int CHUNK_SEG_LDS = 512;
-__global__ __launch_bounds__(BLOCK) void chunk_partials_kernel(ChunkPartialArgs a) {
-  const int c = blockIdx.x;
+// Stage 1, one workgroup per (local chunk, group of CHUNK_GROUP_RUNS runs):
+// thread t sums column offsets t, t + 256, .. of the group's runs in row
+// order, then a fixed shuffle tree per wave and the wave sums in wave order.
+// Stage 2, one thread per local chunk: the group totals in group order.  The
+// host runner repeats exactly this order (kf_host.cpp), so a chunk's sum does
+// not depend on the device or on the order the analysis visited its pixels in.
+// (One workgroup per whole chunk was latency-bound: 256 dependent run loads
+// per thread, one workgroup per CU on a 3882^2 share, 131 us per call.)
+__global__ __launch_bounds__(BLOCK) void chunk_group_kernel(ChunkPartialArgs a) {
+  const int c = blockIdx.x / a.groups, q = blockIdx.x - c * a.groups;
   const int g = a.lc_gid[c];
   if (!a.active[g]) return;   // frozen: its sum is no longer read (workgroup-uniform)
-  __shared__ int sst[CHUNK_SEG_LDS], slen[CHUNK_SEG_LDS];
+  const int s0 = a.lc_ptr[c] + q * CHUNK_GROUP_RUNS, s1 = a.lc_ptr[c + 1];
+  if (s0 >= s1) return;       // past this chunk's runs (workgroup-uniform)
+  const int n = s1 - s0 < CHUNK_GROUP_RUNS ? s1 - s0 : CHUNK_GROUP_RUNS;
+  __shared__ int sst[CHUNK_GROUP_RUNS], slen[CHUNK_GROUP_RUNS];
+  const int t = threadIdx.x;
+  if (t < n) {
+    sst[t] = a.seg_start[s0 + t];
+    slen[t] = a.seg_len[s0 + t];
+  }
+  __syncthreads();
+  bool short_runs = true;     // every run within one element per thread (chunk width <= 256)
+  for (int k = 0; k < n; ++k) short_runs = short_runs && slen[k] <= BLOCK;
   double acc = 0.0;
-  const int s0 = a.lc_ptr[c], s1 = a.lc_ptr[c + 1];
-  for (int b0 = s0; b0 < s1; b0 += CHUNK_SEG_LDS) {
-    const int nb = s1 - b0 < CHUNK_SEG_LDS ? s1 - b0 : CHUNK_SEG_LDS;
-    __syncthreads();
-    for (int i = threadIdx.x; i < nb; i += BLOCK) {
-      sst[i] = a.seg_start[b0 + i];
-      slen[i] = a.seg_len[b0 + i];
-    }
-    __syncthreads();
-    int k = 0;
-    // runs no longer than the workgroup (chunk widths <= 256, the drivers'
-    // 128^2 / 256^2): one element per thread and run, 8 runs' loads issued
-    // before their adds (in run order: the same sums)
-    for (; k + 8 <= nb; k += 8) {
-      bool short_runs = true;
+  if (short_runs) {
+    // all the group's loads in flight before the adds (in run order: the same sums)
+    float v[CHUNK_GROUP_RUNS];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) short_runs = short_runs && slen[k + u] <= BLOCK;
-      if (!short_runs) break;
-      float v[8];
+    for (int k = 0; k < CHUNK_GROUP_RUNS; ++k) v[k] = (k < n && t < slen[k]) ? a.dn[sst[k] + t] : 0.f;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = (int)threadIdx.x < slen[k + u] ? a.dn[sst[k + u] + threadIdx.x] : 0.f;
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if ((int)threadIdx.x < slen[k + u]) acc += (double)v[u];
-    }
-    for (; k < nb; ++k) {
-      const int st = sst[k], len = slen[k];
-      for (int i = threadIdx.x; i < len; i += BLOCK) acc += (double)a.dn[st + i];
-    }
+    for (int k = 0; k < CHUNK_GROUP_RUNS; ++k)
+      if (k < n && t < slen[k]) acc += (double)v[k];
+  } else {
+    for (int k = 0; k < n; ++k)
+      for (int i = t; i < slen[k]; i += BLOCK) acc += (double)a.dn[sst[k] + i];
   }
   __shared__ double red[BLOCK / 64];
   acc = wave_sum(acc);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  if ((t & 63) == 0) red[t >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int w = 0; w < BLOCK / 64; ++w) t += red[w];
-    a.part[g] = t;
+  if (t == 0) {
+    double tot = 0.0;
+    for (int w = 0; w < BLOCK / 64; ++w) tot += red[w];
+    a.gpart[(int64_t)c * a.groups + q] = tot;
   }
+}
+
+__global__ __launch_bounds__(BLOCK) void chunk_total_kernel(ChunkPartialArgs a) {
+  const int c = blockIdx.x * BLOCK + threadIdx.x;
+  if (c >= a.n_local) return;
+  const int g = a.lc_gid[c];
+  if (!a.active[g]) return;
+  const int ng = (a.lc_ptr[c + 1] - a.lc_ptr[c] + CHUNK_GROUP_RUNS - 1) / CHUNK_GROUP_RUNS;
+  double tot = 0.0;
+  for (int q = 0; q < ng; ++q) tot += a.gpart[(int64_t)c * a.groups + q];
+  a.part[g] = tot;
 }
 
 constexpr int DEC_BLOCK = 1024;
@@ -564,7 +566,10 @@ __global__ __launch_bounds__(BLOCK) void chunk_scatter_kernel(ChunkCompactArgs a
 int chunk_compact_blocks(int64_t n) { return (int)((n + KF_CMP_CHUNK - 1) / KF_CMP_CHUNK); }
 
 hipError_t dev_chunk_partials(const ChunkPartialArgs& a, hipStream_t s) {
-  if (a.n_local > 0) hipLaunchKernelGGL(chunk_partials_kernel, dim3(a.n_local), dim3(BLOCK), 0, s, a);
+  if (a.n_local <= 0) return hipSuccess;
+  if (a.groups <= 0 || a.gpart == nullptr || (int64_t)a.n_local * a.groups > INT32_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(chunk_group_kernel, dim3(a.n_local * a.groups), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(chunk_total_kernel, dim3((a.n_local + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a);
   return hipGetLastError();
 }
 

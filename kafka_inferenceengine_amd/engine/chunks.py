@@ -13,8 +13,8 @@ the test per chunk (``EngineConfig.convergence_chunk``):
 
 * the analysis writes each pixel's |x - x0|^2 (``AnalysisArgs.dn_out``);
 * ``chunk_partials`` sums them per chunk over this rank's pixels in a fixed
-  order (runs of one raster row, row order: independent of the visiting order
-  and of the device);
+  order (runs of one raster row in groups of 16 rows, row order: independent
+  of the visiting order and of the device);
 * the per-chunk partials of every rank are all-gathered (C1: one f64 per
   chunk, ~15 KB for a 10980² granule in 256² chunks) and summed in rank order
   by ``chunk_decide`` -- the same decision on every rank -- which marks the
@@ -90,6 +90,8 @@ class ChunkConvergence:
         i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(self.device)  # noqa: E731
         self.seg_start, self.seg_len = i32(seg_start), i32(seg_len)
         self.lc_ptr, self.lc_gid = i32(lc_ptr), i32(lc_gid)
+        self.groups = K.chunk_groups(lc_ptr)
+        self.gpart = torch.zeros(max(lc_gid.size, 1) * self.groups, dtype=torch.float64, device=self.device)
         self.chunk_of = i32(gid) if N else torch.zeros(1, dtype=torch.int32, device=self.device)
         self.local_count = i32(local_count)
         self.counts = counts
@@ -153,7 +155,8 @@ class ChunkConvergence:
 
         self._ready = False
         if self.N:
-            K.chunk_partials(self.dn, self.seg_start, self.seg_len, self.lc_ptr, self.lc_gid, self.active, self.part)
+            K.chunk_partials(self.dn, self.seg_start, self.seg_len, self.lc_ptr, self.lc_gid, self.active, self.part,
+                             self.gpart, self.groups)
         part_all = self.comm.all_gather_vec(self.part)
         K.chunk_decide(part_all, self.comm.world, self.len_x, self.local_count, tol, n_iter, min_iter, max_iter,
                        self.active, self.newly, self._iters, self.info)

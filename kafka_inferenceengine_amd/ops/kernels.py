@@ -492,12 +492,25 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
 
 
 # ------------------------------------------------ per-chunk convergence
-def chunk_partials(dn, seg_start, seg_len, lc_ptr, lc_gid, active, part):
+CHUNK_GROUP_RUNS = 16   # kf_core.h: runs summed per stage-1 workgroup
+
+
+def chunk_groups(lc_ptr) -> int:
+    """Stage-1 groups per local chunk (the most runs of any chunk / CHUNK_GROUP_RUNS)."""
+    runs = np.diff(np.asarray(lc_ptr, dtype=np.int64))
+    return max(1, int(-(-runs.max() // CHUNK_GROUP_RUNS))) if runs.size else 1
+
+
+def chunk_partials(dn, seg_start, seg_len, lc_ptr, lc_gid, active, part, gpart, groups):
     """part[g] = sum of dn over this rank's pixels of each active chunk g
-    (fixed order, kf_kernels.hip:chunk_partials_kernel); other entries kept."""
+    (fixed order, kf_kernels.hip:chunk_group_kernel / chunk_total_kernel);
+    other entries kept.  ``gpart`` [n_local * groups] f64 scratch, ``groups``
+    from :func:`chunk_groups`."""
     n_local = int(lc_gid.numel())
+    if gpart.numel() < n_local * groups or gpart.dtype != torch.float64:
+        raise ValueError("chunk_partials: group scratch too small")
     ext().chunk_partials(_ptr(dn), _ptr(seg_start), _ptr(seg_len), _ptr(lc_ptr), _ptr(lc_gid), n_local,
-                         _ptr(active), _ptr(part), _dev(part), _stream(part))
+                         _ptr(active), _ptr(part), _ptr(gpart), int(groups), _dev(part), _stream(part))
 
 
 def chunk_decide(part_all, world, len_x, local_count, tol, n_iter, min_iter, max_iter, active, newly, iters, info):

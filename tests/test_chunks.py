@@ -83,6 +83,46 @@ def test_chunk_ids_follow_get_chunks():
     assert cc.local_count.numpy().sum() == part.N
 
 
+def _order_model(dn, starts, lens, lc_ptr, c, group=16, T=256):
+    """chunks.py / kf_core.h summation order of one local chunk, in NumPy f64."""
+    tot = 0.0
+    for s0 in range(lc_ptr[c], lc_ptr[c + 1], group):
+        acc = np.zeros(T)
+        for sg in range(s0, min(s0 + group, lc_ptr[c + 1])):
+            for t in range(T):
+                for i in range(t, lens[sg], T):
+                    acc[t] += np.float64(dn[starts[sg] + i])
+        gt = 0.0
+        for w in range(T // 64):
+            v = acc[64 * w:64 * w + 64].copy()
+            off = 32
+            while off:
+                v = v + v[np.arange(64) ^ off]
+                off >>= 1
+            gt += v[0]
+        tot += gt
+    return tot
+
+
+@pytest.mark.parametrize("block", [[48, 40], [300, 20]])
+def test_chunk_partials_summation_order(block):
+    """The host runner sums a chunk in the documented fixed order (runs in
+    groups of 16 raster rows; per group a column-slot f64 sum, the wave xor
+    tree, waves in order; groups in order) -- the order the device kernels
+    are pinned bit-identical to (tests/test_gpu_chunks.py)."""
+    rng = np.random.default_rng(4)
+    m = rng.random((90, 610)) > 0.2
+    part = StripPartition(m, 0, 1)
+    cc = ChunkConvergence(part, block, 7, "cpu", Comm.single("cpu"))
+    dn = (rng.random(part.N) * 10.0 ** rng.integers(-8, 0, part.N)).astype(np.float32)
+    cc.dn.copy_(torch.from_numpy(dn))
+    cc.decide(n_iter=1, tol=1e-30, min_iter=2, max_iter=25)
+    starts, lens, ptr = cc.seg_start.numpy(), cc.seg_len.numpy(), cc.lc_ptr.numpy()
+    gid = cc.lc_gid.numpy()
+    for c in range(gid.size):
+        assert cc.part[gid[c]].item() == _order_model(dn, starts, lens, ptr, c), c
+
+
 def test_chunked_equals_farm_of_engines():
     """Every chunk runs the iterations its own engine runs, date by date, and
     the state is bit-identical to the farm's (the per-pixel analysis does not

@@ -17,15 +17,17 @@ from kafka_inferenceengine_amd.parallel import Comm, StripPartition
 pytestmark = pytest.mark.gpu
 
 
-def test_chunk_kernels_match_host(cuda):
+@pytest.mark.parametrize("block", [[64, 48], [300, 40]])
+def test_chunk_kernels_match_host(cuda, block):
     """chunk_partials is bit-identical on the device and the host runner (same
-    summation order); chunk_decide and chunk_compact agree exactly."""
+    summation order; 300-wide chunks take the runs-longer-than-a-workgroup
+    loop); chunk_decide and chunk_compact agree exactly."""
     rng = np.random.default_rng(0)
     H, W = 700, 530
     mask = rng.random((H, W)) > 0.1
     part = StripPartition(mask, 0, 1)
     N = part.N
-    cc0 = ChunkConvergence(part, [64, 48], 7, "cpu", Comm.single("cpu"))
+    cc0 = ChunkConvergence(part, block, 7, "cpu", Comm.single("cpu"))
     flags = ((rng.random(cc0.nc) > 0.3) & (cc0.counts > 0)).astype(np.uint8)
     # odd chunks far below the tolerance, even ones above: some chunks stop, some go on
     dn = (rng.random(N) * np.where(cc0.chunk_of.numpy() % 2 == 1, 1e-9, 1e-3)).astype(np.float32)
@@ -33,7 +35,7 @@ def test_chunk_kernels_match_host(cuda):
     xs = rng.random((7, N)).astype(np.float32)
     outs = {}
     for dev in ("cpu", cuda):
-        cc = ChunkConvergence(part, [64, 48], 7, dev, Comm.single(dev))
+        cc = ChunkConvergence(part, block, 7, dev, Comm.single(dev))
         cc.dn.copy_(torch.from_numpy(dn))
         cc.active.copy_(torch.from_numpy(flags))
         pend = cc.decide(n_iter=3, tol=2e-6, min_iter=2, max_iter=25)
