@@ -183,11 +183,16 @@ def gp_predict64_torch(em, X, chunk=65536):
 
 
 def oracle_run_blocks_torch(obs, state_mask, maps, time_grid, prior_mean, prior_cinv, propagated=(6,), q=None,
-                            tol=1e-3, min_iterations=2, max_iterations=25, x0=None, A0=None, device="cuda"):
+                            tol=1e-3, min_iterations=2, max_iterations=25, x0=None, A0=None, device="cuda",
+                            cast_f32=False):
     """:func:`oracle_run_blocks` in float64 torch on ``device`` (same loop, same
     per-pixel normal equations, solved by batched float64 Cholesky): the
     oracle of the 1024^2 slice.  Returns (x [N, n], A [N, n, n], iters) on the
-    host."""
+    host.
+
+    ``cast_f32``: the reference's one precision loss -- its solver casts the
+    normal equations to float32 and solves in single precision
+    (solvers.py:127-134); everything else stays float64."""
     import torch
 
     dev = torch.device(device)
@@ -232,7 +237,12 @@ def oracle_run_blocks_torch(obs, state_mask, maps, time_grid, prior_mean, prior_
                     yp = y + (h * x_prev).sum(1) - H0
                     A += w[:, None, None] * h[:, :, None] * h[:, None, :]
                     rhs += (w * yp)[:, None] * h
-                xa = torch.cholesky_solve(rhs[..., None], torch.linalg.cholesky(A))[..., 0]
+                if cast_f32:
+                    A32, r32 = A.float(), rhs.float()
+                    xa = torch.cholesky_solve(r32[..., None], torch.linalg.cholesky(A32))[..., 0].double()
+                    A = A32.double()
+                else:
+                    xa = torch.cholesky_solve(rhs[..., None], torch.linalg.cholesky(A))[..., 0]
                 norm = float(torch.linalg.norm((xa - x_prev).reshape(-1))) / float(N * n)
                 x_prev = xa
                 if norm < tol and n_iter >= min_iterations:
