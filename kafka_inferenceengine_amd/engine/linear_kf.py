@@ -127,6 +127,9 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         self.previous_state = None
         self._cache = RecordCache()
         self._tables = TableCache()
+        # per-date band lists a source hands out again for every date of a pool
+        # slot (``band_specs_static`` sources): id -> [list, (spec, band) pairs, table]
+        self._bands_memo = {}
         self._prop_bufs = {}            # fused-propagation argument blocks on the device, by content
         self._prop_dicts = {}           # propagation argument dicts by (propagator, prior, Q) identity
         self._partials = K.partials_buffer(max(self.N, 1), self.device)
@@ -588,7 +591,7 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         if not (cfg.return_innovations or cfg.spatial_gamma > 0 or
                 self.band_comm is not None or any(sp.kind == OP_PRECOMP for sp in specs)) and \
                 self._split_plan_kind(specs) is None:
-            table = self._tables.get(specs, [d for _, d in bands], self.n_params, self._cache, self.device)
+            table = self._band_table(bands, specs, [d for _, d in bands])
             # the next date's observed-first order too: its passes run on the
             # device after this date's launches, under the host's norm wait and
             # step bookkeeping, instead of between the two dates' analyses
@@ -674,7 +677,18 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         with self.timer.phase("ingest"):
             if hasattr(obs, "get_device_bands") and len(mine) == nb:
                 dbs = obs.get_device_bands(date)     # one acquire of the date's buffers
-                return [(self._operator_spec(db, b, date), db) for b, db in enumerate(dbs)]
+                if not getattr(obs, "band_specs_static", False):
+                    return [(self._operator_spec(db, b, date), db) for b, db in enumerate(dbs)]
+                # the source hands out the same band list for every date of a
+                # pool slot and its operators do not depend on the date: the
+                # (spec, band) pairs and their band table are built once per list
+                hit = self._bands_memo.get(id(dbs))
+                if hit is None or hit[0] is not dbs:
+                    if len(self._bands_memo) >= 32:
+                        self._bands_memo.clear()
+                    hit = self._bands_memo[id(dbs)] = [dbs, [(self._operator_spec(db, b, date), db)
+                                                             for b, db in enumerate(dbs)], None]
+                return hit[1]
             for b in mine:
                 if hasattr(obs, "get_device_band_data"):
                     db = obs.get_device_band_data(date, b)
@@ -683,6 +697,16 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
                 spec = self._operator_spec(db, b, date)
                 out.append((spec, db))
         return out
+
+    def _band_table(self, bands, specs, dbs) -> K.BandTable:
+        """The band table of ``bands`` (TableCache); memoised with the pairs
+        list of a ``band_specs_static`` source (:meth:`_device_bands`)."""
+        for hit in self._bands_memo.values():
+            if hit[1] is bands:
+                if hit[2] is None:
+                    hit[2] = self._tables.get(specs, dbs, self.n_params, self._cache, self.device)
+                return hit[2]
+        return self._tables.get(specs, dbs, self.n_params, self._cache, self.device)
 
     def _band_from_reference(self, data) -> DeviceBand:
         """Reference record (full strip rasters, sparse diagonal inverse variance)."""
@@ -805,7 +829,7 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
         elif h0_outs is not None:
             table = build_table(specs, dbs, n, self._cache, self.device, h0_outs)
         elif table is None:
-            table = self._tables.get(specs, dbs, n, self._cache, self.device)
+            table = self._band_table(bands, specs, dbs)
         prop = None
         if (isinstance(forecast, LazyForecast) and forecast.kind == (COVARIANCE if gain else PRECISION)
                 and not (precomp or split or bp) and N):

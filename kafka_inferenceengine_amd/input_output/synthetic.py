@@ -88,6 +88,7 @@ class SyntheticObservations:
     """Generic synthetic multi-band source (see module docstring)."""
 
     sensor = "synthetic"
+    band_specs_static = True     # band_spec(date, b) does not depend on the date
 
     def __init__(self, state_mask, dates, band_specs, truth_center, truth_spread, truth_lo=None, truth_hi=None,
                  *, partition=None, encoding: str = "dn16", scale: float = 1e-4, rel_unc: float = 0.05,
@@ -283,10 +284,22 @@ class SyntheticObservations:
                           aux=aux)
 
     def get_device_bands(self, date):
-        """Every band of ``date`` from one pool-entry acquire (one stream wait)."""
+        """Every band of ``date`` from one pool-entry acquire (one stream wait).
+        A pool entry's band records are built once and handed out again for
+        every date that uses the entry (the same buffers, scalars and
+        operators), so the engine can reuse what it derived from them."""
         e = self._entry(self.pool_index(date), date)
         aux = self._aux_local()
-        return [self._band(e, b, aux) for b in range(self.bands_per_observation[date])]
+        nb = self.bands_per_observation[date]
+        key = (e.data_ptr(), tuple(e.shape), e.dtype, nb, None if aux is None else aux.data_ptr(), self.encoding,
+               self.scale, self.rel_unc, self.unc_floor, id(self.metadata), tuple(map(id, self.band_specs)))
+        lists = self.__dict__.setdefault("_band_lists", {})
+        hit = lists.get(key)
+        if hit is None:
+            if len(lists) >= 64:
+                lists.clear()
+            hit = lists[key] = [self._band(e, b, aux) for b in range(nb)]
+        return hit
 
     def get_band_data(self, date, band):
         """Reference record on this rank's strip raster (numpy, float64)."""

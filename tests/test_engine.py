@@ -835,3 +835,24 @@ def test_aliased_mean_raster_equals_written_one(spatial):
     assert list(oa.history) == list(ob.history)
     for t in oa.history:
         assert torch.equal(oa.history[t][0], ob.history[t][0]) and torch.equal(oa.history[t][1], ob.history[t][1])
+
+
+def test_band_lists_memoised_per_pool_slot():
+    """A synthetic source hands out one band list per pool slot (same buffers,
+    same operators); the engine derives its (spec, band) pairs and band table
+    once per list, and a changed source setting gives a new list."""
+    mask = np.ones((12, 10), bool)
+    dates = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(4)]
+    obs = k.SyntheticBHRObservations(mask, dates=dates, n_train=20, device="cpu", stream=False, n_pool=2)
+    kf = k.LinearKalman(obs, k.DeviceOutput(k.TIP_PARAMETERS), mask, k.create_nonlinear_observation_operator,
+                        k.TIP_PARAMETERS, device="cpu")
+    a, b, c = obs.get_device_bands(dates[0]), obs.get_device_bands(dates[1]), obs.get_device_bands(dates[2])
+    assert a is c and a is not b                      # dates 0 and 2 share pool slot 0
+    pa, pc = kf._device_bands(dates[0]), kf._device_bands(dates[2])
+    assert pa is pc and [db for _, db in pa] == a
+    specs, dbs = [s for s, _ in pa], [d for _, d in pa]
+    t1 = kf._band_table(pa, specs, dbs)
+    assert kf._band_table(pc, specs, dbs) is t1
+    assert kf._tables.key(specs, dbs, 7, "cpu") == kf._tables.key(specs, [d for _, d in pc], 7, "cpu")
+    obs.rel_unc = 0.1
+    assert obs.get_device_bands(dates[0]) is not a
