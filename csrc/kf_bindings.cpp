@@ -123,6 +123,7 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(AnalysisArgs, partials_first, double*)
       .PTR_FIELD(AnalysisArgs, order, const int32_t*)
       .def_readwrite("n_visit", &AnalysisArgs::n_visit)
+      .PTR_FIELD(AnalysisArgs, n_visit_dev, const int32_t*)
       .PTR_FIELD(AnalysisArgs, dn_out, float*)
       .def_readwrite("a_rows", &AnalysisArgs::a_rows)
       .def_readwrite("dom_check", &AnalysisArgs::dom_check)
@@ -154,6 +155,7 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .def_readwrite("gpm_frags", &GainArgs::gpm_frags)
       .def_readwrite("gn_fused", &GainArgs::gn_fused)
       .def_readwrite("n_visit", &GainArgs::n_visit)
+      .PTR_FIELD(GainArgs, n_visit_dev, const int32_t*)
       .def_readwrite("pdiag_rows", &GainArgs::pdiag_rows)
       .PTR_FIELD(GainArgs, partials_first, double*)
       .PTR_FIELD(GainArgs, order, const int32_t*)
@@ -368,7 +370,7 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
   });
   m.def("chunk_decide", [](uintptr_t part_all, int world, int nc, uintptr_t len_x, uintptr_t local_count, double tol,
                            int n_iter, int min_iter, int max_iter, uintptr_t active, uintptr_t newly, uintptr_t iters,
-                           uintptr_t info, bool device, uintptr_t stream) {
+                           uintptr_t info, uintptr_t px_out, bool device, uintptr_t stream) {
     ChunkDecideArgs a{};
     a.part_all = P<const double>(part_all);
     a.world = world;
@@ -383,6 +385,7 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
     a.newly = P<uint8_t>(newly);
     a.iters = P<int32_t>(iters);
     a.info = P<double>(info);
+    a.px_out = P<int32_t>(px_out);
     if (device) check_hip(dev_chunk_decide(a, (hipStream_t)stream), "chunk_decide");
     else host_chunk_decide(a);
   });
@@ -390,11 +393,12 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
   // -> kept slots on the host runner, -1 on the device (the count is known from chunk_decide's info)
   m.def("chunk_compact", [](uintptr_t order_in, int64_t n_in, uintptr_t chunk_of, uintptr_t active, uintptr_t newly,
                             uintptr_t counts, uintptr_t order_out, uintptr_t x_src, uintptr_t x_dst, int np, int64_t ld,
-                            bool device, uintptr_t stream) -> int64_t {
+                            uintptr_t n_in_dev, bool device, uintptr_t stream) -> int64_t {
     if (n_in > (int64_t)INT32_MAX) throw std::runtime_error("chunk_compact: more than 2^31 slots");
     ChunkCompactArgs a{};
     a.order_in = P<const int32_t>(order_in);
     a.n_in = n_in;
+    a.n_in_dev = P<const int32_t>(n_in_dev);
     a.chunk_of = P<const int32_t>(chunk_of);
     a.active = P<const uint8_t>(active);
     a.newly = P<const uint8_t>(newly);

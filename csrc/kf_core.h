@@ -308,6 +308,10 @@ struct AnalysisArgs {
   // (EngineConfig.convergence_chunk) visits only the pixels of the chunks that
   // have not converged, order[0 .. n_visit)
   int64_t n_visit;
+  // null, or the count of slots to visit in device memory (<= n_visit, which
+  // then only bounds the grid): a launch queued before the host has read the
+  // count, the per-chunk loop's iterations past the first read decision
+  const int32_t* n_visit_dev;
   // per-pixel |x - x0|^2 of the launch's last iteration (the per-chunk norms,
   // chunk_partials_kernel), stored at the pixel index; may be null
   float* dn_out;
@@ -323,8 +327,14 @@ struct AnalysisArgs {
   float dom_hi[MAX_D];
 };
 
-// slots visited by an analysis launch
-KF_HD int64_t visit_count(const AnalysisArgs& a) { return a.n_visit > 0 ? a.n_visit : a.N; }
+// slots visited by a launch: n_visit (0: N), or the device count (<= that bound)
+KF_HD int64_t visit_bounded(int64_t n_visit, int64_t N, const int32_t* n_dev) {
+  const int64_t n = n_visit > 0 ? n_visit : N;
+  if (!n_dev) return n;
+  const int64_t d = *n_dev;
+  return d < 0 ? 0 : (d < n ? d : n);
+}
+KF_HD int64_t visit_count(const AnalysisArgs& a) { return visit_bounded(a.n_visit, a.N, a.n_visit_dev); }
 
 // the linearisation point outside the launch's GP domain box (NaN counts as
 // outside); AP: the launch arguments in any address space
@@ -1409,6 +1419,7 @@ struct GainArgs {
   double* partials_first;  // per-block sum (x_1 - x_0)^2 of the first fused iteration
   const int32_t* order;  // visiting order (null: 0..N-1)
   int64_t n_visit;       // visiting slots (0: N)
+  const int32_t* n_visit_dev;  // null, or the device count of slots (<= n_visit), as AnalysisArgs
   float* dn_out;         // per-pixel |x - x0|^2 of the last iteration (per-chunk norms); may be null
   // stored rows: bit j set -> p_out row tri(j, j) receives the analysis
   // PRECISION diagonal entry (P^-1)_jj and no covariance row is stored (what a
@@ -1418,7 +1429,7 @@ struct GainArgs {
   int32_t pad_;
 };
 
-KF_HD int64_t visit_count(const GainArgs& a) { return a.n_visit > 0 ? a.n_visit : a.N; }
+KF_HD int64_t visit_count(const GainArgs& a) { return visit_bounded(a.n_visit, a.N, a.n_visit_dev); }
 
 // The partial-prior-reset forecast (forecast_partial) of an analysis held as a
 // covariance, returned as a covariance: Pa^-1 = inv(P_a) supplies the
@@ -2372,6 +2383,7 @@ struct ChunkDecideArgs {
   int32_t* iters;            // [nc] out: Gauss-Newton iterations of the chunk (set when it stops)
   double* info;              // [4] chunks still active (all ranks), largest norm tested, this rank's active
                              // pixels, chunks stopped at this iteration
+  int32_t* px_out;           // null, or this rank's active pixels as an int (the next launch's device count)
 };
 
 // the reference's exit test (linear_kf.py:297-304) for one chunk
@@ -2382,6 +2394,7 @@ KF_HD bool chunk_stops(double norm, int n_iter, int min_iter, int max_iter, doub
 struct ChunkCompactArgs {
   const int32_t* order_in;   // visiting order of the last launch (null: 0..n_in-1)
   int64_t n_in;
+  const int32_t* n_in_dev;   // null, or the device count of order_in's slots (<= n_in, the grid bound)
   const int32_t* chunk_of;   // [N] global chunk of each local pixel
   const uint8_t* active;
   const uint8_t* newly;

@@ -327,12 +327,14 @@ int host_chunk_decide(const ChunkDecideArgs& a) {
   a.info[1] = mx;
   a.info[2] = (double)px;
   a.info[3] = (double)n_new;
+  if (a.px_out) *a.px_out = px;
   return 0;
 }
 
 int64_t host_chunk_compact(const ChunkCompactArgs& a) {
   int64_t k = 0;
-  for (int64_t q = 0; q < a.n_in; ++q) {
+  const int64_t n_in = visit_bounded(a.n_in, a.n_in, a.n_in_dev);
+  for (int64_t q = 0; q < n_in; ++q) {
     const int p = a.order_in ? a.order_in[q] : (int)q;
     const int g = a.chunk_of[p];
     if (a.active[g]) {

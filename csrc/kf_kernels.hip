@@ -496,6 +496,7 @@ __global__ __launch_bounds__(DEC_BLOCK) void chunk_decide_kernel(ChunkDecideArgs
     a.info[1] = m;
     a.info[2] = (double)np_;
     a.info[3] = (double)nn;
+    if (a.px_out) *a.px_out = np_;
   }
 }
 
@@ -513,10 +514,11 @@ __device__ __forceinline__ int cmp_slot_px(const ChunkCompactArgs& a, int64_t q)
 __global__ __launch_bounds__(BLOCK) void chunk_count_kernel(ChunkCompactArgs a) {
   __shared__ int red[BLOCK / 64];
   const int64_t q0 = (int64_t)blockIdx.x * KF_CMP_CHUNK + (int64_t)threadIdx.x * CMP_PT;
+  const int64_t n_in = visit_bounded(a.n_in, a.n_in, a.n_in_dev);
   int n = 0;
   for (int i = 0; i < CMP_PT; ++i) {
     const int64_t q = q0 + i;
-    if (q >= a.n_in) break;
+    if (q >= n_in) break;
     const int p = cmp_slot_px(a, q);
     const int g = a.chunk_of[p];
     if (a.active[g]) {
@@ -539,12 +541,13 @@ __global__ __launch_bounds__(BLOCK) void chunk_scatter_kernel(ChunkCompactArgs a
   __shared__ int wtot[BLOCK / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t q0 = (int64_t)blockIdx.x * KF_CMP_CHUNK + (int64_t)threadIdx.x * CMP_PT;
+  const int64_t n_in = visit_bounded(a.n_in, a.n_in, a.n_in_dev);
   uint32_t keep = 0;
   int px[CMP_PT];
   for (int i = 0; i < CMP_PT; ++i) {
     const int64_t q = q0 + i;
     px[i] = 0;
-    if (q < a.n_in) {
+    if (q < n_in) {
       px[i] = cmp_slot_px(a, q);
       if (a.active[a.chunk_of[px[i]]]) keep |= 1u << i;
     }

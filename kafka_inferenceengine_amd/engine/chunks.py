@@ -103,6 +103,9 @@ class ChunkConvergence:
         self._static = None   # set_static(): every tested chunk stopped at this iteration (filled lazily)
         self.part = torch.zeros(self.nc, dtype=torch.float64, device=self.device)
         self.info = torch.zeros(4, dtype=torch.float64, device=self.device)
+        # this rank's active pixels after the decisions of odd / even iterations
+        # (int32): the device counts of launches queued before the host reads them
+        self.px = torch.zeros(2, dtype=torch.int32, device=self.device)
         self.dn = torch.zeros(max(N, 1), dtype=torch.float32, device=self.device)
         self.orders = [torch.empty(max(N, 1), dtype=torch.int32, device=self.device) for _ in range(2)]
         self.scratch = K.chunk_compact_scratch(max(N, 1), self.device)
@@ -139,10 +142,17 @@ class ChunkConvergence:
         self._ready = False
         return {int(n_iter): self.tested} if self.tested else {}
 
+    def px_slot(self, n_iter: int) -> torch.Tensor:
+        """int32 [1] that iteration ``n_iter``'s decision writes this rank's
+        active pixel count to (two slots alternate: a decision never overwrites
+        a count a queued launch or compaction has still to read)."""
+        return self.px[n_iter % 2:n_iter % 2 + 1]
+
     def decide(self, n_iter: int, tol: float, min_iter: int, max_iter: int):
         """Per-chunk norms of the last launch's dn and the exit test; returns
         a pending read-back of (active chunks, largest norm, this rank's
-        active pixels, chunks stopped now).
+        active pixels, chunks stopped now), and leaves the pixel count in
+        :meth:`px_slot` too.
 
         The decision is rank-uniform (every rank sums the same gathered
         partials in rank order) but not rank-count invariant by construction:
@@ -159,19 +169,23 @@ class ChunkConvergence:
                              self.gpart, self.groups)
         part_all = self.comm.all_gather_vec(self.part)
         K.chunk_decide(part_all, self.comm.world, self.len_x, self.local_count, tol, n_iter, min_iter, max_iter,
-                       self.active, self.newly, self._iters, self.info)
-        return PendingSum(self.info, 1, 4)
+                       self.active, self.newly, self._iters, self.info, px_out=self.px_slot(n_iter))
+        # (a device result goes to its own pinned mailbox slot; the host runner's
+        # is copied, the next decision may run before this one is read)
+        return PendingSum(self.info if self.device.type == "cuda" else self.info.clone(), 1, 4)
 
-    def compact(self, order_in, n_in: int, n_out: int, x_src, x_dst):
+    def compact(self, order_in, n_in: int, n_out, x_src, x_dst, n_in_dev=None):
         """Visiting order of the next launch (the active chunks' pixels of
-        order_in[:n_in]); the stopped chunks' x copied x_src -> x_dst."""
+        order_in[:n_in]); the stopped chunks' x copied x_src -> x_dst.
+        ``n_in_dev``: order_in's slot count on the device (``n_in`` then only
+        bounds it); ``n_out`` (None: not read yet) checks the host runner."""
         out = self.orders[0]
         if order_in is not None and order_in.data_ptr() == out.data_ptr():
             out = self.orders[1]
         if n_in:
             got = K.chunk_compact(order_in, n_in, self.chunk_of, self.active, self.newly, self.scratch, out,
-                                  x_src, x_dst)
-            if got is not None and got != n_out:
+                                  x_src, x_dst, n_in_dev=n_in_dev)
+            if got is not None and n_out is not None and got != n_out:
                 raise RuntimeError(f"chunk_compact kept {got} pixels, chunk_decide counted {n_out}")
         return out
 

@@ -25,6 +25,13 @@ class EngineConfig:
     # 128^2) whose ||dx|| / len(x) is tested on its own, converged chunks frozen;
     # None: one test over the whole tile / strip set (the norm of one filter)
     convergence_chunk: list | None = None
+    # per-chunk loop past the first decision that keeps chunks iterating: up to
+    # this many further iterations are queued before their exit decisions are
+    # read (each launch reads its pixel count on the device; the launches past
+    # the real end visit nothing), so the host's read-back leaves the
+    # critical path of long tails (prosail10_hard: up to 26 iterations).  0: read
+    # every decision before the next launch
+    gn_lookahead: int = 2
     # analysis precision stored per date: "auto" keeps what the next forecast
     # reads (LAI propagator: the TLAI diagonal; prior reset: nothing) unless a
     # checkpoint is due, the date is the run's last, the output is not fused or
@@ -126,6 +133,9 @@ class EngineConfig:
             raise ValueError("band_parallel must be >= 1")
         if self.min_iterations < 1 or self.max_iterations < self.min_iterations:
             raise ValueError("bad iteration limits")
+        if int(self.gn_lookahead) < 0:
+            raise ValueError("gn_lookahead must be >= 0")
+        self.gn_lookahead = int(self.gn_lookahead)
         if self.store_precision not in ("auto", "always"):
             raise ValueError("store_precision must be 'auto' or 'always'")
         if isinstance(self.convergence_chunk, str) and self.convergence_chunk.strip().lower() in ("", "0", "tile",

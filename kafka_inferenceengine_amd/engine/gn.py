@@ -268,6 +268,13 @@ class GaussNewtonMixin:
             cc.begin()          # (normally queued at the end of the previous date, off this date's host path)
         n_iter, n_visit, vis, full = 1, N, order, True
         norms = []
+        # the tail past the first decision that keeps chunks iterating: up to
+        # ``gn_lookahead`` iterations queued ahead of the read-backs, each
+        # launch / compaction reading its pixel count on the device (n_dev);
+        # n_visit stays a host bound (the last count read: counts only shrink)
+        depth = cfg.gn_lookahead if not (run.bp or precomp) else 0
+        pending = []            # (iteration, its decision) not read yet
+        tail, n_dev, n_end = False, None, None
         while True:
             A_keep = P_out if n_iter >= cfg.min_iterations else None
             out_now = out_t if n_iter >= cfg.min_iterations else None
@@ -277,6 +284,8 @@ class GaussNewtonMixin:
             kw = dict(prop=prop, order=vis, dn_out=None if static else cc.dn)
             if not full:
                 kw["n_visit"] = n_visit
+                if n_dev is not None:
+                    kw["n_visit_dev"] = n_dev
             with self.timer.phase("analysis"):
                 if N and n_visit:
                     first2 = fuse and n_iter == 1
@@ -305,23 +314,40 @@ class GaussNewtonMixin:
                 n_iter += 1
                 continue
             with self.timer.phase("converge"):
-                pend = cc.decide(n_iter, cfg.convergence_tolerance, cfg.min_iterations, cfg.max_iterations)
+                pending.append((n_iter, cc.decide(n_iter, cfg.convergence_tolerance, cfg.min_iterations,
+                                                  cfg.max_iterations)))
             if self._lookahead_fn is not None:
                 self._lookahead_fn()
                 self._lookahead_fn = None
-            n_act, mx, px, n_new = (pend.result(j) for j in range(4))
-            n_act, px = int(n_act), int(px)
-            norms.append(float(mx))
-            LOG.info("Iteration # %d: %d of %d chunks converged, %d still iterating, largest chunk norm %g",
-                     n_iter, int(n_new), cc.tested, n_act, mx)
-            if n_act == 0:
+            read = None
+            # read the oldest decision unless the tail may queue one more iteration first
+            while pending and not (tail and len(pending) <= depth and n_iter <= cfg.max_iterations):
+                k, pend = pending.pop(0)
+                n_act, mx, px, n_new = (pend.result(j) for j in range(4))
+                n_act, px = int(n_act), int(px)
+                norms.append(float(mx))
+                LOG.info("Iteration # %d: %d of %d chunks converged, %d still iterating, largest chunk norm %g",
+                         k, int(n_new), cc.tested, n_act, mx)
+                if n_act == 0:
+                    n_end = k           # the later queued iterations (if any) visit nothing
+                    break
+                if k > cfg.max_iterations:      # chunk_decide bails every chunk out past max_iterations
+                    raise RuntimeError("per-chunk loop past max_iterations with active chunks")
+                read = (k, px)
+                tail = depth > 0
+            if n_end is not None:
                 break
-            if n_iter > cfg.max_iterations:      # chunk_decide bails every chunk out past max_iterations
-                raise RuntimeError("per-chunk loop past max_iterations with active chunks")
+            # queue iteration n_iter + 1: its pixel count is exact when this
+            # iteration's decision was just read, else on the device only
+            exact = read is not None and read[0] == n_iter
             with self.timer.phase("converge"):
-                vis = cc.compact(vis, n_visit if N else 0, px, x_prev, x_new)
-            n_visit, full = px, False
+                vis = cc.compact(vis, n_visit if N else 0, read[1] if exact else None, x_prev, x_new, n_in_dev=n_dev)
+            if read is not None:
+                n_visit = min(n_visit, read[1])
+            n_dev = None if exact else cc.px_slot(n_iter)
+            full = False
             n_iter += 1
+        n_iter = n_end
         def bail(hist, max_it=cfg.max_iterations):
             if max(hist or {0: 0}) > max_it:
                 LOG.warning("Bailing out after 25 iterations!!!!!!")

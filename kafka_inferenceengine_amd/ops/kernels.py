@@ -300,7 +300,7 @@ def gp_operator_supported(n_params, d) -> bool:
 def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=None, b_out=None, status=None,
              partials=None, N=None, solve=True, fast=True, variant=None, a_in=None, b_in=None, prop=None,
              out=None, reg=None, x0_out=None, gn_fused=1, partials_first=None, order=None, n_visit=None,
-             dn_out=None, a_rows=None):
+             dn_out=None, a_rows=None, n_visit_dev=None):
     """K1 fused Gauss-Newton analysis (information form).
 
     ``gn_fused=2`` runs two Gauss-Newton iterations in this launch: the first
@@ -330,7 +330,9 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     GP; each pixel's result is the same in any order (the per-workgroup norm
     partials sum different pixel sets).  ``n_visit``: visit only
     ``order[:n_visit]`` (the per-chunk Gauss-Newton loop's active pixels;
-    needs ``order``).
+    needs ``order``).  ``n_visit_dev`` (int32 [>= 1], device): the count to
+    visit read by the kernel itself (at most ``n_visit``, which then only
+    sizes the grid) -- a launch queued before the host has read the count.
 
     ``dn_out`` (float32 [N]): each visited pixel's |x - x0|^2 of the launch's
     last iteration, at its pixel index (per-chunk convergence norms).
@@ -346,7 +348,7 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     key = None
     if reg is None:
         key = (n_params, _table_key(bands), N, bool(solve), bool(fast),
-               DEFAULT_VARIANT if variant is None else variant, gn_fused, n_visit, a_rows,
+               DEFAULT_VARIANT if variant is None else variant, gn_fused, n_visit, _sig(n_visit_dev), a_rows,
                None if prop is None else (prop.device_copy().data_ptr(), prop.args.ld, prop.args.N, prop.fused,
                                           prop.device),
                _sig(x_prev), _sig(x_f), _sig(pf_inv), _sig(x_out), _sig(a_out), _sig(b_out), _sig(status),
@@ -469,6 +471,11 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
         if gn_fused != 1 or reg is not None:
             raise ValueError("n_visit: single-iteration launches without the regulariser")
         a.n_visit = nv
+    if n_visit_dev is not None:
+        if n_visit is None:
+            raise ValueError("n_visit_dev needs n_visit (the bound that sizes the grid)")
+        _check_vec(n_visit_dev, 1, "n_visit_dev", torch.int32, dev)
+        a.n_visit_dev = _ptr(n_visit_dev)
     if dn_out is not None:
         _check_vec(dn_out, N, "dn_out", torch.float32, dev)
         a.dn_out = _ptr(dn_out)
@@ -513,35 +520,42 @@ def chunk_partials(dn, seg_start, seg_len, lc_ptr, lc_gid, active, part, gpart, 
                          _ptr(active), _ptr(part), _ptr(gpart), int(groups), _dev(part), _stream(part))
 
 
-def chunk_decide(part_all, world, len_x, local_count, tol, n_iter, min_iter, max_iter, active, newly, iters, info):
+def chunk_decide(part_all, world, len_x, local_count, tol, n_iter, min_iter, max_iter, active, newly, iters, info,
+                 px_out=None):
     """The reference's exit test per chunk (linear_kf.py:297-304) on the
     all-gathered partials [world, nc]; info <- (active chunks, largest norm
-    tested, this rank's active pixels, chunks stopped now)."""
+    tested, this rank's active pixels, chunks stopped now); ``px_out`` (int32
+    [>= 1]) <- this rank's active pixels (the next launch's device count)."""
     nc = int(active.numel())
     if part_all.numel() != world * nc or len_x.numel() != nc or local_count.numel() != nc:
         raise ValueError("chunk_decide: inconsistent chunk vectors")
     ext().chunk_decide(_ptr(part_all), int(world), nc, _ptr(len_x), _ptr(local_count), float(tol), int(n_iter),
                        int(min_iter), int(max_iter), _ptr(active), _ptr(newly), _ptr(iters), _ptr(info),
-                       _dev(active), _stream(active))
+                       _ptr(px_out), _dev(active), _stream(active))
 
 
 def chunk_compact_scratch(n: int, device) -> torch.Tensor:
     return torch.empty(int(ext().chunk_compact_blocks(max(int(n), 1))) + 1, dtype=torch.int32, device=device)
 
 
-def chunk_compact(order_in, n_in, chunk_of, active, newly, counts, order_out, x_src=None, x_dst=None):
+def chunk_compact(order_in, n_in, chunk_of, active, newly, counts, order_out, x_src=None, x_dst=None, n_in_dev=None):
     """order_out <- the slots of order_in[:n_in] (None: 0..n_in-1) whose chunk
     is active, stable; x of the pixels whose chunk stopped now copied x_src ->
-    x_dst ([n_p, ld]).  Returns the kept count on the host runner, None on the
-    device (chunk_decide's info holds it)."""
+    x_dst ([n_p, ld]).  ``n_in_dev`` (int32 [>= 1]): the slot count read on the
+    device (at most ``n_in``, which then only sizes the grid).  Returns the
+    kept count on the host runner, None on the device (chunk_decide's info
+    holds it)."""
     n_in = int(n_in)
+    if n_in_dev is not None and (n_in_dev.dtype != torch.int32 or n_in_dev.device != chunk_of.device):
+        raise ValueError("chunk_compact: n_in_dev must be an int32 tensor on the chunk map's device")
     if order_in is not None and order_in.data_ptr() == order_out.data_ptr():
         raise ValueError("chunk_compact: order_out must not alias order_in")
     np_, ld = (0, 0) if x_src is None else (int(x_src.shape[0]), int(x_src.shape[1]))
     if x_src is not None and (x_dst is None or x_dst.shape != x_src.shape):
         raise ValueError("chunk_compact: x_src / x_dst of one shape")
     r = ext().chunk_compact(_ptr(order_in), n_in, _ptr(chunk_of), _ptr(active), _ptr(newly), _ptr(counts),
-                            _ptr(order_out), _ptr(x_src), _ptr(x_dst), np_, ld, _dev(chunk_of), _stream(chunk_of))
+                            _ptr(order_out), _ptr(x_src), _ptr(x_dst), np_, ld, _ptr(n_in_dev), _dev(chunk_of),
+                            _stream(chunk_of))
     return None if r < 0 else int(r)
 
 
@@ -584,7 +598,7 @@ def obs_order(bands: BandTable, N: int, device, out=None, scratch=None, groups=N
 
 def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status=None, partials=None, N=None,
          joseph=False, prop=None, out=None, fast=True, gn_fused=1, partials_first=None, order=None, n_visit=None,
-         dn_out=None, pdiag_rows=0):
+         dn_out=None, pdiag_rows=0, n_visit_dev=None):
     """K1g covariance/gain-form analysis (sequential scalar band updates).
 
     ``prop`` (:func:`prop_args` with ``fused=True`` over the analysis
@@ -596,8 +610,8 @@ def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status
 
     K1's launch features (:func:`analysis`): ``gn_fused=2`` runs iterations 1
     and 2 in this launch (the first iteration's norm partials to
-    ``partials_first``); ``order`` / ``n_visit`` the visiting order and the
-    per-chunk subset; ``dn_out`` every visited pixel's |x - x0|^2.
+    ``partials_first``); ``order`` / ``n_visit`` / ``n_visit_dev`` the visiting
+    order and the per-chunk subset; ``dn_out`` every visited pixel's |x - x0|^2.
     ``pdiag_rows`` (bit j): store only the analysis precision diagonal entries
     (P^-1)_jj of these parameters, into ``p_out`` rows tri(j, j) -- the rows a
     fused forecast with ``PropArgs.pa_pdiag`` reads (the stored-rows policy);
@@ -668,6 +682,11 @@ def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status
         if gn_fused != 1:
             raise ValueError("n_visit: single-iteration launches")
         a.n_visit = nv
+    if n_visit_dev is not None:
+        if n_visit is None:
+            raise ValueError("n_visit_dev needs n_visit (the bound that sizes the grid)")
+        _check_vec(n_visit_dev, 1, "n_visit_dev", torch.int32, dev)
+        a.n_visit_dev = _ptr(n_visit_dev)
     if dn_out is not None:
         _check_vec(dn_out, N, "dn_out", torch.float32, dev)
         a.dn_out = _ptr(dn_out)

@@ -103,3 +103,18 @@ def test_chunked_1024_hard_prosail_equals_farm(cuda):
     assert any(len(h) > 1 for h in hist), f"chunks should need different iteration counts: {hist}"
     assert worst <= 1e-5, worst
     print(f"per-chunk GN histograms {hist}; max |x - farm| {worst:g}")
+
+
+def test_chunk_tail_lookahead_on_device(cuda):
+    """The tail's queued iterations on the device (counts read by the
+    kernels, decisions read late) equal reading every decision first, and the
+    host runner."""
+    from test_chunks import _chunked_run, _mask
+
+    mask = _mask()
+    ref = _chunked_run(mask, 0, device=cuda)
+    got = _chunked_run(mask, 3, device=cuda, emulators=ref[-1])
+    assert max(ref[3]) > 4
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+    assert got[2] == ref[2] and got[3] == ref[3] and got[4] == ref[4]
+    assert np.array_equal(got[5], ref[5])
