@@ -156,9 +156,11 @@ def oracle_run_blocks(obs, state_mask, maps, time_grid, prior_mean, prior_cinv, 
     return x_a, A_a, iters
 
 
-def gp_predict64_torch(em, X, chunk=65536):
+def gp_predict64_torch(em, X, chunk=65536, f32=()):
     """gp_predict64 in float64 torch on X's device (the 1024^2 slice: ~10^9
-    kernel evaluations per band and iteration, minutes in NumPy)."""
+    kernel evaluations per band and iteration, minutes in NumPy).  ``f32``:
+    parts evaluated in float32 instead, to locate a float32 pipeline's loss
+    ("exponent": the squared distances; "sums": the kernel-weighted sums)."""
     import torch
 
     dev = X.device
@@ -174,9 +176,13 @@ def gp_predict64_torch(em, X, chunk=65536):
     for s in range(0, X.shape[0], chunk):
         Xc = X[s:s + chunk] - c
         xx = (Xc * Xc * lam).sum(1)
-        d2 = xx[:, None] + tt[None, :] - 2.0 * (Xc * lam) @ Tc.T
+        if "exponent" in f32:
+            Xf, Tf, lf = Xc.float(), Tc.float(), lam.float()
+            d2 = ((Xf * Xf * lf).sum(1)[:, None] + (Tf * Tf * lf).sum(1)[None, :] - 2.0 * (Xf * lf) @ Tf.T).double()
+        else:
+            d2 = xx[:, None] + tt[None, :] - 2.0 * (Xc * lam) @ Tc.T
         k = em.signal * torch.exp(-0.5 * torch.clamp(d2, min=0.0))
-        S = k @ B
+        S = (k.float() @ B.float()).double() if "sums" in f32 else k @ B
         H[s:s + chunk] = em.mean + S[:, 0]
         dH[s:s + chunk] = -lam * (Xc * S[:, :1] - S[:, 1:])
     return H, dH
@@ -184,7 +190,7 @@ def gp_predict64_torch(em, X, chunk=65536):
 
 def oracle_run_blocks_torch(obs, state_mask, maps, time_grid, prior_mean, prior_cinv, propagated=(6,), q=None,
                             tol=1e-3, min_iterations=2, max_iterations=25, x0=None, A0=None, device="cuda",
-                            cast_f32=False):
+                            cast_f32=False, gp_f32=()):
     """:func:`oracle_run_blocks` in float64 torch on ``device`` (same loop, same
     per-pixel normal equations, solved by batched float64 Cholesky): the
     oracle of the 1024^2 slice.  Returns (x [N, n], A [N, n, n], iters) on the
@@ -192,7 +198,8 @@ def oracle_run_blocks_torch(obs, state_mask, maps, time_grid, prior_mean, prior_
 
     ``cast_f32``: the reference's one precision loss -- its solver casts the
     normal equations to float32 and solves in single precision
-    (solvers.py:127-134); everything else stays float64."""
+    (solvers.py:127-134); everything else stays float64.  ``gp_f32``: GP parts
+    in float32 (:func:`gp_predict64_torch`)."""
     import torch
 
     dev = torch.device(device)
@@ -231,7 +238,7 @@ def oracle_run_blocks_torch(obs, state_mask, maps, time_grid, prior_mean, prior_
                 A = A_f.clone()
                 rhs = torch.einsum("nij,nj->ni", A_f, x_f)
                 for b, (y, w, em) in enumerate(raw):
-                    H0, dH = gp_predict64_torch(em, x_prev[:, list(maps[b])].contiguous())
+                    H0, dH = gp_predict64_torch(em, x_prev[:, list(maps[b])].contiguous(), f32=gp_f32)
                     h = torch.zeros((N, n), dtype=torch.float64, device=dev)
                     h[:, list(maps[b])] = dH
                     yp = y + (h * x_prev).sum(1) - H0
