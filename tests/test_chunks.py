@@ -154,24 +154,24 @@ def test_chunked_equals_farm_of_engines():
     assert all("chunk_iters" not in r for r in kf2.metrics.records)
 
 
-def _chunked_run(mask, lookahead, device="cpu", emulators=None):
-    kf, obs, prior = _engine(mask, {"convergence_chunk": [BLOCK, BLOCK], "gn_lookahead": lookahead},
-                             emulators=emulators, device=device)
+def _chunked_run(mask, lookahead, device="cpu", emulators=None, form="information"):
+    kf, obs, prior = _engine(mask, {"convergence_chunk": [BLOCK, BLOCK], "gn_lookahead": lookahead,
+                                    "analysis_form": form}, emulators=emulators, device=device)
     st = kf.run(GRID, kf.state_from_prior(prior), None, None)
     return (st.x[:, :st.N].cpu().numpy(), st.P[:, :st.N].cpu().numpy(), [h["chunk_iters"][0] for h in kf.history],
             [h["gn_iterations"][0] for h in kf.history], [h["norms"] for h in kf.history],
             kf._chunks.iters.cpu().numpy(), obs.emulators)
 
 
-@pytest.mark.parametrize("lookahead", [1, 3])
-def test_chunk_tail_lookahead_equals_reading_every_decision(lookahead):
+@pytest.mark.parametrize("lookahead,form", [(1, "information"), (3, "information"), (2, "gain")])
+def test_chunk_tail_lookahead_equals_reading_every_decision(lookahead, form):
     """The tail's queued iterations (EngineConfig.gn_lookahead: launches and
     compactions that read their pixel counts on the device, decisions read
     late) give the same states, precisions, per-chunk iteration counts and
     per-iteration norms as reading every decision before the next launch."""
     mask = _mask()
-    ref = _chunked_run(mask, 0)
-    got = _chunked_run(mask, lookahead, emulators=ref[-1])
+    ref = _chunked_run(mask, 0, form=form)
+    got = _chunked_run(mask, lookahead, emulators=ref[-1], form=form)
     assert max(ref[3]) > 4, "the problem should have a tail past the first decision"
     assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
     assert got[2] == ref[2] and got[3] == ref[3] and got[4] == ref[4]
