@@ -442,7 +442,7 @@ def main():
                                    "convergence": "per chunk" if ec.convergence_chunk else "tile",
                                    "store_precision": ec.store_precision, "observed_first": ec.observed_first,
                                    "fuse_gn": ec.fuse_gn, "analysis_form": ec.analysis_form,
-                                   "phase_telemetry": telemetry}
+                                   "line_tables": ec.line_tables, "phase_telemetry": telemetry}
         if chunk_hist:
             rec["config"]["convergence_chunk"] = kf.config.convergence_chunk
             rec["config"]["chunk_gn_histogram"] = {str(i): chunk_hist[i] for i in sorted(chunk_hist)}

@@ -141,6 +141,11 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(AnalysisArgs, reg_nbr, const int32_t*)
       .PTR_FIELD(AnalysisArgs, reg_v, float*)
       .PTR_FIELD(AnalysisArgs, x0_out, float*)
+      .PTR_FIELD(AnalysisArgs, line_tab, const float*)
+      .def_readwrite("line_t0", &AnalysisArgs::line_t0)
+      .def_readwrite("line_inv_h", &AnalysisArgs::line_inv_h)
+      .def_readwrite("line_n", &AnalysisArgs::line_n)
+      .def_readwrite("line_j", &AnalysisArgs::line_j)
       .GEO_FIELDS(AnalysisArgs, reg_geo);
 
   py::class_<GainArgs>(m, "GainArgs")
@@ -158,6 +163,11 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
       .PTR_FIELD(GainArgs, n_visit_dev, const int32_t*)
       .def_readwrite("pdiag_rows", &GainArgs::pdiag_rows)
       .PTR_FIELD(GainArgs, partials_first, double*)
+      .PTR_FIELD(GainArgs, line_tab, const float*)
+      .def_readwrite("line_t0", &GainArgs::line_t0)
+      .def_readwrite("line_inv_h", &GainArgs::line_inv_h)
+      .def_readwrite("line_n", &GainArgs::line_n)
+      .def_readwrite("line_j", &GainArgs::line_j)
       .PTR_FIELD(GainArgs, order, const int32_t*)
       .PTR_FIELD(GainArgs, dn_out, float*)
       .PTR_FIELD(GainArgs, prop, const PropArgs*)

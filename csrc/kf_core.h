@@ -325,6 +325,18 @@ struct AnalysisArgs {
   int32_t dom_check;
   float dom_lo[MAX_D];
   float dom_hi[MAX_D];
+  // Line tables (matrix-core kernels): the launch's first Gauss-Newton
+  // iteration is linearised at a partial-reset forecast (x_prev null), whose
+  // parameters other than the single propagated one (line_j; -1: none) are the
+  // reset mean for every pixel.  Each GP band's value and input gradient there
+  // are functions of x_f,j alone, tabulated on the host in float64 as cubic
+  // Hermite pieces over line_n intervals from line_t0 (spacing 1 / line_inv_h):
+  // [line_n][n_bands][D + 1][4] coefficients in s = (t - t_k) / h (value, then
+  // d/d input d).  A wave whose observed pixels all lie inside the table
+  // evaluates the polynomials instead of the GP sums (models/gp.py:line_table).
+  const float* line_tab;
+  float line_t0, line_inv_h;
+  int32_t line_n, line_j;
 };
 
 // slots visited by a launch: n_visit (0: N), or the device count (<= that bound)
@@ -1427,6 +1439,10 @@ struct GainArgs {
   // entries); 0: the full analysis covariance
   uint32_t pdiag_rows;
   int32_t pad_;
+  // line tables of the first iteration at the fused forecast (as AnalysisArgs.line_*)
+  const float* line_tab;
+  float line_t0, line_inv_h;
+  int32_t line_n, line_j;
 };
 
 KF_HD int64_t visit_count(const GainArgs& a) { return visit_bounded(a.n_visit, a.N, a.n_visit_dev); }
@@ -1587,8 +1603,8 @@ KF_HD float gain_finish(const GA& a, int64_t p, float (&x)[NP], float (&P)[ntri(
                         uint8_t st, int nobs, const float* dA);
 
 // One pixel of K1g over a.gn_fused (1 or 2) Gauss-Newton iterations.
-// EVAL(bi, x0, y, w, H0, h, ok) -> bool use: decodes band bi and, where it is
-// used, evaluates its operator at x0 (the matrix-core evaluator runs for the
+// EVAL(bi, it, x0, y, w, H0, h, ok) -> bool use: decodes band bi and, where it
+// is used, evaluates its operator at x0 (iteration it of the launch) (the matrix-core evaluator runs for the
 // whole wave: every lane calls it, act = false lanes included).  Iteration 2
 // restarts from the forecast linearised at iteration 1's x; the returned
 // |x - x0|^2 is the last iteration's, dn1 the first's.
@@ -1632,7 +1648,7 @@ KF_HD float gain_pixel(const GA& a, int64_t p, bool act, float& dn1, EVAL&& eval
     for (int bi = 0; bi < a.n_bands; ++bi) {
       float y, w, H0, h[NP];
       bool ok;
-      const bool use = eval(bi, x0, y, w, H0, h, ok);
+      const bool use = eval(bi, it, x0, y, w, H0, h, ok);
       if (use && !ok) st |= ST_BAD_OP;
       if (use && ok) {
         ++nobs;
@@ -1649,7 +1665,7 @@ KF_HD float gain_pixel(const GA& a, int64_t p, bool act, float& dn1, EVAL&& eval
 template <int NP, int FD = 0, int FOBS = 0>
 KF_HD float pixel_gain(const GainArgs& a, int64_t p, float& dn1) {
   const int64_t ld = a.ld;
-  return gain_pixel<NP>(a, p, true, dn1, [&](int bi, const float (&x0)[NP], float& y, float& w, float& H0,
+  return gain_pixel<NP>(a, p, true, dn1, [&](int bi, int, const float (&x0)[NP], float& y, float& w, float& H0,
                                              float (&h)[NP], bool& ok) -> bool {
     const BandDesc bd = cptr(a.bands)[bi];
     decode_obs<FOBS>(bd, p, y, w);

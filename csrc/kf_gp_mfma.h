@@ -437,6 +437,46 @@ __device__ __forceinline__ void gpm_patch_c(kf_h8 (&xb)[2][gpm_k_steps(D)], floa
   xb[1][KK] = __builtin_bit_cast(kf_h8, b1);
 }
 
+// Line tables (AnalysisArgs.line_* / GainArgs.line_*): the first Gauss-Newton
+// iteration at a partial-reset forecast sees every parameter but the
+// propagated one at the reset mean, so each band's GP value and gradient are
+// cubic pieces in that one parameter (models/gp.py:line_table).  line_pos finds
+// the lane's interval (in: x_f,j inside the table; outside, or not finite, the
+// wave takes the GP sums) and line_eval one band's D + 1 polynomials.
+struct LinePos {
+  const float* row;   // the interval's coefficients, band 0
+  float s;            // (t - t_k) / h in [0, 1]
+  bool in;
+};
+
+template <int NP, typename LA>
+__device__ __forceinline__ LinePos line_pos(const KF_CONST_AS LA* la, const float (&x0)[NP], int row_floats) {
+  const int n = la->line_n;
+  const float t = la->line_j >= 0 ? gather_state_u<NP>(x0, la->line_j) : la->line_t0;
+  const float u = (t - la->line_t0) * la->line_inv_h;
+  LinePos r;
+  r.in = u >= 0.f && u <= (float)n;
+  // clamped (NaN -> 0) so every lane's loads stay inside the table
+  const float uc = fminf(fmaxf(u, 0.f), (float)n);
+  const int k = min((int)uc, n - 1);
+  r.s = uc - (float)k;
+  r.row = la->line_tab + (int64_t)k * row_floats;
+  return r;
+}
+
+template <int D>
+__device__ __forceinline__ void line_eval(const float* row, float s, float& H0, float (&g)[D]) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const f4* r = (const f4*)row;
+  f4 c = r[0];
+  H0 = fmaf(fmaf(fmaf(c.w, s, c.z), s, c.y), s, c.x);
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    c = r[1 + d];
+    g[d] = fmaf(fmaf(fmaf(c.w, s, c.z), s, c.y), s, c.x);
+  }
+}
+
 #endif
 
 }  // namespace kf
@@ -609,6 +649,11 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
       gpm_operands<D>(sxi, 0.f, sxb, c0);
     }
   }
+  // the first iteration at the fused forecast: line tables when the host set
+  // them (the kernels specialised for the fused forecast only: SPEC_ANY is the
+  // first date's launch, without one, and the generic oracle, variant 18)
+  const bool line = SPEC != SPEC_ANY && it == 0 && !a.x_prev &&
+                    opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr())->line_tab;
   // one band: GP sums on the matrix cores, value and Jacobian, normal equations.
   // MKC: the band's map kind when known at compile time (LAYOUT), else -1
   auto band = [&](int bi, auto mkc) {
@@ -626,7 +671,21 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
     constexpr bool TIPK = NP == 7 && D == 4;
     const int mk = MKC >= 0 ? MKC : (TIPK ? bdp->map_kind : GPM_MAP_RUNTIME);
     const bool any = __any(use);
-    if (any) {
+    bool tabled = false;
+    if (any && line) {
+      // wave-uniform: every observed lane's x_f,j inside the table
+      const KF_CONST_AS AnalysisArgs* la =
+          opaque((const KF_CONST_AS AnalysisArgs*)__builtin_amdgcn_kernarg_segment_ptr());
+      const LinePos lp = line_pos<NP>(la, x0, a.n_bands * (D + 1) * 4);
+      if (__all(lp.in || !use)) {
+        line_eval<D>(lp.row + bi * (D + 1) * 4, lp.s, H0, g);
+        tabled = true;
+        ok = finitef(H0);
+#pragma unroll
+        for (int d = 0; d < D; ++d) ok = ok && finitef(g[d]);
+      }
+    }
+    if (any && !tabled) {
       float xi[D], c = 0.f;
       if (TIPK && mk == GPM_MAP_TIP_VIS) {
         gpm_inputs_const<NP, D, GPM_MAP_TIP_VIS>(bdp, x0, xi, c);
@@ -745,7 +804,7 @@ __device__ __forceinline__ float pixel_analysis_mfma(const AnalysisArgs& a, int6
 template <int NP, int D, int FOBS>
 __device__ __forceinline__ float pixel_gain_mfma(const GainArgs& a, int64_t p, bool act, const kf_h8* lds,
                                                  float& dn1) {
-  return gain_pixel<NP>(a, p, act, dn1, [&](int bi, const float (&x0)[NP], float& y, float& w, float& H0,
+  return gain_pixel<NP>(a, p, act, dn1, [&](int bi, int it, const float (&x0)[NP], float& y, float& w, float& H0,
                                             float (&h)[NP], bool& ok) -> bool {
     int off = 0;
     for (int bj = 0; bj < bi; ++bj) off += cptr(a.bands)[bj].gpm_nchunk * gpm_frags_per_chunk(D);
@@ -757,7 +816,32 @@ __device__ __forceinline__ float pixel_gain_mfma(const GainArgs& a, int64_t p, b
     for (int j = 0; j < NP; ++j) h[j] = 0.f;
     ok = false;
     const int nch = bdp->gpm_nchunk;
-    if (__any(use)) {
+    bool tabled = false;
+    const KF_CONST_AS GainArgs* la = opaque((const KF_CONST_AS GainArgs*)__builtin_amdgcn_kernarg_segment_ptr());
+    if (it == 0 && !a.x_prev && la->line_tab && __any(use)) {
+      // the first iteration at the fused forecast: line tables (pixel_analysis_mfma)
+      const LinePos lp = line_pos<NP>(la, x0, a.n_bands * (D + 1) * 4);
+      if (__all(lp.in || !use)) {
+        float g[D];
+        line_eval<D>(lp.row + bi * (D + 1) * 4, lp.s, H0, g);
+        const KF_CONST_AS BandDesc* q = opaque(bdp);
+        if (q->map_identity) {
+#pragma unroll
+          for (int d = 0; d < D && d < NP; ++d) h[d] = g[d];
+        } else {
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+#pragma unroll
+            for (int j = 0; j < NP; ++j) h[j] += (q->map[d] == j) ? g[d] : 0.f;
+          }
+        }
+        tabled = true;
+        ok = finitef(H0);
+#pragma unroll
+        for (int j = 0; j < NP; ++j) ok = ok && finitef(h[j]);
+      }
+    }
+    if (!tabled && __any(use)) {
       float xi[D], c = 0.f;
       gpm_inputs<NP, D>(bdp, x0, xi, c);
       c *= -0.5f * LOG2E;

@@ -242,7 +242,7 @@ def build_table(specs, obs_list, n_params, cache, device, h0_outs=None, pre=None
         dsc, kp = band_desc(spec, ob, n_params, cache, h0, ph0, ph)
         descs.append(dsc)
         keep += kp
-    return K.make_band_table(descs, device, keep)
+    return K.make_band_table(descs, device, keep, specs)
 
 
 def operator_table(specs, n_params, cache, device, aux=None) -> K.BandTable:

@@ -107,6 +107,9 @@ class EngineConfig:
     fuse_gn: bool = True                      # GN iterations 1 and 2 in one launch (iteration 1 can never
                                               # end the loop, linear_kf.py:297-304); plain fused path only
     fuse_output: bool = True                  # device outputs written by the final analysis iteration
+    line_tables: bool = True                  # first GN iteration at a fused partial-reset forecast from
+                                              # float64 cubic line tables instead of the GP sums (the
+                                              # forecast varies in one parameter only; models/gp.py)
     return_innovations: bool = False
     metrics_path: str | None = None           # JSONL metrics (per date / timestep)
     checkpoint_dir: str | None = None

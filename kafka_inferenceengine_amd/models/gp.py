@@ -319,7 +319,8 @@ def mfma_tables(records, n_pos_pairs: int, lam):
     out = np.zeros((nch, gpm_frags_per_chunk(D), 8), dtype=np.float16)
     for ch in range(nch):
         for kk in range(NK):
-            out[ch, 64 * kk:64 * (kk + 1)] = kexp[ch * 32 + (lane & 31)[:, None], 16 * kk + 8 * (lane >> 5)[:, None] + j]
+            out[ch, 64 * kk:64 * (kk + 1)] = kexp[ch * 32 + (lane & 31)[:, None],
+                                                  16 * kk + 8 * (lane >> 5)[:, None] + j]
         base = 64 * NK
         for qq in range(2):
             for hh in range(2):
@@ -367,6 +368,140 @@ def mfma_emulate(table, n_chunks: int, scale: float, D: int, xi, c):
         ml = (m - mh).astype(np.float16).astype(np.float64)
         S += (mh + ml) @ (A[0] + A[1]).T
     return S * (scale * np.exp2(cl_))[:, None]
+
+
+# --------------------------------------------------------------------------
+# line tables (csrc/kf_gp_mfma.h line_pos / line_eval)
+#
+# The first Gauss-Newton iteration of a date is linearised at the forecast
+# (linear_kf.py:253-262: x_prev = x_forecast).  Under a partial prior reset
+# (kf_tools.py:propagate_information_filter_LAI, the prior-only "propagator")
+# every parameter but the propagated one is the prior mean at every pixel, so
+# each band's H0 and dH/dx at the forecast are functions of one scalar t =
+# x_f,j.  The table holds those D + 1 functions as cubic Hermite pieces built
+# from float64 values and t-derivatives at the nodes; it is refined until the
+# midpoint error is below LINE_RTOL of the GP's term scale (sum |alpha_i k_i|),
+# i.e. well inside the float32 accumulation error of the GP sums it replaces.
+
+LINE_RTOL = 2e-8
+LINE_MIN_INTERVALS = 256
+LINE_MAX_INTERVALS = 8192
+
+
+def _gp_terms(spec, X):
+    """Per training point weights m [n, P] and input-gradient factors a [n, P, D]
+    of one GP band at inputs X [n, D] (f = offset + sum m, df/dx_d = sum m a_d):
+    from the float64 emulator when it exposes its parameters, else from the
+    band's float32 records (the values the VALU kernel reads)."""
+    em = getattr(spec, "emulator", None)
+    lam = np.asarray(spec.coef, dtype=np.float64)[:X.shape[1]]
+    if em is not None and all(hasattr(em, k) for k in ("inputs", "alpha", "lam", "signal", "mean")):
+        diff = X[:, None, :] - np.asarray(em.inputs, dtype=np.float64)[None]          # [n, P, D]
+        lam = np.asarray(em.lam, dtype=np.float64)
+        k = em.signal * np.exp(-0.5 * np.einsum("npd,d->np", diff * diff, lam))
+        return float(em.mean), k * np.asarray(em.alpha, dtype=np.float64)[None], -lam[None, None, :] * diff, lam
+    rec = np.asarray(spec.records, dtype=np.float64)
+    D = rec.shape[1] - 1
+    pts = rec.transpose(0, 2, 1).reshape(-1, D + 1)
+    sgn = np.where(np.arange(pts.shape[0]) < 2 * int(spec.gp_pos_pairs), 1.0, -1.0)
+    keep = pts[:, 0] > -1e29
+    L, B, sgn = pts[keep, 0], pts[keep, 1:], sgn[keep]
+    xi = X - np.asarray(spec.center, dtype=np.float64)[None, :D]
+    c = -0.5 * LOG2E * (xi * xi * lam[None]).sum(1)
+    m = sgn[None] * np.exp2(L[None] + xi @ B.T + c[:, None])
+    a = np.log(2.0) * B[None] - lam[None, None, :] * xi[:, None, :]
+    return float(spec.offset), m, a, lam
+
+
+def line_functions(spec, fixed, j: int, t):
+    """Value and input gradient of GP band ``spec`` along the forecast line and
+    their t-derivatives: ``F, dF [len(t), D+1]`` (column 0 = H0, 1 + d = dH/dx_d).
+    Inputs read the state through ``spec.state_map``; state j is t, every other
+    state its ``fixed`` value (j < 0: no input varies)."""
+    smap = [int(v) for v in spec.state_map]
+    D = len(smap)
+    t = np.asarray(t, dtype=np.float64)
+    e = np.array([1.0 if (j >= 0 and s == j) else 0.0 for s in smap])
+    X = np.empty((t.size, D))
+    for d, s in enumerate(smap):
+        X[:, d] = t if e[d] else float(fixed[s])
+    off, m, a, lam = _gp_terms(spec, X)
+    z = a @ e                                                  # [n, P]: d(log m)/dt
+    S0 = m.sum(1)
+    F = np.empty((t.size, D + 1))
+    dF = np.empty_like(F)
+    F[:, 0] = off + S0
+    F[:, 1:] = np.einsum("np,npd->nd", m, a)
+    dF[:, 0] = (m * z).sum(1)
+    dF[:, 1:] = np.einsum("np,npd->nd", m * z, a) - (lam * e)[None, :] * S0[:, None]
+    return F, dF, np.abs(m).sum(1)
+
+
+def line_range(specs, j: int, margin: float = 0.5):
+    """Table range of t = x_j: the training boxes of the inputs reading state j
+    (OperatorSpec.domain_lo/hi, centred) widened by ``margin`` of their width
+    per side; None when no band reads j or a box is unknown."""
+    lo, hi = np.inf, -np.inf
+    for sp in specs:
+        for d, s in enumerate(sp.state_map):
+            if int(s) != j:
+                continue
+            if sp.domain_lo is None or sp.domain_hi is None:
+                return None
+            a = float(sp.domain_lo[d]) + float(sp.center[d])
+            b = float(sp.domain_hi[d]) + float(sp.center[d])
+            lo, hi = min(lo, a), max(hi, b)
+    if not np.isfinite(lo) or not hi > lo:
+        return None
+    w = hi - lo
+    return lo - margin * w, hi + margin * w
+
+
+def line_table(specs, fixed, j: int):
+    """Cubic Hermite line tables of every band of ``specs`` (all GP with the same
+    input count D) for the kernels' first iteration at a partial-reset forecast:
+    ``(coef float32 [n, n_bands, D+1, 4], t0, inv_h, n)`` with coefficients of
+    s = (t - t_k) * inv_h in [0, 1] (c0 + s c1 + s^2 c2 + s^3 c3), or None
+    (no range, or the refinement limit reached).  ``fixed``: the forecast's
+    state for the reset parameters (the kernel's float32 reset mean)."""
+    if not specs:
+        return None
+    D = len(specs[0].state_map)
+    if j < 0:
+        # no propagated parameter: one constant point, one interval from t0 = 0
+        cols = [line_functions(sp, fixed, -1, np.zeros(1))[0][0] for sp in specs]
+        out = np.zeros((1, len(specs), D + 1, 4))
+        out[0, :, :, 0] = np.stack(cols)
+        return out.astype(np.float32), 0.0, 1.0, 1
+    rng = line_range(specs, j)
+    if rng is None:
+        return None
+    # t0 and the spacing (a power of two) exact in float32: the kernel's
+    # u = (t - t0) * inv_h then only rounds t - t0
+    t0 = float(np.float32(rng[0]))
+    t1 = rng[1]
+    h = 2.0 ** np.floor(np.log2((t1 - t0) / LINE_MIN_INTERVALS))
+    while True:
+        n = int(np.ceil((t1 - t0) / h))
+        if n > LINE_MAX_INTERVALS:
+            return None
+        nodes = t0 + h * np.arange(n + 1)
+        mids = nodes[:-1] + 0.5 * h
+        coef = np.empty((n, len(specs), D + 1, 4))
+        worst = 0.0
+        for b, sp in enumerate(specs):
+            F, dF, _ = line_functions(sp, fixed, j, nodes)
+            y0, y1, d0, d1 = F[:-1], F[1:], h * dF[:-1], h * dF[1:]
+            c = coef[:, b]
+            c[..., 0], c[..., 1] = y0, d0
+            c[..., 2] = 3.0 * (y1 - y0) - 2.0 * d0 - d1
+            c[..., 3] = 2.0 * (y0 - y1) + d0 + d1
+            Fm, _, scale = line_functions(sp, fixed, j, mids)
+            pm = c[..., 0] + 0.5 * c[..., 1] + 0.25 * c[..., 2] + 0.125 * c[..., 3]
+            worst = max(worst, float((np.abs(pm - Fm) / np.maximum(scale, 1e-300)[:, None]).max()))
+        if worst <= LINE_RTOL:
+            return coef.astype(np.float32), t0, float(1.0 / h), n
+        h *= 0.5
 
 
 # --------------------------------------------------------------------------

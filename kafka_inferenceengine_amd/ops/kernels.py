@@ -130,6 +130,7 @@ class BandTable:
     gpm_global: bool = False  # GP on the matrix cores, tables read from global memory (too large for LDS)
     layout: int = 0         # BAND_LAYOUT_*: a band layout the kernels know at compile time (0: runtime)
     dom: tuple | None = None  # GP domain box in state space (lo, hi lists; ST_OUT_OF_DOMAIN)
+    specs: tuple = ()       # the bands' OperatorSpecs (line tables of the first iteration at the forecast)
 
     @property
     def ptr(self) -> int:
@@ -226,7 +227,7 @@ def small_h2d(cpu: torch.Tensor, device) -> torch.Tensor:
     return cpu.pin_memory().to(device, non_blocking=True)
 
 
-def make_band_table(descs: list, device, keepalive=()) -> BandTable:
+def make_band_table(descs: list, device, keepalive=(), specs=()) -> BandTable:
     raw = ext().pack_band_descs(descs)
     cpu = torch.frombuffer(bytearray(raw), dtype=torch.uint8) if raw else torch.zeros(8, dtype=torch.uint8)
     buf = small_h2d(cpu, device)
@@ -255,7 +256,7 @@ def make_band_table(descs: list, device, keepalive=()) -> BandTable:
           and len({tuple(d.center[:fast_d]) for d in descs}) == 1):
         layout = BAND_LAYOUT_SHARED_X
     return BandTable(buf, len(descs), tuple(keepalive), fast_d, fast_obs, gpm_frags, gpm_global, layout,
-                     _state_domain(descs))
+                     _state_domain(descs), tuple(specs))
 
 
 def _state_domain(descs):
@@ -274,6 +275,60 @@ def _state_domain(descs):
             hi[j] = min(hi[j], float(dh[i]) + float(c[i]))
             any_ = True
     return (lo, hi) if any_ else None
+
+
+# ------------------------------------------------------ line tables
+# The matrix-core kernels' first Gauss-Newton iteration at a fused partial-reset
+# forecast reads every band's value and gradient from cubic line tables
+# (kf_gp_mfma.h line_pos / line_eval, models/gp.py:line_table) instead of
+# running the GP sums: at the forecast every parameter but the propagated one
+# is the reset mean.  On by default; tests and bench A/B switch it per call.
+LINE_TABLES = True
+_LINE_CACHE: dict = {}
+
+
+def _prop_single(mask: int):
+    """The one propagated parameter of a partial-reset forecast, -1 for none
+    (prior reset), None for several (no line)."""
+    mask = int(mask)
+    if mask == 0:
+        return -1
+    return mask.bit_length() - 1 if mask & (mask - 1) == 0 else None
+
+
+def line_fields(bands: BandTable, prop, n_params: int, dev):
+    """(table, t0, inv_h, n, j) of the launch's first iteration at the fused
+    forecast ``prop``, or None (no GP matrix-core bands, several propagated
+    parameters, no table range, or the host runner).  Built once per (band
+    specs, reset mean, j) in float64 and kept on the device."""
+    if dev.type != "cuda" or prop is None or bands.fast_d <= 0 or not bands.specs or \
+            not (bands.gpm_frags > 0 or bands.gpm_global):
+        return None
+    if any(getattr(sp, "kind", None) != OP_GP or len(sp.state_map) != bands.fast_d for sp in bands.specs):
+        return None
+    j = _prop_single(prop.args.prop_mask)
+    if j is None:
+        return None
+    fixed = tuple(float(v) for v in list(prop.args.reset_mean)[:n_params])
+    key = (tuple(id(sp) for sp in bands.specs), fixed, j, dev)
+    hit = _LINE_CACHE.get(key)
+    if hit is None:
+        from ..models.gp import line_table
+
+        r = line_table(list(bands.specs), np.asarray(fixed, dtype=np.float64), j)
+        tab = None if r is None else torch.from_numpy(np.ascontiguousarray(r[0])).to(dev)
+        if len(_LINE_CACHE) >= 32:
+            _LINE_CACHE.clear()
+        hit = _LINE_CACHE[key] = (bands.specs, None if r is None else (tab, r[1], r[2], r[3], j))
+    return hit[1]
+
+
+def _set_line(a, bands, prop, n_params, dev, x_prev, line):
+    if x_prev is not None or not (LINE_TABLES if line is None else line):
+        return
+    lf = line_fields(bands, prop, n_params, dev)
+    if lf is not None:
+        a.line_tab, a.line_t0, a.line_inv_h, a.line_n, a.line_j = _ptr(lf[0]), lf[1], lf[2], lf[3], lf[4]
 
 
 # ------------------------------------------------------------------ ops
@@ -300,7 +355,7 @@ def gp_operator_supported(n_params, d) -> bool:
 def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=None, b_out=None, status=None,
              partials=None, N=None, solve=True, fast=True, variant=None, a_in=None, b_in=None, prop=None,
              out=None, reg=None, x0_out=None, gn_fused=1, partials_first=None, order=None, n_visit=None,
-             dn_out=None, a_rows=None, n_visit_dev=None):
+             dn_out=None, a_rows=None, n_visit_dev=None, line=None):
     """K1 fused Gauss-Newton analysis (information form).
 
     ``gn_fused=2`` runs two Gauss-Newton iterations in this launch: the first
@@ -337,7 +392,9 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
     ``dn_out`` (float32 [N]): each visited pixel's |x - x0|^2 of the launch's
     last iteration, at its pixel index (per-chunk convergence norms).
     ``a_rows``: bit mask of the packed precision rows stored to ``a_out``
-    (None / 0: every row; EngineConfig.store_precision).
+    (None / 0: every row; EngineConfig.store_precision).  ``line``: the first
+    iteration at the fused forecast from line tables (:func:`line_fields`;
+    None: ``LINE_TABLES``).
 
     Launch memo: the engine's steady state repeats the same operands date
     after date (buffers alternate, arguments are memoised upstream), so a call
@@ -353,7 +410,8 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
                                           prop.device),
                _sig(x_prev), _sig(x_f), _sig(pf_inv), _sig(x_out), _sig(a_out), _sig(b_out), _sig(status),
                _sig(partials), _sig(a_in), _sig(b_in), _sig(x0_out), _sig(partials_first), _sig(order), _sig(dn_out),
-               None if out is None else (_sig(out[0]), _sig(out[1]), _sig(out[2])))
+               None if out is None else (_sig(out[0]), _sig(out[1]), _sig(out[2])),
+               LINE_TABLES if line is None else bool(line))
         hit = _ANALYSIS_MEMO.get(key)
         if hit is not None:
             a, grid = hit
@@ -485,6 +543,8 @@ def analysis(n_params, bands: BandTable, x_prev, x_f, pf_inv, x_out=None, a_out=
         if int(a_rows) >> nt:
             raise ValueError(f"a_rows has bits past the {nt} packed rows")
         a.a_rows = int(a_rows)
+    if fast:
+        _set_line(a, bands, prop, n_params, dev, x_prev, line)
     grid = grid_for(nv)
     if partials is not None and partials.numel() < grid:
         raise ValueError("partials must hold one entry per workgroup (partials_buffer)")
@@ -598,7 +658,7 @@ def obs_order(bands: BandTable, N: int, device, out=None, scratch=None, groups=N
 
 def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status=None, partials=None, N=None,
          joseph=False, prop=None, out=None, fast=True, gn_fused=1, partials_first=None, order=None, n_visit=None,
-         dn_out=None, pdiag_rows=0, n_visit_dev=None):
+         dn_out=None, pdiag_rows=0, n_visit_dev=None, line=None):
     """K1g covariance/gain-form analysis (sequential scalar band updates).
 
     ``prop`` (:func:`prop_args` with ``fused=True`` over the analysis
@@ -615,7 +675,8 @@ def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status
     ``pdiag_rows`` (bit j): store only the analysis precision diagonal entries
     (P^-1)_jj of these parameters, into ``p_out`` rows tri(j, j) -- the rows a
     fused forecast with ``PropArgs.pa_pdiag`` reads (the stored-rows policy);
-    0 stores the full covariance."""
+    0 stores the full covariance.  ``line``: line tables for the first
+    iteration at the fused forecast, as :func:`analysis`."""
     check_np(n_params)
     ref = next(t for t in (x_prev, x_f, x_out) if t is not None)
     N = int(ref.shape[1] if N is None else N)
@@ -694,6 +755,8 @@ def gain(n_params, bands: BandTable, x_prev, x_f, p_f, x_out, p_out=None, status
         if int(pdiag_rows) >> n_params:
             raise ValueError(f"pdiag_rows has bits past the {n_params} parameters")
         a.pdiag_rows = int(pdiag_rows)
+    if a.gpm_frags > 0:
+        _set_line(a, bands, prop, n_params, dev, x_prev, line)
     grid = grid_for(nv)
     ext().gain(n_params, a, grid, _dev(ref), _stream(ref))
     _set_valid(partials, grid)

@@ -101,3 +101,65 @@ def test_table_point_order_cuts_f32_accumulation_error():
     (hg, gg), (ho, go) = err(grouped), err(ordered)
     assert ho < hg / 4 and go < gg / 3, (hg, gg, ho, go)
     assert ho < 4e-6 and go < 1e-5, (ho, go)
+
+
+# --------------------------------------------------------------- line tables
+def _tip_line_specs():
+    import kafka_inferenceengine_amd as k
+
+    ems = gp.make_tip_emulators(500, 0)
+    return [k.gp_spec(ems[b], k.TIP_BAND_MAPPER[b]) for b in (0, 1)], np.asarray(k.tip_prior()[0], np.float32)
+
+
+def _eval_f32(tab, t):
+    """The kernels' arithmetic (line_pos / line_eval) in float32."""
+    coef, t0, inv_h, n = tab
+    t = np.asarray(t, np.float32)
+    u = (t - np.float32(t0)) * np.float32(inv_h)
+    uc = np.minimum(np.maximum(u, np.float32(0)), np.float32(n))
+    kk = np.minimum(uc.astype(np.int64), n - 1)
+    s = (uc - kk.astype(np.float32))[:, None, None]
+    c = coef[kk]
+    return ((c[..., 3] * s + c[..., 2]) * s + c[..., 1]) * s + c[..., 0]
+
+
+def test_line_table_matches_float64_gp():
+    """The JRC-TIP bands along the LAI propagator's forecast line: the float32
+    evaluation of the cubic pieces equals the float64 GP value and gradient to
+    a few 1e-8 of the GP's term scale over the whole table, on the emulator's
+    parameters and on its float32 records alike."""
+    specs, fixed = _tip_line_specs()
+    tab = gp.line_table(specs, fixed, 6)
+    assert tab is not None
+    coef, t0, inv_h, n = tab
+    assert coef.shape == (n, 2, 5, 4) and np.float32(t0) == t0 and np.log2(inv_h).is_integer()
+    t = np.random.default_rng(0).uniform(t0, t0 + n / inv_h, 20000).astype(np.float32)
+    p = _eval_f32(tab, t)
+    for b, sp in enumerate(specs):
+        F, _, scale = gp.line_functions(sp, fixed, 6, t.astype(np.float64))
+        assert (np.abs(p[:, b] - F) / scale[:, None]).max() < 1e-7
+        rec = gp.line_functions(type("S", (), dict(vars(sp), emulator=None))(), fixed, 6, t[:200].astype(np.float64))
+        assert (np.abs(rec[0] - F[:200]) / scale[:200, None]).max() < 1e-6
+    # every band input reading state 6 is covered (training box + margin)
+    lo = min(sp.domain_lo[d] + sp.center[d] for sp in specs for d, s in enumerate(sp.state_map) if s == 6)
+    assert t0 < lo
+
+
+def test_line_table_derivatives_and_constant_point():
+    """The tabulated t-derivatives are the GP's (finite differences), and with
+    nothing propagated the table is one constant interval at the reset mean."""
+    specs, fixed = _tip_line_specs()
+    t = np.array([0.2, 0.45, 0.8])
+    F, dF, _ = gp.line_functions(specs[1], fixed, 6, t)
+    e = 1e-5
+    Fp, _, _ = gp.line_functions(specs[1], fixed, 6, t + e)
+    Fm, _, _ = gp.line_functions(specs[1], fixed, 6, t - e)
+    assert np.allclose((Fp - Fm) / (2 * e), dF, rtol=1e-6, atol=1e-8)
+    x = np.tile(fixed.astype(np.float64), (3, 1))
+    x[:, 6] = t
+    H, dH = specs[1].emulator.predict(x[:, specs[1].state_map])
+    assert np.allclose(F[:, 0], H, rtol=0, atol=1e-12) and np.allclose(F[:, 1:], dH, rtol=0, atol=1e-12)
+    coef, t0, inv_h, n = gp.line_table(specs, fixed, -1)
+    assert n == 1 and t0 == 0.0 and not coef[..., 1:].any()
+    H0, dH0 = specs[0].emulator.predict(fixed[specs[0].state_map].astype(np.float64)[None])
+    assert np.isclose(coef[0, 0, 0, 0], H0[0], rtol=1e-7) and np.allclose(coef[0, 0, 1:, 0], dH0[0], rtol=1e-6)

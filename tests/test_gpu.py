@@ -431,7 +431,8 @@ def test_specialised_prosail_kernel_equals_generic_gpu(cuda):
     mask = np.ones((64, 80), bool)
     grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=5 * i) for i in range(4)]
     outs = []
-    old = K.DEFAULT_VARIANT
+    old, old_line = K.DEFAULT_VARIANT, K.LINE_TABLES
+    K.LINE_TABLES = False   # variant 18 has no line tables (kf_gp_mfma.h)
     try:
         for variant in (0, 18):
             K.DEFAULT_VARIANT = variant
@@ -444,7 +445,7 @@ def test_specialised_prosail_kernel_equals_generic_gpu(cuda):
                         kf.state_from_prior(prior), None, None)
             outs.append((st.x.cpu(), st.P.cpu(), [h.get("norms") for h in kf.history]))
     finally:
-        K.DEFAULT_VARIANT = old
+        K.DEFAULT_VARIANT, K.LINE_TABLES = old, old_line
     assert outs[0][2] == outs[1][2]
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
@@ -462,7 +463,8 @@ def test_specialised_tip_kernel_equals_generic_gpu(cuda, spatial, n_train):
     grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
     reg = dict(spatial_gamma=5.0, spatial_params=[6]) if spatial else {}
     outs = []
-    old = K.DEFAULT_VARIANT
+    old, old_line = K.DEFAULT_VARIANT, K.LINE_TABLES
+    K.LINE_TABLES = False   # variant 18 has no line tables (kf_gp_mfma.h)
     try:
         for variant in (0, 18):
             K.DEFAULT_VARIANT = variant
@@ -477,7 +479,7 @@ def test_specialised_tip_kernel_equals_generic_gpu(cuda, spatial, n_train):
             outs.append((st.x.cpu(), st.P.cpu(), [h.get("norms") for h in kf.history],
                          {t: (m.cpu(), u.cpu()) for t, (m, u) in out.history.items()}))
     finally:
-        K.DEFAULT_VARIANT = old
+        K.DEFAULT_VARIANT, K.LINE_TABLES = old, old_line
     (xa, Pa, na, ha), (xb, Pb, nb, hb) = outs
     assert na == nb and torch.equal(xa, xb) and torch.equal(Pa, Pb)
     for t in ha:
