@@ -194,7 +194,7 @@ class GaussNewtonMixin:
             fx, fP = (None, None) if prop is not None else (fc.x, fc.P)
             K.gain(n, run.table, x_prev, fx, fP, x_new, run.P_out, run.status, self._partials, N=N,
                    joseph=self.config.joseph, prop=prop, out=run.out_t, gn_fused=2, partials_first=self._partials1,
-                   order=run.order, pdiag_rows=run.pdiag_rows, line=self.config.line_tables)
+                   order=run.order, pdiag_rows=run.pdiag_rows, line=self._line_opt)
         elif run.fuse_sp:
             self._regularised_iteration(run.table, x_prev, fc, x_new, run.P_out, run.status, prop, run.out_t,
                                         final=True, partials_first=self._partials1, a_rows=run.a_rows)
@@ -202,7 +202,7 @@ class GaussNewtonMixin:
             K.analysis(n, run.table, x_prev, None if prop is not None else fc.x, None if prop is not None else fc.P,
                        x_new, run.P_out, None, run.status, self._partials, N=N, prop=prop, out=run.out_t,
                        gn_fused=2, partials_first=self._partials1, order=run.order, a_rows=run.a_rows,
-                       line=self.config.line_tables)
+                       line=self._line_opt)
 
     def _launch_iteration(self, run: "_GNRun", n_iter, x_prev, x_new, A_keep, out_now):
         """One Gauss-Newton iteration's device work, by mode: the gain form
@@ -215,11 +215,11 @@ class GaussNewtonMixin:
         if run.gain:
             K.gain(n, table, x_prev, fx, fP, x_new, A_keep, run.status, self._partials, N=N, joseph=cfg.joseph,
                    prop=prop, out=out_now, order=run.order, pdiag_rows=run.pdiag_rows if A_keep is not None else 0,
-                   line=self.config.line_tables)
+                   line=self._line_opt)
         elif run.first_plain and n_iter == 1:
             # the unfused form of fuse_sp's first iteration (same kernel path)
             K.analysis(n, table, x_prev, fx, fP, x_new, None, None, run.status, self._partials, N=N, prop=prop,
-                       order=run.order, line=self.config.line_tables)
+                       order=run.order, line=self._line_opt)
             self._reg_log.append({"solver": "plain", "rho": 0.0, "sweeps": 0, "r2": None, "count": 0})
         elif cfg.spatial_gamma > 0:
             self._regularised_iteration(table, x_prev, fc, x_new, A_keep, run.status, prop, out_now,
@@ -230,7 +230,7 @@ class GaussNewtonMixin:
             self._split_iteration(run.split, x_prev, fc, x_new, A_keep, run.status)
         else:
             K.analysis(n, table, x_prev, fx, fP, x_new, A_keep, None, run.status, self._partials, N=N, prop=prop,
-                       out=out_now, order=run.order, a_rows=run.a_rows, line=self.config.line_tables)
+                       out=out_now, order=run.order, a_rows=run.a_rows, line=self._line_opt)
 
     def _chunk_state(self):
         from .chunks import ChunkConvergence
@@ -298,13 +298,13 @@ class GaussNewtonMixin:
                         K.gain(n, table, x_prev, fx, fP, x_new, P_out if first2 else A_keep, status, None, N=N,
                                joseph=cfg.joseph, out=out_t if first2 else out_now, gn_fused=2 if first2 else 1,
                                pdiag_rows=run.pdiag_rows if (first2 or A_keep is not None) else 0, **kw,
-                               line=self.config.line_tables)
+                               line=self._line_opt)
                     elif first2:
                         K.analysis(n, table, x_prev, fx, fP, x_new, P_out, None, status, None, N=N, out=out_t,
-                                   gn_fused=2, a_rows=a_rows, **kw, line=self.config.line_tables)
+                                   gn_fused=2, a_rows=a_rows, **kw, line=self._line_opt)
                     else:
                         K.analysis(n, table, x_prev, fx, fP, x_new, A_keep, None, status, None, N=N, out=out_now,
-                                   a_rows=a_rows, **kw, line=self.config.line_tables)
+                                   a_rows=a_rows, **kw, line=self._line_opt)
             if n_iter == 1:
                 cc.resolve()    # the previous dates' histograms, under this launch (read-backs done long ago)
             if fuse and n_iter == 1:

@@ -465,6 +465,12 @@ class LinearKalman(GaussNewtonMixin, SpatialPriorMixin):
             return materialize()
         return LazyForecast(src, d, None, self._q_pix, materialize, kind=COVARIANCE, cache=self._prop_bufs)
 
+    @property
+    def _line_opt(self):
+        """The launches' ``line`` option: EngineConfig.line_tables False turns the
+        line tables off; True leaves them to ops.kernels.LINE_TABLES (on)."""
+        return None if self.config.line_tables else False
+
     def _analysis_kind(self):
         return COVARIANCE if self.config.analysis_form == "gain" else PRECISION
 

@@ -69,7 +69,7 @@ class SpatialPriorMixin:
         if not rows:   # nothing regularised: plain analysis
             K.analysis(n, table, x_prev, fx, fP, x_out, A_out, None, status, self._partials, N=N, prop=prop, out=out,
                        gn_fused=2 if fused else 1, partials_first=partials_first, order=self._visit, a_rows=a_rows,
-                       line=self.config.line_tables)
+                       line=self._line_opt)
             return
         k = len(rows)
         ld = x_out.shape[1]
@@ -85,7 +85,7 @@ class SpatialPriorMixin:
                    x0_out=None if x_ref is x_prev else x0_buf,
                    out=None if out is None else (None, out[1], out[2]),
                    gn_fused=2 if fused else 1, partials_first=partials_first, order=self._visit, a_rows=a_rows,
-                   line=self.config.line_tables)
+                   line=self._line_opt)
         if fused:
             self._reg_log.append({"solver": "plain", "rho": 0.0, "sweeps": 0, "r2": None, "count": 0})
         nbr = None if geo else reg.nbr

@@ -38,7 +38,7 @@ def test_line_first_iteration_h0_against_float64(cuda, pmask):
     float32 rounding, and is at least as close as the GP sums on the matrix
     cores (LAI propagator: TLAI varies, the rest at the prior mean; prior
     reset: one point for every pixel)."""
-    prob = C.tip_problem(N=20000, seed=4, n_train=500)
+    prob = C.tip_problem(N=20000, seed=4, n_train=500, dn16=True)   # DN16: the SPEC_PROP kernels
     n, N = prob["n"], prob["N"]
     mu, _, Pi = k.tip_prior()
     rng = np.random.default_rng(4)
@@ -91,32 +91,29 @@ def test_line_tables_engine_runs_close_to_gp_sums(cuda, cfg):
     mask[10:30, 40:90] = False
     outs = []
     for line in (True, False):
-        old = K.LINE_TABLES
-        K.LINE_TABLES = line
-        try:
-            if cfg == "tip":
-                grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
-                obs = k.SyntheticBHRObservations(mask, n_train=500, device=cuda, stream=False, n_pool=3, field_cell=8)
-                kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS,
-                                    device=cuda, state_propagation=k.propagate_information_filter_LAI)
-                kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
-                st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
-            else:
-                grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=5 * i) for i in range(4)]
-                obs = k.SyntheticS2Observations(mask, dates=grid, n_bands=10, n_train=250, device=cuda, stream=False,
-                                                n_pool=2)
-                prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
-                kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
-                                    state_propagation=None, prior=prior, device=cuda)
-                st = kf.run([grid[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in grid],
-                            kf.state_from_prior(prior), None, None)
-            torch.cuda.synchronize()
-            outs.append((st.x[:, :st.N].cpu().numpy(), [h.get("gn_iterations") for h in kf.history],
-                         kf.last_status[:st.N].cpu().numpy()))
-        finally:
-            K.LINE_TABLES = old
+        cfg_e = k.EngineConfig(line_tables=line)
+        if cfg == "tip":
+            grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
+            obs = k.SyntheticBHRObservations(mask, n_train=500, device=cuda, stream=False, n_pool=3, field_cell=8)
+            kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS,
+                                device=cuda, state_propagation=k.propagate_information_filter_LAI, config=cfg_e)
+            kf.set_trajectory_uncertainty(np.array([0, 0, 0, 0, 0, 0, 0.04]))
+            st = kf.run(grid, kf.state_from_prior(k.JRCPrior(k.TIP_PARAMETERS, mask)), None, None)
+        else:
+            grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=5 * i) for i in range(4)]
+            obs = k.SyntheticS2Observations(mask, dates=grid, n_bands=10, n_train=250, device=cuda, stream=False,
+                                            n_pool=2)
+            prior = k.SAILPrior(k.SAIL_PARAMETERS, mask)
+            kf = k.LinearKalman(obs, None, mask, k.create_prosail_observation_operator, k.SAIL_PARAMETERS,
+                                state_propagation=None, prior=prior, device=cuda, config=cfg_e)
+            st = kf.run([grid[0] - dt.timedelta(days=1)] + [d + dt.timedelta(days=1) for d in grid],
+                        kf.state_from_prior(prior), None, None)
+        torch.cuda.synchronize()
+        outs.append((st.x[:, :st.N].cpu().numpy(), [h.get("gn_iterations") for h in kf.history],
+                     kf.last_status[:st.N].cpu().numpy()))
     (xa, ia, sa), (xb, ib, sb) = outs
     assert ia == ib
     assert np.isfinite(xa).all()
+    assert not np.array_equal(xa, xb)      # the line path ran (first iteration differs in the last bits)
     ok = (sa & K.ST_FALLBACK) == 0
     assert np.abs(xa - xb)[:, ok].max() < 2e-3, np.abs(xa - xb)[:, ok].max()
