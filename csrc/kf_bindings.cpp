@@ -362,8 +362,8 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
   });
   // per-chunk Gauss-Newton convergence (kf_core.h ChunkPartialArgs ...)
   m.def("chunk_partials", [](uintptr_t dn, uintptr_t seg_start, uintptr_t seg_len, uintptr_t lc_ptr, uintptr_t lc_gid,
-                             int n_local, uintptr_t active, uintptr_t part, uintptr_t gpart, int groups, bool device,
-                             uintptr_t stream) {
+                             int n_local, uintptr_t active, uintptr_t part, uintptr_t gpart, int groups,
+                             uintptr_t qinv, int64_t clamp, bool device, uintptr_t stream) {
     ChunkPartialArgs a{};
     a.dn = P<const float>(dn);
     a.seg_start = P<const int32_t>(seg_start);
@@ -372,17 +372,20 @@ PYBIND11_MODULE(KF_MODULE_NAME, m) {
     a.lc_gid = P<const int32_t>(lc_gid);
     a.n_local = n_local;
     a.active = P<const uint8_t>(active);
-    a.part = P<double>(part);
-    a.gpart = P<double>(gpart);
+    a.part = P<int64_t>(part);
+    a.gpart = P<int64_t>(gpart);
     a.groups = groups;
+    a.qinv = P<const double>(qinv);
+    a.clamp = clamp;
     if (device) check_hip(dev_chunk_partials(a, (hipStream_t)stream), "chunk_partials");
     else host_chunk_partials(a);
   });
   m.def("chunk_decide", [](uintptr_t part_all, int world, int nc, uintptr_t len_x, uintptr_t local_count, double tol,
                            int n_iter, int min_iter, int max_iter, uintptr_t active, uintptr_t newly, uintptr_t iters,
-                           uintptr_t info, uintptr_t px_out, bool device, uintptr_t stream) {
+                           uintptr_t info, uintptr_t px_out, double unit, bool device, uintptr_t stream) {
     ChunkDecideArgs a{};
-    a.part_all = P<const double>(part_all);
+    a.part_all = P<const int64_t>(part_all);
+    a.unit = unit;
     a.world = world;
     a.nc = nc;
     a.len_x = P<const double>(len_x);

@@ -2397,13 +2397,27 @@ struct ChunkPartialArgs {
   const int32_t* lc_gid;     // [n_local] global chunk id (get_chunks order, 0-based)
   int32_t n_local;
   const uint8_t* active;     // [nc] chunks still iterating (frozen ones are skipped)
-  double* part;              // [nc] this rank's sum per global chunk
-  double* gpart;             // [n_local * groups] scratch: the group totals
+  int64_t* part;             // [nc] this rank's sum per global chunk, in quanta (chunk_quant)
+  int64_t* gpart;            // [n_local * groups] scratch: the group totals
   int32_t groups;            // >= ceil(runs / CHUNK_GROUP_RUNS) of every local chunk
+  const double* qinv;        // [nc] quanta per unit of |dx|^2 of each chunk (engine/chunks.py:quantum)
+  int64_t clamp;             // largest quanta one pixel contributes (twice the exit threshold)
 };
 
+// One pixel's |dx|^2 in integer quanta of its chunk's squared norm: the sums
+// are exact, so a chunk's total (and its exit test) does not depend on how
+// the strips of the ranks cut it, nor on the order of the adds -- 1, 4 and 8
+// ranks decide alike by construction.  A pixel at or above the clamp (twice
+// the chunk's threshold on its own), or NaN, counts as the clamp: the chunk
+// does not stop, as the reference's ``norm < tol`` is false for it.
+KF_HD int64_t chunk_quant(float dn, double qinv, int64_t clamp) {
+  const double v = (double)dn * qinv;
+  if (!(v < (double)clamp)) return clamp;
+  return (int64_t)(v + 0.5);
+}
+
 struct ChunkDecideArgs {
-  const double* part_all;    // [world][nc] all ranks' partials (all-gathered)
+  const int64_t* part_all;   // [world][nc] all ranks' partials in quanta (all-gathered)
   int32_t world, nc;
   const double* len_x;       // [nc] n_params x active pixels of the chunk (all ranks)
   const int32_t* local_count;  // [nc] this rank's pixels of the chunk
@@ -2415,6 +2429,7 @@ struct ChunkDecideArgs {
   double* info;              // [4] chunks still active (all ranks), largest norm tested, this rank's active
                              // pixels, chunks stopped at this iteration
   int32_t* px_out;           // null, or this rank's active pixels as an int (the next launch's device count)
+  double unit;               // squared chunk norm ||dx||^2 / len_x^2 of one quantum
 };
 
 // the reference's exit test (linear_kf.py:297-304) for one chunk

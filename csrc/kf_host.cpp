@@ -262,38 +262,19 @@ int host_obs_order(const BandDesc* bands, const int32_t* grp, int nb, int G, int
   }
   return 0;
 }
-// Per-chunk Gauss-Newton convergence: the device kernels' arithmetic in the
-// same order (per group of CHUNK_GROUP_RUNS runs: thread-strided f64 sums, the
-// xor shuffle tree of wave_sum, the wave sums in order; then the group totals
-// in order), so a chunk's sum is bit-identical on both paths.
+// Per-chunk Gauss-Newton convergence: each pixel's |dx|^2 in integer quanta
+// of its chunk (chunk_quant) summed exactly, as on the device (any order
+// gives the same total).
 int host_chunk_partials(const ChunkPartialArgs& a) {
-  constexpr int T = HBLOCK;
 #pragma omp parallel for schedule(dynamic, 1)
   for (int c = 0; c < a.n_local; ++c) {
     const int g = a.lc_gid[c];
     if (!a.active[g]) continue;
-    double tot = 0.0;
-    for (int s0 = a.lc_ptr[c]; s0 < a.lc_ptr[c + 1]; s0 += CHUNK_GROUP_RUNS) {
-      const int s1 = std::min(s0 + CHUNK_GROUP_RUNS, a.lc_ptr[c + 1]);
-      double acc[T];
-      for (int t = 0; t < T; ++t) acc[t] = 0.0;
-      for (int sg = s0; sg < s1; ++sg) {
-        const int st = a.seg_start[sg], len = a.seg_len[sg];
-        for (int t = 0; t < T; ++t)
-          for (int i = t; i < len; i += T) acc[t] += (double)a.dn[st + i];
-      }
-      double gt = 0.0;
-      for (int w = 0; w < T / 64; ++w) {
-        double v[64];
-        for (int l = 0; l < 64; ++l) v[l] = acc[64 * w + l];
-        for (int off = 32; off > 0; off >>= 1) {
-          double nv[64];
-          for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
-          for (int l = 0; l < 64; ++l) v[l] = nv[l];
-        }
-        gt += v[0];
-      }
-      tot += gt;
+    const double qi = a.qinv[g];
+    int64_t tot = 0;
+    for (int sg = a.lc_ptr[c]; sg < a.lc_ptr[c + 1]; ++sg) {
+      const int st = a.seg_start[sg], len = a.seg_len[sg];
+      for (int i = 0; i < len; ++i) tot += chunk_quant(a.dn[st + i], qi, a.clamp);
     }
     a.part[g] = tot;
   }
@@ -307,9 +288,9 @@ int host_chunk_decide(const ChunkDecideArgs& a) {
     const bool was = a.active[g] != 0;
     bool stop = false;
     if (was) {
-      double tot = 0.0;
+      int64_t tot = 0;
       for (int r = 0; r < a.world; ++r) tot += a.part_all[(int64_t)r * a.nc + g];
-      const double norm = sqrt(tot > 0.0 ? tot : 0.0) / a.len_x[g];
+      const double norm = sqrt((double)tot * a.unit);
       mx = std::max(mx, norm);
       stop = chunk_stops(norm, a.n_iter, a.min_iter, a.max_iter, a.tol);
     }

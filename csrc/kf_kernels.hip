@@ -407,28 +407,28 @@ __global__ __launch_bounds__(BLOCK) void chunk_group_kernel(ChunkPartialArgs a) 
   __syncthreads();
   bool short_runs = true;     // every run within one element per thread (chunk width <= 256)
   for (int k = 0; k < n; ++k) short_runs = short_runs && slen[k] <= BLOCK;
-  double acc = 0.0;
+  const double qi = a.qinv[g];
+  const int64_t cl = a.clamp;
+  // integer quanta (chunk_quant): exact sums, any order
+  int64_t acc = 0;
   if (short_runs) {
-    // all the group's loads in flight before the adds (in run order: the same sums)
+    // all the group's loads in flight before the adds
     float v[CHUNK_GROUP_RUNS];
 #pragma unroll
     for (int k = 0; k < CHUNK_GROUP_RUNS; ++k) v[k] = (k < n && t < slen[k]) ? a.dn[sst[k] + t] : 0.f;
 #pragma unroll
     for (int k = 0; k < CHUNK_GROUP_RUNS; ++k)
-      if (k < n && t < slen[k]) acc += (double)v[k];
+      if (k < n && t < slen[k]) acc += chunk_quant(v[k], qi, cl);
   } else {
     for (int k = 0; k < n; ++k)
-      for (int i = t; i < slen[k]; i += BLOCK) acc += (double)a.dn[sst[k] + i];
+      for (int i = t; i < slen[k]; i += BLOCK) acc += chunk_quant(a.dn[sst[k] + i], qi, cl);
   }
-  __shared__ double red[BLOCK / 64];
-  acc = wave_sum(acc);
-  if ((t & 63) == 0) red[t >> 6] = acc;
+  __shared__ unsigned long long tot;
+  if (t == 0) tot = 0ull;
   __syncthreads();
-  if (t == 0) {
-    double tot = 0.0;
-    for (int w = 0; w < BLOCK / 64; ++w) tot += red[w];
-    a.gpart[(int64_t)c * a.groups + q] = tot;
-  }
+  if (acc) atomicAdd(&tot, (unsigned long long)acc);   // LDS integer adds: exact in any order
+  __syncthreads();
+  if (t == 0) a.gpart[(int64_t)c * a.groups + q] = (int64_t)tot;
 }
 
 __global__ __launch_bounds__(BLOCK) void chunk_total_kernel(ChunkPartialArgs a) {
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(BLOCK) void chunk_total_kernel(ChunkPartialArgs a) 
   const int g = a.lc_gid[c];
   if (!a.active[g]) return;
   const int ng = (a.lc_ptr[c + 1] - a.lc_ptr[c] + CHUNK_GROUP_RUNS - 1) / CHUNK_GROUP_RUNS;
-  double tot = 0.0;
+  int64_t tot = 0;
   for (int q = 0; q < ng; ++q) tot += a.gpart[(int64_t)c * a.groups + q];
   a.part[g] = tot;
 }
@@ -452,9 +452,9 @@ __global__ __launch_bounds__(DEC_BLOCK) void chunk_decide_kernel(ChunkDecideArgs
     const bool was = a.active[g] != 0;
     bool stop = false;
     if (was) {
-      double tot = 0.0;
-      for (int r = 0; r < a.world; ++r) tot += a.part_all[(int64_t)r * a.nc + g];   // rank order
-      const double norm = sqrt(tot > 0.0 ? tot : 0.0) / a.len_x[g];
+      int64_t tot = 0;
+      for (int r = 0; r < a.world; ++r) tot += a.part_all[(int64_t)r * a.nc + g];   // exact
+      const double norm = sqrt((double)tot * a.unit);
       mx = norm > mx ? norm : mx;
       stop = chunk_stops(norm, a.n_iter, a.min_iter, a.max_iter, a.tol);
     }

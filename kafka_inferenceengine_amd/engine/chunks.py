@@ -12,13 +12,14 @@ the same test is vacuous (the norm scales like rms(dx) / sqrt(n_p N)).
 the test per chunk (``EngineConfig.convergence_chunk``):
 
 * the analysis writes each pixel's |x - x0|^2 (``AnalysisArgs.dn_out``);
-* ``chunk_partials`` sums them per chunk over this rank's pixels in a fixed
-  order (runs of one raster row in groups of 16 rows, row order: independent
-  of the visiting order and of the device);
-* the per-chunk partials of every rank are all-gathered (C1: one f64 per
-  chunk, ~15 KB for a 10980² granule in 256² chunks) and summed in rank order
-  by ``chunk_decide`` -- the same decision on every rank -- which marks the
-  chunks that stop now;
+* ``chunk_partials`` sums them per chunk over this rank's pixels as integer
+  quanta of the chunk's squared norm (:meth:`ChunkConvergence.quantum`): the
+  sums are exact, so they do not depend on the order of the adds, on the
+  device, or on where strip boundaries cut a chunk;
+* the per-chunk partials of every rank are all-gathered (C1: one int64 per
+  chunk, ~15 KB for a 10980² granule in 256² chunks) and added by
+  ``chunk_decide`` -- the same decision on every rank and for any rank count
+  -- which marks the chunks that stop now;
 * ``chunk_compact`` removes the stopped chunks' pixels from the visiting
   order (stable, so the observed-first order of ``obs_order`` survives) and
   copies their final x into the next launch's output buffer: later launches
@@ -91,7 +92,7 @@ class ChunkConvergence:
         self.seg_start, self.seg_len = i32(seg_start), i32(seg_len)
         self.lc_ptr, self.lc_gid = i32(lc_ptr), i32(lc_gid)
         self.groups = K.chunk_groups(lc_ptr)
-        self.gpart = torch.zeros(max(lc_gid.size, 1) * self.groups, dtype=torch.float64, device=self.device)
+        self.gpart = torch.zeros(max(lc_gid.size, 1) * self.groups, dtype=torch.int64, device=self.device)
         self.chunk_of = i32(gid) if N else torch.zeros(1, dtype=torch.int32, device=self.device)
         self.local_count = i32(local_count)
         self.counts = counts
@@ -101,7 +102,8 @@ class ChunkConvergence:
         self.newly = torch.zeros(self.nc, dtype=torch.uint8, device=self.device)
         self._iters = torch.zeros(self.nc, dtype=torch.int32, device=self.device)
         self._static = None   # set_static(): every tested chunk stopped at this iteration (filled lazily)
-        self.part = torch.zeros(self.nc, dtype=torch.float64, device=self.device)
+        self.part = torch.zeros(self.nc, dtype=torch.int64, device=self.device)
+        self._quanta = {}
         self.info = torch.zeros(4, dtype=torch.float64, device=self.device)
         # this rank's active pixels after the decisions of odd / even iterations
         # (int32): the device counts of launches queued before the host reads them
@@ -148,28 +150,46 @@ class ChunkConvergence:
         a count a queued launch or compaction has still to read)."""
         return self.px[n_iter % 2:n_iter % 2 + 1]
 
+    def quantum(self, tol: float):
+        """(qinv [nc], clamp, unit) of the integer norm sums for exit tolerance
+        ``tol``.  A chunk's squared norm ||dx||^2 / len_x^2 is counted in quanta
+        of ``unit`` = tol^2 / 2^(61 - B) (B: bits of the largest chunk's pixel
+        count), so the threshold tol^2 is 2^(61 - B) quanta -- 2^44 for 256²
+        chunks, a resolution far below float32 |dx|^2 rounding -- and one pixel
+        contributes at most ``clamp`` = twice that: no chunk total can overflow
+        int64, and a clamped pixel still keeps its chunk iterating.  tol <= 0
+        (stop at max_iterations only) quantises against 1e-3."""
+        hit = self._quanta.get(float(tol))
+        if hit is None:
+            B = int(max(int(self.counts.max()) if self.counts.size else 1, 1)).bit_length()
+            thr = 2 ** (61 - B)
+            t = float(tol) if tol > 0 else 1e-3
+            unit = t * t / thr
+            lx = np.maximum(self.counts, 1) * float(self.n_params)
+            qinv = torch.from_numpy(1.0 / (lx * lx * unit)).to(self.device)
+            hit = self._quanta[float(tol)] = (qinv, 2 * thr, unit)
+        return hit
+
     def decide(self, n_iter: int, tol: float, min_iter: int, max_iter: int):
         """Per-chunk norms of the last launch's dn and the exit test; returns
         a pending read-back of (active chunks, largest norm, this rank's
         active pixels, chunks stopped now), and leaves the pixel count in
         :meth:`px_slot` too.
 
-        The decision is rank-uniform (every rank sums the same gathered
-        partials in rank order) but not rank-count invariant by construction:
-        a chunk cut by a strip boundary sums its pixels in per-rank groups, so
-        its f64 norm can differ in the last bits between 1, 4 and 8 ranks, and a
-        chunk whose norm sits within that rounding of ``tol`` could stop one
-        iteration apart.  The 1 / 4 / 8-rank equality tests
-        (tests/test_chunks.py, the 8-rank bench rehearsal) pin the cases run."""
+        The decision is rank-uniform and rank-count invariant by
+        construction: the partials are exact integer sums of per-pixel quanta
+        (:meth:`quantum`), so 1, 4 and 8 ranks add up the same totals
+        whatever the strip cuts."""
         from ..parallel.comm import PendingSum
 
         self._ready = False
+        qinv, clamp, unit = self.quantum(tol)
         if self.N:
             K.chunk_partials(self.dn, self.seg_start, self.seg_len, self.lc_ptr, self.lc_gid, self.active, self.part,
-                             self.gpart, self.groups)
+                             self.gpart, self.groups, qinv, clamp)
         part_all = self.comm.all_gather_vec(self.part)
         K.chunk_decide(part_all, self.comm.world, self.len_x, self.local_count, tol, n_iter, min_iter, max_iter,
-                       self.active, self.newly, self._iters, self.info, px_out=self.px_slot(n_iter))
+                       self.active, self.newly, self._iters, self.info, px_out=self.px_slot(n_iter), unit=unit)
         # (a device result goes to its own pinned mailbox slot; the host runner's
         # is copied, the next decision may run before this one is read)
         return PendingSum(self.info if self.device.type == "cuda" else self.info.clone(), 1, 4)

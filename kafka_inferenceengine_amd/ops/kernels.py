@@ -569,30 +569,37 @@ def chunk_groups(lc_ptr) -> int:
     return max(1, int(-(-runs.max() // CHUNK_GROUP_RUNS))) if runs.size else 1
 
 
-def chunk_partials(dn, seg_start, seg_len, lc_ptr, lc_gid, active, part, gpart, groups):
-    """part[g] = sum of dn over this rank's pixels of each active chunk g
-    (fixed order, kf_kernels.hip:chunk_group_kernel / chunk_total_kernel);
-    other entries kept.  ``gpart`` [n_local * groups] f64 scratch, ``groups``
-    from :func:`chunk_groups`."""
+def chunk_partials(dn, seg_start, seg_len, lc_ptr, lc_gid, active, part, gpart, groups, qinv, clamp):
+    """part[g] = this rank's pixels' dn of each active chunk g in integer quanta
+    (kf_core.h:chunk_quant with ``qinv[g]`` quanta per unit and ``clamp``
+    quanta at most per pixel; exact sums, kf_kernels.hip:chunk_group_kernel /
+    chunk_total_kernel); other entries kept.  ``part`` int64 [nc], ``gpart``
+    [n_local * groups] int64 scratch, ``groups`` from :func:`chunk_groups`."""
     n_local = int(lc_gid.numel())
-    if gpart.numel() < n_local * groups or gpart.dtype != torch.float64:
-        raise ValueError("chunk_partials: group scratch too small")
+    if gpart.numel() < n_local * groups or gpart.dtype != torch.int64 or part.dtype != torch.int64:
+        raise ValueError("chunk_partials: int64 part / group scratch of the right size")
+    if qinv.dtype != torch.float64 or qinv.numel() != part.numel():
+        raise ValueError("chunk_partials: qinv must be float64 [nc]")
     ext().chunk_partials(_ptr(dn), _ptr(seg_start), _ptr(seg_len), _ptr(lc_ptr), _ptr(lc_gid), n_local,
-                         _ptr(active), _ptr(part), _ptr(gpart), int(groups), _dev(part), _stream(part))
+                         _ptr(active), _ptr(part), _ptr(gpart), int(groups), _ptr(qinv), int(clamp), _dev(part),
+                         _stream(part))
 
 
 def chunk_decide(part_all, world, len_x, local_count, tol, n_iter, min_iter, max_iter, active, newly, iters, info,
-                 px_out=None):
+                 px_out=None, unit=1.0):
     """The reference's exit test per chunk (linear_kf.py:297-304) on the
-    all-gathered partials [world, nc]; info <- (active chunks, largest norm
-    tested, this rank's active pixels, chunks stopped now); ``px_out`` (int32
-    [>= 1]) <- this rank's active pixels (the next launch's device count)."""
+    all-gathered integer partials [world, nc] (norm = sqrt(total * unit));
+    info <- (active chunks, largest norm tested, this rank's active pixels,
+    chunks stopped now); ``px_out`` (int32 [>= 1]) <- this rank's active
+    pixels (the next launch's device count)."""
     nc = int(active.numel())
     if part_all.numel() != world * nc or len_x.numel() != nc or local_count.numel() != nc:
         raise ValueError("chunk_decide: inconsistent chunk vectors")
+    if part_all.dtype != torch.int64:
+        raise ValueError("chunk_decide: int64 partials")
     ext().chunk_decide(_ptr(part_all), int(world), nc, _ptr(len_x), _ptr(local_count), float(tol), int(n_iter),
                        int(min_iter), int(max_iter), _ptr(active), _ptr(newly), _ptr(iters), _ptr(info),
-                       _ptr(px_out), _dev(active), _stream(active))
+                       _ptr(px_out), float(unit), _dev(active), _stream(active))
 
 
 def chunk_compact_scratch(n: int, device) -> torch.Tensor:

@@ -83,44 +83,51 @@ def test_chunk_ids_follow_get_chunks():
     assert cc.local_count.numpy().sum() == part.N
 
 
-def _order_model(dn, starts, lens, lc_ptr, c, group=16, T=256):
-    """chunks.py / kf_core.h summation order of one local chunk, in NumPy f64."""
-    tot = 0.0
-    for s0 in range(lc_ptr[c], lc_ptr[c + 1], group):
-        acc = np.zeros(T)
-        for sg in range(s0, min(s0 + group, lc_ptr[c + 1])):
-            for t in range(T):
-                for i in range(t, lens[sg], T):
-                    acc[t] += np.float64(dn[starts[sg] + i])
-        gt = 0.0
-        for w in range(T // 64):
-            v = acc[64 * w:64 * w + 64].copy()
-            off = 32
-            while off:
-                v = v + v[np.arange(64) ^ off]
-                off >>= 1
-            gt += v[0]
-        tot += gt
-    return tot
+def _quant_model(dn, qinv, clamp):
+    """kf_core.h chunk_quant in NumPy: float64 product, clamp (NaN too), round half up."""
+    v = dn.astype(np.float64) * qinv
+    out = np.full(v.shape, clamp, dtype=np.int64)
+    ok = v < clamp
+    out[ok] = (v[ok] + 0.5).astype(np.int64)
+    return out
 
 
 @pytest.mark.parametrize("block", [[48, 40], [300, 20]])
-def test_chunk_partials_summation_order(block):
-    """The host runner sums a chunk in the documented fixed order (runs in
-    groups of 16 raster rows; per group a column-slot f64 sum, the wave xor
-    tree, waves in order; groups in order) -- the order the device kernels
-    are pinned bit-identical to (tests/test_gpu_chunks.py)."""
+def test_chunk_partials_are_exact_integer_sums(block):
+    """The host runner's per-chunk partial is the exact integer sum of the
+    pixels' quanta (kf_core.h chunk_quant) -- the device kernels are pinned
+    bit-identical to it (tests/test_gpu_chunks.py) -- and a strip split of
+    the same raster adds up to the same totals (rank-count invariance)."""
     rng = np.random.default_rng(4)
     m = rng.random((90, 610)) > 0.2
     part = StripPartition(m, 0, 1)
     cc = ChunkConvergence(part, block, 7, "cpu", Comm.single("cpu"))
-    dn = (rng.random(part.N) * 10.0 ** rng.integers(-8, 0, part.N)).astype(np.float32)
+    dn = (rng.random(part.N) * 10.0 ** rng.integers(-12, 2, part.N)).astype(np.float32)
+    dn[::97] = np.nan
     cc.dn.copy_(torch.from_numpy(dn))
-    cc.decide(n_iter=1, tol=1e-30, min_iter=2, max_iter=25)
-    starts, lens, ptr = cc.seg_start.numpy(), cc.seg_len.numpy(), cc.lc_ptr.numpy()
-    gid = cc.lc_gid.numpy()
-    for c in range(gid.size):
-        assert cc.part[gid[c]].item() == _order_model(dn, starts, lens, ptr, c), c
+    cc.decide(n_iter=1, tol=1e-3, min_iter=2, max_iter=25)
+    qinv, clamp, unit = cc.quantum(1e-3)
+    chunk_of = cc.chunk_of.numpy()
+    q = _quant_model(dn, qinv.numpy()[chunk_of], clamp)
+    want = np.bincount(chunk_of, weights=None, minlength=cc.nc) * 0
+    for g in np.unique(chunk_of):
+        want[g] = int(q[chunk_of == g].sum())
+        assert cc.part[g].item() == want[g], g
+    # the same raster cut into 3 strips: per-strip partials add up exactly
+    tot = np.zeros(cc.nc, dtype=np.int64)
+    for r in range(3):
+        sp = StripPartition(m, r, 3)
+        cr = ChunkConvergence(sp, block, 7, "cpu", Comm.single("cpu"))
+        assert cr.quantum(1e-3)[2] == unit
+        d = np.full(sp.N, 0, np.float32)
+        gl = np.asarray(sp.local_idx) + sp.r0 * m.shape[1]
+        full = np.full(m.size, 0, np.float32)
+        full[np.flatnonzero(m.ravel())] = dn
+        d[:] = full[gl]
+        cr.dn.copy_(torch.from_numpy(d))
+        cr.decide(n_iter=1, tol=1e-3, min_iter=2, max_iter=25)
+        tot += cr.part.numpy()
+    assert np.array_equal(tot, cc.part.numpy())
 
 
 def test_chunked_equals_farm_of_engines():
