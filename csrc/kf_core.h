@@ -255,8 +255,7 @@ enum AnalysisVariant : int32_t {
   AV_RUNTIME_LAYOUT = 10,    // JRC-TIP bands through the runtime-layout kernel (BAND_LAYOUT_TIP's oracle)
   AV_PER_BAND_OPERAND = 14,  // BAND_LAYOUT_SHARED_X: exponent operand rebuilt per band
   AV_BLOCK_ORDER = 16,       // exponent MFMAs block by block (gpm_il_default's other order)
-  AV_GENERIC_SPEC = 18,      // fused forecast through the generic launch instead of SPEC_PROP
-  AV_PROP_PF = 19            // SPEC_PROP_PF (next group's forecast inputs loaded ahead) for any table size
+  AV_GENERIC_SPEC = 18       // fused forecast through the generic launch instead of SPEC_PROP
 };
 
 struct AnalysisArgs {

@@ -552,7 +552,7 @@ static bool l_analysis_fast(const AnalysisArgs& a, int grid, hipStream_t s, int*
     if (!a.prop || a.variant == AV_BLOCK_ORDER || a.variant == AV_GENERIC_SPEC)                     \
       KF_MFMA_GO(OBS_, BS_, MINW_, LAY_)                                                            \
     else if (a.reg_v) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP_REG)                      \
-    else if (small || a.variant == AV_PROP_PF) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP_PF) \
+    else if (small) KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP_PF)                          \
     else KF_MFMA_GO1(OBS_, BS_, MINW_, LAY_, IL_, SPEC_PROP)                                        \
   }
       // Launch bound of 3 workgroups per CU (MINW = 3, as the LDS tables

@@ -168,7 +168,6 @@ class Variant(IntEnum):
     PER_BAND_OPERAND = 14    # BAND_LAYOUT_SHARED_X: exponent operand rebuilt per band
     BLOCK_ORDER = 16         # exponent MFMAs block by block
     GENERIC_SPEC = 18        # fused forecast through the generic launch instead of SPEC_PROP
-    PROP_PF = 19             # SPEC_PROP_PF (next group's forecast inputs ahead) for any table size (A/B)
 
 
 # analysis variant of launches that pass none (tests switch it to an oracle path;
