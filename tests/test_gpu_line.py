@@ -83,7 +83,7 @@ def test_line_tables_are_used_and_cached(cuda):
     assert K.line_fields(tab, None, n, cuda) is None
 
 
-@pytest.mark.parametrize("cfg", ["tip", "prosail"])
+@pytest.mark.parametrize("cfg", ["tip", "tip_gain", "prosail"])
 def test_line_tables_engine_runs_close_to_gp_sums(cuda, cfg):
     """Whole runs with and without line tables: the same Gauss-Newton counts and
     states within the matrix-core GP's own float32 error."""
@@ -91,8 +91,8 @@ def test_line_tables_engine_runs_close_to_gp_sums(cuda, cfg):
     mask[10:30, 40:90] = False
     outs = []
     for line in (True, False):
-        cfg_e = k.EngineConfig(line_tables=line)
-        if cfg == "tip":
+        cfg_e = k.EngineConfig(line_tables=line, analysis_form="gain" if cfg == "tip_gain" else "information")
+        if cfg.startswith("tip"):
             grid = [dt.datetime(2017, 1, 1) + dt.timedelta(days=16 * i) for i in range(5)]
             obs = k.SyntheticBHRObservations(mask, n_train=500, device=cuda, stream=False, n_pool=3, field_cell=8)
             kf = k.LinearKalman(obs, None, mask, k.create_nonlinear_observation_operator, k.TIP_PARAMETERS,
