@@ -1650,7 +1650,8 @@ KF_HD float gain_pixel(const GA& a, int64_t p, bool act, float& dn1, EVAL&& eval
         dn1 = fmaf(d, d, dn1);
         x0[j] = x[j];
       }
-      gain_load_forecast<NP>(a, p, xf, P, cd, cd_ok);
+      // through an opaque pixel index: recomputed, not kept live across iteration 1 (CSE)
+      gain_load_forecast<NP>(a, opaque_lane(p), xf, P, cd, cd_ok);
       st = st_fc;
       nobs = 0;
     }

@@ -223,9 +223,11 @@ static void gpm_lds_attr(K kernel, size_t bytes) {
 }
 
 // K1g with the GP on the matrix cores (JRC-TIP: tables staged in LDS once per
-// workgroup, as analysis_mfma_kernel).
+// workgroup, as analysis_mfma_kernel).  3 workgroups per CU (168 VGPRs, 80 B
+// of scratch per lane) run 6 % faster than 2 (201 VGPRs, 64 B): tip7 gain
+// 24.05 vs 25.52 ms/step (profiles/r6_v25_gain_three_waves_ab.jsonl).
 template <int NP, int D, int FOBS>
-__global__ __launch_bounds__(BLOCK) void gain_mfma_kernel(GainArgs a) {
+__global__ __launch_bounds__(BLOCK, 3) void gain_mfma_kernel(GainArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   extern __shared__ kf_h8 gpm_lds[];
   {

@@ -59,6 +59,8 @@ HOT = {   # kernel: (min waves per SIMD, max scratch bytes per lane)
     "_ZN2kf22analysis_mfma_g_kernelILi10ELi10ELi2ELb0ELb0ELi0EEEvNS_12AnalysisArgsE": (2, 0),
     "_ZN2kf22analysis_mfma_g_kernelILi10ELi10ELi2ELb0ELb1ELi0EEEvNS_12AnalysisArgsE": (2, 0),
     "_ZN2kf22analysis_mfma_g_kernelILi10ELi10ELi2ELb0ELb1ELi1EEEvNS_12AnalysisArgsE": (2, 0),   # prosail10 (fused forecast)
+    # JRC-TIP gain form: 3 waves per SIMD by launch bound, a few registers spilled (measured faster than 2 waves)
+    "_ZN2kf16gain_mfma_kernelILi7ELi4ELi2EEEvNS_8GainArgsE": (3, 80),
 }
 
 
